@@ -1,0 +1,252 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident block scan+sum throughput (BASELINE.json metric), one JSON line on rank 0.
+
+Workload at N=1 (BASELINE.json configs[1]): a 256 MiB fp32 gradient, BLOCK_SIZE=256 (64 lanes, 8 partitions),
+reference generator at -r 0.095 (10 % of blocks non-zero = 90 % block-sparse), one worker, already resident
+in HBM.  One step = one pass of the hot path over it: the fused worker scan + aggregator sum kernel
+(flags, row masks, summed non-zero blocks) and the next-offset kernel.  Four input/output buffer sets are
+rotated so that no step re-reads data the 256 MiB Infinity Cache still holds from the previous use.
+N>1 (torch.distributed.run, one rank per GPU): each rank is worker r with its own 256 MiB tensor (seed r+1) and
+aggregator for shard r; a step is the full sparse all-reduce (omr.dist): local scan, RCCL exchange of the
+non-zero blocks over xGMI, rank-order shard sums, RCCL all-gather of the sums, in-place scatter.
+
+value   = bytes of gradient processed by all ranks per second (decimal GB/s, logical tensor bytes; the
+          reference's "alg bw" divides the same quantity by 2^30: client.cc:445)
+roofline= the dominant kernel (k_scan1) timed with HIP events on its own stream inside the timed region;
+          achieved = its algorithmic bytes per launch / its mean duration
+cpu_baseline = the oracle's C restatement of the reference loop (client.cc:19-31 + server.cc:83-99) on this
+          host, 8 pthreads one per partition as client.cc:384-392, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "omnireduce-rdma-demo_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from omr import Layout, ops  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--size-mib", type=int, default=256)
+    p.add_argument("--block-size", type=int, default=256)
+    p.add_argument("--density", type=float, default=0.095, help="reference -r (0.095 -> 10%% non-zero)")
+    p.add_argument("--workers", type=int, default=1, help="m worker tensors per GPU (N=1 only)")
+    p.add_argument("--rotate", type=int, default=4, help="buffer sets rotated to defeat the Infinity Cache")
+    p.add_argument("--cpu-rounds", type=int, default=101)
+    p.add_argument("--cpu-warmups", type=int, default=10)
+    p.add_argument("--cpu-threads", type=int, default=8)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
+                   help="rocprofv3 PMC summary giving HBM traffic per launch (optional)")
+    return p.parse_args()
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def algorithmic_scan_bytes(L: Layout, bitmaps, m: int) -> int:
+    """Bytes k_scan1/k_scanm must move per launch: read m*S, write the summed blocks (union non-zero blocks
+    and lane heads), the m int32 flag arrays and the row masks."""
+    nb, B = L.nb, L.block_size
+    union = np.zeros(nb, dtype=bool)
+    for bm in bitmaps:
+        union |= bm.astype(bool)
+    heads = ((np.arange(nb) // L.num_lanes) % L.rows_per_part) == 0
+    written = int(np.count_nonzero(union | heads))
+    masks = (m if m == 1 else m + 1) * L.rows * 8
+    return m * L.nbytes + written * B * 4 + m * nb * 4 + masks
+
+
+def step_algorithmic_bytes(L: Layout, bitmaps, m: int) -> int:
+    """m*S + d_union*S + m*nb*8 (flag + next per block per worker)."""
+    nb = L.nb
+    union = np.zeros(nb, dtype=bool)
+    for bm in bitmaps:
+        union |= bm.astype(bool)
+    return m * L.nbytes + int(np.count_nonzero(union)) * L.block_size * 4 + m * nb * 8
+
+
+def read_pmc(path: str, workload: str):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(L: Layout, bm: np.ndarray, args):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker / CPU baseline only (never the product path)
+    x = oracle.fill(bm, L.block_size)
+    t, _, _, _ = oracle.cpu_baseline(x, bm, L.n, L.block_size, L.num_lanes, L.num_threads, args.cpu_threads, 1,
+                                     args.cpu_warmups, args.cpu_rounds)
+    t_ref, _, _, _ = oracle.cpu_baseline(x, bm, L.n, L.block_size, L.num_lanes, L.num_threads, args.cpu_threads,
+                                         0, args.cpu_warmups, args.cpu_rounds)
+    t1, _, _, _ = oracle.cpu_baseline(x, bm, L.n, L.block_size, L.num_lanes, L.num_threads, 1, 1, 1, 5)
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(L.nbytes / t / 1e9, 3),
+        "unit": "GB/s",
+        "cores": args.cpu_threads,
+        "kind": "port",
+        "sample": (f"config 2 tensor ({L.nbytes >> 20} MiB, B={L.block_size}, -r {args.density}), data-derived "
+                   f"fp32 scan + next offsets + block aggregate, {args.cpu_warmups} warm-up + {args.cpu_rounds} "
+                   f"rounds, {args.cpu_threads} pthreads one per partition (client.cc:384-392)"),
+        "ms_per_round": round(t * 1e3, 3),
+        "reference_faithful_bitmap_walk": {"value": round(L.nbytes / t_ref / 1e9, 3), "unit": "GB/s",
+                                           "ms_per_round": round(t_ref * 1e3, 3),
+                                           "note": "reads the generator bitmap, never the zero blocks"},
+        "one_thread": {"value": round(L.nbytes / t1 / 1e9, 3), "unit": "GB/s", "ms_per_round": round(t1 * 1e3, 3)},
+        "host": {"nproc": os.cpu_count(), "cpu_model": cpu_model},
+    }
+
+
+def main():
+    args = parse()
+    ws, rank, local = dist_env()
+    n_gpus = ws if ws > 1 else args.gpus
+    if ws > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if ws > 1 else 0)
+    L = Layout.from_bytes(args.size_mib << 20, args.block_size)
+    m = args.workers if ws == 1 else 1
+    workload = (f"config2: {args.size_mib} MiB fp32 per rank, block_size={args.block_size}, -r {args.density} "
+                f"(90% block-sparse), {m} worker(s) per GPU, device-resident scan+sum")
+
+    # ---- inputs (reference generator, seed = worker id + 1: client.cc:396) -------------------------------
+    worker_ids = [rank * m + w for w in range(m)]
+    bitmaps = [ops.gen_bitmap(wid, args.density, L.nb) for wid in worker_ids]
+    sets = []
+    for _ in range(max(1, args.rotate)):
+        xs = [ops.fill_blocks(torch.from_numpy(bm).to(dev), L, mode=0) for bm in bitmaps]
+        sets.append((xs, torch.zeros(L.n, dtype=torch.float32, device=dev)))
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+    if ws > 1:
+        from omr import dist
+        engine = dist.SparseAllreduce(L, device=dev)
+        state = [engine.prepare(xs[0]) for xs, _ in sets]
+
+        def step(i):
+            k = i % len(sets)
+            return engine.run(sets[k][0][0], state[k], ev=None)
+    else:
+        plan = ops.ScanSumPlan(L, m, device=dev)
+
+        def step(i, ev=None):
+            xs, out = sets[i % len(sets)]
+            if ev is not None:
+                ev[0].record(stream)
+            plan.run(xs, out, with_next=False)
+            if ev is not None:
+                ev[1].record(stream)
+            plan.resolve_next()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)] if ws == 1 else None
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        if ws == 1:
+            step(args.warmup + i, kev[i])
+        else:
+            step(args.warmup + i)
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+
+    roofline = None
+    if ws == 1:
+        kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
+        kbytes = algorithmic_scan_bytes(L, bitmaps, m)
+        achieved = kbytes / (kms * 1e-3) / 1e9
+        traffic = read_pmc(args.pmc, workload)
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                    "kernel": "k_scan1" if m == 1 else "k_scanm", "kernel_ms": round(kms, 5),
+                    "algorithmic_bytes_per_launch": kbytes}
+        sbytes = step_algorithmic_bytes(L, bitmaps, m)
+        roofline["step_algorithmic_bytes"] = sbytes
+        roofline["step_frac"] = round(sbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+
+    if rank != 0:
+        if ws > 1:
+            torch.distributed.destroy_process_group()
+        return
+    total_bytes = n_gpus * m * L.nbytes
+    value = total_bytes / (ms_per_step * 1e-3) / 1e9
+    line = {
+        "metric": "GB/s device-resident block scan+sum, 256 MiB fp32 @ 90% block-sparse",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (reference generator client.cc:396-421: srand(rank+1), -r 0.095, 0.01f blocks)",
+        "config": {"workload": workload, "tensor_bytes_per_rank": L.nbytes, "block_size": L.block_size,
+                   "num_lanes": L.num_lanes, "num_threads": L.num_threads, "density_r": args.density,
+                   "nonzero_fraction": round(float(np.mean([bm.mean() for bm in bitmaps])), 5),
+                   "workers_per_gpu": m, "rotating_buffer_sets": len(sets),
+                   "parallelism": "single GPU" if n_gpus == 1 else f"dp{n_gpus} sparse all-reduce (RCCL)"},
+        "alg_bw_GiBps_reference_style": round(total_bytes / (ms_per_step * 1e-3) / 2 ** 30, 2),
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if ws == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(L, bitmaps[0], args)
+    print(json.dumps(line), flush=True)
+    if ws > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+/*
+ * omr.h — C ABI of the MI355X-native OmniReduce sparse-block hot path.
+ *
+ * This is the drop-in boundary for the two hot loops of Phlix1/OmniReduce-RDMA-Demo:
+ *   - the worker-side non-zero-block scan   (reference client.cc:19-31, driven from client.cc:87-102, :191-205)
+ *   - the aggregator-side per-block fp32 sum (reference server.cc:83-99, the add at server.cc:97-98)
+ * on the block/lane/partition layout fixed by reference common.h:27-42.
+ *
+ * The reference has no plugin/FFI API of its own: its seams are internal C++ calls on `struct resources*`
+ * (common.h:79-105, :106-128).  Each entry point below names the reference function/loop it replaces.
+ *
+ * Conventions:
+ *   - plain C types only; every buffer is caller-owned; device pointers unless a parameter says "host";
+ *   - `omr_stream_t` is a hipStream_t (NULL = the default stream); every launch is asynchronous on it and
+ *     performs no allocation and no host synchronisation, so a caller may capture calls into a hipGraph;
+ *   - return 0 on success, OMR_EINVAL (<0) on a bad argument (message in omr_last_error()), or a positive
+ *     hipError_t code if a launch failed;
+ *   - calls on disjoint buffers/streams are safe to issue concurrently (the reference runs one pthread per
+ *     partition on disjoint ranges, client.cc:384-392).
+ *
+ * Layout vocabulary (reference common.h:27-42):
+ *   n            floats in the gradient tensor (DATA_SIZE, common.h:40)
+ *   block_size   floats per block (BLOCK_SIZE, common.h:32); supported: 256, 512, 1024
+ *   num_lanes    NUM_BLOCKS = NUM_SLOTS*MESSAGE_SIZE/BLOCK_SIZE (common.h:36-37): 64 at B=256, 16 at B=1024
+ *   num_parts    NUM_THREADS partitions of n/num_parts floats each (common.h:35, :38)
+ *   block b      floats [b*B, (b+1)*B); lane bid = b % num_lanes (client.cc:23, server.cc:85)
+ *   row          num_lanes consecutive blocks (one block per lane); a partition is rows_per_part rows
+ *   offset       uint32 float-element index of a block's first element (client.cc:19, common.cc:407)
+ *   sentinel     omr_sentinel(B, num_lanes) + bid*B marks "no further non-zero block in this lane"
+ *                (client.cc:24, :42; server.cc:16)
+ *   row mask     uint64 per row, bit l set iff block (row, lane l) is non-zero  (this build's compact flag form)
+ */
+#ifndef OMR_H
+#define OMR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMR_ABI_VERSION 1
+#define OMR_EINVAL (-1)
+#define OMR_MAX_WORKERS 16 /* reference caps peers at 10: common.h:59 peer_names[10] */
+
+/* Reference layout constants (common.h:31, :36). */
+#define OMR_MESSAGE_SIZE 1024u
+#define OMR_NUM_SLOTS 16u
+#define OMR_NUM_THREADS 8u
+
+typedef void* omr_stream_t; /* hipStream_t */
+
+/* ---------------------------------------------------------------- layout helpers (common.h:27-42) */
+
+int omr_abi_version(void);
+const char* omr_last_error(void);
+
+/* NUM_BLOCKS for a block size: NUM_SLOTS*MESSAGE_SIZE/BLOCK_SIZE (common.h:33, :36-37). */
+uint32_t omr_num_lanes(uint32_t block_size);
+
+/* Sentinel base (UINT32_MAX/B/NB-1)*NB*B = 4294934528 for every supported B (client.cc:24, server.cc:16). */
+uint32_t omr_sentinel(uint32_t block_size, uint32_t num_lanes);
+
+/* 0 iff (n, B, NB, parts) is a layout this library runs: B in {256,512,1024}, NB*B a multiple of 256,
+ * NB <= 64, n a multiple of parts*NB*B, n <= sentinel base (uint32 offsets, client.cc:24). */
+int omr_layout_check(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts);
+
+/* ---------------------------------------------------------------- synthetic input (client.cc:396-421) */
+
+/* Reference generator: srand(worker_id+1); for every block i in order,
+ * bitmap[i] = (rand()%100/(double)101 < density_ratio) (client.cc:396, :406-414).
+ * glibc rand() is restated (TYPE_3 additive feedback) so the library does not touch the process-global
+ * libc generator.  `bitmap` is HOST memory.  *nonzero_count (may be NULL) gets the count (client.cc:410). */
+int omr_gen_bitmap(uint32_t worker_id, double density_ratio, uint64_t num_blocks, int32_t* bitmap,
+                   uint64_t* nonzero_count);
+
+/* Fill `buf` (n = num_blocks*block_size floats, device) from a device bitmap:
+ * mode 0: the reference fill, 0.01f in flagged blocks and 0 elsewhere (client.cc:401-404, :415-419);
+ * mode 1: flagged blocks get uniform [-1,1) values from a counter hash of (seed, element index), others 0
+ *         (the random-valued tolerance variant of SURVEY.md §8d). */
+int omr_fill_blocks_f32(const int32_t* bitmap, uint64_t num_blocks, uint32_t block_size, int mode,
+                        uint32_t seed, float* buf, omr_stream_t stream);
+
+/* ---------------------------------------------------------------- ★1 worker scan (client.cc:19-31) */
+
+/* Worker-side non-zero-block scan of one fp32 gradient (replaces find_next_nonzero_block, client.cc:19-31,
+ * and its drivers client.cc:87-102 / :191-205, with the flag derived from the data as north_star requires
+ * instead of the generator's precomputed bitmap, client.cc:26):
+ *   flags[b]        (int32, may be NULL)   1 iff some element of block b is != 0.0f (-0.0 counts as zero,
+ *                                          NaN as non-zero); the reference's `int *bitmap` (common.h:98)
+ *   row_masks[r]    (uint64, required)     bit l = flags[r*NB + l]
+ *   next_offsets[b] (uint32, may be NULL)  find_next_nonzero_block(b*B + B*NB): offset of the first non-zero
+ *                                          block after b in the same lane and partition, else sentinel+bid*B
+ */
+int omr_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                 int32_t* flags, uint64_t* row_masks, uint32_t* next_offsets, omr_stream_t stream);
+
+/* ---------------------------------------------------------------- ★1+★3 fused scan + aggregation */
+
+/* m worker scans plus the aggregator sum in one HBM pass over the m tensors (server.cc:83-99):
+ *   bufs            HOST array of m device pointers (worker rank order), 1 <= m <= OMR_MAX_WORKERS
+ *   flags           [m][nb] int32 per-worker flags, or NULL
+ *   row_masks       [m][rows] per-worker row masks, then (m > 1 only) [rows] union masks at index m
+ *   next_offsets    [m][nb] per-worker chains, then (m > 1 only) [nb] aggregator chain = next over the union
+ *                   (server.cc:86-96: min over workers of their next offsets), or NULL
+ *   out             dense fp32[n] or NULL: for every block that is non-zero in some worker, and for every
+ *                   lane-head block (row 0 of a partition, always sent: client.cc:201-205), out block =
+ *                   ((0.0f + x_0) + x_1) + ... + x_{m-1} (rank order, accumulator zeroed first as at
+ *                   server.cc:148-150); other blocks of `out` are not written (pass a worker's own buffer
+ *                   for the reference's in-place result, client.cc:89). out may alias bufs[i].
+ */
+int omr_scan_sum_f32(const float* const* bufs, uint32_t m, uint64_t n, uint32_t block_size,
+                     uint32_t num_lanes, uint32_t num_parts, int32_t* flags, uint64_t* row_masks,
+                     uint32_t* next_offsets, float* out, omr_stream_t stream);
+
+/* Next-offset chains from row masks (client.cc:19-31 for one worker; for a union mask, the aggregator's
+ * min_next chain server.cc:86-96).  `count` mask arrays of `rows` each, stride `rows`; output stride nb. */
+int omr_next_offsets(const uint64_t* row_masks, uint32_t count, uint64_t n, uint32_t block_size,
+                     uint32_t num_lanes, uint32_t num_parts, uint32_t* next_offsets, omr_stream_t stream);
+
+/* ---------------------------------------------------------------- ★3 aggregator sum over a block list */
+
+/* For each listed global block index b: out[b*B + j] = ((0.0f + in_0) + in_1) + ... for j < B
+ * (server.cc:97-98 in rank order; the accumulator zeroing of server.cc:148-150 is the 0.0f start).
+ * `inputs` is a HOST array of m device pointers, dense layout. */
+int omr_block_sum_f32(const float* const* inputs, uint32_t m, const uint32_t* block_list, uint32_t num_list,
+                      uint32_t block_size, float* out, omr_stream_t stream);
+
+/* ---------------------------------------------------------------- compaction and block movement */
+
+/* Bytes of device workspace omr_compact needs for `rows` rows. */
+size_t omr_compact_workspace_bytes(uint64_t rows);
+
+/* List the set bits of row masks in increasing block order: block_list[k] = global block index
+ * (row*NB + lane) of the k-th non-zero block; *count (device uint32) = total.  Rows [row_begin, row_end). */
+int omr_compact(const uint64_t* row_masks, uint64_t row_begin, uint64_t row_end, uint32_t num_lanes,
+                uint32_t* block_list, uint32_t* count, void* workspace, size_t workspace_bytes,
+                omr_stream_t stream);
+
+/* Pack listed blocks contiguously (the worker-side gather of common.cc:405-407) / scatter them back in
+ * place (the worker-side result copy of client.cc:89). */
+int omr_gather_blocks_f32(const float* src, const uint32_t* block_list, uint32_t num_list,
+                          uint32_t block_size, float* packed, omr_stream_t stream);
+int omr_scatter_blocks_f32(const float* packed, const uint32_t* block_list, uint32_t num_list,
+                           uint32_t block_size, float* dst, omr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OMR_H */

@@ -1,0 +1,747 @@
+// omr_kernels.hip — CDNA4 (gfx950) kernels + C ABI for the OmniReduce sparse-block hot path.
+//
+// Reference behaviour implemented here (Phlix1/OmniReduce-RDMA-Demo, read-only at /root/reference):
+//   worker scan    client.cc:19-31 find_next_nonzero_block, drivers client.cc:87-102 and :191-205
+//   aggregator sum server.cc:83-99 (block_next_offset / min_next bookkeeping :84-96, the add :97-98)
+//   layout         common.h:27-42 (BLOCK_SIZE, NUM_BLOCKS lanes, NUM_THREADS partitions)
+//   generator      client.cc:396-421
+// Design: the hot path is HBM-bound integer/byte work plus one fp32 add per element; no MFMA.
+//   k_scan1 / k_scanm : one wave per 64 KiB row (num_lanes blocks).  Every block is read once with
+//                       16-byte-per-lane coalesced loads (a 256-float block is exactly one wave-wide
+//                       dwordx4 load), the non-zero flag is a wavefront ballot, and the aggregator sum is
+//                       fused into the same pass so non-zero blocks are written straight from registers.
+//   k_next            : next-offset chains from the uint64 row masks (tiny: 8 B per 64 KiB row);
+//                       one workgroup per 64-row segment, lane columns transposed with ballots.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "omr.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return OMR_EINVAL;
+}
+
+int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return static_cast<int>(e);
+  }
+  return 0;
+}
+
+// Native 16-byte vectors: one dwordx4 per lane, a wave-wide load moves 1 KiB = one 256-float block.
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+struct WorkerPtrs {
+  const float* p[OMR_MAX_WORKERS];
+};
+
+constexpr int kWavesPerWG = 4;
+constexpr int kWGThreads = 64 * kWavesPerWG;
+constexpr int kMaxGrid = 2048;  // 8 workgroups per CU over 256 CUs; grid-stride beyond (guide G11)
+
+// ---------------------------------------------------------------- device helpers
+
+// Non-zero test of 4 floats: x != 0.0f for any of them, with -0.0 zero and NaN non-zero.  OR-ing the raw
+// bits and then clearing bit 31 is the bitwise OR of the four |x| bit patterns, so it is exact.
+__device__ __forceinline__ uint32_t nz_bits(const v4f& v) {
+  const v4u u = __builtin_bit_cast(v4u, v);
+  return (u.x | u.y | u.z | u.w) & 0x7fffffffu;
+}
+
+template <bool NT>
+__device__ __forceinline__ v4f ld4(const v4f* p) {
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(p);
+  } else {
+    return *p;
+  }
+}
+
+__device__ __forceinline__ v4f add4(const v4f& a, const v4f& b) { return a + b; }
+
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
+
+constexpr int pow2floor(int x) {
+  int r = 1;
+  while (r * 2 <= x) r *= 2;
+  return r;
+}
+
+struct ScanArgs {
+  WorkerPtrs x;
+  uint32_t m;
+  uint32_t lanes;          // NUM_BLOCKS
+  uint32_t rows_per_part;  // rows per partition
+  uint32_t pad;
+  uint64_t rows;           // total rows
+  uint64_t nb;             // total blocks
+  int32_t* flags;          // [m][nb] or null
+  uint64_t* masks;         // [m (+1 union)][rows]
+  float* out;              // dense or null
+};
+
+// ---------------------------------------------------------------- k_scan1: one worker, fused scan + sum
+//
+// Wave w handles rows w, w + nwaves, ...  A row is `lanes` blocks of VEC*256 floats; it is swept in
+// sub-batches of SUB blocks = 16 dwordx4 loads (16 KiB) per wave, all issued before the first use.
+// Per block: ballot(any element non-zero) -> flag bit; if the block is non-zero (or the row is a lane-head
+// row, always sent by the reference: client.cc:201-205) the aggregated block 0.0f + x (server.cc:148-150
+// zero, :97-98 add) is stored straight from registers.
+template <int VEC, bool NT>
+__global__ __launch_bounds__(kWGThreads) void k_scan1(ScanArgs a) {
+  constexpr int B4 = 64 * VEC;  // v4fs per block
+  constexpr int SUB = pow2floor(16 / VEC);
+  const int lane = threadIdx.x & 63;
+  const v4f* __restrict__ x = reinterpret_cast<const v4f*>(a.x.p[0]);
+  v4f* __restrict__ out = reinterpret_cast<v4f*>(a.out);
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
+  for (uint64_t row = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + (threadIdx.x >> 6); row < a.rows;
+       row += nwaves) {
+    const bool head = (row % a.rows_per_part) == 0;
+    const uint64_t rowbase = row * a.lanes * B4;
+    uint64_t wm = 0;
+    for (uint32_t l0 = 0; l0 < a.lanes; l0 += SUB) {
+      v4f v[SUB][VEC];
+      const v4f* src = x + rowbase + static_cast<uint64_t>(l0) * B4 + lane;
+#pragma unroll
+      for (int s = 0; s < SUB; ++s)
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) v[s][q] = ld4<NT>(src + s * B4 + q * 64);
+#pragma unroll
+      for (int s = 0; s < SUB; ++s) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
+        const bool nz = wave_ballot(o != 0) != 0;
+        wm |= static_cast<uint64_t>(nz) << (l0 + s);
+        if (out != nullptr && (nz || head)) {
+          v4f* dst = out + rowbase + static_cast<uint64_t>(l0 + s) * B4 + lane;
+          const v4f z = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) dst[q * 64] = add4(z, v[s][q]);
+        }
+      }
+    }
+    if (lane == 0) a.masks[row] = wm;
+    if (a.flags != nullptr && lane < static_cast<int>(a.lanes))
+      a.flags[row * a.lanes + lane] = static_cast<int32_t>((wm >> lane) & 1u);
+  }
+}
+
+// ---------------------------------------------------------------- k_scanm: m >= 2 workers on one device
+//
+// Same row sweep; per sub-batch the m workers' blocks are read in rank order and accumulated from +0.0f
+// (server.cc:148-150, :97-98).  Adding a zero-flagged worker's block (all +-0.0) to an accumulator that
+// started at +0.0 never changes it, so summing every worker equals the reference, which only adds the
+// workers that sent the block.  Lane w keeps worker w's row mask (no runtime-indexed register arrays).
+template <int VEC, bool NT>
+__global__ __launch_bounds__(kWGThreads) void k_scanm(ScanArgs a) {
+  constexpr int B4 = 64 * VEC;
+  constexpr int SUB = pow2floor(8 / VEC);
+  const int lane = threadIdx.x & 63;
+  v4f* __restrict__ out = reinterpret_cast<v4f*>(a.out);
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
+  for (uint64_t row = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + (threadIdx.x >> 6); row < a.rows;
+       row += nwaves) {
+    const bool head = (row % a.rows_per_part) == 0;
+    const uint64_t rowbase = row * a.lanes * B4;
+    uint64_t lane_wm = 0;  // lane w: worker w's mask
+    uint64_t um = 0;       // union mask (wave-uniform)
+    for (uint32_t l0 = 0; l0 < a.lanes; l0 += SUB) {
+      v4f acc[SUB][VEC];
+#pragma unroll
+      for (int s = 0; s < SUB; ++s)
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[s][q] = v4f{0.f, 0.f, 0.f, 0.f};
+      uint32_t sub_any = 0;
+
+      for (uint32_t w = 0; w < a.m; ++w) {
+        const v4f* src = reinterpret_cast<const v4f*>(a.x.p[w]) + rowbase +
+                            static_cast<uint64_t>(l0) * B4 + lane;
+        v4f v[SUB][VEC];
+#pragma unroll
+        for (int s = 0; s < SUB; ++s)
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) v[s][q] = ld4<NT>(src + s * B4 + q * 64);
+        uint32_t wbits = 0;
+#pragma unroll
+        for (int s = 0; s < SUB; ++s) {
+          uint32_t o = 0;
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            o |= nz_bits(v[s][q]);
+            acc[s][q] = add4(acc[s][q], v[s][q]);
+          }
+          wbits |= static_cast<uint32_t>(wave_ballot(o != 0) != 0) << s;
+        }
+        if (lane == static_cast<int>(w)) lane_wm |= static_cast<uint64_t>(wbits) << l0;
+        sub_any |= wbits;
+      }
+      um |= static_cast<uint64_t>(sub_any) << l0;
+      if (out != nullptr) {
+#pragma unroll
+        for (int s = 0; s < SUB; ++s) {
+          if (((sub_any >> s) & 1u) || head) {
+            v4f* dst = out + rowbase + static_cast<uint64_t>(l0 + s) * B4 + lane;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) dst[q * 64] = acc[s][q];
+          }
+        }
+      }
+    }
+    if (lane < static_cast<int>(a.m)) a.masks[static_cast<uint64_t>(lane) * a.rows + row] = lane_wm;
+    if (lane == 0) a.masks[static_cast<uint64_t>(a.m) * a.rows + row] = um;
+    if (a.flags != nullptr) {
+      for (uint32_t w = 0; w < a.m; ++w) {
+        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(lane_wm), w);
+        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(lane_wm >> 32), w);
+        const uint64_t wmw = (static_cast<uint64_t>(hi) << 32) | lo;
+        if (lane < static_cast<int>(a.lanes))
+          a.flags[w * a.nb + row * a.lanes + lane] = static_cast<int32_t>((wmw >> lane) & 1u);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- k_next: next-offset chains
+//
+// next[b] for block b = (row r, lane l) = offset of the first row r' > r of the same partition whose
+// mask has bit l, else sentinel + l*B (find_next_nonzero_block(b*B + B*NB), client.cc:19-31).
+// Workgroup = one segment of <= 64 rows of one partition and one mask array (blockIdx.y).
+// Wave 0 transposes the segment's row masks into per-lane column masks with `lanes` ballots and finds,
+// per lane, the first set row after the segment by sweeping later rows 256 at a time (4 per lane).
+struct NextArgs {
+  const uint64_t* masks;
+  uint32_t* next;
+  uint64_t rows;           // rows per mask array
+  uint64_t nb;             // blocks per array (output stride)
+  uint32_t rows_per_part;
+  uint32_t segs_per_part;
+  uint32_t lanes;
+  uint32_t block;
+  uint32_t sentinel;
+};
+
+__global__ __launch_bounds__(kWGThreads) void k_next(NextArgs a) {
+  __shared__ uint64_t s_col[64];
+  __shared__ uint32_t s_carry[64];
+  const uint64_t* masks = a.masks + static_cast<uint64_t>(blockIdx.y) * a.rows;
+  uint32_t* next = a.next + static_cast<uint64_t>(blockIdx.y) * a.nb;
+  const uint32_t part = blockIdx.x / a.segs_per_part;
+  const uint32_t seg = blockIdx.x % a.segs_per_part;
+  const uint64_t part_row0 = static_cast<uint64_t>(part) * a.rows_per_part;
+  const uint64_t part_end = part_row0 + a.rows_per_part;
+  const uint64_t row0 = part_row0 + static_cast<uint64_t>(seg) * 64;
+  const uint64_t seg_end = (row0 + 64 < part_end) ? row0 + 64 : part_end;
+  const int lane = threadIdx.x & 63;
+  const uint32_t row_stride = a.lanes * a.block;  // floats per row
+
+  if (threadIdx.x < 64) {
+    const uint64_t r = row0 + lane;
+    const uint64_t rm = (r < seg_end) ? masks[r] : 0;
+    uint64_t mycol = 0;
+    for (uint32_t l = 0; l < a.lanes; ++l) {
+      const uint64_t b = wave_ballot((rm >> l) & 1u);
+      if (lane == static_cast<int>(l)) mycol = b;
+    }
+    uint32_t carry = a.sentinel + static_cast<uint32_t>(lane) * a.block;
+    uint64_t pending = (a.lanes >= 64) ? ~0ull : ((1ull << a.lanes) - 1);
+    for (uint64_t look = seg_end; pending != 0 && look < part_end; look += 256) {
+      uint64_t lm[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t rr = look + static_cast<uint64_t>(k) * 64 + lane;
+        lm[k] = (rr < part_end) ? masks[rr] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint64_t p = pending;
+        while (p != 0) {
+          const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(p));
+          p &= p - 1;
+          const uint64_t b = wave_ballot((lm[k] >> l) & 1u);
+          if (b != 0) {
+            const uint64_t hit = look + static_cast<uint64_t>(k) * 64 + __builtin_ctzll(b);
+            if (lane == static_cast<int>(l)) carry = static_cast<uint32_t>(hit) * row_stride + l * a.block;
+            pending &= ~(1ull << l);
+          }
+        }
+      }
+    }
+    s_col[lane] = mycol;
+    s_carry[lane] = carry;
+  }
+  __syncthreads();
+  const uint32_t nrows = static_cast<uint32_t>(seg_end - row0);
+  const uint32_t total = nrows * a.lanes;
+  for (uint32_t idx = threadIdx.x; idx < total; idx += kWGThreads) {
+    const uint32_t i = idx / a.lanes;
+    const uint32_t l = idx - i * a.lanes;
+    const uint64_t c = (i >= 63) ? 0 : (s_col[l] >> (i + 1));
+    uint32_t v;
+    if (c != 0) {
+      const uint64_t hit = row0 + i + 1 + __builtin_ctzll(c);
+      v = static_cast<uint32_t>(hit) * row_stride + l * a.block;
+    } else {
+      v = s_carry[l];
+    }
+    next[(row0 + i) * a.lanes + l] = v;
+  }
+}
+
+// ---------------------------------------------------------------- compaction (mask -> block list)
+
+constexpr int kCompactRows = kWGThreads;  // rows per workgroup
+
+__device__ __forceinline__ uint32_t wg_reduce_sum(uint32_t v, uint32_t* s_tmp) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) s_tmp[wave] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (int w = 0; w < kWavesPerWG; ++w) t += s_tmp[w];
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(kWGThreads) void k_compact_count(const uint64_t* masks, uint64_t row_begin,
+                                                              uint64_t row_end, uint32_t* chunk_sum) {
+  __shared__ uint32_t s_tmp[kWavesPerWG];
+  const uint64_t r = row_begin + static_cast<uint64_t>(blockIdx.x) * kCompactRows + threadIdx.x;
+  const uint32_t pc = (r < row_end) ? static_cast<uint32_t>(__builtin_popcountll(masks[r])) : 0u;
+  const uint32_t t = wg_reduce_sum(pc, s_tmp);
+  if (threadIdx.x == 0) chunk_sum[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(kWGThreads) void k_compact_write(const uint64_t* masks, uint64_t row_begin,
+                                                              uint64_t row_end, uint32_t lanes,
+                                                              const uint32_t* chunk_sum, uint32_t* list,
+                                                              uint32_t* count) {
+  __shared__ uint32_t s_tmp[kWavesPerWG];
+  __shared__ uint32_t s_wave[kWavesPerWG];
+  uint32_t base_part = 0;
+  for (uint32_t c = threadIdx.x; c < blockIdx.x; c += kWGThreads) base_part += chunk_sum[c];
+  const uint32_t base = wg_reduce_sum(base_part, s_tmp);
+  const uint64_t r = row_begin + static_cast<uint64_t>(blockIdx.x) * kCompactRows + threadIdx.x;
+  const uint64_t rm = (r < row_end) ? masks[r] : 0;
+  const uint32_t pc = static_cast<uint32_t>(__builtin_popcountll(rm));
+  // inclusive wave scan
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = pc;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) s_wave[wave] = inc;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (int w = 0; w < wave; ++w) wbase += s_wave[w];
+  uint32_t pos = base + wbase + inc - pc;
+  uint64_t bits = rm;
+  while (bits != 0) {
+    const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(bits));
+    bits &= bits - 1;
+    list[pos++] = static_cast<uint32_t>(r * lanes + l);
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kWGThreads - 1) *count = pos;
+}
+
+// ---------------------------------------------------------------- block movement / list sum
+
+template <int VEC>
+__global__ __launch_bounds__(kWGThreads) void k_gather(const float* src, const uint32_t* list, uint32_t num,
+                                                       float* packed) {
+  constexpr int B4 = 64 * VEC;
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerWG;
+  for (uint32_t k = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6); k < num; k += nwaves) {
+    const v4f* s = reinterpret_cast<const v4f*>(src) + static_cast<uint64_t>(list[k]) * B4 + lane;
+    v4f* d = reinterpret_cast<v4f*>(packed) + static_cast<uint64_t>(k) * B4 + lane;
+    v4f v[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) v[q] = s[q * 64];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) d[q * 64] = v[q];
+  }
+}
+
+template <int VEC>
+__global__ __launch_bounds__(kWGThreads) void k_scatter(const float* packed, const uint32_t* list,
+                                                        uint32_t num, float* dst) {
+  constexpr int B4 = 64 * VEC;
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerWG;
+  for (uint32_t k = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6); k < num; k += nwaves) {
+    const v4f* s = reinterpret_cast<const v4f*>(packed) + static_cast<uint64_t>(k) * B4 + lane;
+    v4f* d = reinterpret_cast<v4f*>(dst) + static_cast<uint64_t>(list[k]) * B4 + lane;
+    v4f v[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) v[q] = s[q * 64];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) d[q * 64] = v[q];
+  }
+}
+
+template <int VEC>
+__global__ __launch_bounds__(kWGThreads) void k_list_sum(WorkerPtrs in, uint32_t m, const uint32_t* list,
+                                                         uint32_t num, float* out) {
+  constexpr int B4 = 64 * VEC;
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerWG;
+  for (uint32_t k = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6); k < num; k += nwaves) {
+    const uint64_t off = static_cast<uint64_t>(list[k]) * B4 + lane;
+    v4f acc[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) acc[q] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (uint32_t w = 0; w < m; ++w) {
+      const v4f* s = reinterpret_cast<const v4f*>(in.p[w]) + off;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc[q] = add4(acc[q], s[q * 64]);
+    }
+    v4f* d = reinterpret_cast<v4f*>(out) + off;
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) d[q * 64] = acc[q];
+  }
+}
+
+// ---------------------------------------------------------------- synthetic fill (client.cc:401-419)
+
+__device__ __forceinline__ float hash_uniform(uint64_t idx, uint32_t seed) {
+  uint64_t z = idx + 0x9E3779B97F4A7C15ull * (static_cast<uint64_t>(seed) + 1ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const int32_t u = static_cast<int32_t>(z >> 40) - (1 << 23);  // [-2^23, 2^23)
+  return static_cast<float>(u) * (1.0f / 8388608.0f);           // exact, [-1, 1)
+}
+
+__global__ __launch_bounds__(kWGThreads) void k_fill(const int32_t* bitmap, uint64_t n4, uint32_t block4,
+                                                     int mode, uint32_t seed, float* buf) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWGThreads;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kWGThreads + threadIdx.x; i < n4; i += stride) {
+    const bool on = bitmap[i / block4] == 1;
+    v4f v = v4f{0.f, 0.f, 0.f, 0.f};
+    if (on) {
+      if (mode == 0) {
+        v = v4f{0.01f, 0.01f, 0.01f, 0.01f};
+      } else {
+        v.x = hash_uniform(i * 4 + 0, seed);
+        v.y = hash_uniform(i * 4 + 1, seed);
+        v.z = hash_uniform(i * 4 + 2, seed);
+        v.w = hash_uniform(i * 4 + 3, seed);
+      }
+    }
+    reinterpret_cast<v4f*>(buf)[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------- host-side validation
+
+struct Layout {
+  uint64_t n, nb, rows;
+  uint32_t block, lanes, parts, rows_per_part, vec;
+};
+
+int make_layout(uint64_t n, uint32_t block, uint32_t lanes, uint32_t parts, Layout* L) {
+  if (block != 256 && block != 512 && block != 1024)
+    return fail("block_size %u unsupported (256, 512, 1024)", block);
+  if (lanes == 0 || lanes > 64) return fail("num_lanes %u out of range (1..64)", lanes);
+  if (parts == 0) return fail("num_parts must be >= 1");
+  const uint64_t row_floats = static_cast<uint64_t>(lanes) * block;
+  if (n == 0 || n % (row_floats * parts) != 0)
+    return fail("n=%llu is not a multiple of num_parts*num_lanes*block_size=%llu",
+                static_cast<unsigned long long>(n), static_cast<unsigned long long>(row_floats * parts));
+  if (n > omr_sentinel(block, lanes))
+    return fail("n=%llu exceeds the uint32 offset space (sentinel %u, client.cc:24)",
+                static_cast<unsigned long long>(n), omr_sentinel(block, lanes));
+  L->n = n;
+  L->block = block;
+  L->lanes = lanes;
+  L->parts = parts;
+  L->nb = n / block;
+  L->rows = L->nb / lanes;
+  L->rows_per_part = static_cast<uint32_t>(L->rows / parts);
+  L->vec = block / 256;
+  return 0;
+}
+
+hipStream_t S(omr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+unsigned grid_for(uint64_t work_items_per_wave_units) {
+  uint64_t g = (work_items_per_wave_units + kWavesPerWG - 1) / kWavesPerWG;
+  if (g > kMaxGrid) g = kMaxGrid;
+  if (g == 0) g = 1;
+  return static_cast<unsigned>(g);
+}
+
+int launch_next(const Layout& L, const uint64_t* masks, uint32_t count, uint32_t* next, hipStream_t st) {
+  NextArgs na;
+  na.masks = masks;
+  na.next = next;
+  na.rows = L.rows;
+  na.nb = L.nb;
+  na.rows_per_part = L.rows_per_part;
+  na.segs_per_part = (L.rows_per_part + 63) / 64;
+  na.lanes = L.lanes;
+  na.block = L.block;
+  na.sentinel = omr_sentinel(L.block, L.lanes);
+  dim3 grid(L.parts * na.segs_per_part, count);
+  k_next<<<grid, kWGThreads, 0, st>>>(na);
+  return launch_status("k_next");
+}
+
+#ifndef OMR_SCAN_NT
+#define OMR_SCAN_NT 1
+#endif
+constexpr bool kNT = OMR_SCAN_NT != 0;
+
+int launch_scan(const Layout& L, const ScanArgs& a, hipStream_t st) {
+  const unsigned g = grid_for(L.rows);
+  if (a.m == 1) {
+    switch (L.vec) {
+      case 1: k_scan1<1, kNT><<<g, kWGThreads, 0, st>>>(a); break;
+      case 2: k_scan1<2, kNT><<<g, kWGThreads, 0, st>>>(a); break;
+      default: k_scan1<4, kNT><<<g, kWGThreads, 0, st>>>(a); break;
+    }
+    return launch_status("k_scan1");
+  }
+  switch (L.vec) {
+    case 1: k_scanm<1, kNT><<<g, kWGThreads, 0, st>>>(a); break;
+    case 2: k_scanm<2, kNT><<<g, kWGThreads, 0, st>>>(a); break;
+    default: k_scanm<4, kNT><<<g, kWGThreads, 0, st>>>(a); break;
+  }
+  return launch_status("k_scanm");
+}
+
+}  // namespace
+
+// ================================================================ C ABI
+
+extern "C" {
+
+int omr_abi_version(void) { return OMR_ABI_VERSION; }
+
+const char* omr_last_error(void) { return g_err; }
+
+uint32_t omr_num_lanes(uint32_t block_size) {
+  if (block_size == 0 || (OMR_NUM_SLOTS * OMR_MESSAGE_SIZE) % block_size != 0) return 0;
+  return OMR_NUM_SLOTS * OMR_MESSAGE_SIZE / block_size;
+}
+
+uint32_t omr_sentinel(uint32_t block_size, uint32_t num_lanes) {
+  if (block_size == 0 || num_lanes == 0) return 0;
+  // (UINT32_MAX/BLOCK_SIZE/NUM_BLOCKS-1)*NUM_BLOCKS*BLOCK_SIZE, uint32 arithmetic (client.cc:24)
+  return (UINT32_MAX / block_size / num_lanes - 1u) * num_lanes * block_size;
+}
+
+int omr_layout_check(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts) {
+  Layout L;
+  return make_layout(n, block_size, num_lanes, num_parts, &L);
+}
+
+int omr_gen_bitmap(uint32_t worker_id, double density_ratio, uint64_t num_blocks, int32_t* bitmap,
+                   uint64_t* nonzero_count) {
+  if (bitmap == nullptr && num_blocks != 0) return fail("bitmap is NULL");
+  // glibc srandom_r/random_r TYPE_3 (x**31 + x**3 + 1): r[0] = seed, r[i] = 16807*r[i-1] mod (2^31-1)
+  // for i < 31 (Schrage's method, as glibc), r[i] = r[i-31] for 31 <= i < 34, then r[i] = r[i-31] + r[i-3]
+  // (mod 2^32); the k-th rand() is r[k+344] >> 1.
+  uint32_t seed = worker_id + 1u;  // srand(res.myId+1), client.cc:396
+  if (seed == 0) seed = 1;
+  uint32_t r[34];
+  r[0] = seed;
+  for (int i = 1; i < 31; ++i) {
+    const int32_t prev = static_cast<int32_t>(r[i - 1]);
+    const int32_t hi = prev / 127773, lo = prev % 127773;
+    int32_t word = 16807 * lo - 2836 * hi;
+    if (word < 0) word += 2147483647;
+    r[i] = static_cast<uint32_t>(word);
+  }
+  for (int i = 31; i < 34; ++i) r[i] = r[i - 31];
+  // ring of the last 34 values; index k holds r[k mod 34]
+  uint64_t idx = 34;
+  auto step = [&]() -> uint32_t {
+    const uint32_t v = r[(idx - 31) % 34] + r[(idx - 3) % 34];
+    r[idx % 34] = v;
+    ++idx;
+    return v;
+  };
+  for (int i = 34; i < 344; ++i) step();
+  uint64_t count = 0;
+  for (uint64_t i = 0; i < num_blocks; ++i) {
+    const int rv = static_cast<int>(step() >> 1);
+    const double rnum = rv % 100 / static_cast<double>(101);  // client.cc:407
+    const bool on = rnum < density_ratio;                      // client.cc:408 (myId != -1 always)
+    bitmap[i] = on ? 1 : 0;
+    count += on;
+  }
+  if (nonzero_count != nullptr) *nonzero_count = count;
+  return 0;
+}
+
+int omr_fill_blocks_f32(const int32_t* bitmap, uint64_t num_blocks, uint32_t block_size, int mode,
+                        uint32_t seed, float* buf, omr_stream_t stream) {
+  if (block_size == 0 || block_size % 4 != 0) return fail("block_size %u must be a multiple of 4", block_size);
+  if (mode != 0 && mode != 1) return fail("fill mode %d unknown", mode);
+  if (num_blocks == 0) return 0;
+  if (bitmap == nullptr || buf == nullptr) return fail("fill: NULL pointer");
+  const uint64_t n4 = num_blocks * block_size / 4;
+  uint64_t g = (n4 + kWGThreads - 1) / kWGThreads;
+  if (g > 8192) g = 8192;
+  k_fill<<<static_cast<unsigned>(g), kWGThreads, 0, S(stream)>>>(bitmap, n4, block_size / 4, mode, seed, buf);
+  return launch_status("k_fill");
+}
+
+int omr_scan_sum_f32(const float* const* bufs, uint32_t m, uint64_t n, uint32_t block_size,
+                     uint32_t num_lanes, uint32_t num_parts, int32_t* flags, uint64_t* row_masks,
+                     uint32_t* next_offsets, float* out, omr_stream_t stream) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  if (m == 0 || m > OMR_MAX_WORKERS) return fail("m=%u out of range (1..%d)", m, OMR_MAX_WORKERS);
+  if (bufs == nullptr) return fail("bufs is NULL");
+  if (row_masks == nullptr) return fail("row_masks is NULL");
+  ScanArgs a;
+  memset(&a, 0, sizeof(a));
+  for (uint32_t w = 0; w < m; ++w) {
+    if (bufs[w] == nullptr) return fail("bufs[%u] is NULL", w);
+    if (reinterpret_cast<uintptr_t>(bufs[w]) % 16 != 0) return fail("bufs[%u] not 16-byte aligned", w);
+    a.x.p[w] = bufs[w];
+  }
+  if (out != nullptr && reinterpret_cast<uintptr_t>(out) % 16 != 0) return fail("out not 16-byte aligned");
+  a.m = m;
+  a.lanes = L.lanes;
+  a.rows_per_part = L.rows_per_part;
+  a.rows = L.rows;
+  a.nb = L.nb;
+  a.flags = flags;
+  a.masks = row_masks;
+  a.out = out;
+  hipStream_t st = S(stream);
+  if (int rc = launch_scan(L, a, st)) return rc;
+  if (next_offsets != nullptr) {
+    const uint32_t count = (m == 1) ? 1u : m + 1u;
+    if (int rc = launch_next(L, row_masks, count, next_offsets, st)) return rc;
+  }
+  return 0;
+}
+
+int omr_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                 int32_t* flags, uint64_t* row_masks, uint32_t* next_offsets, omr_stream_t stream) {
+  const float* bufs[1] = {buf};
+  return omr_scan_sum_f32(bufs, 1, n, block_size, num_lanes, num_parts, flags, row_masks, next_offsets,
+                          nullptr, stream);
+}
+
+int omr_next_offsets(const uint64_t* row_masks, uint32_t count, uint64_t n, uint32_t block_size,
+                     uint32_t num_lanes, uint32_t num_parts, uint32_t* next_offsets, omr_stream_t stream) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  if (count == 0) return 0;
+  if (row_masks == nullptr || next_offsets == nullptr) return fail("next_offsets: NULL pointer");
+  return launch_next(L, row_masks, count, next_offsets, S(stream));
+}
+
+int omr_block_sum_f32(const float* const* inputs, uint32_t m, const uint32_t* block_list, uint32_t num_list,
+                      uint32_t block_size, float* out, omr_stream_t stream) {
+  if (block_size != 256 && block_size != 512 && block_size != 1024)
+    return fail("block_size %u unsupported (256, 512, 1024)", block_size);
+  if (m == 0 || m > OMR_MAX_WORKERS) return fail("m=%u out of range (1..%d)", m, OMR_MAX_WORKERS);
+  if (num_list == 0) return 0;
+  if (inputs == nullptr || block_list == nullptr || out == nullptr) return fail("block_sum: NULL pointer");
+  WorkerPtrs in;
+  memset(&in, 0, sizeof(in));
+  for (uint32_t w = 0; w < m; ++w) {
+    if (inputs[w] == nullptr) return fail("inputs[%u] is NULL", w);
+    in.p[w] = inputs[w];
+  }
+  const unsigned g = grid_for(num_list);
+  hipStream_t st = S(stream);
+  switch (block_size / 256) {
+    case 1: k_list_sum<1><<<g, kWGThreads, 0, st>>>(in, m, block_list, num_list, out); break;
+    case 2: k_list_sum<2><<<g, kWGThreads, 0, st>>>(in, m, block_list, num_list, out); break;
+    default: k_list_sum<4><<<g, kWGThreads, 0, st>>>(in, m, block_list, num_list, out); break;
+  }
+  return launch_status("k_list_sum");
+}
+
+size_t omr_compact_workspace_bytes(uint64_t rows) {
+  return static_cast<size_t>((rows + kCompactRows - 1) / kCompactRows + 1) * sizeof(uint32_t);
+}
+
+int omr_compact(const uint64_t* row_masks, uint64_t row_begin, uint64_t row_end, uint32_t num_lanes,
+                uint32_t* block_list, uint32_t* count, void* workspace, size_t workspace_bytes,
+                omr_stream_t stream) {
+  if (row_end < row_begin) return fail("compact: row_end < row_begin");
+  if (num_lanes == 0 || num_lanes > 64) return fail("num_lanes %u out of range", num_lanes);
+  if (count == nullptr) return fail("compact: count is NULL");
+  hipStream_t st = S(stream);
+  const uint64_t rows = row_end - row_begin;
+  if (rows == 0) {
+    const hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) {
+      snprintf(g_err, sizeof(g_err), "compact memset: %s", hipGetErrorString(e));
+      return static_cast<int>(e);
+    }
+    return 0;
+  }
+  if (row_masks == nullptr || block_list == nullptr || workspace == nullptr)
+    return fail("compact: NULL pointer");
+  if (workspace_bytes < omr_compact_workspace_bytes(rows)) return fail("compact: workspace too small");
+  const uint64_t chunks = (rows + kCompactRows - 1) / kCompactRows;
+  if (chunks > 0x7fffffffull) return fail("compact: too many rows");
+  uint32_t* chunk_sum = static_cast<uint32_t*>(workspace);
+  k_compact_count<<<static_cast<unsigned>(chunks), kWGThreads, 0, st>>>(row_masks, row_begin, row_end,
+                                                                        chunk_sum);
+  if (int rc = launch_status("k_compact_count")) return rc;
+  k_compact_write<<<static_cast<unsigned>(chunks), kWGThreads, 0, st>>>(row_masks, row_begin, row_end,
+                                                                        num_lanes, chunk_sum, block_list,
+                                                                        count);
+  return launch_status("k_compact_write");
+}
+
+int omr_gather_blocks_f32(const float* src, const uint32_t* block_list, uint32_t num_list,
+                          uint32_t block_size, float* packed, omr_stream_t stream) {
+  if (block_size != 256 && block_size != 512 && block_size != 1024)
+    return fail("block_size %u unsupported (256, 512, 1024)", block_size);
+  if (num_list == 0) return 0;
+  if (src == nullptr || block_list == nullptr || packed == nullptr) return fail("gather: NULL pointer");
+  const unsigned g = grid_for(num_list);
+  hipStream_t st = S(stream);
+  switch (block_size / 256) {
+    case 1: k_gather<1><<<g, kWGThreads, 0, st>>>(src, block_list, num_list, packed); break;
+    case 2: k_gather<2><<<g, kWGThreads, 0, st>>>(src, block_list, num_list, packed); break;
+    default: k_gather<4><<<g, kWGThreads, 0, st>>>(src, block_list, num_list, packed); break;
+  }
+  return launch_status("k_gather");
+}
+
+int omr_scatter_blocks_f32(const float* packed, const uint32_t* block_list, uint32_t num_list,
+                           uint32_t block_size, float* dst, omr_stream_t stream) {
+  if (block_size != 256 && block_size != 512 && block_size != 1024)
+    return fail("block_size %u unsupported (256, 512, 1024)", block_size);
+  if (num_list == 0) return 0;
+  if (packed == nullptr || block_list == nullptr || dst == nullptr) return fail("scatter: NULL pointer");
+  const unsigned g = grid_for(num_list);
+  hipStream_t st = S(stream);
+  switch (block_size / 256) {
+    case 1: k_scatter<1><<<g, kWGThreads, 0, st>>>(packed, block_list, num_list, dst); break;
+    case 2: k_scatter<2><<<g, kWGThreads, 0, st>>>(packed, block_list, num_list, dst); break;
+    default: k_scatter<4><<<g, kWGThreads, 0, st>>>(packed, block_list, num_list, dst); break;
+  }
+  return launch_status("k_scatter");
+}
+
+}  // extern "C"

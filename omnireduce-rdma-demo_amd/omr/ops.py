@@ -1,0 +1,215 @@
+"""Device-tensor front end of the C ABI (include/omr.h).
+
+Every function here is a thin call through libomr.so on torch-allocated HBM buffers and the current HIP
+stream; torch provides memory and streams only.  Names follow the reference: the worker scan
+(client.cc:19-31), the aggregator sum (server.cc:83-99), the generator (client.cc:396-421).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .layout import Layout
+
+
+def _stream(stream: Optional[torch.cuda.Stream] = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("expected a device (HIP) tensor")
+    if not t.is_contiguous():
+        raise ValueError("expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def _ptr_array(ts: Sequence[torch.Tensor]):
+    arr = (ctypes.c_void_p * len(ts))()
+    for i, t in enumerate(ts):
+        arr[i] = _ptr(t)
+    return arr
+
+
+def _check_f32(t: torch.Tensor, n: int, name: str) -> None:
+    if t.dtype != torch.float32 or t.numel() != n:
+        raise ValueError(f"{name}: expected float32[{n}], got {t.dtype}[{t.numel()}]")
+
+
+# ------------------------------------------------------------------ generator (client.cc:396-421)
+
+def gen_bitmap(worker_id: int, density_ratio: float, num_blocks: int) -> np.ndarray:
+    """The reference bitmap of worker `worker_id` (srand(myId+1); rand()%100/(double)101 < r)."""
+    lib = _lib.load()
+    bm = np.empty(num_blocks, dtype=np.int32)
+    cnt = ctypes.c_uint64(0)
+    _lib.check(lib.omr_gen_bitmap(worker_id, float(density_ratio), num_blocks,
+                                  bm.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cnt)), "omr_gen_bitmap")
+    return bm
+
+
+def fill_blocks(bitmap: torch.Tensor, layout: Layout, mode: int = 0, seed: int = 0,
+                out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """Device fill from a device int32 bitmap: mode 0 = 0.01f (client.cc:415-419), 1 = hashed [-1,1)."""
+    if bitmap.dtype != torch.int32 or bitmap.numel() != layout.nb:
+        raise ValueError("bitmap must be int32[nb]")
+    if out is None:
+        out = torch.empty(layout.n, dtype=torch.float32, device=bitmap.device)
+    _check_f32(out, layout.n, "out")
+    _lib.check(_lib.load().omr_fill_blocks_f32(_ptr(bitmap), layout.nb, layout.block_size, mode, seed,
+                                               _ptr(out), _stream(stream)), "omr_fill_blocks_f32")
+    return out
+
+
+def make_worker_buffer(worker_id: int, density_ratio: float, layout: Layout, device="cuda", mode: int = 0,
+                       seed: Optional[int] = None) -> torch.Tensor:
+    bm = torch.from_numpy(gen_bitmap(worker_id, density_ratio, layout.nb)).to(device)
+    return fill_blocks(bm, layout, mode=mode, seed=worker_id + 1 if seed is None else seed)
+
+
+# ------------------------------------------------------------------ scan + sum
+
+@dataclass
+class ScanResult:
+    flags: Optional[torch.Tensor]  # int32 [m][nb]
+    masks: torch.Tensor  # uint64-as-int64 [m(+1)][rows]
+    next_offsets: Optional[torch.Tensor]  # uint32-as-int32 [m(+1)][nb]
+    out: Optional[torch.Tensor]
+
+
+class ScanSumPlan:
+    """Preallocated outputs for repeated fused scan+sum launches (no allocation per call, capturable).
+
+    flags        int32  [m, nb]             per-worker block flags (the reference's int *bitmap)
+    masks        int64  [m(+1), rows]       per-worker row masks (+ the union row at index m when m > 1)
+    next_offsets int32  [m(+1), nb]         per-worker next-offset chains (+ the aggregator chain), uint32 bits
+    """
+
+    def __init__(self, layout: Layout, m: int = 1, with_flags: bool = True, with_next: bool = True,
+                 device="cuda"):
+        if not 1 <= m <= _lib.OMR_MAX_WORKERS:
+            raise ValueError(f"m={m} out of range")
+        _lib.check(_lib.load().omr_layout_check(layout.n, layout.block_size, layout.num_lanes,
+                                                layout.num_threads), "omr_layout_check")
+        self.layout, self.m = layout, m
+        arrays = m if m == 1 else m + 1
+        self.flags = torch.empty((m, layout.nb), dtype=torch.int32, device=device) if with_flags else None
+        self.masks = torch.empty((arrays, layout.rows), dtype=torch.int64, device=device)
+        self.next_offsets = (torch.empty((arrays, layout.nb), dtype=torch.int32, device=device)
+                             if with_next else None)
+
+    def run(self, bufs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None, stream=None,
+            with_next: bool = True) -> ScanResult:
+        """Fused scan (+ sum into `out`) and, unless with_next=False, the next-offset chains."""
+        L = self.layout
+        if len(bufs) != self.m:
+            raise ValueError(f"expected {self.m} worker buffers, got {len(bufs)}")
+        for i, b in enumerate(bufs):
+            _check_f32(b, L.n, f"bufs[{i}]")
+        if out is not None:
+            _check_f32(out, L.n, "out")
+        arr = _ptr_array(bufs)
+        nxt = self.next_offsets if with_next else None
+        _lib.check(_lib.load().omr_scan_sum_f32(arr, self.m, L.n, L.block_size, L.num_lanes, L.num_threads,
+                                                _ptr(self.flags), _ptr(self.masks), _ptr(nxt),
+                                                _ptr(out), _stream(stream)), "omr_scan_sum_f32")
+        return ScanResult(self.flags, self.masks, self.next_offsets, out)
+
+    def resolve_next(self, stream=None) -> torch.Tensor:
+        """Next-offset chains from the masks of the last run (the second kernel of run())."""
+        L = self.layout
+        if self.next_offsets is None:
+            raise ValueError("plan built with with_next=False")
+        _lib.check(_lib.load().omr_next_offsets(_ptr(self.masks), self.masks.shape[0], L.n, L.block_size,
+                                                L.num_lanes, L.num_threads, _ptr(self.next_offsets),
+                                                _stream(stream)), "omr_next_offsets")
+        return self.next_offsets
+
+
+def scan(buf: torch.Tensor, layout: Layout, stream=None) -> ScanResult:
+    """Worker-side scan (client.cc:19-31): flags, row masks and next offsets of one gradient buffer."""
+    return ScanSumPlan(layout, 1, device=buf.device).run([buf], None, stream)
+
+
+def scan_sum(bufs: Sequence[torch.Tensor], layout: Layout, out: Optional[torch.Tensor] = None,
+             stream=None) -> ScanResult:
+    """m worker scans + aggregator sum (server.cc:83-99) in one HBM pass."""
+    if out is None:
+        out = torch.zeros(layout.n, dtype=torch.float32, device=bufs[0].device)
+    return ScanSumPlan(layout, len(bufs), device=bufs[0].device).run(bufs, out, stream)
+
+
+def next_offsets(masks: torch.Tensor, layout: Layout, stream=None) -> torch.Tensor:
+    """Next-offset chains from row masks [count, rows] (client.cc:19-31; server.cc:86-96 on a union)."""
+    if masks.dim() == 1:
+        masks = masks.view(1, -1)
+    if masks.dtype != torch.int64 or masks.shape[1] != layout.rows:
+        raise ValueError("masks must be int64[count, rows]")
+    count = masks.shape[0]
+    nxt = torch.empty((count, layout.nb), dtype=torch.int32, device=masks.device)
+    _lib.check(_lib.load().omr_next_offsets(_ptr(masks.contiguous()), count, layout.n, layout.block_size,
+                                            layout.num_lanes, layout.num_threads, _ptr(nxt), _stream(stream)),
+               "omr_next_offsets")
+    return nxt
+
+
+# ------------------------------------------------------------------ compaction and block movement
+
+class CompactPlan:
+    def __init__(self, rows: int, num_lanes: int, device="cuda"):
+        self.rows, self.num_lanes = rows, num_lanes
+        ws = _lib.load().omr_compact_workspace_bytes(rows)
+        self.workspace = torch.empty(ws, dtype=torch.uint8, device=device)
+        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+        self.block_list = torch.empty(rows * num_lanes, dtype=torch.int32, device=device)
+
+    def run(self, masks: torch.Tensor, row_begin: int = 0, row_end: Optional[int] = None, stream=None):
+        row_end = self.rows if row_end is None else row_end
+        _lib.check(_lib.load().omr_compact(_ptr(masks), row_begin, row_end, self.num_lanes,
+                                           _ptr(self.block_list), _ptr(self.count), _ptr(self.workspace),
+                                           self.workspace.numel(), _stream(stream)), "omr_compact")
+        return self.block_list, self.count
+
+
+def compact(masks: torch.Tensor, layout: Layout, row_begin: int = 0, row_end: Optional[int] = None,
+            stream=None) -> torch.Tensor:
+    """Global indices of the non-zero blocks of rows [row_begin, row_end), increasing (synchronises)."""
+    plan = CompactPlan(layout.rows, layout.num_lanes, device=masks.device)
+    lst, cnt = plan.run(masks.contiguous(), row_begin, row_end, stream)
+    return lst[: int(cnt.item())].clone()
+
+
+def gather_blocks(src: torch.Tensor, block_list: torch.Tensor, num: int, block_size: int,
+                  packed: torch.Tensor, stream=None) -> torch.Tensor:
+    """Pack listed blocks contiguously (worker gather, common.cc:405-407)."""
+    if num:
+        _lib.check(_lib.load().omr_gather_blocks_f32(_ptr(src), _ptr(block_list), num, block_size,
+                                                     _ptr(packed), _stream(stream)), "omr_gather_blocks_f32")
+    return packed
+
+
+def scatter_blocks(packed: torch.Tensor, block_list: torch.Tensor, num: int, block_size: int,
+                   dst: torch.Tensor, stream=None) -> torch.Tensor:
+    """Write packed blocks back in place (worker result copy, client.cc:89)."""
+    if num:
+        _lib.check(_lib.load().omr_scatter_blocks_f32(_ptr(packed), _ptr(block_list), num, block_size,
+                                                      _ptr(dst), _stream(stream)), "omr_scatter_blocks_f32")
+    return dst
+
+
+def block_sum(inputs: Sequence[torch.Tensor], block_list: torch.Tensor, num: int, block_size: int,
+              out: torch.Tensor, stream=None) -> torch.Tensor:
+    """out[b] = ((0 + in_0[b]) + in_1[b]) + ... for listed blocks b (server.cc:97-98, rank order)."""
+    if num:
+        arr = _ptr_array(inputs)
+        _lib.check(_lib.load().omr_block_sum_f32(arr, len(inputs), _ptr(block_list), num, block_size,
+                                                 _ptr(out), _stream(stream)), "omr_block_sum_f32")
+    return out

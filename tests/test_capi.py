@@ -1,0 +1,90 @@
+"""C-ABI tests that need no GPU: the library loads, exports every symbol include/omr.h declares, and its
+host-only logic (layout validation, sentinel, the reference generator restatement) is right."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+from omr import _lib, Layout
+from omr import ops
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "omr.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(omr_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == sorted(_lib.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.omr_abi_version() == 1
+
+
+@pytest.mark.parametrize("B,NB", [(256, 64), (512, 32), (1024, 16)])
+def test_num_lanes_and_sentinel(B, NB):
+    lib = _lib.load()
+    assert lib.omr_num_lanes(B) == NB  # common.h:36-37
+    assert lib.omr_sentinel(B, NB) == 4294934528 == Layout(n=8 * NB * B, block_size=B).sentinel
+
+
+def test_layout_check_rejects_bad_layouts():
+    lib = _lib.load()
+    assert lib.omr_layout_check(1 << 20, 256, 64, 8) == 0
+    assert lib.omr_layout_check(64 << 20, 256, 64, 8) == 0
+    assert lib.omr_layout_check(256 << 20, 1024, 16, 8) == 0
+    assert lib.omr_layout_check(1 << 30, 256, 64, 8) == 0  # config 5: 4 GiB per rank
+    assert lib.omr_layout_check(1 << 20, 128, 128, 8) == _lib.OMR_EINVAL  # NB > 64 unsupported
+    assert b"block_size" in lib.omr_last_error()
+    assert lib.omr_layout_check((1 << 20) + 256, 256, 64, 8) == _lib.OMR_EINVAL  # ragged partition
+    assert lib.omr_layout_check(0, 256, 64, 8) == _lib.OMR_EINVAL
+    assert lib.omr_layout_check(1 << 32, 256, 64, 8) == _lib.OMR_EINVAL  # past the uint32 sentinel
+
+
+def test_entry_points_validate_before_launching():
+    """Argument errors return OMR_EINVAL without touching the device (safe on a GPU-less host)."""
+    lib = _lib.load()
+    assert lib.omr_scan_f32(None, 1 << 20, 300, 64, 8, None, None, None, None) == _lib.OMR_EINVAL
+    assert lib.omr_scan_sum_f32(None, 0, 1 << 20, 256, 64, 8, None, None, None, None, None) == _lib.OMR_EINVAL
+    assert lib.omr_block_sum_f32(None, 1, None, 4, 100, None, None) == _lib.OMR_EINVAL
+    assert lib.omr_block_sum_f32(None, 1, None, 0, 256, None, None) == 0  # empty list is a no-op
+    assert lib.omr_compact(None, 5, 3, 64, None, None, None, 0, None) == _lib.OMR_EINVAL
+    assert lib.omr_fill_blocks_f32(None, 4, 256, 7, 0, None, None) == _lib.OMR_EINVAL
+
+
+@pytest.mark.parametrize("wid", [0, 1, 2, 7])
+@pytest.mark.parametrize("r", [0.095, 0.0099, 0.49, 1.0, 0.3])
+def test_product_generator_equals_glibc(wid, r):
+    """omr_gen_bitmap restates glibc rand(); the oracle calls glibc srand/rand as client.cc:396-414 does."""
+    nb = 20000
+    assert (ops.gen_bitmap(wid, r, nb) == oracle.gen_bitmap(wid, r, nb)).all()
+
+
+def test_product_generator_count():
+    lib = _lib.load()
+    bm = np.empty(4096, dtype=np.int32)
+    cnt = ctypes.c_uint64()
+    assert lib.omr_gen_bitmap(0, 0.095, 4096, bm.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cnt)) == 0
+    assert cnt.value == int(bm.sum())
+
+
+def test_layout_class():
+    L = Layout.from_bytes(256 << 20, 256)
+    assert (L.n, L.num_lanes, L.nb, L.rows, L.rows_per_part) == (64 << 20, 64, 262144, 4096, 512)
+    L3 = Layout.from_bytes(1 << 30, 1024)
+    assert (L3.num_lanes, L3.rows_per_part, L3.blocks_per_message) == (16, 2048, 1)
+    assert L.lane_of(L.head_offset(3, 17)) == 17 and L.partition_of(L.head_offset(3, 17)) == 3
+    assert L.global_slot(2, 5) == 37
+    with pytest.raises(ValueError):
+        Layout(n=(1 << 20) + 256)
