@@ -75,6 +75,11 @@ def algorithmic_scan_bytes(L: Layout, bitmaps, m: int) -> int:
     return m * L.nbytes + written * B * 4 + m * nb * 4 + masks
 
 
+def scan_only_bytes(L: Layout) -> int:
+    """Worker scan without the fused sum (N>1): read S, write int32 flags and row masks."""
+    return L.nbytes + L.nb * 4 + L.rows * 8
+
+
 def step_algorithmic_bytes(L: Layout, bitmaps, m: int) -> int:
     """m*S + d_union*S + m*nb*8 (flag + next per block per worker)."""
     nb = L.nb
@@ -156,11 +161,12 @@ def main():
     if ws > 1:
         from omr import dist
         engine = dist.SparseAllreduce(L, device=dev)
-        state = [engine.prepare(xs[0]) for xs, _ in sets]
+        for xs, out in sets:  # out-of-place result buffers keep every step's input pristine
+            out.copy_(xs[0])
 
-        def step(i):
-            k = i % len(sets)
-            return engine.run(sets[k][0][0], state[k], ev=None)
+        def step(i, ev=None):
+            xs, out = sets[i % len(sets)]
+            engine.run(xs[0], out=out, ev=ev)
     else:
         plan = ops.ScanSumPlan(L, m, device=dev)
 
@@ -181,13 +187,10 @@ def main():
     torch.cuda.synchronize()
 
     kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)] if ws == 1 else None
+           for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if ws == 1:
-            step(args.warmup + i, kev[i])
-        else:
-            step(args.warmup + i)
+        step(args.warmup + i, kev[i])
     torch.cuda.synchronize()
     if ws > 1:
         torch.distributed.barrier()
@@ -200,18 +203,20 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     roofline = None
-    if ws == 1:
+    if True:
         kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
-        kbytes = algorithmic_scan_bytes(L, bitmaps, m)
+        kbytes = algorithmic_scan_bytes(L, bitmaps, m) if ws == 1 else scan_only_bytes(L)
         achieved = kbytes / (kms * 1e-3) / 1e9
         traffic = read_pmc(args.pmc, workload)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "kernel": "k_scan1" if m == 1 else "k_scanm", "kernel_ms": round(kms, 5),
+                    "kernel": ("k_scan1" if m == 1 else "k_scanm") + ("" if ws == 1 else " (worker scan, no out)"),
+                    "kernel_ms": round(kms, 5),
                     "algorithmic_bytes_per_launch": kbytes}
-        sbytes = step_algorithmic_bytes(L, bitmaps, m)
-        roofline["step_algorithmic_bytes"] = sbytes
-        roofline["step_frac"] = round(sbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        if ws == 1:
+            sbytes = step_algorithmic_bytes(L, bitmaps, m)
+            roofline["step_algorithmic_bytes"] = sbytes
+            roofline["step_frac"] = round(sbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
 
     if rank != 0:
         if ws > 1:

@@ -145,6 +145,28 @@ int omr_gather_blocks_f32(const float* src, const uint32_t* block_list, uint32_t
 int omr_scatter_blocks_f32(const float* packed, const uint32_t* block_list, uint32_t num_list,
                            uint32_t block_size, float* dst, omr_stream_t stream);
 
+/* ---------------------------------------------------------------- multi-GPU sparse exchange helpers */
+
+/* out[r] = OR of `count` mask arrays (stride `rows`) — the union the aggregator's min_next chain runs over
+ * (server.cc:86-96); with heads != 0 every lane-head row (r % rows_per_part == 0) is forced to all lanes,
+ * giving the set of blocks the aggregator returns (lane heads are always sent: client.cc:201-205). */
+int omr_mask_union(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
+                   uint32_t num_lanes, int heads, uint64_t* out, omr_stream_t stream);
+
+/* Exclusive prefix of per-row popcounts: prefix[a*(rows+1) + r] = set bits of array a in rows [0, r). */
+size_t omr_prefix_workspace_bytes(uint64_t rows, uint32_t count);
+int omr_row_prefix(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t* prefix, void* workspace,
+                   size_t workspace_bytes, omr_stream_t stream);
+
+/* Aggregator shard sum over packed worker streams (server.cc:83-99 with the RDMA hop replaced by RCCL):
+ * worker w's stream holds its non-zero blocks of rows [row_begin, ...) in increasing order, starting at block
+ * recv_offsets[w] (device uint64[count]) of `recv`.  For the k-th listed global block b:
+ * out[k*B + j] = ((0.0f + x_w0[b][j]) + x_w1[b][j]) + ... over the workers whose mask has b, in rank order. */
+int omr_sparse_block_sum_f32(const float* recv, const uint64_t* recv_offsets, const uint64_t* row_masks,
+                             uint32_t count, uint64_t rows, const uint32_t* prefix, uint64_t row_begin,
+                             uint32_t num_lanes, const uint32_t* block_list, uint32_t num_list,
+                             uint32_t block_size, float* out, omr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -96,49 +96,68 @@ struct ScanArgs {
 
 // ---------------------------------------------------------------- k_scan1: one worker, fused scan + sum
 //
-// Wave w handles rows w, w + nwaves, ...  A row is `lanes` blocks of VEC*256 floats; it is swept in
-// sub-batches of SUB blocks = 16 dwordx4 loads (16 KiB) per wave, all issued before the first use.
-// Per block: ballot(any element non-zero) -> flag bit; if the block is non-zero (or the row is a lane-head
-// row, always sent by the reference: client.cc:201-205) the aggregated block 0.0f + x (server.cc:148-150
-// zero, :97-98 add) is stored straight from registers.
+// Work unit = a chunk of CH consecutive blocks of one row (CH = 16 blocks = 16 KiB at B=256; 8 blocks at
+// B=512/1024), swept grid-stride by 8-wave workgroups so that the waves in flight at any moment cover one
+// contiguous stretch of HBM.  A wave issues all CH*VEC 16-byte-per-lane loads of its chunk (non-temporal:
+// the gradient is read once) before the first use.  Per block: ballot(any element non-zero) -> flag bit; if
+// the block is non-zero (or sits in a lane-head row, which the reference always sends: client.cc:201-205)
+// the aggregated block 0.0f + x (server.cc:148-150 zero, :97-98 add) is stored straight from registers.
+// The chunk's CH flag bits are one byte-aligned piece of the row's uint64 mask, stored directly.
+constexpr int kScanWaves = 8;  // 512-thread workgroups (tools/tune_scan.py: fastest of 4/8/16 on MI355X)
+
+template <int VEC>
+constexpr int scan_chunk_blocks() {
+  return (16 / VEC) > 8 ? (16 / VEC) : 8;
+}
+
 template <int VEC, bool NT>
-__global__ __launch_bounds__(kWGThreads) void k_scan1(ScanArgs a) {
+__global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
   constexpr int B4 = 64 * VEC;  // v4fs per block
-  constexpr int SUB = pow2floor(16 / VEC);
+  constexpr int CH = scan_chunk_blocks<VEC>();
   const int lane = threadIdx.x & 63;
   const v4f* __restrict__ x = reinterpret_cast<const v4f*>(a.x.p[0]);
   v4f* __restrict__ out = reinterpret_cast<v4f*>(a.out);
-  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
-  for (uint64_t row = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + (threadIdx.x >> 6); row < a.rows;
-       row += nwaves) {
+  uint8_t* __restrict__ mask_bytes = reinterpret_cast<uint8_t*>(a.masks);
+  const uint32_t cpr = a.lanes / CH;  // chunks per row
+  const uint64_t chunks = a.rows * cpr;
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kScanWaves;
+  for (uint64_t c = static_cast<uint64_t>(blockIdx.x) * kScanWaves + (threadIdx.x >> 6); c < chunks;
+       c += nwaves) {
+    const uint64_t row = c / cpr;
+    const uint32_t l0 = static_cast<uint32_t>(c - row * cpr) * CH;
     const bool head = (row % a.rows_per_part) == 0;
-    const uint64_t rowbase = row * a.lanes * B4;
-    uint64_t wm = 0;
-    for (uint32_t l0 = 0; l0 < a.lanes; l0 += SUB) {
-      v4f v[SUB][VEC];
-      const v4f* src = x + rowbase + static_cast<uint64_t>(l0) * B4 + lane;
+    const uint64_t base = c * CH * B4;  // chunks tile each row, so chunk c starts at c*CH blocks
+    v4f v[CH][VEC];
 #pragma unroll
-      for (int s = 0; s < SUB; ++s)
+    for (int s = 0; s < CH; ++s)
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) v[s][q] = ld4<NT>(src + s * B4 + q * 64);
+      for (int q = 0; q < VEC; ++q) v[s][q] = ld4<NT>(x + base + s * B4 + q * 64 + lane);
+    uint32_t bits = 0;
 #pragma unroll
-      for (int s = 0; s < SUB; ++s) {
-        uint32_t o = 0;
+    for (int s = 0; s < CH; ++s) {
+      uint32_t o = 0;
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
-        const bool nz = wave_ballot(o != 0) != 0;
-        wm |= static_cast<uint64_t>(nz) << (l0 + s);
-        if (out != nullptr && (nz || head)) {
-          v4f* dst = out + rowbase + static_cast<uint64_t>(l0 + s) * B4 + lane;
-          const v4f z = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
+      const bool nz = wave_ballot(o != 0) != 0;
+      bits |= static_cast<uint32_t>(nz) << s;
+      if (out != nullptr && (nz || head)) {
+        const v4f z = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int q = 0; q < VEC; ++q) dst[q * 64] = add4(z, v[s][q]);
-        }
+        for (int q = 0; q < VEC; ++q) out[base + s * B4 + q * 64 + lane] = add4(z, v[s][q]);
       }
     }
-    if (lane == 0) a.masks[row] = wm;
-    if (a.flags != nullptr && lane < static_cast<int>(a.lanes))
-      a.flags[row * a.lanes + lane] = static_cast<int32_t>((wm >> lane) & 1u);
+    if (lane == 0) {
+      uint8_t* mp = mask_bytes + row * 8 + l0 / 8;
+      if constexpr (CH == 16) {
+        *reinterpret_cast<uint16_t*>(mp) = static_cast<uint16_t>(bits);
+      } else {
+        *mp = static_cast<uint8_t>(bits);
+      }
+    } else if (l0 + CH == a.lanes && lane < 8 && static_cast<uint32_t>(lane) >= a.lanes / 8) {
+      mask_bytes[row * 8 + lane] = 0;  // bits of lanes >= NB (rows narrower than 64 lanes)
+    }
+    if (a.flags != nullptr && lane < CH)
+      a.flags[row * a.lanes + l0 + lane] = static_cast<int32_t>((bits >> lane) & 1u);
   }
 }
 
@@ -221,9 +240,11 @@ __global__ __launch_bounds__(kWGThreads) void k_scanm(ScanArgs a) {
 //
 // next[b] for block b = (row r, lane l) = offset of the first row r' > r of the same partition whose
 // mask has bit l, else sentinel + l*B (find_next_nonzero_block(b*B + B*NB), client.cc:19-31).
-// Workgroup = one segment of <= 64 rows of one partition and one mask array (blockIdx.y).
-// Wave 0 transposes the segment's row masks into per-lane column masks with `lanes` ballots and finds,
-// per lane, the first set row after the segment by sweeping later rows 256 at a time (4 per lane).
+// Workgroup = one segment of <= 64 rows of one partition and one mask array (blockIdx.y).  A wave holds
+// 64 row masks (lane i = row i) and turns them into 64 column masks (lane l = lane-column l, bit i = row i)
+// with a 6-stage butterfly bit transpose, so "first non-zero row per lane" is one ctz per thread.
+// Wave 0 transposes the segment itself; all four waves then sweep the rows after it, 256 per round, until
+// every lane has found its first non-zero row (or the partition ends).
 struct NextArgs {
   const uint64_t* masks;
   uint32_t* next;
@@ -236,9 +257,35 @@ struct NextArgs {
   uint32_t sentinel;
 };
 
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = __shfl_xor(static_cast<uint32_t>(v), m, 64);
+  const uint32_t hi = __shfl_xor(static_cast<uint32_t>(v >> 32), m, 64);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// 64x64 bit-matrix transpose across a wave: in, lane r holds row r (bit c = element (r, c)); out, lane c
+// holds column c (bit r = element (r, c)).  Stage j swaps bit j of the row index with bit j of the column.
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t a, int lane) {
+  constexpr uint64_t M[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                             0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int j = 32 >> s;
+    const uint64_t m = M[s];
+    const uint64_t x = shfl_xor64(a, j);
+    a = (lane & j) ? ((a & ~m) | ((x & ~m) >> j)) : ((a & m) | ((x & m) << j));
+  }
+  return a;
+}
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
 __global__ __launch_bounds__(kWGThreads) void k_next(NextArgs a) {
   __shared__ uint64_t s_col[64];
-  __shared__ uint32_t s_carry[64];
+  __shared__ uint32_t s_first[kWavesPerWG][64];
+  __shared__ uint32_t s_carry_row[64];
+  __shared__ int s_done;
+  if (threadIdx.x == 0) s_done = 0;
   const uint64_t* masks = a.masks + static_cast<uint64_t>(blockIdx.y) * a.rows;
   uint32_t* next = a.next + static_cast<uint64_t>(blockIdx.y) * a.nb;
   const uint32_t part = blockIdx.x / a.segs_per_part;
@@ -248,58 +295,54 @@ __global__ __launch_bounds__(kWGThreads) void k_next(NextArgs a) {
   const uint64_t row0 = part_row0 + static_cast<uint64_t>(seg) * 64;
   const uint64_t seg_end = (row0 + 64 < part_end) ? row0 + 64 : part_end;
   const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   const uint32_t row_stride = a.lanes * a.block;  // floats per row
 
-  if (threadIdx.x < 64) {
-    const uint64_t r = row0 + lane;
-    const uint64_t rm = (r < seg_end) ? masks[r] : 0;
-    uint64_t mycol = 0;
-    for (uint32_t l = 0; l < a.lanes; ++l) {
-      const uint64_t b = wave_ballot((rm >> l) & 1u);
-      if (lane == static_cast<int>(l)) mycol = b;
-    }
-    uint32_t carry = a.sentinel + static_cast<uint32_t>(lane) * a.block;
-    uint64_t pending = (a.lanes >= 64) ? ~0ull : ((1ull << a.lanes) - 1);
-    for (uint64_t look = seg_end; pending != 0 && look < part_end; look += 256) {
-      uint64_t lm[4];
+  // the segment's own masks and the first look-ahead rows are loaded together (independent round trips)
+  const uint64_t r = row0 + lane;
+  const uint64_t seg_mask = (wave == 0 && r < seg_end) ? masks[r] : 0ull;
+  uint64_t look = seg_end;
+  uint64_t rr = look + static_cast<uint64_t>(wave) * 64 + lane;
+  uint64_t look_mask = (rr < part_end) ? masks[rr] : 0ull;
+  if (wave == 0) {
+    s_col[lane] = wave_transpose64(seg_mask, lane);
+    s_carry_row[lane] = kNone;
+  }
+  while (look < part_end) {
+    const uint64_t col = wave_transpose64(look_mask, lane);
+    s_first[wave][lane] = col ? static_cast<uint32_t>(look + wave * 64 + __builtin_ctzll(col)) : kNone;
+    __syncthreads();
+    if (wave == 0) {
+      uint32_t cr = s_carry_row[lane];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint64_t rr = look + static_cast<uint64_t>(k) * 64 + lane;
-        lm[k] = (rr < part_end) ? masks[rr] : 0;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint64_t p = pending;
-        while (p != 0) {
-          const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(p));
-          p &= p - 1;
-          const uint64_t b = wave_ballot((lm[k] >> l) & 1u);
-          if (b != 0) {
-            const uint64_t hit = look + static_cast<uint64_t>(k) * 64 + __builtin_ctzll(b);
-            if (lane == static_cast<int>(l)) carry = static_cast<uint32_t>(hit) * row_stride + l * a.block;
-            pending &= ~(1ull << l);
-          }
-        }
-      }
+      for (int w = 0; w < kWavesPerWG; ++w)
+        if (cr == kNone) cr = s_first[w][lane];
+      s_carry_row[lane] = cr;
+      const uint64_t open = __ballot(lane < static_cast<int>(a.lanes) && cr == kNone);
+      if (lane == 0) s_done = (open == 0);
     }
-    s_col[lane] = mycol;
-    s_carry[lane] = carry;
+    __syncthreads();
+    if (s_done) break;
+    look += 64 * kWavesPerWG;
+    rr = look + static_cast<uint64_t>(wave) * 64 + lane;
+    look_mask = (rr < part_end) ? masks[rr] : 0ull;
   }
   __syncthreads();
   const uint32_t nrows = static_cast<uint32_t>(seg_end - row0);
-  const uint32_t total = nrows * a.lanes;
+  const uint32_t lshift = static_cast<uint32_t>(__builtin_ctz(a.lanes));  // lanes is a power of two
+  const uint32_t total = nrows << lshift;
   for (uint32_t idx = threadIdx.x; idx < total; idx += kWGThreads) {
-    const uint32_t i = idx / a.lanes;
-    const uint32_t l = idx - i * a.lanes;
+    const uint32_t i = idx >> lshift;
+    const uint32_t l = idx & (a.lanes - 1);
     const uint64_t c = (i >= 63) ? 0 : (s_col[l] >> (i + 1));
     uint32_t v;
     if (c != 0) {
-      const uint64_t hit = row0 + i + 1 + __builtin_ctzll(c);
-      v = static_cast<uint32_t>(hit) * row_stride + l * a.block;
+      v = static_cast<uint32_t>(row0 + i + 1 + __builtin_ctzll(c)) * row_stride + l * a.block;
     } else {
-      v = s_carry[l];
+      const uint32_t cr = s_carry_row[l];
+      v = (cr != kNone) ? cr * row_stride + l * a.block : a.sentinel + l * a.block;
     }
-    next[(row0 + i) * a.lanes + l] = v;
+    next[(row0 << lshift) + idx] = v;
   }
 }
 
@@ -358,6 +401,101 @@ __global__ __launch_bounds__(kWGThreads) void k_compact_write(const uint64_t* ma
     list[pos++] = static_cast<uint32_t>(r * lanes + l);
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kWGThreads - 1) *count = pos;
+}
+
+// ---------------------------------------------------------------- multi-GPU exchange helpers
+//
+// The N-rank sparse all-reduce (omr/dist.py) moves only non-zero blocks between ranks.  Aggregator s owns a
+// contiguous range of rows (the reference shards message slots over aggregators, common.cc:381-383); worker w
+// sends it its non-zero blocks of that range in increasing block order.  These kernels derive every block's
+// position in such a packed stream from the all-gathered row masks, so no index lists cross the link.
+
+// out[r] = OR over `count` mask arrays of row r; lane-head rows (r % rows_per_part == 0) forced to all lanes
+// when heads != 0 (the reference always sends lane heads: client.cc:201-205).
+__global__ __launch_bounds__(kWGThreads) void k_mask_union(const uint64_t* masks, uint32_t count, uint64_t rows,
+                                                           uint32_t rows_per_part, uint64_t lane_bits, int heads,
+                                                           uint64_t* out) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWGThreads;
+  for (uint64_t r = static_cast<uint64_t>(blockIdx.x) * kWGThreads + threadIdx.x; r < rows; r += stride) {
+    uint64_t u = 0;
+    for (uint32_t w = 0; w < count; ++w) u |= masks[static_cast<uint64_t>(w) * rows + r];
+    if (heads && (r % rows_per_part) == 0) u |= lane_bits;
+    out[r] = u;
+  }
+}
+
+// prefix[a][r] = number of set bits of array a in rows [0, r), r = 0..rows (exclusive scan of popcounts).
+__global__ __launch_bounds__(kWGThreads) void k_prefix_chunks(const uint64_t* masks, uint64_t rows,
+                                                              uint32_t* chunk_sum) {
+  __shared__ uint32_t s_tmp[kWavesPerWG];
+  const uint64_t* m = masks + static_cast<uint64_t>(blockIdx.y) * rows;
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kCompactRows + threadIdx.x;
+  const uint32_t pc = (r < rows) ? static_cast<uint32_t>(__builtin_popcountll(m[r])) : 0u;
+  const uint32_t t = wg_reduce_sum(pc, s_tmp);
+  if (threadIdx.x == 0) chunk_sum[static_cast<uint64_t>(blockIdx.y) * gridDim.x + blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(kWGThreads) void k_prefix_write(const uint64_t* masks, uint64_t rows,
+                                                             const uint32_t* chunk_sum, uint32_t* prefix) {
+  __shared__ uint32_t s_tmp[kWavesPerWG];
+  __shared__ uint32_t s_wave[kWavesPerWG];
+  const uint64_t* m = masks + static_cast<uint64_t>(blockIdx.y) * rows;
+  const uint32_t* cs = chunk_sum + static_cast<uint64_t>(blockIdx.y) * gridDim.x;
+  uint32_t* pre = prefix + static_cast<uint64_t>(blockIdx.y) * (rows + 1);
+  uint32_t base_part = 0;
+  for (uint32_t c = threadIdx.x; c < blockIdx.x; c += kWGThreads) base_part += cs[c];
+  const uint32_t base = wg_reduce_sum(base_part, s_tmp);
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * kCompactRows + threadIdx.x;
+  const uint32_t pc = (r < rows) ? static_cast<uint32_t>(__builtin_popcountll(m[r])) : 0u;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = pc;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) s_wave[wave] = inc;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (int w = 0; w < wave; ++w) wbase += s_wave[w];
+  if (r < rows) pre[r] = base + wbase + inc - pc;
+  if (r == rows - 1) pre[rows] = base + wbase + inc;
+}
+
+// Aggregator shard sum over packed worker streams (server.cc:97-98, rank order from a zeroed accumulator):
+// for the k-th listed block b = (row r, lane l) of this shard, worker w contributes iff bit l of its mask
+// row r is set, and its block sits at position prefix_w[r] - prefix_w[row_begin] + popcount(mask_w[r] below
+// bit l) of w's packed stream, which starts at block recv_off[w] of `recv`.
+template <int VEC>
+__global__ __launch_bounds__(kWGThreads) void k_sparse_sum(const float* recv, const uint64_t* recv_off,
+                                                           const uint64_t* masks, uint32_t count, uint64_t rows,
+                                                           const uint32_t* prefix, uint64_t row_begin,
+                                                           uint32_t lshift, const uint32_t* list, uint32_t num,
+                                                           float* out) {
+  constexpr int B4 = 64 * VEC;
+  const int lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * kWavesPerWG;
+  const v4f* src = reinterpret_cast<const v4f*>(recv);
+  for (uint32_t k = blockIdx.x * kWavesPerWG + (threadIdx.x >> 6); k < num; k += nwaves) {
+    const uint32_t b = list[k];
+    const uint64_t r = b >> lshift;
+    const uint32_t l = b & ((1u << lshift) - 1u);
+    v4f acc[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) acc[q] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (uint32_t w = 0; w < count; ++w) {
+      const uint64_t mw = masks[static_cast<uint64_t>(w) * rows + r];
+      if ((mw >> l) & 1u) {
+        const uint32_t* pw = prefix + static_cast<uint64_t>(w) * (rows + 1);
+        const uint64_t idx = recv_off[w] + (pw[r] - pw[row_begin]) +
+                             static_cast<uint64_t>(__builtin_popcountll(mw & ((1ull << l) - 1ull)));
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[q] = add4(acc[q], src[idx * B4 + q * 64 + lane]);
+      }
+    }
+    v4f* dst = reinterpret_cast<v4f*>(out) + static_cast<uint64_t>(k) * B4 + lane;
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) dst[q * 64] = acc[q];
+  }
 }
 
 // ---------------------------------------------------------------- block movement / list sum
@@ -459,7 +597,9 @@ struct Layout {
 int make_layout(uint64_t n, uint32_t block, uint32_t lanes, uint32_t parts, Layout* L) {
   if (block != 256 && block != 512 && block != 1024)
     return fail("block_size %u unsupported (256, 512, 1024)", block);
-  if (lanes == 0 || lanes > 64) return fail("num_lanes %u out of range (1..64)", lanes);
+  if (lanes < 8 || lanes > 64 || (lanes & (lanes - 1)) != 0)
+    return fail("num_lanes %u unsupported (a power of two in 8..64)", lanes);
+  if (lanes % (block == 256 ? 16u : 8u) != 0) return fail("num_lanes %u too small for block_size %u", lanes, block);
   if (parts == 0) return fail("num_parts must be >= 1");
   const uint64_t row_floats = static_cast<uint64_t>(lanes) * block;
   if (n == 0 || n % (row_floats * parts) != 0)
@@ -509,13 +649,20 @@ int launch_next(const Layout& L, const uint64_t* masks, uint32_t count, uint32_t
 #endif
 constexpr bool kNT = OMR_SCAN_NT != 0;
 
+unsigned scan_grid(uint64_t chunks) {
+  uint64_t g = (chunks + kScanWaves - 1) / kScanWaves;
+  if (g > kMaxGrid) g = kMaxGrid;
+  return static_cast<unsigned>(g ? g : 1);
+}
+
 int launch_scan(const Layout& L, const ScanArgs& a, hipStream_t st) {
   const unsigned g = grid_for(L.rows);
   if (a.m == 1) {
+    constexpr int T = 64 * kScanWaves;
     switch (L.vec) {
-      case 1: k_scan1<1, kNT><<<g, kWGThreads, 0, st>>>(a); break;
-      case 2: k_scan1<2, kNT><<<g, kWGThreads, 0, st>>>(a); break;
-      default: k_scan1<4, kNT><<<g, kWGThreads, 0, st>>>(a); break;
+      case 1: k_scan1<1, kNT><<<scan_grid(L.nb / scan_chunk_blocks<1>()), T, 0, st>>>(a); break;
+      case 2: k_scan1<2, kNT><<<scan_grid(L.nb / scan_chunk_blocks<2>()), T, 0, st>>>(a); break;
+      default: k_scan1<4, kNT><<<scan_grid(L.nb / scan_chunk_blocks<4>()), T, 0, st>>>(a); break;
     }
     return launch_status("k_scan1");
   }
@@ -710,6 +857,64 @@ int omr_compact(const uint64_t* row_masks, uint64_t row_begin, uint64_t row_end,
                                                                         num_lanes, chunk_sum, block_list,
                                                                         count);
   return launch_status("k_compact_write");
+}
+
+size_t omr_prefix_workspace_bytes(uint64_t rows, uint32_t count) {
+  return static_cast<size_t>((rows + kCompactRows - 1) / kCompactRows) * count * sizeof(uint32_t) + 16;
+}
+
+int omr_mask_union(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
+                   uint32_t num_lanes, int heads, uint64_t* out, omr_stream_t stream) {
+  if (rows == 0) return 0;
+  if (row_masks == nullptr || out == nullptr) return fail("mask_union: NULL pointer");
+  if (num_lanes == 0 || num_lanes > 64) return fail("num_lanes %u out of range", num_lanes);
+  if (heads && rows_per_part == 0) return fail("mask_union: rows_per_part must be > 0 with heads");
+  const uint64_t lane_bits = (num_lanes == 64) ? ~0ull : ((1ull << num_lanes) - 1);
+  uint64_t g = (rows + kWGThreads - 1) / kWGThreads;
+  if (g > 4096) g = 4096;
+  k_mask_union<<<static_cast<unsigned>(g), kWGThreads, 0, S(stream)>>>(row_masks, count, rows, rows_per_part,
+                                                                       lane_bits, heads, out);
+  return launch_status("k_mask_union");
+}
+
+int omr_row_prefix(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t* prefix, void* workspace,
+                   size_t workspace_bytes, omr_stream_t stream) {
+  if (rows == 0 || count == 0) return 0;
+  if (row_masks == nullptr || prefix == nullptr || workspace == nullptr) return fail("row_prefix: NULL pointer");
+  if (workspace_bytes < omr_prefix_workspace_bytes(rows, count)) return fail("row_prefix: workspace too small");
+  const uint64_t chunks = (rows + kCompactRows - 1) / kCompactRows;
+  if (chunks > 65535u * 16u) return fail("row_prefix: too many rows");
+  dim3 grid(static_cast<unsigned>(chunks), count);
+  hipStream_t st = S(stream);
+  uint32_t* cs = static_cast<uint32_t*>(workspace);
+  k_prefix_chunks<<<grid, kWGThreads, 0, st>>>(row_masks, rows, cs);
+  if (int rc = launch_status("k_prefix_chunks")) return rc;
+  k_prefix_write<<<grid, kWGThreads, 0, st>>>(row_masks, rows, cs, prefix);
+  return launch_status("k_prefix_write");
+}
+
+int omr_sparse_block_sum_f32(const float* recv, const uint64_t* recv_offsets, const uint64_t* row_masks,
+                             uint32_t count, uint64_t rows, const uint32_t* prefix, uint64_t row_begin,
+                             uint32_t num_lanes, const uint32_t* block_list, uint32_t num_list,
+                             uint32_t block_size, float* out, omr_stream_t stream) {
+  if (block_size != 256 && block_size != 512 && block_size != 1024)
+    return fail("block_size %u unsupported (256, 512, 1024)", block_size);
+  if (num_lanes < 1 || num_lanes > 64 || (num_lanes & (num_lanes - 1)) != 0)
+    return fail("num_lanes %u must be a power of two <= 64", num_lanes);
+  if (count == 0 || count > OMR_MAX_WORKERS) return fail("count=%u out of range", count);
+  if (num_list == 0) return 0;
+  if (recv_offsets == nullptr || row_masks == nullptr || prefix == nullptr || block_list == nullptr ||
+      out == nullptr)
+    return fail("sparse_block_sum: NULL pointer");
+  const uint32_t lshift = static_cast<uint32_t>(__builtin_ctz(num_lanes));
+  const unsigned g = grid_for(num_list);
+  hipStream_t st = S(stream);
+  switch (block_size / 256) {
+    case 1: k_sparse_sum<1><<<g, kWGThreads, 0, st>>>(recv, recv_offsets, row_masks, count, rows, prefix, row_begin, lshift, block_list, num_list, out); break;
+    case 2: k_sparse_sum<2><<<g, kWGThreads, 0, st>>>(recv, recv_offsets, row_masks, count, rows, prefix, row_begin, lshift, block_list, num_list, out); break;
+    default: k_sparse_sum<4><<<g, kWGThreads, 0, st>>>(recv, recv_offsets, row_masks, count, rows, prefix, row_begin, lshift, block_list, num_list, out); break;
+  }
+  return launch_status("k_sparse_sum");
 }
 
 int omr_gather_blocks_f32(const float* src, const uint32_t* block_list, uint32_t num_list,

@@ -42,6 +42,11 @@ SIGNATURES = {
     "omr_compact": (c_int, [c_vp, c_u64, c_u64, c_u32, c_vp, c_vp, c_vp, c_size, c_vp]),
     "omr_gather_blocks_f32": (c_int, [c_vp, c_vp, c_u32, c_u32, c_vp, c_vp]),
     "omr_scatter_blocks_f32": (c_int, [c_vp, c_vp, c_u32, c_u32, c_vp, c_vp]),
+    "omr_mask_union": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_int, c_vp, c_vp]),
+    "omr_prefix_workspace_bytes": (c_size, [c_u64, c_u32]),
+    "omr_row_prefix": (c_int, [c_vp, c_u32, c_u64, c_vp, c_vp, c_size, c_vp]),
+    "omr_sparse_block_sum_f32": (c_int, [c_vp, c_vp, c_vp, c_u32, c_u64, c_vp, c_u64, c_u32, c_vp, c_u32, c_u32,
+                                         c_vp, c_vp]),
 }
 
 _lib = None
