@@ -52,7 +52,13 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
                    help="rocprofv3 PMC summary giving HBM traffic per launch (optional)")
+    p.add_argument("--print-workload", action="store_true", help="print the workload string and exit")
     return p.parse_args()
+
+
+def workload_string(args, m: int) -> str:
+    return (f"{args.size_mib} MiB fp32 per rank, block_size={args.block_size}, -r {args.density}, {m} worker(s) "
+            f"per GPU, device-resident scan+sum")
 
 
 def dist_env():
@@ -138,6 +144,9 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
 def main():
     args = parse()
     ws, rank, local = dist_env()
+    if args.print_workload:
+        print(workload_string(args, args.workers if ws == 1 else 1))
+        return
     n_gpus = ws if ws > 1 else args.gpus
     if ws > 1:
         torch.cuda.set_device(local)
@@ -145,8 +154,7 @@ def main():
     dev = torch.device("cuda", local if ws > 1 else 0)
     L = Layout.from_bytes(args.size_mib << 20, args.block_size)
     m = args.workers if ws == 1 else 1
-    workload = (f"config2: {args.size_mib} MiB fp32 per rank, block_size={args.block_size}, -r {args.density} "
-                f"(90% block-sparse), {m} worker(s) per GPU, device-resident scan+sum")
+    workload = workload_string(args, m)
 
     # ---- inputs (reference generator, seed = worker id + 1: client.cc:396) -------------------------------
     worker_ids = [rank * m + w for w in range(m)]

@@ -110,29 +110,46 @@ constexpr int scan_chunk_blocks() {
   return (16 / VEC) > 8 ? (16 / VEC) : 8;
 }
 
-template <int VEC, bool NT>
+// Cache policy (tools/tune_scan.py, MI355X): loads are buffer loads with aux 2 (nt: read-once stream); the
+// aggregated blocks are buffer stores with aux 17 (sc0 sc1: system-scope write-through), which leaves no
+// dirty lines in the XCD L2s for the kernel-boundary write-back to flush before k_next can start.
+constexpr int kLoadAux = 2;
+constexpr int kStoreAux = 17;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, static_cast<int>(bytes), 0x00020000);
+}
+
+template <int VEC>
 __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
-  constexpr int B4 = 64 * VEC;  // v4fs per block
+  constexpr int B4 = 64 * VEC;  // 16-byte vectors per block
   constexpr int CH = scan_chunk_blocks<VEC>();
+  constexpr uint32_t kChunkBytes = CH * B4 * 16;
   const int lane = threadIdx.x & 63;
-  const v4f* __restrict__ x = reinterpret_cast<const v4f*>(a.x.p[0]);
-  v4f* __restrict__ out = reinterpret_cast<v4f*>(a.out);
+  // wave index made provably uniform so the buffer descriptors below live in SGPRs (no waterfall loops, T20)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const float* __restrict__ x = a.x.p[0];
+  float* __restrict__ out = a.out;
   uint8_t* __restrict__ mask_bytes = reinterpret_cast<uint8_t*>(a.masks);
-  const uint32_t cpr = a.lanes / CH;  // chunks per row
-  const uint64_t chunks = a.rows * cpr;
-  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kScanWaves;
-  for (uint64_t c = static_cast<uint64_t>(blockIdx.x) * kScanWaves + (threadIdx.x >> 6); c < chunks;
-       c += nwaves) {
-    const uint64_t row = c / cpr;
-    const uint32_t l0 = static_cast<uint32_t>(c - row * cpr) * CH;
+  // rows < 2^18 for any n below the uint32 sentinel, so chunk/row indices are 32-bit (cheap scalar math)
+  const uint32_t cpr_shift = static_cast<uint32_t>(__builtin_ctz(a.lanes / CH));  // chunks per row = 2^shift
+  const uint32_t chunks = static_cast<uint32_t>(a.rows) << cpr_shift;
+  const uint32_t nwaves = gridDim.x * kScanWaves;
+  for (uint32_t c = blockIdx.x * kScanWaves + wave; c < chunks; c += nwaves) {
+    const uint32_t row = c >> cpr_shift;
+    const uint32_t l0 = (c & ((1u << cpr_shift) - 1u)) * CH;
     const bool head = (row % a.rows_per_part) == 0;
-    const uint64_t base = c * CH * B4;  // chunks tile each row, so chunk c starts at c*CH blocks
+    const uint64_t base = static_cast<uint64_t>(c) * CH * B4 * 4;  // float offset of chunk c (= block c*CH)
+    const __amdgpu_buffer_rsrc_t src = chunk_rsrc(x + base, kChunkBytes);
     v4f v[CH][VEC];
 #pragma unroll
     for (int s = 0; s < CH; ++s)
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) v[s][q] = ld4<NT>(x + base + s * B4 + q * 64 + lane);
+      for (int q = 0; q < VEC; ++q)
+        v[s][q] = __builtin_bit_cast(
+            v4f, __builtin_amdgcn_raw_buffer_load_b128(src, ((s * B4 + q * 64 + lane) * 16), 0, kLoadAux));
     uint32_t bits = 0;
+    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(out + base, out != nullptr ? kChunkBytes : 0u);
 #pragma unroll
     for (int s = 0; s < CH; ++s) {
       uint32_t o = 0;
@@ -143,21 +160,23 @@ __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
       if (out != nullptr && (nz || head)) {
         const v4f z = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) out[base + s * B4 + q * 64 + lane] = add4(z, v[s][q]);
+        for (int q = 0; q < VEC; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(z, v[s][q])), dst,
+                                                 (s * B4 + q * 64 + lane) * 16, 0, kStoreAux);
       }
     }
     if (lane == 0) {
-      uint8_t* mp = mask_bytes + row * 8 + l0 / 8;
+      uint8_t* mp = mask_bytes + static_cast<uint64_t>(row) * 8 + l0 / 8;
       if constexpr (CH == 16) {
         *reinterpret_cast<uint16_t*>(mp) = static_cast<uint16_t>(bits);
       } else {
         *mp = static_cast<uint8_t>(bits);
       }
     } else if (l0 + CH == a.lanes && lane < 8 && static_cast<uint32_t>(lane) >= a.lanes / 8) {
-      mask_bytes[row * 8 + lane] = 0;  // bits of lanes >= NB (rows narrower than 64 lanes)
+      mask_bytes[static_cast<uint64_t>(row) * 8 + lane] = 0;  // bits of lanes >= NB (rows narrower than 64)
     }
     if (a.flags != nullptr && lane < CH)
-      a.flags[row * a.lanes + l0 + lane] = static_cast<int32_t>((bits >> lane) & 1u);
+      a.flags[static_cast<uint64_t>(row) * a.lanes + l0 + lane] = static_cast<int32_t>((bits >> lane) & 1u);
   }
 }
 
@@ -660,9 +679,9 @@ int launch_scan(const Layout& L, const ScanArgs& a, hipStream_t st) {
   if (a.m == 1) {
     constexpr int T = 64 * kScanWaves;
     switch (L.vec) {
-      case 1: k_scan1<1, kNT><<<scan_grid(L.nb / scan_chunk_blocks<1>()), T, 0, st>>>(a); break;
-      case 2: k_scan1<2, kNT><<<scan_grid(L.nb / scan_chunk_blocks<2>()), T, 0, st>>>(a); break;
-      default: k_scan1<4, kNT><<<scan_grid(L.nb / scan_chunk_blocks<4>()), T, 0, st>>>(a); break;
+      case 1: k_scan1<1><<<scan_grid(L.nb / scan_chunk_blocks<1>()), T, 0, st>>>(a); break;
+      case 2: k_scan1<2><<<scan_grid(L.nb / scan_chunk_blocks<2>()), T, 0, st>>>(a); break;
+      default: k_scan1<4><<<scan_grid(L.nb / scan_chunk_blocks<4>()), T, 0, st>>>(a); break;
     }
     return launch_status("k_scan1");
   }

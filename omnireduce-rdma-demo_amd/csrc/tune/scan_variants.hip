@@ -149,6 +149,51 @@ __global__ __launch_bounds__(64 * WPG) void t_chunk(TArgs a) {
   }
 }
 
+
+// chunk mapping with the block stores issued as buffer stores carrying a cache policy: SC1 = write-through
+// (aux 16: the line leaves the XCD's L2, so nothing is left dirty for the kernel-boundary write-back),
+// NT = aux 2.
+template <int WPG, int AUX, int LAUX = -1>
+__global__ __launch_bounds__(64 * WPG) void t_chunk_pol(TArgs a) {
+  constexpr int CH = 16, B4 = 64;
+  const int lane = threadIdx.x & 63;
+  const v4f* __restrict__ x = reinterpret_cast<const v4f*>(a.x);
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * WPG;
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * WPG + (threadIdx.x >> 6);
+  const uint32_t cpr = a.lanes / CH;
+  const uint64_t chunks = a.rows * cpr;
+  for (uint64_t c = gw; c < chunks; c += nwaves) {
+    const uint64_t row = c / cpr;
+    const uint32_t l0 = static_cast<uint32_t>(c % cpr) * CH;
+    const bool head = (row % a.rows_per_part) == 0;
+    const uint64_t base = c * CH * B4;
+    v4f v[CH];
+    if constexpr (LAUX < 0) {
+#pragma unroll
+      for (int s = 0; s < CH; ++s) v[s] = ld4<true>(x + base + s * B4 + lane);
+    } else {
+      __amdgpu_buffer_rsrc_t ls = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x) + base * 4, 0,
+                                                                    CH * B4 * 16, 0x00020000);
+#pragma unroll
+      for (int s = 0; s < CH; ++s)
+        v[s] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(ls, (s * B4 + lane) * 16, 0, LAUX));
+    }
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.out + base * 4, 0, CH * B4 * 16, 0x00020000);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const bool nz = __ballot(nz_bits(v[s]) != 0) != 0;
+      bits |= static_cast<uint32_t>(nz) << s;
+      if (nz || head) {
+        const v4f r = v4f{0.f, 0.f, 0.f, 0.f} + v[s];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, r), rs, (s * B4 + lane) * 16, 0, AUX);
+      }
+    }
+    if (lane == 0) reinterpret_cast<uint16_t*>(a.masks)[row * 4 + l0 / 16] = static_cast<uint16_t>(bits);
+    if (lane < CH) a.flags[row * a.lanes + l0 + lane] = static_cast<int32_t>((bits >> lane) & 1u);
+  }
+}
+
 // pure streaming read (OR-reduce, one store per wave) and float4 copy: the HBM ceilings on this box
 template <bool NT, int LOADS>
 __global__ __launch_bounds__(256) void t_read(const float* x, uint64_t n4, uint32_t* sink) {
@@ -184,15 +229,17 @@ static void launch(const TArgs& a, unsigned grid, hipStream_t st) {
 extern "C" {
 
 // variant ids -> (NT, LOADS, WPG, NTS, MAP); grid = min(cap, work/WPG)
-int tune_num_variants() { return 18; }
+int tune_num_variants() { return 28; }
 
 const char* tune_variant_name(int v) {
   static const char* names[] = {
       "row nt L16 w4",      "row plain L16 w4", "row nt L32 w4",    "row nt L8 w4",     "row nt L16 w8",
       "row nt L16 w4 ntst", "chunk nt L16 w4",  "chunk plain L16 w4", "row nt L16 w2", "chunk nt L16 w8",
       "c16 w8",            "c16 w16",          "c32 w8",           "c16 w8 pipe",      "c16 w4 pipe",
-      "c32 w4",            "c16 w8 nostore",   "c16 w4 nostore"};
-  return (v >= 0 && v < 18) ? names[v] : "?";
+      "c32 w4",            "c16 w8 nostore",   "c16 w4 nostore",   "c16 w8 sc1st",     "c16 w8 ntst",
+      "c16 w8 sc0sc1st",   "st19 sc01nt",     "st18 sc1nt",       "st1 sc0",          "st3 sc0nt",
+      "st17 ld2buf",       "st17 ld0buf",     "st17 ld3buf"};
+  return (v >= 0 && v < 28) ? names[v] : "?";
 }
 
 int tune_scan(int v, const float* x, float* out, int32_t* flags, uint64_t* masks, uint64_t rows, uint32_t lanes,
@@ -224,6 +271,16 @@ int tune_scan(int v, const float* x, float* out, int32_t* flags, uint64_t* masks
     case 15: t_chunk<32, 4, false, true><<<grid(chunks / 2, 4), 256, 0, st>>>(a); break;
     case 16: t_chunk<16, 8, false, false><<<grid(chunks, 8), 512, 0, st>>>(a); break;
     case 17: t_chunk<16, 4, false, false><<<grid(chunks, 4), 256, 0, st>>>(a); break;
+    case 18: t_chunk_pol<8, 16><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 19: t_chunk_pol<8, 2><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 20: t_chunk_pol<8, 17><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 21: t_chunk_pol<8, 19><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 22: t_chunk_pol<8, 18><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 23: t_chunk_pol<8, 1><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 24: t_chunk_pol<8, 3><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 25: t_chunk_pol<8, 17, 2><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 26: t_chunk_pol<8, 17, 0><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 27: t_chunk_pol<8, 17, 3><<<grid(chunks, 8), 512, 0, st>>>(a); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;

@@ -35,7 +35,7 @@ def build():
     return lib
 
 
-VARIANTS = list(range(18))
+VARIANTS = list(range(28))
 CAPS = (1024, 2048, 4096)
 
 
@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--variants", default="")
     ap.add_argument("--caps", default="")
+    ap.add_argument("--step", action="store_true",
+                    help="time [variant scan + product k_next] steps with events only around each batch")
+    ap.add_argument("--no-calib", action="store_true")
     args = ap.parse_args()
     global VARIANTS, CAPS
     if args.variants:
@@ -79,7 +82,19 @@ def main():
                           lambda k, v=v, cap=cap: lib.tune_scan(v, xs[k].data_ptr(), outs[k].data_ptr(),
                                                                 flags.data_ptr(), masks.data_ptr(), L.rows,
                                                                 L.num_lanes, L.rows_per_part, cap, st)))
-    for nt in (0, 1):
+    next_out = torch.empty(L.nb, dtype=torch.int32, device=dev)
+    if args.step:
+        lib_omr = __import__("omr")._lib.load()
+        base_cases = cases
+        cases = []
+        for name, nb_, fn in base_cases:
+            def stepfn(k, fn=fn):
+                rc = fn(k)
+                lib_omr.omr_next_offsets(masks.data_ptr(), 1, L.n, L.block_size, L.num_lanes, L.num_threads,
+                                         next_out.data_ptr(), st)
+                return rc
+            cases.append((name + " +next", nb_, stepfn))
+    for nt in ((0, 1) if not args.no_calib else ()):
         for loads in (16, 32):
             for g in (1024, 2048, 4096):
                 cases.append((f"read nt{nt} L{loads} g{g}", L.nbytes,
