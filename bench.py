@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--density", type=float, default=0.095, help="reference -r (0.095 -> 10%% non-zero)")
     p.add_argument("--workers", type=int, default=1, help="m worker tensors per GPU (N=1 only)")
     p.add_argument("--rotate", type=int, default=4, help="buffer sets rotated to defeat the Infinity Cache")
-    p.add_argument("--cpu-rounds", type=int, default=101)
+    p.add_argument("--cpu-rounds", type=int, default=500)
     p.add_argument("--cpu-warmups", type=int, default=10)
     p.add_argument("--cpu-threads", type=int, default=8)
     p.add_argument("--no-cpu", action="store_true")

@@ -114,6 +114,13 @@ int omr_scan_sum_f32(const float* const* bufs, uint32_t m, uint64_t n, uint32_t 
                      uint32_t num_lanes, uint32_t num_parts, int32_t* flags, uint64_t* row_masks,
                      uint32_t* next_offsets, float* out, omr_stream_t stream);
 
+/* The m = 1 fused scan + aggregate over rows [row_begin, row_end) only (a pipelined piece of the tensor, e.g.
+ * the part that has landed from host memory); `buf`, `out`, `flags`, `row_masks` are whole-tensor arrays indexed
+ * by global block/row.  Next offsets need every row: run omr_next_offsets once all pieces are scanned. */
+int omr_scan_sum_rows_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes,
+                          uint32_t num_parts, uint64_t row_begin, uint64_t row_end, int32_t* flags,
+                          uint64_t* row_masks, float* out, omr_stream_t stream);
+
 /* Next-offset chains from row masks (client.cc:19-31 for one worker; for a union mask, the aggregator's
  * min_next chain server.cc:86-96).  `count` mask arrays of `rows` each, stride `rows`; output stride nb. */
 int omr_next_offsets(const uint64_t* row_masks, uint32_t count, uint64_t n, uint32_t block_size,
@@ -166,6 +173,22 @@ int omr_sparse_block_sum_f32(const float* recv, const uint64_t* recv_offsets, co
                              uint32_t count, uint64_t rows, const uint32_t* prefix, uint64_t row_begin,
                              uint32_t num_lanes, const uint32_t* block_list, uint32_t num_list,
                              uint32_t block_size, float* out, omr_stream_t stream);
+
+/* ---------------------------------------------------------------- host-resident end-to-end path */
+
+/* The gradient lives in host memory (the reference's registered region, common.cc:873-914): H2D in row chunks,
+ * in-place scan + aggregate of each landed chunk, D2H back into the same host buffer, overlapped on three HIP
+ * streams; then the next-offset chains.  host_buf should be pinned (omr_host_register or hipHostMalloc).
+ * host_flags / host_next (may be NULL) receive the int32 flags / uint32 next offsets.  *seconds = wall time. */
+typedef struct omr_host_plan omr_host_plan;
+const char* omr_host_last_error(void);
+int omr_host_register(void* ptr, size_t bytes);
+int omr_host_unregister(void* ptr);
+int omr_host_plan_create(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                         uint64_t chunk_rows, omr_host_plan** plan);
+int omr_host_plan_destroy(omr_host_plan* plan);
+int omr_host_scan_sum_f32(omr_host_plan* plan, float* host_buf, int32_t* host_flags, uint32_t* host_next,
+                          double* seconds);
 
 #ifdef __cplusplus
 }

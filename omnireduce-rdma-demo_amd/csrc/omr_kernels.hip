@@ -86,6 +86,8 @@ struct ScanArgs {
   uint32_t m;
   uint32_t lanes;          // NUM_BLOCKS
   uint32_t rows_per_part;  // rows per partition
+  uint32_t row_begin;      // k_scan1 sweeps rows [row_begin, row_end) (a pipelined chunk, or everything)
+  uint32_t row_end;
   uint32_t pad;
   uint64_t rows;           // total rows
   uint64_t nb;             // total blocks
@@ -128,14 +130,14 @@ __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
   const int lane = threadIdx.x & 63;
   // wave index made provably uniform so the buffer descriptors below live in SGPRs (no waterfall loops, T20)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const float* __restrict__ x = a.x.p[0];
-  float* __restrict__ out = a.out;
+  const float* x = a.x.p[0];  // no __restrict__: out may alias x (in-place result, client.cc:89)
+  float* out = a.out;
   uint8_t* __restrict__ mask_bytes = reinterpret_cast<uint8_t*>(a.masks);
   // rows < 2^18 for any n below the uint32 sentinel, so chunk/row indices are 32-bit (cheap scalar math)
   const uint32_t cpr_shift = static_cast<uint32_t>(__builtin_ctz(a.lanes / CH));  // chunks per row = 2^shift
-  const uint32_t chunks = static_cast<uint32_t>(a.rows) << cpr_shift;
+  const uint32_t chunks = a.row_end << cpr_shift;
   const uint32_t nwaves = gridDim.x * kScanWaves;
-  for (uint32_t c = blockIdx.x * kScanWaves + wave; c < chunks; c += nwaves) {
+  for (uint32_t c = (a.row_begin << cpr_shift) + blockIdx.x * kScanWaves + wave; c < chunks; c += nwaves) {
     const uint32_t row = c >> cpr_shift;
     const uint32_t l0 = (c & ((1u << cpr_shift) - 1u)) * CH;
     const bool head = (row % a.rows_per_part) == 0;
@@ -678,10 +680,11 @@ int launch_scan(const Layout& L, const ScanArgs& a, hipStream_t st) {
   const unsigned g = grid_for(L.rows);
   if (a.m == 1) {
     constexpr int T = 64 * kScanWaves;
+    const uint64_t nbr = static_cast<uint64_t>(a.row_end - a.row_begin) * L.lanes;  // blocks in the range
     switch (L.vec) {
-      case 1: k_scan1<1><<<scan_grid(L.nb / scan_chunk_blocks<1>()), T, 0, st>>>(a); break;
-      case 2: k_scan1<2><<<scan_grid(L.nb / scan_chunk_blocks<2>()), T, 0, st>>>(a); break;
-      default: k_scan1<4><<<scan_grid(L.nb / scan_chunk_blocks<4>()), T, 0, st>>>(a); break;
+      case 1: k_scan1<1><<<scan_grid(nbr / scan_chunk_blocks<1>()), T, 0, st>>>(a); break;
+      case 2: k_scan1<2><<<scan_grid(nbr / scan_chunk_blocks<2>()), T, 0, st>>>(a); break;
+      default: k_scan1<4><<<scan_grid(nbr / scan_chunk_blocks<4>()), T, 0, st>>>(a); break;
     }
     return launch_status("k_scan1");
   }
@@ -790,6 +793,8 @@ int omr_scan_sum_f32(const float* const* bufs, uint32_t m, uint64_t n, uint32_t 
   a.m = m;
   a.lanes = L.lanes;
   a.rows_per_part = L.rows_per_part;
+  a.row_begin = 0;
+  a.row_end = static_cast<uint32_t>(L.rows);
   a.rows = L.rows;
   a.nb = L.nb;
   a.flags = flags;
@@ -802,6 +807,32 @@ int omr_scan_sum_f32(const float* const* bufs, uint32_t m, uint64_t n, uint32_t 
     if (int rc = launch_next(L, row_masks, count, next_offsets, st)) return rc;
   }
   return 0;
+}
+
+int omr_scan_sum_rows_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes,
+                          uint32_t num_parts, uint64_t row_begin, uint64_t row_end, int32_t* flags,
+                          uint64_t* row_masks, float* out, omr_stream_t stream) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  if (buf == nullptr || row_masks == nullptr) return fail("scan_sum_rows: NULL pointer");
+  if (row_begin > row_end || row_end > L.rows) return fail("scan_sum_rows: bad row range");
+  if (row_begin == row_end) return 0;
+  if (reinterpret_cast<uintptr_t>(buf) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 16 != 0)
+    return fail("scan_sum_rows: buffers must be 16-byte aligned");
+  ScanArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x.p[0] = buf;
+  a.m = 1;
+  a.lanes = L.lanes;
+  a.rows_per_part = L.rows_per_part;
+  a.row_begin = static_cast<uint32_t>(row_begin);
+  a.row_end = static_cast<uint32_t>(row_end);
+  a.rows = L.rows;
+  a.nb = L.nb;
+  a.flags = flags;
+  a.masks = row_masks;
+  a.out = out;
+  return launch_scan(L, a, S(stream));
 }
 
 int omr_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,

@@ -36,6 +36,7 @@ SIGNATURES = {
     "omr_fill_blocks_f32": (c_int, [c_vp, c_u64, c_u32, c_int, c_u32, c_vp, c_vp]),
     "omr_scan_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp]),
     "omr_scan_sum_f32": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "omr_scan_sum_rows_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "omr_next_offsets": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp]),
     "omr_block_sum_f32": (c_int, [c_vp, c_u32, c_vp, c_u32, c_u32, c_vp, c_vp]),
     "omr_compact_workspace_bytes": (c_size, [c_u64]),
@@ -47,6 +48,12 @@ SIGNATURES = {
     "omr_row_prefix": (c_int, [c_vp, c_u32, c_u64, c_vp, c_vp, c_size, c_vp]),
     "omr_sparse_block_sum_f32": (c_int, [c_vp, c_vp, c_vp, c_u32, c_u64, c_vp, c_u64, c_u32, c_vp, c_u32, c_u32,
                                          c_vp, c_vp]),
+    "omr_host_last_error": (ctypes.c_char_p, []),
+    "omr_host_register": (c_int, [c_vp, c_size]),
+    "omr_host_unregister": (c_int, [c_vp]),
+    "omr_host_plan_create": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u64, c_vp]),
+    "omr_host_plan_destroy": (c_int, [c_vp]),
+    "omr_host_scan_sum_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

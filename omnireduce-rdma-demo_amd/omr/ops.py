@@ -213,3 +213,45 @@ def block_sum(inputs: Sequence[torch.Tensor], block_list: torch.Tensor, num: int
         _lib.check(_lib.load().omr_block_sum_f32(arr, len(inputs), _ptr(block_list), num, block_size,
                                                  _ptr(out), _stream(stream)), "omr_block_sum_f32")
     return out
+
+
+# ------------------------------------------------------------------ host-resident end-to-end path
+
+class HostPlan:
+    """omr_host_plan: H2D -> in-place scan + aggregate -> D2H over row chunks on three HIP streams, for a
+    gradient that starts and ends in pinned host memory (the reference's registered region)."""
+
+    def __init__(self, layout: Layout, chunk_rows: int = 512):
+        self.layout = layout
+        self._p = ctypes.c_void_p()
+        rc = _lib.load().omr_host_plan_create(layout.n, layout.block_size, layout.num_lanes, layout.num_threads,
+                                              chunk_rows, ctypes.byref(self._p))
+        if rc != 0:
+            raise _lib.OmrError(f"omr_host_plan_create rc={rc}: {_lib.load().omr_host_last_error().decode()}")
+
+    def run(self, host_buf: torch.Tensor, flags: Optional[torch.Tensor] = None,
+            next_offsets: Optional[torch.Tensor] = None) -> float:
+        L = self.layout
+        for t, n, dt in ((host_buf, L.n, torch.float32), (flags, L.nb, torch.int32),
+                         (next_offsets, L.nb, torch.int32)):
+            if t is not None and (t.is_cuda or t.dtype != dt or t.numel() != n or not t.is_contiguous()):
+                raise ValueError("host tensors must be contiguous CPU tensors of the layout's size")
+        secs = ctypes.c_double()
+        rc = _lib.load().omr_host_scan_sum_f32(self._p, host_buf.data_ptr(),
+                                               flags.data_ptr() if flags is not None else None,
+                                               next_offsets.data_ptr() if next_offsets is not None else None,
+                                               ctypes.byref(secs))
+        if rc != 0:
+            raise _lib.OmrError(f"omr_host_scan_sum_f32 rc={rc}: {_lib.load().omr_host_last_error().decode()}")
+        return secs.value
+
+    def close(self):
+        if self._p:
+            _lib.load().omr_host_plan_destroy(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

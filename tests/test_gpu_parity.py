@@ -227,3 +227,24 @@ def test_full_size_properties(gpu, nbytes, B, r):
     xb, ob = x.view(L.nb, B), out.view(L.nb, B)
     assert torch.equal(ob[sel], xb[sel])
     assert int(torch.count_nonzero(ob[~sel])) == 0
+
+
+@pytest.mark.parametrize("chunk_rows", [7, 64, 4096])
+def test_host_resident_pipeline(gpu, chunk_rows):
+    """Pinned-host round: H2D chunks, in-place scan+aggregate, D2H (ragged last chunk with chunk_rows=7)."""
+    L = Layout(n=4 << 20, block_size=256)
+    x = _rand_sparse(L, 0.3, 51)[0]
+    x[5 * 256:6 * 256] = -0.0
+    host = torch.from_numpy(x.copy()).pin_memory()
+    flags = torch.empty(L.nb, dtype=torch.int32).pin_memory()
+    nxt = torch.empty(L.nb, dtype=torch.int32).pin_memory()
+    plan = ops.HostPlan(L, chunk_rows=chunk_rows)
+    secs = plan.run(host, flags, nxt)
+    plan.close()
+    f = oracle.flags_from_data(x, 256)
+    exp = x.copy()
+    oracle.block_sum([x], L.n, 256, 64, 8, f, exp)
+    assert secs > 0
+    assert (flags.numpy() == f).all()
+    assert (nxt.numpy().view(np.uint32) == oracle.next_offsets(f, L.n, 256, 64, 8)).all()
+    assert (host.numpy().view(np.uint32) == exp.view(np.uint32)).all()

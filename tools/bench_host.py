@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Host-resident end-to-end rate (north_star: the gradient starts and ends in host memory): a pinned host tensor
+goes H2D in row chunks, is scanned + aggregated in place on the GPU, and comes back D2H (omr_host_plan, three
+overlapped HIP streams), next to the plain H2D / D2H copy rates and the device-resident kernel rate.
+usage: python tools/bench_host.py [--size-mib 4096] [--density 0.49] [--chunk-rows 512] [--reps 5]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "omnireduce-rdma-demo_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from omr import Layout, ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size-mib", type=int, default=4096)
+    ap.add_argument("--block-size", type=int, default=256)
+    ap.add_argument("--density", type=float, default=0.49)
+    ap.add_argument("--chunk-rows", type=int, default=512)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    L = Layout.from_bytes(a.size_mib << 20, a.block_size)
+    dev = torch.device("cuda:0")
+    bm = ops.gen_bitmap(0, a.density, L.nb)
+    xd = ops.fill_blocks(torch.from_numpy(bm).to(dev), L)
+    host = torch.empty(L.n, dtype=torch.float32).pin_memory()
+    pristine = xd.cpu()
+    flags = torch.empty(L.nb, dtype=torch.int32).pin_memory()
+    nxt = torch.empty(L.nb, dtype=torch.int32).pin_memory()
+    plan = ops.HostPlan(L, chunk_rows=a.chunk_rows)
+    e2e = []
+    for r in range(a.reps + 1):
+        host.copy_(pristine)
+        t = plan.run(host, flags, nxt)
+        if r:
+            e2e.append(t)
+    ok = bool((flags.numpy() == bm).all())
+    d = torch.empty(L.n, dtype=torch.float32, device=dev)
+    h2d, d2h = [], []
+    for r in range(a.reps):
+        torch.cuda.synchronize(); t0 = time.perf_counter(); d.copy_(host, non_blocking=True); torch.cuda.synchronize()
+        h2d.append(time.perf_counter() - t0)
+        t0 = time.perf_counter(); host.copy_(d, non_blocking=True); torch.cuda.synchronize()
+        d2h.append(time.perf_counter() - t0)
+    dplan = ops.ScanSumPlan(L, 1, device=dev)
+    out = torch.zeros_like(xd)
+    for _ in range(3):
+        dplan.run([xd], out)
+    torch.cuda.synchronize(); t0 = time.perf_counter()
+    for _ in range(a.reps):
+        dplan.run([xd], out)
+    torch.cuda.synchronize()
+    dev_t = (time.perf_counter() - t0) / a.reps
+    S = L.nbytes
+    res = {"tensor_bytes": S, "block_size": L.block_size, "density_r": a.density,
+           "nonzero_fraction": float(bm.mean()), "chunk_rows": a.chunk_rows, "flags_ok": ok,
+           "e2e_ms": 1e3 * float(np.median(e2e)), "e2e_GBps": S / float(np.median(e2e)) / 1e9,
+           "h2d_GBps": S / float(np.median(h2d)) / 1e9, "d2h_GBps": S / float(np.median(d2h)) / 1e9,
+           "device_resident_ms": dev_t * 1e3, "device_resident_GBps": S / dev_t / 1e9}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
