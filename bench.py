@@ -4,7 +4,8 @@
 Workload at N=1 (BASELINE.json configs[1]): a 256 MiB fp32 gradient, BLOCK_SIZE=256 (64 lanes, 8 partitions),
 reference generator at -r 0.095 (10 % of blocks non-zero = 90 % block-sparse), one worker, already resident
 in HBM.  One step = one pass of the hot path over it: the fused worker scan + aggregator sum kernel
-(flags, row masks, summed non-zero blocks) and the next-offset kernel.  Four input/output buffer sets are
+(flags, row masks, summed non-zero blocks written back in place, as client.cc:89 does) and the next-offset
+kernel.  (0.0f + x == x for the generator's data, so every step sees the same input.)  Four input/output buffer sets are
 rotated so that no step re-reads data the 256 MiB Infinity Cache still holds from the previous use.
 N>1 (torch.distributed.run, one rank per GPU): each rank is worker r with its own 256 MiB tensor (seed r+1) and
 aggregator for shard r; a step is the full sparse all-reduce (omr.dist): local scan, RCCL exchange of the
@@ -180,6 +181,8 @@ def main():
 
         def step(i, ev=None):
             xs, out = sets[i % len(sets)]
+            if m == 1:
+                out = xs[0]  # in place, as the reference returns results into res->buf (client.cc:89)
             if ev is not None:
                 ev[0].record(stream)
             plan.run(xs, out, with_next=False)

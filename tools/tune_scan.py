@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--step", action="store_true",
                     help="time [variant scan + product k_next] steps with events only around each batch")
     ap.add_argument("--no-calib", action="store_true")
+    ap.add_argument("--inplace", action="store_true", help="out aliases x (the reference's in-place result)")
     args = ap.parse_args()
     global VARIANTS, CAPS
     if args.variants:
@@ -66,7 +67,7 @@ def main():
     bmt = torch.from_numpy(bm).to(dev)
     NSET = 4
     xs = [ops.fill_blocks(bmt, L) for _ in range(NSET)]
-    outs = [torch.zeros(L.n, device=dev) for _ in range(NSET)]
+    outs_sep = [torch.zeros(L.n, device=dev) for _ in range(NSET)]
     flags = torch.zeros(L.nb, dtype=torch.int32, device=dev)
     masks = torch.zeros(L.rows, dtype=torch.int64, device=dev)
     sink = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
@@ -77,11 +78,13 @@ def main():
     cases = []
     for v in VARIANTS:
         for cap in CAPS:
-            name = lib.tune_variant_name(v).decode()
-            cases.append((f"{name} cap{cap}", kbytes,
-                          lambda k, v=v, cap=cap: lib.tune_scan(v, xs[k].data_ptr(), outs[k].data_ptr(),
-                                                                flags.data_ptr(), masks.data_ptr(), L.rows,
-                                                                L.num_lanes, L.rows_per_part, cap, st)))
+            for mode in (("sep", "inpl") if args.inplace else ("sep",)):
+                outs = xs if mode == "inpl" else outs_sep
+                name = lib.tune_variant_name(v).decode()
+                cases.append((f"{name} cap{cap} {mode}", kbytes,
+                              lambda k, v=v, cap=cap, outs=outs: lib.tune_scan(
+                                  v, xs[k].data_ptr(), outs[k].data_ptr(), flags.data_ptr(), masks.data_ptr(),
+                                  L.rows, L.num_lanes, L.rows_per_part, cap, st)))
     next_out = torch.empty(L.nb, dtype=torch.int32, device=dev)
     if args.step:
         lib_omr = __import__("omr")._lib.load()
@@ -102,7 +105,8 @@ def main():
                                                                                sink.data_ptr(), g, st)))
         for g in (2048, 8192, 32768):
             cases.append((f"copy nt{nt} g{g}", 2 * L.nbytes,
-                          lambda k, nt=nt, g=g: lib.tune_copy(nt, xs[k].data_ptr(), outs[k].data_ptr(), L.n, g, st)))
+                          lambda k, nt=nt, g=g: lib.tune_copy(nt, xs[k].data_ptr(), outs_sep[k].data_ptr(), L.n, g,
+                                                              st)))
     # correctness of every scan variant against the product kernel
     ref = ops.scan(xs[0], L)
     for ci, (name, _, fn) in enumerate(cases):
