@@ -1,0 +1,70 @@
+/*
+ * omr_dist.h — C ABI of the multi-rank sparse all-reduce (one OmniReduce round across ranks), host side in C++
+ * (omnireduce-rdma-demo_amd/csrc/omr_dist.cpp, library libomr_dist.so, on top of libomr.so).
+ *
+ * Replaces the reference's RDMA transport and per-thread protocol loops for the hot path: every rank is worker r
+ * and aggregator of shard r (README.md:13-22; common.cc:381-383 shards slots over aggregators).  One call =
+ *   worker scan (client.cc:19-31) -> all-gather of row masks -> pack own non-zero blocks (common.cc:405-407) ->
+ *   grouped send/recv to the shard aggregators -> rank-order shard sums (server.cc:97-98) -> sums back to every
+ *   worker (server.cc:162) -> in-place scatter (client.cc:89).
+ *
+ * Two transports:
+ *   RCCL  — one process per GPU over xGMI; bootstrap with omr_dist_unique_id on one rank, shared out of band
+ *           (the ./omr_server rendezvous does this, standing in for the reference's TCP bootstrap common.cc:50-197).
+ *   local — `world` ranks as threads of ONE process (any number of GPUs, several ranks may share a GPU) that
+ *           exchange through device-to-device copies; the loopback stand-in for testing "multi-node" without a
+ *           cluster.
+ * Return convention as omr.h: 0 ok, OMR_EINVAL on bad arguments, otherwise a hip/rccl error code; message in
+ * omr_dist_last_error().
+ */
+#ifndef OMR_DIST_H
+#define OMR_DIST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "omr.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMR_UNIQUE_ID_BYTES 128
+
+typedef struct omr_dist omr_dist;               /* a transport endpoint (one rank) */
+typedef struct omr_local_board omr_local_board; /* shared state of an in-process group */
+typedef struct omr_ar_plan omr_ar_plan;         /* workspaces of one sparse all-reduce shape */
+
+const char* omr_dist_last_error(void);
+
+int omr_dist_unique_id(void* id /* OMR_UNIQUE_ID_BYTES */);
+int omr_dist_create_rccl(const void* id, int rank, int world, omr_dist** out);
+
+omr_local_board* omr_local_board_create(int world);
+void omr_local_board_destroy(omr_local_board* board);
+int omr_dist_create_local(omr_local_board* board, int rank, omr_dist** out);
+
+int omr_dist_rank(const omr_dist* d);
+int omr_dist_world(const omr_dist* d);
+int omr_dist_destroy(omr_dist* d);
+
+/* Workspaces for tensors of n floats on the layout (block_size, num_lanes, num_parts); allocated on the current
+ * HIP device, which must be the device the rank's tensors live on. */
+int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                       omr_ar_plan** out);
+int omr_ar_plan_destroy(omr_ar_plan* plan);
+
+/* One round on this rank.  x: the rank's gradient (device, n floats).  out: receives the all-reduced tensor
+ * (rank-order sums over the union of non-zero blocks plus lane heads); may equal x for the reference's in-place
+ * result, otherwise it must already hold x's values outside that set.  flags / next_offsets / union_next (device,
+ * nb entries each, may be NULL) receive the worker's flags, its next-offset chain and the aggregator chain.
+ * *sent_blocks / *union_blocks (host, may be NULL) receive this rank's off-rank sent blocks and the write-set size.
+ * Synchronises `stream` once (block counts for the transport) and on return. */
+int omr_sparse_allreduce_f32(omr_ar_plan* plan, const float* x, float* out, int32_t* flags,
+                             uint32_t* next_offsets, uint32_t* union_next, uint64_t* sent_blocks,
+                             uint64_t* union_blocks, omr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OMR_DIST_H */

@@ -1,0 +1,295 @@
+// omr_client.cpp — ./omr_client: the worker with the reference CLI and benchmark loop (client.cc:240-491).
+//
+//   ./omr_client [-p port] [-d ib-dev] [-i ib-port] [-g gid-idx] [-s service-level] [-r density] agg_ip[,agg_ip...]
+//
+// MI355X-build extensions:  -n floats (DATA_SIZE, default common.h:40 = 128 Mi)   -b BLOCK_SIZE (256)
+//   -W warm-ups (10)  -R rounds (101) (client.cc:368-369)  -G gpu (default $LOCAL_RANK or 0)
+//   -c  check the result against the rank-order sum of every worker's input (the working CHECK of
+//       client.cc:449-465)    -I  in place (the reference writes results into res->buf, so rounds after the first
+//       start from the previous round's output)    -L k  run k workers as threads of this process over the
+//       loopback transport (no server needed)
+//
+// With an aggregator list, the first entry is the ./omr_server rendezvous: it assigns this worker's ID by IP list
+// position (common.cc:123-133) and relays the RCCL unique id; the round itself is omr_sparse_allreduce_f32 over
+// RCCL (xGMI), every GPU aggregating one shard.  Output lines are the reference's: per round
+// "data size: ... time: ... us; alg bw: ... GB/s" (client.cc:447), the average (client.cc:473), and
+// "test result is N" (client.cc:486).  alg bw keeps the reference formula DATA_SIZE*4/2^30/s (client.cc:445).
+#include <getopt.h>
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "omr.h"
+#include "omr_dist.h"
+#include "omr_net.hpp"
+
+namespace {
+
+struct Opts {
+  int port = 19875, ib_port = 1, gid = -1, sl = 0;  // client.cc:9-18
+  const char* dev = nullptr;
+  double density = 1.0;  // client.cc:253
+  uint64_t n = 128ull << 20;
+  uint32_t block = 256;
+  int warmups = 10, rounds = 101;  // client.cc:368-369
+  int gpu = -1, local = 0;
+  bool check = false, inplace = false;
+};
+
+void usage(const char* argv0) {  // common.cc:1441-1457 (default port and -r text corrected: SURVEY.md §5)
+  fprintf(stdout, "Usage:\n %s <host> connect to server at <host>\n\n", argv0);
+  fprintf(stdout, "Options:\n");
+  fprintf(stdout, " -p, --port <port> listen on/connect to port <port> (default 19875)\n");
+  fprintf(stdout, " -d, --ib-dev <dev> accepted for compatibility (no verbs device is used)\n");
+  fprintf(stdout, " -i, --ib-port <port> accepted for compatibility\n");
+  fprintf(stdout, " -g, --gid_idx <git index> accepted for compatibility\n");
+  fprintf(stdout, " -s, --service-level <sl> accepted for compatibility\n");
+  fprintf(stdout, " -r, --density-ratio <r> fraction of non-zero blocks, as rand()%%100/101 < r (default 1.0)\n");
+  fprintf(stdout, " -n <floats> -b <block size> -W <warm-ups> -R <rounds> -G <gpu> -c (check) -I (in place)\n");
+  fprintf(stdout, " -L <k> run k workers in this process over the loopback transport\n");
+  fprintf(stdout, " -h, --help show this help message\n");
+}
+
+#define HIPOK(x)                                                                 \
+  do {                                                                           \
+    hipError_t _e = (x);                                                         \
+    if (_e != hipSuccess) {                                                      \
+      fprintf(stderr, "%s failed: %s\n", #x, hipGetErrorString(_e));             \
+      return 1;                                                                  \
+    }                                                                            \
+  } while (0)
+
+// the worker's tensor: the reference generator (client.cc:396-421) on the device
+int make_input(uint32_t worker_id, const Opts& o, float* d_x, int32_t* d_bitmap) {
+  const uint64_t nb = o.n / o.block;
+  std::vector<int32_t> bm(nb);
+  uint64_t nz = 0;
+  if (omr_gen_bitmap(worker_id, o.density, nb, bm.data(), &nz)) return 1;
+  HIPOK(hipMemcpy(d_bitmap, bm.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (omr_fill_blocks_f32(d_bitmap, nb, o.block, 0, 0, d_x, nullptr)) return 1;
+  HIPOK(hipDeviceSynchronize());
+  return 0;
+}
+
+int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer) {
+  HIPOK(hipSetDevice(gpu));
+  const int rank = omr_dist_rank(d), world = omr_dist_world(d);
+  const uint32_t lanes = omr_num_lanes(o.block);
+  const uint64_t nb = o.n / o.block;
+  if (omr_layout_check(o.n, o.block, lanes, OMR_NUM_THREADS)) {
+    fprintf(stderr, "bad layout: %s\n", omr_last_error());
+    return 1;
+  }
+  float *d_x = nullptr, *d_out = nullptr;
+  int32_t* d_bitmap = nullptr;
+  HIPOK(hipMalloc(&d_x, o.n * sizeof(float)));
+  HIPOK(hipMalloc(&d_out, o.n * sizeof(float)));
+  HIPOK(hipMalloc(&d_bitmap, nb * sizeof(int32_t)));
+  if (make_input(static_cast<uint32_t>(rank), o, d_x, d_bitmap)) return 1;  // srand(res.myId+1)
+  HIPOK(hipMemcpy(d_out, d_x, o.n * sizeof(float), hipMemcpyDeviceToDevice));
+  omr_ar_plan* plan = nullptr;
+  if (omr_ar_plan_create(d, o.n, o.block, lanes, OMR_NUM_THREADS, &plan)) {
+    fprintf(stderr, "omr_ar_plan_create: %s\n", omr_dist_last_error());
+    return 1;
+  }
+  hipStream_t st;
+  HIPOK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  if (printer) std::cout << "density: " << o.density << std::endl;  // client.cc:405
+  const double gib = o.n * sizeof(float) / (1024.0 * 1024.0 * 1024.0);
+  double avg_bw = 0.0;
+  unsigned long avg_time_usec = 0;
+  int print_count = 0;
+  auto start = std::chrono::steady_clock::now();
+  for (int round = 0; round < o.warmups + o.rounds; ++round) {
+    float* out = o.inplace ? d_x : d_out;
+    uint64_t sent = 0, uni = 0;
+    if (omr_sparse_allreduce_f32(plan, d_x, out, nullptr, nullptr, nullptr, &sent, &uni, st)) {
+      fprintf(stderr, "failed to run the round: %s\n", omr_dist_last_error());  // client.cc:131-135
+      return 1;
+    }
+    if (round >= o.warmups) {  // client.cc:439-448, print_freq 1
+      if (round - o.warmups > 0) {
+        const auto now = std::chrono::steady_clock::now();
+        const unsigned long us =
+            static_cast<unsigned long>(std::chrono::duration_cast<std::chrono::microseconds>(now - start).count());
+        const double bw = gib / (us / 1e6);
+        ++print_count;
+        avg_time_usec += us;
+        avg_bw += bw;
+        if (printer)
+          fprintf(stdout, "data size: %lu Bytes; time: %lu us; alg bw: %f GB/s\n",
+                  static_cast<unsigned long>(o.n * sizeof(float)), us, bw);
+      }
+      start = std::chrono::steady_clock::now();
+    }
+  }
+  int rc = 0;
+  if (o.check) {  // the CHECK of client.cc:449-465, done right: expected = rank-order sum of every input
+    std::vector<float*> bufs(world);
+    for (int w = 0; w < world; ++w) {
+      HIPOK(hipMalloc(&bufs[w], o.n * sizeof(float)));
+      if (make_input(static_cast<uint32_t>(w), o, bufs[w], d_bitmap)) return 1;
+    }
+    float* d_exp = nullptr;
+    uint64_t* d_masks = nullptr;
+    HIPOK(hipMalloc(&d_exp, o.n * sizeof(float)));
+    HIPOK(hipMalloc(&d_masks, (world + 1) * (nb / lanes) * sizeof(uint64_t)));
+    HIPOK(hipMemcpy(d_exp, bufs[rank], o.n * sizeof(float), hipMemcpyDeviceToDevice));
+    std::vector<const float*> cb(bufs.begin(), bufs.end());
+    if (world <= OMR_MAX_WORKERS &&
+        omr_scan_sum_f32(cb.data(), world, o.n, o.block, lanes, OMR_NUM_THREADS, nullptr, d_masks, nullptr, d_exp,
+                         nullptr) == 0) {
+      HIPOK(hipDeviceSynchronize());
+      std::vector<float> got(o.n), exp(o.n);
+      HIPOK(hipMemcpy(got.data(), o.inplace ? d_x : d_out, o.n * sizeof(float), hipMemcpyDeviceToHost));
+      HIPOK(hipMemcpy(exp.data(), d_exp, o.n * sizeof(float), hipMemcpyDeviceToHost));
+      bool ok = true;
+      for (uint64_t i = 0; i < o.n; ++i)
+        if (memcmp(&got[i], &exp[i], sizeof(float)) != 0) {
+          std::cout << "error: " << exp[i] << "<---->" << got[i] << std::endl;  // client.cc:453-456
+          ok = false;
+          break;
+        }
+      if (ok && printer) std::cout << "check OK" << std::endl;
+      if (!ok) rc = 1;
+    } else {
+      fprintf(stderr, "check skipped: %s\n", omr_last_error());
+    }
+    for (float* b : bufs) (void)hipFree(b);
+    (void)hipFree(d_exp);
+    (void)hipFree(d_masks);
+  }
+  if (printer && print_count > 0)  // client.cc:473
+    fprintf(stdout, "data size: %lu Bytes; average time: %lu us; average alg bw: %f GB/s\n",
+            static_cast<unsigned long>(o.n * sizeof(float)), avg_time_usec / print_count, avg_bw / print_count);
+  omr_ar_plan_destroy(plan);
+  (void)hipStreamDestroy(st);
+  (void)hipFree(d_x);
+  (void)hipFree(d_out);
+  (void)hipFree(d_bitmap);
+  return rc;
+}
+
+}  // namespace
+
+int main(int argc, char* argv[]) {
+  Opts o;
+  static option longopts[] = {{"port", 1, nullptr, 'p'},          {"ib-dev", 1, nullptr, 'd'},
+                              {"ib-port", 1, nullptr, 'i'},       {"gid-idx", 1, nullptr, 'g'},
+                              {"service-level", 1, nullptr, 's'}, {"density-ratio", 1, nullptr, 'r'},
+                              {"help", 0, nullptr, 'h'},          {nullptr, 0, nullptr, 0}};
+  while (true) {
+    int c = getopt_long(argc, argv, "p:d:i:g:s:r:n:b:W:R:G:L:cIh", longopts, nullptr);
+    if (c == -1) break;
+    switch (c) {
+      case 'p': o.port = static_cast<int>(strtoul(optarg, nullptr, 0)); break;
+      case 'd': o.dev = optarg; break;
+      case 'i': o.ib_port = static_cast<int>(strtoul(optarg, nullptr, 0)); break;
+      case 'g': o.gid = static_cast<int>(strtoul(optarg, nullptr, 0)); break;
+      case 's': o.sl = static_cast<int>(strtoul(optarg, nullptr, 0)); break;
+      case 'r':
+        o.density = strtod(optarg, nullptr);
+        if (o.density < 0) o.density = 1.0;  // client.cc:302-308
+        break;
+      case 'n': o.n = strtoull(optarg, nullptr, 0); break;
+      case 'b': o.block = static_cast<uint32_t>(strtoul(optarg, nullptr, 0)); break;
+      case 'W': o.warmups = atoi(optarg); break;
+      case 'R': o.rounds = atoi(optarg); break;
+      case 'G': o.gpu = atoi(optarg); break;
+      case 'L': o.local = atoi(optarg); break;
+      case 'c': o.check = true; break;
+      case 'I': o.inplace = true; break;
+      default: usage(argv[0]); return 1;
+    }
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    fprintf(stderr, "no HIP device\n");
+    fprintf(stdout, "\ntest result is 1\n");
+    return 1;
+  }
+  std::vector<std::string> aggs = omrnet::split_list(optind == argc - 1 ? argv[optind] : nullptr);
+  omrnet::print_config(false, aggs, o.port, o.dev, o.ib_port, o.gid, o.sl);
+  int rc = 0;
+  if (o.local > 0) {  // loopback: k workers as threads, GPUs round-robin
+    omr_local_board* board = omr_local_board_create(o.local);
+    std::vector<int> rcs(o.local, 0);
+    std::vector<std::thread> th;
+    std::cout << "Number of aggregators: " << o.local << "; Number of workers is " << o.local
+              << "; My ID is 0 (loopback, " << ndev << " GPU(s))" << std::endl;
+    printf("Connected.\n");
+    for (int t = 0; t < o.local; ++t)
+      th.emplace_back([&, t] {
+        if (hipSetDevice(t % ndev) != hipSuccess) {
+          rcs[t] = 1;
+          return;
+        }
+        omr_dist* d = nullptr;
+        if (omr_dist_create_local(board, t, &d)) {
+          rcs[t] = 1;
+          return;
+        }
+        rcs[t] = run_worker(d, o, t % ndev, t == 0);
+        omr_dist_destroy(d);
+      });
+    for (auto& t : th) t.join();
+    omr_local_board_destroy(board);
+    for (int r : rcs) rc |= r;
+    fprintf(stdout, "\ntest result is %d\n", rc);
+    return rc;
+  }
+  if (aggs.empty()) {
+    usage(argv[0]);
+    return 1;
+  }
+  const char* lr = getenv("LOCAL_RANK");
+  const int gpu = o.gpu >= 0 ? o.gpu : (lr ? atoi(lr) : 0) % ndev;
+  fprintf(stdout, "start connected\n");  // client.cc:348
+  int fd = omrnet::connect_to(aggs[0].c_str(), o.port);
+  if (fd < 0) {
+    fprintf(stderr, "failed to connect to %s:%d\n", aggs[0].c_str(), o.port);
+    fprintf(stdout, "\ntest result is 1\n");
+    return 1;
+  }
+  omrnet::Hello h{omrnet::kMagic, gpu};
+  omrnet::Assign a{};
+  char uid[omrnet::kIdBytes];
+  if (!omrnet::send_all(fd, &h, sizeof(h)) || !omrnet::recv_all(fd, &a, sizeof(a)) || a.magic != omrnet::kMagic) {
+    fprintf(stderr, "rendezvous failed\n");
+    fprintf(stdout, "\ntest result is 1\n");
+    return 1;
+  }
+  if (hipSetDevice(gpu) != hipSuccess) return 1;
+  if (a.rank == 0) {
+    if (omr_dist_unique_id(uid) || !omrnet::send_all(fd, uid, sizeof(uid))) {
+      fprintf(stderr, "failed to create/send the RCCL id: %s\n", omr_dist_last_error());
+      return 1;
+    }
+  } else if (!omrnet::recv_all(fd, uid, sizeof(uid))) {
+    fprintf(stderr, "failed to receive the RCCL id\n");
+    return 1;
+  }
+  omr_dist* d = nullptr;
+  if (omr_dist_create_rccl(uid, a.rank, a.world, &d)) {
+    fprintf(stderr, "failed to connect: %s\n", omr_dist_last_error());
+    fprintf(stdout, "\ntest result is 1\n");
+    return 1;
+  }
+  std::cout << "Number of aggregators: " << a.world << "; Number of workers is " << a.world << "; My ID is "
+            << a.rank << std::endl;  // client.cc:364 (every GPU aggregates one shard)
+  printf("Connected.\n");
+  rc = run_worker(d, o, gpu, a.rank == 0);
+  omr_dist_destroy(d);
+  omrnet::Done done{omrnet::kMagic, a.rank, rc};
+  omrnet::send_all(fd, &done, sizeof(done));
+  ::close(fd);
+  fprintf(stdout, "\ntest result is %d\n", rc);
+  return rc;
+}

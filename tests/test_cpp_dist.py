@@ -1,0 +1,117 @@
+"""C++ host path (libomr_dist.so, ./omr_client, ./omr_server) on the GPU.
+
+The multi-rank round in C++ is checked against the oracle with the in-process loopback transport (several ranks
+as threads sharing one GPU), and the two CLI drivers are run end to end: loopback workers with the working
+CHECK (-c), and a server + one RCCL worker over the TCP rendezvous.  (RCCL refuses two ranks on one GPU, so the
+multi-rank RCCL leg runs on multi-GPU nodes only.)"""
+import ctypes
+import os
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from omr import Layout, _lib
+
+pytestmark = pytest.mark.gpu
+PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "omnireduce-rdma-demo_amd")
+BIN = os.path.join(PKG, "bin")
+
+
+def dist_lib():
+    _lib.load()
+    L = ctypes.CDLL(os.path.join(PKG, "omr", "libomr_dist.so"))
+    vp, u64, u32, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    L.omr_local_board_create.restype = vp
+    L.omr_local_board_create.argtypes = [i]
+    L.omr_local_board_destroy.argtypes = [vp]
+    L.omr_dist_create_local.argtypes = [vp, i, vp]
+    L.omr_dist_destroy.argtypes = [vp]
+    L.omr_ar_plan_create.argtypes = [vp, u64, u32, u32, u32, vp]
+    L.omr_ar_plan_destroy.argtypes = [vp]
+    L.omr_sparse_allreduce_f32.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.omr_dist_last_error.restype = ctypes.c_char_p
+    return L
+
+
+@pytest.mark.parametrize("world,B,density", [(2, 256, 0.095), (3, 1024, 0.0099), (4, 512, 0.49)])
+def test_cpp_round_loopback(gpu, world, B, density):
+    L = Layout(n=2 << 20, block_size=B)
+    D = dist_lib()
+    bufs = [oracle.fill(oracle.gen_bitmap(w, density, L.nb), B, mode=1, seed=w + 7) for w in range(world)]
+    uf = oracle.union_flags([oracle.flags_from_data(b, B) for b in bufs])
+    board = D.omr_local_board_create(world)
+    errs, results = [], [None] * world
+
+    def rank(r):
+        try:
+            torch.cuda.set_device(0)
+            x = torch.from_numpy(bufs[r].copy()).cuda()
+            out = x.clone()
+            flags = torch.empty(L.nb, dtype=torch.int32, device="cuda")
+            nxt = torch.empty(L.nb, dtype=torch.int32, device="cuda")
+            unext = torch.empty(L.nb, dtype=torch.int32, device="cuda")
+            d, plan = ctypes.c_void_p(), ctypes.c_void_p()
+            assert D.omr_dist_create_local(board, r, ctypes.byref(d)) == 0
+            assert D.omr_ar_plan_create(d, L.n, B, L.num_lanes, 8, ctypes.byref(plan)) == 0
+            st = torch.cuda.Stream()
+            for _ in range(2):
+                rc = D.omr_sparse_allreduce_f32(plan, x.data_ptr(), out.data_ptr(), flags.data_ptr(), nxt.data_ptr(),
+                                                unext.data_ptr(), None, None, st.cuda_stream)
+                assert rc == 0, D.omr_dist_last_error()
+            torch.cuda.synchronize()
+            results[r] = (out.cpu().numpy(), flags.cpu().numpy(), nxt.cpu().numpy().view(np.uint32),
+                          unext.cpu().numpy().view(np.uint32))
+            D.omr_ar_plan_destroy(plan)
+            D.omr_dist_destroy(d)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    D.omr_local_board_destroy(board)
+    assert not errs, errs
+    un = oracle.next_offsets(uf, L.n, B, L.num_lanes, 8)
+    for r in range(world):
+        exp = bufs[r].copy()
+        oracle.block_sum(bufs, L.n, B, L.num_lanes, 8, uf, exp)
+        out, fl, nx, unx = results[r]
+        assert (out.view(np.uint32) == exp.view(np.uint32)).all(), f"rank {r} sum"
+        f = oracle.flags_from_data(bufs[r], B)
+        assert (fl == f).all()
+        assert (nx == oracle.next_offsets(f, L.n, B, L.num_lanes, 8)).all()
+        assert (unx == un).all()
+
+
+def _run(cmd, timeout=300):
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    return p.returncode, p.stdout + p.stderr
+
+
+def test_client_loopback_cli(gpu):
+    rc, out = _run([os.path.join(BIN, "omr_client"), "-L", "3", "-n", str(4 << 20), "-r", "0.095", "-W", "2",
+                    "-R", "4", "-c"])
+    assert rc == 0, out
+    assert "check OK" in out and "average alg bw" in out and "test result is 0" in out
+
+
+def test_server_client_rccl_one_worker(gpu):
+    port = "19877"
+    srv = subprocess.Popen([os.path.join(BIN, "omr_server"), "-p", port, "127.0.0.1"], stdout=subprocess.PIPE,
+                           stderr=subprocess.STDOUT, text=True)
+    try:
+        rc, out = _run([os.path.join(BIN, "omr_client"), "-p", port, "-n", str(4 << 20), "-r", "0.095", "-W", "1",
+                        "-R", "3", "-c", "127.0.0.1"])
+        sout, _ = srv.communicate(timeout=60)
+    finally:
+        if srv.poll() is None:
+            srv.kill()
+    assert rc == 0, out
+    assert "check OK" in out and "My ID is 0" in out
+    assert srv.returncode == 0 and "test result is 0" in sout, sout
