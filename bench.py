@@ -54,6 +54,11 @@ def parse():
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
                    help="rocprofv3 PMC summary giving HBM traffic per launch (optional)")
     p.add_argument("--print-workload", action="store_true", help="print the workload string and exit")
+    p.add_argument("--force-dist", action="store_true",
+                   help="take the N>1 (distributed) code path even at WORLD_SIZE=1 (rehearsal under torchrun)")
+    p.add_argument("--dist-impl", choices=("cpp", "torch"), default="cpp",
+                   help="N>1 round driver: C++ (libomr_dist.so, RCCL from C++) or Python (omr.dist over "
+                        "torch.distributed); same protocol and kernels")
     return p.parse_args()
 
 
@@ -145,16 +150,17 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
 def main():
     args = parse()
     ws, rank, local = dist_env()
+    dist_mode = ws > 1 or args.force_dist
     if args.print_workload:
         print(workload_string(args, args.workers if ws == 1 else 1))
         return
     n_gpus = ws if ws > 1 else args.gpus
-    if ws > 1:
+    if dist_mode:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if ws > 1 else 0)
+    dev = torch.device("cuda", local if dist_mode else 0)
     L = Layout.from_bytes(args.size_mib << 20, args.block_size)
-    m = args.workers if ws == 1 else 1
+    m = args.workers if not dist_mode else 1
     workload = workload_string(args, m)
 
     # ---- inputs (reference generator, seed = worker id + 1: client.cc:396) -------------------------------
@@ -167,15 +173,19 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
-    if ws > 1:
-        from omr import dist
-        engine = dist.SparseAllreduce(L, device=dev)
+    if dist_mode:
+        if args.dist_impl == "cpp":
+            from omr import cdist
+            engine = cdist.CppSparseAllreduce(L, device=dev)
+        else:
+            from omr import dist
+            engine = dist.SparseAllreduce(L, device=dev)
         for xs, out in sets:  # out-of-place result buffers keep every step's input pristine
             out.copy_(xs[0])
 
         def step(i, ev=None):
             xs, out = sets[i % len(sets)]
-            engine.run(xs[0], out=out, ev=ev)
+            engine.run(xs[0], out=out, ev=None if args.dist_impl == "cpp" else ev)
     else:
         plan = ops.ScanSumPlan(L, m, device=dev)
 
@@ -193,7 +203,7 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    if ws > 1:
+    if dist_mode:
         torch.distributed.barrier()
     torch.cuda.synchronize()
 
@@ -203,34 +213,44 @@ def main():
     for i in range(args.steps):
         step(args.warmup + i, kev[i])
     torch.cuda.synchronize()
-    if ws > 1:
+    if dist_mode:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if ws > 1:
+    if dist_mode:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
 
     roofline = None
+    if dist_mode and args.dist_impl == "cpp":
+        # the C++ round is one call; time its worker-scan kernel in its own event-bracketed loop, same data
+        plan1 = ops.ScanSumPlan(L, 1, with_next=False, device=dev)
+        for i in range(min(args.steps, 50)):
+            xs, _ = sets[i % len(sets)]
+            kev[i][0].record(stream)
+            plan1.run(xs, None, with_next=False)
+            kev[i][1].record(stream)
+        torch.cuda.synchronize()
+        kev = kev[:min(args.steps, 50)]
     if True:
         kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
-        kbytes = algorithmic_scan_bytes(L, bitmaps, m) if ws == 1 else scan_only_bytes(L)
+        kbytes = algorithmic_scan_bytes(L, bitmaps, m) if not dist_mode else scan_only_bytes(L)
         achieved = kbytes / (kms * 1e-3) / 1e9
         traffic = read_pmc(args.pmc, workload)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "kernel": ("k_scan1" if m == 1 else "k_scanm") + ("" if ws == 1 else " (worker scan, no out)"),
+                    "kernel": ("k_scan1" if m == 1 else "k_scanm") + ("" if not dist_mode else " (worker scan, no out)"),
                     "kernel_ms": round(kms, 5),
                     "algorithmic_bytes_per_launch": kbytes}
-        if ws == 1:
+        if not dist_mode:
             sbytes = step_algorithmic_bytes(L, bitmaps, m)
             roofline["step_algorithmic_bytes"] = sbytes
             roofline["step_frac"] = round(sbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
 
     if rank != 0:
-        if ws > 1:
+        if dist_mode:
             torch.distributed.destroy_process_group()
         return
     total_bytes = n_gpus * m * L.nbytes
@@ -252,15 +272,16 @@ def main():
                    "num_lanes": L.num_lanes, "num_threads": L.num_threads, "density_r": args.density,
                    "nonzero_fraction": round(float(np.mean([bm.mean() for bm in bitmaps])), 5),
                    "workers_per_gpu": m, "rotating_buffer_sets": len(sets),
-                   "parallelism": "single GPU" if n_gpus == 1 else f"dp{n_gpus} sparse all-reduce (RCCL)"},
+                   "parallelism": "single GPU" if n_gpus == 1 else
+                   f"dp{n_gpus} sparse all-reduce over RCCL ({args.dist_impl} round driver)"},
         "alg_bw_GiBps_reference_style": round(total_bytes / (ms_per_step * 1e-3) / 2 ** 30, 2),
         "roofline": roofline,
         "cpu_baseline": None,
     }
-    if ws == 1 and not args.no_cpu:
+    if not dist_mode and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(L, bitmaps[0], args)
     print(json.dumps(line), flush=True)
-    if ws > 1:
+    if dist_mode:
         torch.distributed.destroy_process_group()
 
 

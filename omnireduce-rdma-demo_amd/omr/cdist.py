@@ -1,0 +1,106 @@
+"""ctypes binding of the C++ multi-rank round (include/omr_dist.h, libomr_dist.so).
+
+`CppSparseAllreduce` runs the same OmniReduce round as omr.dist.SparseAllreduce, but the whole round — kernels,
+block-count sync, RCCL all-gather and grouped send/recv — is driven from C++ (omr_dist.hip).  Python only
+bootstraps the RCCL communicator: rank 0's unique id is broadcast over the torch.distributed group the job was
+launched with (torch.distributed.run), standing in for the reference's TCP bootstrap.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .layout import Layout
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libomr_dist.so")
+UNIQUE_ID_BYTES = 128
+_dl = None
+
+
+def load():
+    global _dl
+    if _dl is not None:
+        return _dl
+    _lib.load()  # libomr.so first (libomr_dist.so links it), after torch's HIP/RCCL runtimes
+    if not os.path.exists(LIB_PATH):
+        raise _lib.OmrError(f"libomr_dist.so not found at {LIB_PATH}: build with `make -C omnireduce-rdma-demo_amd`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, u32, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "omr_dist_last_error": (ctypes.c_char_p, []),
+        "omr_dist_unique_id": (i, [vp]),
+        "omr_dist_create_rccl": (i, [vp, i, i, vp]),
+        "omr_local_board_create": (vp, [i]),
+        "omr_local_board_destroy": (None, [vp]),
+        "omr_dist_create_local": (i, [vp, i, vp]),
+        "omr_dist_rank": (i, [vp]),
+        "omr_dist_world": (i, [vp]),
+        "omr_dist_destroy": (i, [vp]),
+        "omr_ar_plan_create": (i, [vp, u64, u32, u32, u32, vp]),
+        "omr_ar_plan_destroy": (i, [vp]),
+        "omr_sparse_allreduce_f32": (i, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    _dl = L
+    return L
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise _lib.OmrError(f"{what} failed (rc={rc}): {load().omr_dist_last_error().decode(errors='replace')}")
+
+
+class CppSparseAllreduce:
+    """One rank of the C++ round over RCCL; the torch.distributed default group supplies rank/world and the
+    unique-id broadcast."""
+
+    def __init__(self, L: Layout, device, group=None):
+        D = load()
+        self.L = L
+        self.device = torch.device(device)
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = torch.zeros(UNIQUE_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            _check(D.omr_dist_unique_id(uid.data_ptr()), "omr_dist_unique_id")
+        bdev = self.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        t = uid.to(bdev)
+        dist.broadcast(t, 0, group=group)
+        uid.copy_(t.cpu())
+        self._d = ctypes.c_void_p()
+        _check(D.omr_dist_create_rccl(uid.data_ptr(), rank, world, ctypes.byref(self._d)), "omr_dist_create_rccl")
+        self._p = ctypes.c_void_p()
+        _check(D.omr_ar_plan_create(self._d, L.n, L.block_size, L.num_lanes, L.num_threads, ctypes.byref(self._p)),
+               "omr_ar_plan_create")
+        self.rank, self.world = rank, world
+
+    def run(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, ev=None, flags=None, next_offsets=None,
+            union_next=None):
+        out = x if out is None else out
+        sent, uni = ctypes.c_uint64(), ctypes.c_uint64()
+        st = torch.cuda.current_stream(self.device)
+        if ev is not None:  # the round starts with the worker scan kernel on this stream
+            ev[0].record(st)
+        ptr = (lambda t: t.data_ptr() if t is not None else None)
+        _check(load().omr_sparse_allreduce_f32(self._p, x.data_ptr(), out.data_ptr(), ptr(flags), ptr(next_offsets),
+                                               ptr(union_next), ctypes.byref(sent), ctypes.byref(uni),
+                                               st.cuda_stream), "omr_sparse_allreduce_f32")
+        if ev is not None:
+            ev[1].record(st)
+        return sent.value, uni.value
+
+    def close(self):
+        D = load()
+        if self._p:
+            D.omr_ar_plan_destroy(self._p)
+            self._p = ctypes.c_void_p()
+        if self._d:
+            D.omr_dist_destroy(self._d)
+            self._d = ctypes.c_void_p()
