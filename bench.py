@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
                    help="rocprofv3 PMC summary giving HBM traffic per launch (optional)")
     p.add_argument("--print-workload", action="store_true", help="print the workload string and exit")
+    p.add_argument("--kernel", choices=("fused", "twopass"), default="fused",
+                   help="N=1, m=1: single-pass k_scan1f (default) or k_scan1 + k_next")
     p.add_argument("--force-dist", action="store_true",
                    help="take the N>1 (distributed) code path even at WORLD_SIZE=1 (rehearsal under torchrun)")
     p.add_argument("--dist-impl", choices=("cpp", "torch"), default="cpp",
@@ -85,6 +87,15 @@ def algorithmic_scan_bytes(L: Layout, bitmaps, m: int) -> int:
     written = int(np.count_nonzero(union | heads))
     masks = (m if m == 1 else m + 1) * L.rows * 8
     return m * L.nbytes + written * B * 4 + m * nb * 4 + masks
+
+
+def fused_bytes(L: Layout, bm) -> int:
+    """k_scan1f per launch: read S, write the aggregated blocks (non-zero + lane heads), int32 flags and uint32
+    next offsets for every block (S + d*S + nb*8, plus the head blocks)."""
+    nb, B = L.nb, L.block_size
+    heads = ((np.arange(nb) // L.num_lanes) % L.rows_per_part) == 0
+    written = int(np.count_nonzero(bm.astype(bool) | heads))
+    return L.nbytes + written * B * 4 + nb * 8
 
 
 def scan_only_bytes(L: Layout) -> int:
@@ -187,7 +198,8 @@ def main():
             xs, out = sets[i % len(sets)]
             engine.run(xs[0], out=out, ev=None if args.dist_impl == "cpp" else ev)
     else:
-        plan = ops.ScanSumPlan(L, m, device=dev)
+        fused = m == 1 and args.kernel == "fused"
+        plan = ops.ScanSumPlan(L, m, device=dev, fused=fused)
 
         def step(i, ev=None):
             xs, out = sets[i % len(sets)]
@@ -195,10 +207,11 @@ def main():
                 out = xs[0]  # in place, as the reference returns results into res->buf (client.cc:89)
             if ev is not None:
                 ev[0].record(stream)
-            plan.run(xs, out, with_next=False)
+            plan.run(xs, out, with_next=fused)
             if ev is not None:
                 ev[1].record(stream)
-            plan.resolve_next()
+            if not fused:
+                plan.resolve_next()
 
     for i in range(args.warmup):
         step(i)
@@ -224,6 +237,10 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     roofline = None
+    kernel_name = ("k_scan1f (single pass: scan + sum + next)" if (m == 1 and args.kernel == "fused") else
+                   ("k_scan1" if m == 1 else "k_scanm"))
+    if dist_mode:
+        kernel_name = "k_scan1 (worker scan, no out)"
     if dist_mode and args.dist_impl == "cpp":
         # the C++ round is one call; time its worker-scan kernel in its own event-bracketed loop, same data
         plan1 = ops.ScanSumPlan(L, 1, with_next=False, device=dev)
@@ -236,12 +253,17 @@ def main():
         kev = kev[:min(args.steps, 50)]
     if True:
         kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
-        kbytes = algorithmic_scan_bytes(L, bitmaps, m) if not dist_mode else scan_only_bytes(L)
+        if dist_mode:
+            kbytes = scan_only_bytes(L)
+        elif m == 1 and args.kernel == "fused":
+            kbytes = fused_bytes(L, bitmaps[0])
+        else:
+            kbytes = algorithmic_scan_bytes(L, bitmaps, m)
         achieved = kbytes / (kms * 1e-3) / 1e9
         traffic = read_pmc(args.pmc, workload)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "kernel": ("k_scan1" if m == 1 else "k_scanm") + ("" if not dist_mode else " (worker scan, no out)"),
+                    "kernel": kernel_name,
                     "kernel_ms": round(kms, 5),
                     "algorithmic_bytes_per_launch": kbytes}
         if not dist_mode:

@@ -114,6 +114,17 @@ int omr_scan_sum_f32(const float* const* bufs, uint32_t m, uint64_t n, uint32_t 
                      uint32_t num_lanes, uint32_t num_parts, int32_t* flags, uint64_t* row_masks,
                      uint32_t* next_offsets, float* out, omr_stream_t stream);
 
+/* Single-pass m = 1 worker step (one launch): flags, next offsets AND the aggregated blocks, computed per
+ * (partition, lane) column so that every find_next_nonzero_block chain (client.cc:19-31) is resolved inside one
+ * workgroup.  Same outputs as omr_scan_sum_f32 with m = 1 (row masks are not produced).  When the layout has too
+ * few columns to fill the chip (e.g. B = 1024), columns are split into segments that meet through device
+ * atomics in `workspace`: omr_scan_workspace_bytes() bytes (0 = none needed), zero-filled once by the caller
+ * (e.g. hipMemset), left zeroed by every call; one workspace per concurrently running call. */
+size_t omr_scan_workspace_bytes(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts);
+int omr_scan_sum_fused_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes,
+                           uint32_t num_parts, int32_t* flags, uint32_t* next_offsets, float* out, void* workspace,
+                           size_t workspace_bytes, omr_stream_t stream);
+
 /* The m = 1 fused scan + aggregate over rows [row_begin, row_end) only (a pipelined piece of the tensor, e.g.
  * the part that has landed from host memory); `buf`, `out`, `flags`, `row_masks` are whole-tensor arrays indexed
  * by global block/row.  Next offsets need every row: run omr_next_offsets once all pieces are scanned. */

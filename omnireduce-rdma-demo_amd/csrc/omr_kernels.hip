@@ -75,6 +75,8 @@ __device__ __forceinline__ v4f add4(const v4f& a, const v4f& b) { return a + b; 
 
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
 
+constexpr uint32_t kNone = 0xFFFFFFFFu;  // "no row" marker
+
 constexpr int pow2floor(int x) {
   int r = 1;
   while (r * 2 <= x) r *= 2;
@@ -179,6 +181,177 @@ __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
     }
     if (a.flags != nullptr && lane < CH)
       a.flags[static_cast<uint64_t>(row) * a.lanes + l0 + lane] = static_cast<int32_t>((bits >> lane) & 1u);
+  }
+}
+
+// ---------------------------------------------------------------- k_scan1f: single-pass scan + sum + next
+//
+// One launch for the whole m = 1 worker step.  Work is split by COLUMN instead of by address: a workgroup owns
+// one lane l of one partition p (or a segment of its rows, when there are too few columns to fill the chip),
+// i.e. exactly the blocks one find_next_nonzero_block chain walks (client.cc:19-31).  Each wave streams batches
+// of 16 dwordx4 loads (16 rows of the column: 1 KiB each, 64 KiB apart — measured as fast as contiguous
+// chunks), ballots the flags, stores the aggregated non-zero blocks, and ORs the flag bits into the column's
+// bit vector in LDS.  Next offsets then need no other workgroup: every row's successor is a ctz over the LDS
+// bit vector (plus a suffix "next non-zero word" index).  With K > 1 segments per column, each segment
+// publishes {first, last} non-zero row through device-scope atomics; the segment whose arrival count completes
+// the column fills in the rows whose successor lies in a later segment (tail rows).  Workgroup -> (p, l, k) is
+// permuted so that one partition's columns share an XCD, letting the L2 merge their 4-byte flag/next stores
+// into whole lines (speed only, never correctness).
+struct FusedArgs {
+  const float* x;
+  float* out;
+  int32_t* flags;
+  uint32_t* next;
+  uint32_t* cnt;       // [parts*lanes] arrival counters (K > 1), zero between launches
+  uint64_t* summary;   // [parts*lanes*K] {first << 32 | last} per segment (K > 1)
+  uint32_t lanes, rpp, K, S, block, sentinel, nwords;
+};
+
+template <int VEC, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
+  constexpr int RB = 16 / VEC;  // rows per batch = 16 dwordx4 loads per lane
+  extern __shared__ uint64_t s_words[];                                  // column bits, row i -> word i/64
+  uint32_t* s_nw = reinterpret_cast<uint32_t*>(s_words + a.nwords);      // first non-zero word >= w
+  __shared__ uint32_t s_first, s_last;
+  __shared__ int s_fix;
+  __shared__ uint32_t s_carry[64];
+  __shared__ uint32_t s_seg_last[64];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t k = lin % a.K, col = lin / a.K;
+  const uint32_t l = col % a.lanes, p = col / a.lanes;
+  const uint32_t r0 = k * a.S;                                  // segment's first row within the partition
+  const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;  // its global row
+  for (uint32_t w = threadIdx.x; w < a.nwords; w += blockDim.x) s_words[w] = 0;
+  if (threadIdx.x == 0) {
+    s_first = kNone;
+    s_last = 0;
+  }
+  __syncthreads();
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  for (uint32_t j = wave; j * RB < a.S; j += WAVES) {
+    const uint32_t rr = j * RB;
+    const uint32_t nrow = (a.S - rr < static_cast<uint32_t>(RB)) ? a.S - rr : RB;
+    const uint64_t blk0 = (row0 + rr) * a.lanes + l;  // block of the batch's first row
+    const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, nrow * row_bytes);
+    v4f v[RB][VEC];
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                              src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
+    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + blk0 * a.block, a.out != nullptr ? nrow * row_bytes : 0u);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
+      const bool nz = wave_ballot(o != 0) != 0 && static_cast<uint32_t>(s) < nrow;
+      bits |= static_cast<uint32_t>(nz) << s;
+      const bool head = (r0 + rr + s) == 0;  // lane head: row 0 of the partition, always sent (client.cc:201-205)
+      if (a.out != nullptr && (nz || (head && static_cast<uint32_t>(s) < nrow))) {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
+                                                 dst, s * row_bytes + (q * 64 + lane) * 16, 0, kStoreAux);
+      }
+    }
+    if (a.flags != nullptr && static_cast<uint32_t>(lane) < nrow)
+      a.flags[blk0 + static_cast<uint64_t>(lane) * a.lanes] = static_cast<int32_t>((bits >> lane) & 1u);
+    if (lane == 0 && bits != 0) atomicOr(reinterpret_cast<unsigned long long*>(&s_words[rr / 64]),
+                                         static_cast<unsigned long long>(bits) << (rr % 64));
+  }
+  __syncthreads();
+  // suffix index of the first non-zero word (log-step min scan; nwords <= blockDim by launch construction)
+  const uint32_t w = threadIdx.x;
+  uint32_t nwv = (w < a.nwords && s_words[w] != 0) ? w : kNone;
+  if (w < a.nwords) {
+    s_nw[w] = nwv;
+    if (s_words[w] != 0) {
+      atomicMin(&s_first, w * 64 + static_cast<uint32_t>(__builtin_ctzll(s_words[w])));
+      atomicMax(&s_last, w * 64 + 63 - static_cast<uint32_t>(__builtin_clzll(s_words[w])));
+    }
+  }
+  if (w == 0) s_nw[a.nwords] = kNone;
+  __syncthreads();
+  for (uint32_t off = 1; off < a.nwords; off <<= 1) {
+    const uint32_t other = (w + off < a.nwords) ? s_nw[w + off] : kNone;
+    __syncthreads();
+    if (w < a.nwords && other < nwv) {
+      nwv = other;
+      s_nw[w] = nwv;
+    }
+    __syncthreads();
+  }
+  // next offsets of the segment's rows (client.cc:19-31: first non-zero block after row i in lane l)
+  const uint32_t lane_b = l * a.block;
+  const uint32_t row_stride = a.lanes * a.block;
+  const bool last_seg = (k + 1 == a.K);
+  for (uint32_t i = threadIdx.x; i < a.S; i += blockDim.x) {
+    const uint32_t j = i + 1;
+    uint32_t nr = kNone;
+    if (j < a.S) {
+      const uint64_t m = s_words[j / 64] >> (j % 64);
+      if (m != 0) {
+        nr = j + static_cast<uint32_t>(__builtin_ctzll(m));
+      } else if (j / 64 + 1 < a.nwords) {
+        const uint32_t w2 = s_nw[j / 64 + 1];
+        if (w2 != kNone) nr = w2 * 64 + static_cast<uint32_t>(__builtin_ctzll(s_words[w2]));
+      }
+    }
+    uint32_t val;
+    if (nr != kNone) {
+      val = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+    } else if (last_seg) {
+      val = a.sentinel + lane_b;
+    } else {
+      continue;  // successor in a later segment: written by the column's finishing segment below
+    }
+    a.next[(row0 + i) * a.lanes + l] = val;
+  }
+  if (a.K == 1) return;
+  // multi-segment column: publish {first, last}, count arrivals; the last arriver fixes every tail row
+  if (threadIdx.x == 0) {
+    const uint64_t sm = (static_cast<uint64_t>(s_first) << 32) | (s_first == kNone ? kNone : s_last);
+    (void)__hip_atomic_exchange(&a.summary[static_cast<uint64_t>(col) * a.K + k], sm, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&a.cnt[col], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_fix = (old == a.K - 1);
+  }
+  __syncthreads();
+  if (!s_fix) return;
+  if (threadIdx.x < a.K) {  // read every segment's summary at the coherence point (atomic RMW), K <= 64
+    const uint64_t sm = __hip_atomic_fetch_or(&a.summary[static_cast<uint64_t>(col) * a.K + threadIdx.x], 0ull,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_carry[threadIdx.x] = static_cast<uint32_t>(sm >> 32);  // first (temporarily)
+    s_seg_last[threadIdx.x] = static_cast<uint32_t>(sm);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // carry[k'] = first non-zero row (partition-relative) in segments after k'
+    uint32_t c = kNone;
+    for (int kk = static_cast<int>(a.K) - 1; kk >= 0; --kk) {
+      const uint32_t first = s_carry[kk];
+      s_carry[kk] = c;
+      if (first != kNone) c = static_cast<uint32_t>(kk) * a.S + first;
+    }
+    __hip_atomic_store(&a.cnt[col], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+  }
+  __syncthreads();
+  const uint64_t part_row0 = static_cast<uint64_t>(p) * a.rpp;
+  const uint32_t tail_total = (a.K - 1) * a.S;
+  for (uint32_t t = threadIdx.x; t < tail_total; t += blockDim.x) {
+    const uint32_t kk = t / a.S, i = t % a.S;
+    const uint32_t last = s_seg_last[kk];  // kNone when the segment is all zero
+    if (last != kNone && i < last) continue;  // a later non-zero row of its own segment follows: done locally
+    const uint32_t c = s_carry[kk];
+    const uint32_t val = (c != kNone) ? static_cast<uint32_t>(part_row0 + c) * row_stride + lane_b
+                                      : a.sentinel + lane_b;
+    a.next[(part_row0 + static_cast<uint64_t>(kk) * a.S + i) * a.lanes + l] = val;
   }
 }
 
@@ -298,8 +471,6 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t a, int lane) {
   }
   return a;
 }
-
-constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 __global__ __launch_bounds__(kWGThreads) void k_next(NextArgs a) {
   __shared__ uint64_t s_col[64];
@@ -670,6 +841,64 @@ int launch_next(const Layout& L, const uint64_t* masks, uint32_t count, uint32_t
 #endif
 constexpr bool kNT = OMR_SCAN_NT != 0;
 
+// Column split of the single-pass kernel: K segments per (partition, lane) column, enough workgroups to give
+// every CU two (>= 512), each segment a whole number of 64-row LDS words that fits one bit-index scan.
+constexpr int kFusedWaves = 8;
+struct FusedShape {
+  uint32_t K = 0, S = 0, nwords = 0;
+};
+
+FusedShape fused_shape(const Layout& L) {
+  FusedShape f;
+  const uint64_t cols = static_cast<uint64_t>(L.parts) * L.lanes;
+  uint32_t K = 1;
+  while (cols * K < 512 && L.rows_per_part % (2 * K) == 0 && L.rows_per_part / (2 * K) >= 64 && 2 * K <= 64) K *= 2;
+  while ((L.rows_per_part / K + 63) / 64 > 64u * kFusedWaves && L.rows_per_part % (2 * K) == 0 && 2 * K <= 64)
+    K *= 2;
+  const uint32_t S = L.rows_per_part / K;
+  const uint32_t nwords = (S + 63) / 64;
+  if (L.rows_per_part % K != 0 || nwords > 64u * kFusedWaves) return f;  // not representable: K = 0
+  f.K = K;
+  f.S = S;
+  f.nwords = nwords;
+  return f;
+}
+
+size_t fused_workspace_bytes(const Layout& L, const FusedShape& f) {
+  if (f.K <= 1) return 0;
+  const uint64_t cols = static_cast<uint64_t>(L.parts) * L.lanes;
+  return cols * sizeof(uint32_t) + cols * f.K * sizeof(uint64_t) + 16;
+}
+
+int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* out, int32_t* flags, uint32_t* next,
+                 void* ws, hipStream_t st) {
+  FusedArgs a;
+  a.x = x;
+  a.out = out;
+  a.flags = flags;
+  a.next = next;
+  const uint64_t cols = static_cast<uint64_t>(L.parts) * L.lanes;
+  a.cnt = static_cast<uint32_t*>(ws);
+  a.summary = ws ? reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + ((cols * sizeof(uint32_t) + 15) / 16) * 16)
+                 : nullptr;
+  a.lanes = L.lanes;
+  a.rpp = L.rows_per_part;
+  a.K = f.K;
+  a.S = f.S;
+  a.block = L.block;
+  a.sentinel = omr_sentinel(L.block, L.lanes);
+  a.nwords = f.nwords;
+  const unsigned grid = static_cast<unsigned>(cols * f.K);
+  const size_t lds = f.nwords * sizeof(uint64_t) + (f.nwords + 1) * sizeof(uint32_t);
+  constexpr int T = 64 * kFusedWaves;
+  switch (L.vec) {
+    case 1: k_scan1f<1, kFusedWaves><<<grid, T, lds, st>>>(a); break;
+    case 2: k_scan1f<2, kFusedWaves><<<grid, T, lds, st>>>(a); break;
+    default: k_scan1f<4, kFusedWaves><<<grid, T, lds, st>>>(a); break;
+  }
+  return launch_status("k_scan1f");
+}
+
 unsigned scan_grid(uint64_t chunks) {
   uint64_t g = (chunks + kScanWaves - 1) / kScanWaves;
   if (g > kMaxGrid) g = kMaxGrid;
@@ -833,6 +1062,28 @@ int omr_scan_sum_rows_f32(const float* buf, uint64_t n, uint32_t block_size, uin
   a.masks = row_masks;
   a.out = out;
   return launch_scan(L, a, S(stream));
+}
+
+size_t omr_scan_workspace_bytes(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts) {
+  Layout L;
+  if (make_layout(n, block_size, num_lanes, num_parts, &L)) return 0;
+  return fused_workspace_bytes(L, fused_shape(L));
+}
+
+int omr_scan_sum_fused_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes,
+                           uint32_t num_parts, int32_t* flags, uint32_t* next_offsets, float* out, void* workspace,
+                           size_t workspace_bytes, omr_stream_t stream) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  if (buf == nullptr || next_offsets == nullptr) return fail("scan_sum_fused: buf and next_offsets are required");
+  if (reinterpret_cast<uintptr_t>(buf) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 16 != 0)
+    return fail("scan_sum_fused: buffers must be 16-byte aligned");
+  const FusedShape f = fused_shape(L);
+  if (f.K == 0) return fail("scan_sum_fused: rows_per_part=%u has no supported column split", L.rows_per_part);
+  const size_t need = fused_workspace_bytes(L, f);
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need))
+    return fail("scan_sum_fused: needs a zero-initialised workspace of %zu bytes", need);
+  return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream));
 }
 
 int omr_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,

@@ -194,6 +194,44 @@ __global__ __launch_bounds__(64 * WPG) void t_chunk_pol(TArgs a) {
   }
 }
 
+
+// column mapping probe: a wave owns CH consecutive rows of ONE lane of one partition (CH blocks at a 64 KiB
+// stride instead of CH consecutive blocks).  Flags only (no row masks): a bandwidth probe for a column-major
+// work split in which next offsets would be wave-local.
+template <int CH, int WPG, int SAUX>
+__global__ __launch_bounds__(64 * WPG) void t_col(TArgs a) {
+  constexpr int B4 = 64;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * WPG;
+  const uint32_t segs = a.rows / CH;              // column segments per lane (all partitions)
+  const uint32_t units = segs * a.lanes;
+  for (uint32_t u = blockIdx.x * WPG + wave; u < units; u += nwaves) {
+    const uint32_t l = u % a.lanes, seg = u / a.lanes;
+    const uint32_t r0 = seg * CH;
+    v4f v[CH];
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const uint64_t blk = static_cast<uint64_t>(r0 + s) * a.lanes + l;
+      v[s] = ld4<true>(reinterpret_cast<const v4f*>(a.x) + blk * B4 + lane);
+    }
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < CH; ++s) {
+      const uint64_t blk = static_cast<uint64_t>(r0 + s) * a.lanes + l;
+      const bool nz = __ballot(nz_bits(v[s]) != 0) != 0;
+      bits |= static_cast<uint32_t>(nz) << s;
+      const bool head = ((r0 + s) % a.rows_per_part) == 0;
+      if (nz || head) {
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.out + blk * 256, 0, 1024, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v4f{0.f, 0.f, 0.f, 0.f} + v[s]), rs,
+                                               lane * 16, 0, SAUX);
+      }
+    }
+    if (lane < CH) a.flags[static_cast<uint64_t>(r0 + lane) * a.lanes + l] = static_cast<int32_t>((bits >> lane) & 1u);
+  }
+}
+
 // pure streaming read (OR-reduce, one store per wave) and float4 copy: the HBM ceilings on this box
 template <bool NT, int LOADS>
 __global__ __launch_bounds__(256) void t_read(const float* x, uint64_t n4, uint32_t* sink) {
@@ -229,7 +267,7 @@ static void launch(const TArgs& a, unsigned grid, hipStream_t st) {
 extern "C" {
 
 // variant ids -> (NT, LOADS, WPG, NTS, MAP); grid = min(cap, work/WPG)
-int tune_num_variants() { return 28; }
+int tune_num_variants() { return 31; }
 
 const char* tune_variant_name(int v) {
   static const char* names[] = {
@@ -238,8 +276,9 @@ const char* tune_variant_name(int v) {
       "c16 w8",            "c16 w16",          "c32 w8",           "c16 w8 pipe",      "c16 w4 pipe",
       "c32 w4",            "c16 w8 nostore",   "c16 w4 nostore",   "c16 w8 sc1st",     "c16 w8 ntst",
       "c16 w8 sc0sc1st",   "st19 sc01nt",     "st18 sc1nt",       "st1 sc0",          "st3 sc0nt",
-      "st17 ld2buf",       "st17 ld0buf",     "st17 ld3buf"};
-  return (v >= 0 && v < 28) ? names[v] : "?";
+      "st17 ld2buf",       "st17 ld0buf",     "st17 ld3buf",      "col16 w8",         "col16 w16",
+      "col32 w8"};
+  return (v >= 0 && v < 31) ? names[v] : "?";
 }
 
 int tune_scan(int v, const float* x, float* out, int32_t* flags, uint64_t* masks, uint64_t rows, uint32_t lanes,
@@ -281,6 +320,9 @@ int tune_scan(int v, const float* x, float* out, int32_t* flags, uint64_t* masks
     case 25: t_chunk_pol<8, 17, 2><<<grid(chunks, 8), 512, 0, st>>>(a); break;
     case 26: t_chunk_pol<8, 17, 0><<<grid(chunks, 8), 512, 0, st>>>(a); break;
     case 27: t_chunk_pol<8, 17, 3><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 28: t_col<16, 8, 17><<<grid(chunks, 8), 512, 0, st>>>(a); break;
+    case 29: t_col<16, 16, 17><<<grid(chunks, 16), 1024, 0, st>>>(a); break;
+    case 30: t_col<32, 8, 17><<<grid(chunks / 2, 8), 512, 0, st>>>(a); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;

@@ -94,17 +94,24 @@ class ScanSumPlan:
     """
 
     def __init__(self, layout: Layout, m: int = 1, with_flags: bool = True, with_next: bool = True,
-                 device="cuda"):
+                 device="cuda", fused: bool = False):
+        """fused=True (m = 1 only): one single-pass launch (omr_scan_sum_fused_f32) producing flags, next
+        offsets and the aggregated blocks; no row masks."""
         if not 1 <= m <= _lib.OMR_MAX_WORKERS:
             raise ValueError(f"m={m} out of range")
-        _lib.check(_lib.load().omr_layout_check(layout.n, layout.block_size, layout.num_lanes,
-                                                layout.num_threads), "omr_layout_check")
-        self.layout, self.m = layout, m
+        lib = _lib.load()
+        _lib.check(lib.omr_layout_check(layout.n, layout.block_size, layout.num_lanes, layout.num_threads),
+                   "omr_layout_check")
+        if fused and (m != 1 or not with_next):
+            raise ValueError("the fused single-pass kernel is the m = 1 step with next offsets")
+        self.layout, self.m, self.fused = layout, m, fused
         arrays = m if m == 1 else m + 1
         self.flags = torch.empty((m, layout.nb), dtype=torch.int32, device=device) if with_flags else None
-        self.masks = torch.empty((arrays, layout.rows), dtype=torch.int64, device=device)
+        self.masks = None if fused else torch.empty((arrays, layout.rows), dtype=torch.int64, device=device)
         self.next_offsets = (torch.empty((arrays, layout.nb), dtype=torch.int32, device=device)
                              if with_next else None)
+        ws = lib.omr_scan_workspace_bytes(layout.n, layout.block_size, layout.num_lanes, layout.num_threads)
+        self.workspace = torch.zeros(max(ws, 16), dtype=torch.uint8, device=device) if fused else None
 
     def run(self, bufs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None, stream=None,
             with_next: bool = True) -> ScanResult:
@@ -116,6 +123,12 @@ class ScanSumPlan:
             _check_f32(b, L.n, f"bufs[{i}]")
         if out is not None:
             _check_f32(out, L.n, "out")
+        if self.fused:
+            _lib.check(_lib.load().omr_scan_sum_fused_f32(
+                _ptr(bufs[0]), L.n, L.block_size, L.num_lanes, L.num_threads, _ptr(self.flags),
+                _ptr(self.next_offsets), _ptr(out), _ptr(self.workspace), self.workspace.numel(), _stream(stream)),
+                "omr_scan_sum_fused_f32")
+            return ScanResult(self.flags, self.masks, self.next_offsets, out)
         arr = _ptr_array(bufs)
         nxt = self.next_offsets if with_next else None
         _lib.check(_lib.load().omr_scan_sum_f32(arr, self.m, L.n, L.block_size, L.num_lanes, L.num_threads,

@@ -248,3 +248,69 @@ def test_host_resident_pipeline(gpu, chunk_rows):
     assert (flags.numpy() == f).all()
     assert (nxt.numpy().view(np.uint32) == oracle.next_offsets(f, L.n, 256, 64, 8)).all()
     assert (host.numpy().view(np.uint32) == exp.view(np.uint32)).all()
+
+
+# ------------------------------------------------------------------ single-pass fused kernel (k_scan1f)
+
+def assert_fused_parity(x, L, out_init=None, reps=2):
+    """Fused single launch vs the oracle; run twice so the self-resetting segment counters are exercised."""
+    dev = torch.device("cuda:0")
+    xd = torch.from_numpy(x).to(dev)
+    plan = ops.ScanSumPlan(L, 1, device=dev, fused=True)
+    for _ in range(reps):
+        out = torch.from_numpy(out_init.copy()).to(dev) if out_init is not None else torch.zeros(L.n, device=dev)
+        res = plan.run([xd], out)
+        torch.cuda.synchronize()
+        f = oracle.flags_from_data(x, L.block_size)
+        assert (res.flags[0].cpu().numpy() == f).all(), "flags"
+        assert (u32(res.next_offsets[0]) == oracle.next_offsets(f, L.n, L.block_size, L.num_lanes,
+                                                                L.num_threads)).all(), "next"
+        exp = np.zeros(L.n, dtype=np.float32) if out_init is None else out_init.copy()
+        oracle.block_sum([x], L.n, L.block_size, L.num_lanes, L.num_threads, f, exp)
+        assert (out.cpu().numpy().view(np.uint32) == exp.view(np.uint32)).all(), "sum"
+    ncols = L.num_threads * L.num_lanes  # the arrival counters lead the workspace; summaries are overwritten
+    assert int(plan.workspace[: 4 * ncols].count_nonzero()) == 0, "segment counters must be left zeroed"
+
+
+@pytest.mark.parametrize("n,B,parts,density", [
+    (1 << 20, 256, 8, 0.3),        # config 1 layout: 8 rows per partition, K = 1
+    (4 << 20, 256, 8, 0.095),      # K = 1, S = 32
+    (16 << 20, 256, 8, 0.01),      # K = 1, S = 128 (two LDS words)
+    (16 << 20, 1024, 8, 0.0099),   # 128 columns -> K = 2 segments
+    (64 << 20, 1024, 8, 0.0099),   # K = 4 (config 3 split)
+    (16 << 20, 1024, 1, 0.0005),   # one partition, 16 columns -> K = 16, long empty stretches
+    (8 << 20, 512, 8, 0.49),       # B = 512
+    (4 << 20, 256, 8, 0.0),        # all zero: every chain is the sentinel
+    (4 << 20, 256, 8, 1.0),        # dense
+])
+def test_fused_parity(gpu, n, B, parts, density):
+    L = Layout(n=n, block_size=B, num_threads=parts)
+    x = oracle.fill(oracle.gen_bitmap(3, density, L.nb), B, mode=1, seed=5)
+    assert_fused_parity(x, L)
+
+
+def test_fused_edge_values(gpu):
+    L = Layout(n=1 << 20)
+    x = np.zeros(L.n, dtype=np.float32)
+    B = L.block_size
+    x[0:B] = -0.0
+    x[64 * B + 9] = np.nan
+    x[200 * B + 255] = np.float32(1e-45)
+    x[L.n - 1] = -3.0
+    assert_fused_parity(x, L, out_init=np.full(L.n, -0.0, dtype=np.float32))
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("nbytes,B,r", [(256 << 20, 256, 0.095), (1 << 30, 1024, 0.0099)])
+def test_fused_full_size(gpu, nbytes, B, r):
+    L = Layout.from_bytes(nbytes, B)
+    bm = ops.gen_bitmap(0, r, L.nb)
+    x = ops.fill_blocks(torch.from_numpy(bm).to(gpu), L, mode=1, seed=1)
+    ref = x.clone()
+    plan = ops.ScanSumPlan(L, 1, device=gpu, fused=True)
+    for _ in range(3):
+        res = plan.run([x], x)  # in place, as the bench runs it
+    torch.cuda.synchronize()
+    assert (res.flags[0].cpu().numpy() == bm).all()
+    assert (u32(res.next_offsets[0]) == oracle.next_offsets(bm, L.n, B, L.num_lanes, 8)).all()
+    assert torch.equal(x, ref)  # 0.0f + x == x for these values: the in-place result is the input
