@@ -207,9 +207,9 @@ struct FusedArgs {
   uint32_t lanes, rpp, K, S, block, sentinel, nwords;
 };
 
-template <int VEC, int WAVES>
+template <int VEC, int WAVES, int LOADS = 16, bool XCD_MAP = true>
 __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
-  constexpr int RB = 16 / VEC;  // rows per batch = 16 dwordx4 loads per lane
+  constexpr int RB = LOADS / VEC;  // rows per batch: LOADS dwordx4 loads per lane in flight
   extern __shared__ uint64_t s_words[];                                  // column bits, row i -> word i/64
   uint32_t* s_nw = reinterpret_cast<uint32_t*>(s_words + a.nwords);      // first non-zero word >= w
   __shared__ uint32_t s_first, s_last;
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t T = gridDim.x, bid = blockIdx.x;
-  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t lin = (XCD_MAP && T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
   const uint32_t k = lin % a.K, col = lin / a.K;
   const uint32_t l = col % a.lanes, p = col / a.lanes;
   const uint32_t r0 = k * a.S;                                  // segment's first row within the partition
@@ -842,7 +842,8 @@ int launch_next(const Layout& L, const uint64_t* masks, uint32_t count, uint32_t
 constexpr bool kNT = OMR_SCAN_NT != 0;
 
 // Column split of the single-pass kernel: K segments per (partition, lane) column, enough workgroups to give
-// every CU two (>= 512), each segment a whole number of 64-row LDS words that fits one bit-index scan.
+// every CU one (>= 256: tools/tune_fused.py measured K = 1 best at 512 columns (B=256) and K = 2 best at 128
+// columns (B=1024)), each segment small enough for one LDS bit-index scan.
 constexpr int kFusedWaves = 8;
 struct FusedShape {
   uint32_t K = 0, S = 0, nwords = 0;
@@ -852,7 +853,7 @@ FusedShape fused_shape(const Layout& L) {
   FusedShape f;
   const uint64_t cols = static_cast<uint64_t>(L.parts) * L.lanes;
   uint32_t K = 1;
-  while (cols * K < 512 && L.rows_per_part % (2 * K) == 0 && L.rows_per_part / (2 * K) >= 64 && 2 * K <= 64) K *= 2;
+  while (cols * K < 256 && L.rows_per_part % (2 * K) == 0 && L.rows_per_part / (2 * K) >= 64 && 2 * K <= 64) K *= 2;
   while ((L.rows_per_part / K + 63) / 64 > 64u * kFusedWaves && L.rows_per_part % (2 * K) == 0 && 2 * K <= 64)
     K *= 2;
   const uint32_t S = L.rows_per_part / K;
@@ -928,6 +929,7 @@ int launch_scan(const Layout& L, const ScanArgs& a, hipStream_t st) {
 }  // namespace
 
 // ================================================================ C ABI
+#ifndef OMR_NO_CAPI
 
 extern "C" {
 
@@ -1251,3 +1253,5 @@ int omr_scatter_blocks_f32(const float* packed, const uint32_t* block_list, uint
 }
 
 }  // extern "C"
+#endif  // OMR_NO_CAPI
+

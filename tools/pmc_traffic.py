@@ -50,7 +50,7 @@ def per_launch(csv_path, kernel, counter):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="k_scan1")
+    ap.add_argument("--kernel", default="k_scan1f")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc_r01.json"))
     ap.add_argument("--workdir", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
