@@ -60,6 +60,9 @@ def parse():
                    help="N=1, m=1: single-pass k_scan1f (default) or k_scan1 + k_next")
     p.add_argument("--force-dist", action="store_true",
                    help="take the N>1 (distributed) code path even at WORLD_SIZE=1 (rehearsal under torchrun)")
+    p.add_argument("--dist-mode", choices=("reduce", "allreduce"), default="reduce",
+                   help="N>1 step: workers -> aggregators reduce-scatter (BASELINE config 4, default) or the full "
+                        "all-reduce (sums back to every worker)")
     p.add_argument("--dist-impl", choices=("cpp", "torch"), default="cpp",
                    help="N>1 round driver: C++ (libomr_dist.so, RCCL from C++) or Python (omr.dist over "
                         "torch.distributed); same protocol and kernels")
@@ -199,7 +202,8 @@ def main():
 
         def step(i, ev=None):
             xs, out = sets[i % len(sets)]
-            engine.run(xs[0], out=out, ev=None if args.dist_impl == "cpp" else ev)
+            engine.run(xs[0], out=out, ev=None if args.dist_impl == "cpp" else ev,
+                       mode=0 if args.dist_mode == "allreduce" else 1)
     else:
         fused = m == 1 and args.kernel == "fused"
         plan = ops.ScanSumPlan(L, m, device=dev, fused=fused)
@@ -301,7 +305,8 @@ def main():
                    "nonzero_fraction": round(float(np.mean([bm.mean() for bm in bitmaps])), 5),
                    "workers_per_gpu": m, "rotating_buffer_sets": len(sets),
                    "parallelism": "single GPU" if n_gpus == 1 else
-                   f"dp{n_gpus} sparse all-reduce over RCCL ({args.dist_impl} round driver)"},
+                   f"dp{n_gpus} sparse {'all-reduce' if args.dist_mode == 'allreduce' else 'reduce-scatter'} over "
+                   f"RCCL ({args.dist_impl} round driver)"},
         "alg_bw_GiBps_reference_style": round(total_bytes / (ms_per_step * 1e-3) / 2 ** 30, 2),
         "roofline": roofline,
         "cpu_baseline": None,

@@ -64,6 +64,17 @@ int omr_sparse_allreduce_f32(omr_ar_plan* plan, const float* x, float* out, int3
                              uint32_t* next_offsets, uint32_t* union_next, uint64_t* sent_blocks,
                              uint64_t* union_blocks, omr_stream_t stream);
 
+/* The round with a choice of how far it goes:
+ *   OMR_ROUND_ALLREDUCE       as omr_sparse_allreduce_f32 (workers get every shard's sums back);
+ *   OMR_ROUND_REDUCE_SCATTER  stops at the aggregators: `out` receives only this rank's shard sums (its part of
+ *                             the write set, in place) — the worker -> aggregator "reduce" of BASELINE config 4;
+ *                             *union_blocks = this shard's write-set size. */
+#define OMR_ROUND_ALLREDUCE 0
+#define OMR_ROUND_REDUCE_SCATTER 1
+int omr_sparse_round_f32(omr_ar_plan* plan, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
+                         uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
+                         omr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -242,7 +242,7 @@ int omr_dist_destroy(omr_dist* d) {
 int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p == nullptr) return 0;
   void* devs[] = {p->masks_all, p->umask,    p->prefix,    p->my_list,    p->full_list,  p->shard_list,
-                  p->count,     p->packed,   p->recv,      p->recv_off,   p->sums,       p->results,
+                  p->count,     p->packed,   p->recv_off,  p->sums,       p->results,
                   p->flags_ws,  p->next_ws,  p->unext_ws,  p->bounds_dev, p->counts_dev, p->prefix_ws,
                   p->compact_ws};
   for (void* v : devs) (void)hipFree(v);
@@ -284,8 +284,10 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   A(dev_alloc(&p->full_list, p->nb));
   A(dev_alloc(&p->shard_list, p->shard_nb));
   A(dev_alloc(&p->count, 3));
-  A(dev_alloc(&p->packed, n));
-  A(dev_alloc(&p->recv, static_cast<size_t>(N) * p->shard_nb * block_size));
+  // one allocation: packed own blocks, then the peers' streams, so the shard sum addresses the rank's own
+  // contribution in place (no copy into the receive area)
+  A(dev_alloc(&p->packed, n + static_cast<size_t>(N) * p->shard_nb * block_size));
+  if (rc == 0) p->recv = p->packed + n;
   A(dev_alloc(&p->recv_off, N));
   A(dev_alloc(&p->sums, p->shard_nb * block_size));
   A(dev_alloc(&p->results, n));
@@ -312,10 +314,12 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   return 0;
 }
 
-int omr_sparse_allreduce_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
-                             uint32_t* union_next, uint64_t* sent_blocks, uint64_t* union_blocks,
-                             omr_stream_t stream) {
-  if (p == nullptr || x == nullptr || out == nullptr) return derr(OMR_EINVAL, "sparse_allreduce: NULL");
+int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
+                         uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
+                         omr_stream_t stream) {
+  if (p == nullptr || x == nullptr || out == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL");
+  if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER)
+    return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int N = p->N, me = p->me;
   const uint64_t rows = p->rows, B = p->B;
@@ -350,21 +354,20 @@ int omr_sparse_allreduce_f32(omr_ar_plan* p, const float* x, float* out, int32_t
                             stream), "omr_compact"));
   TRY(omr_check(omr_gather_blocks_f32(x, p->my_list, static_cast<uint32_t>(total_send), p->B, p->packed, stream),
                 "omr_gather_blocks_f32"));
+  // stream offsets (in blocks) from p->packed: peers' streams in the receive area, this rank's own slice
+  // where the gather left it
   std::vector<uint64_t> roff(N);
   uint64_t acc = 0;
   for (int w = 0; w < N; ++w) {
     roff[w] = acc;
-    acc += per(w, me);
-    p->recv_off_host[w] = roff[w];
+    if (w != me) acc += per(w, me);
+    p->recv_off_host[w] = (w == me) ? cnt(me, me) : p->n / p->B + roff[w];
   }
   std::vector<Slice> sends(N), recvs(N);
   for (int s = 0; s < N; ++s) {
-    sends[s] = Slice{p->packed + cnt(me, s) * B, per(me, s) * B * sizeof(float)};
-    recvs[s] = Slice{p->recv + roff[s] * B, per(s, me) * B * sizeof(float)};
+    sends[s] = Slice{p->packed + cnt(me, s) * B, s == me ? 0 : per(me, s) * B * sizeof(float)};
+    recvs[s] = Slice{p->recv + roff[s] * B, s == me ? 0 : per(s, me) * B * sizeof(float)};
   }
-  if (per(me, me))
-    TRY(hip_check(hipMemcpyAsync(recvs[me].ptr, sends[me].ptr, sends[me].bytes, hipMemcpyDeviceToDevice, st),
-                  "hipMemcpyAsync own slice"));
   TRY(hip_check(hipMemcpyAsync(p->recv_off, p->recv_off_host, N * sizeof(uint64_t), hipMemcpyHostToDevice, st),
                 "hipMemcpyAsync recv_off"));
   TRY(p->d->exchange(sends, recvs, st));
@@ -373,9 +376,17 @@ int omr_sparse_allreduce_f32(omr_ar_plan* p, const float* x, float* out, int32_t
   const uint64_t nres_me = per(N, me);
   TRY(omr_check(omr_compact(wset, r0, r1, p->lanes, p->shard_list, p->count + 1, p->compact_ws,
                             p->compact_ws_bytes, stream), "omr_compact shard"));
-  TRY(omr_check(omr_sparse_block_sum_f32(p->recv, p->recv_off, p->masks_all, N, rows, p->prefix, r0, p->lanes,
+  TRY(omr_check(omr_sparse_block_sum_f32(p->packed, p->recv_off, p->masks_all, N, rows, p->prefix, r0, p->lanes,
                                          p->shard_list, static_cast<uint32_t>(nres_me), p->B, p->sums, stream),
                 "omr_sparse_block_sum_f32"));
+  if (mode == OMR_ROUND_REDUCE_SCATTER) {  // aggregator keeps its shard: sums written in place into `out`
+    TRY(omr_check(omr_scatter_blocks_f32(p->sums, p->shard_list, static_cast<uint32_t>(nres_me), p->B, out, stream),
+                  "omr_scatter_blocks_f32 shard"));
+    TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
+    if (sent_blocks) *sent_blocks = total_send - per(me, me);
+    if (union_blocks) *union_blocks = nres_me;
+    return 0;
+  }
   // 6. sums back to every worker, scattered in place
   std::vector<Slice> rs(N), rr(N);
   for (int s = 0; s < N; ++s) {
@@ -396,6 +407,13 @@ int omr_sparse_allreduce_f32(omr_ar_plan* p, const float* x, float* out, int32_t
   if (sent_blocks) *sent_blocks = total_send - per(me, me);
   if (union_blocks) *union_blocks = total_res;
   return 0;
+}
+
+int omr_sparse_allreduce_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
+                             uint32_t* union_next, uint64_t* sent_blocks, uint64_t* union_blocks,
+                             omr_stream_t stream) {
+  return omr_sparse_round_f32(p, x, out, flags, next_offsets, union_next, OMR_ROUND_ALLREDUCE, sent_blocks,
+                              union_blocks, stream);
 }
 
 }  // extern "C"

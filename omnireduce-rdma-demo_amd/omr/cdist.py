@@ -45,6 +45,7 @@ def load():
         "omr_ar_plan_create": (i, [vp, u64, u32, u32, u32, vp]),
         "omr_ar_plan_destroy": (i, [vp]),
         "omr_sparse_allreduce_f32": (i, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        "omr_sparse_round_f32": (i, [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -81,17 +82,21 @@ class CppSparseAllreduce:
                "omr_ar_plan_create")
         self.rank, self.world = rank, world
 
+    ALLREDUCE, REDUCE_SCATTER = 0, 1
+
     def run(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, ev=None, flags=None, next_offsets=None,
-            union_next=None):
+            union_next=None, mode: int = 0):
+        """mode 0: all-reduce (every worker gets every shard's sums); 1: reduce-scatter (stop at the
+        aggregators: `out` gets this rank's shard sums only)."""
         out = x if out is None else out
         sent, uni = ctypes.c_uint64(), ctypes.c_uint64()
         st = torch.cuda.current_stream(self.device)
         if ev is not None:  # the round starts with the worker scan kernel on this stream
             ev[0].record(st)
         ptr = (lambda t: t.data_ptr() if t is not None else None)
-        _check(load().omr_sparse_allreduce_f32(self._p, x.data_ptr(), out.data_ptr(), ptr(flags), ptr(next_offsets),
-                                               ptr(union_next), ctypes.byref(sent), ctypes.byref(uni),
-                                               st.cuda_stream), "omr_sparse_allreduce_f32")
+        _check(load().omr_sparse_round_f32(self._p, x.data_ptr(), out.data_ptr(), ptr(flags), ptr(next_offsets),
+                                           ptr(union_next), mode, ctypes.byref(sent), ctypes.byref(uni),
+                                           st.cuda_stream), "omr_sparse_round_f32")
         if ev is not None:
             ev[1].record(st)
         return sent.value, uni.value

@@ -168,10 +168,11 @@ class SparseAllreduce:
         self.results = torch.empty(L.n, dtype=f32, device=dev)        # all shards' sums, shard-major
         self.bounds_t = torch.tensor(self.bounds, dtype=torch.long, device=dev)
 
-    def run(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, ev=None) -> RoundResult:
+    def run(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, ev=None, mode: int = 0) -> RoundResult:
         """One round.  The result is scattered into `out` (default: x itself, the reference's in-place result,
         client.cc:89); an out-of-place `out` must already hold x's values outside the write set.  `ev` =
-        optional (start, end) events recorded around the worker-scan kernel."""
+        optional (start, end) events recorded around the worker-scan kernel.  mode 0 = all-reduce, 1 =
+        reduce-scatter (stop at the aggregators: only this rank's shard of the write set is written)."""
         L, N, me, be, B = self.L, self.world, self.rank, self.be, self.L.block_size
         if x.numel() != L.n or x.dtype != torch.float32:
             raise ValueError("x must be float32[n]")
@@ -209,6 +210,9 @@ class SparseAllreduce:
         be.compact(self.masks_all[N], r0, r1, self.shard_list, self.count[1:2])
         be.sparse_sum(self.recv, self.recv_off, self.masks_all[:N], self.prefix, r0, self.shard_list, nres[me],
                       self.sums)
+        if mode == 1:  # reduce-scatter: the aggregator keeps its shard (sums scattered in place into `out`)
+            be.scatter(self.sums, self.shard_list, nres[me], out)
+            return RoundResult(flags, masks_r, nxt, unext, nres[me], total_send - per[me][me])
         # 6. results back to every worker, scattered in place
         res_off = [cnt[N][s] - cnt[N][0] for s in range(N)]
         my_sums = self.sums[:nres[me] * B]

@@ -33,6 +33,7 @@ def dist_lib():
     L.omr_ar_plan_create.argtypes = [vp, u64, u32, u32, u32, vp]
     L.omr_ar_plan_destroy.argtypes = [vp]
     L.omr_sparse_allreduce_f32.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.omr_sparse_round_f32.argtypes = [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]
     L.omr_dist_last_error.restype = ctypes.c_char_p
     return L
 
@@ -87,6 +88,50 @@ def test_cpp_round_loopback(gpu, world, B, density):
         assert (fl == f).all()
         assert (nx == oracle.next_offsets(f, L.n, B, L.num_lanes, 8)).all()
         assert (unx == un).all()
+
+
+def test_cpp_reduce_scatter_loopback(gpu):
+    world, B = 3, 256
+    L = Layout(n=2 << 20, block_size=B)
+    D = dist_lib()
+    bufs = [oracle.fill(oracle.gen_bitmap(w, 0.2, L.nb), B, mode=1, seed=w + 3) for w in range(world)]
+    uf = oracle.union_flags([oracle.flags_from_data(b, B) for b in bufs])
+    board = D.omr_local_board_create(world)
+    errs, outs = [], [None] * world
+
+    def rank(r):
+        try:
+            torch.cuda.set_device(0)
+            x = torch.from_numpy(bufs[r].copy()).cuda()
+            out = x.clone()
+            d, plan = ctypes.c_void_p(), ctypes.c_void_p()
+            assert D.omr_dist_create_local(board, r, ctypes.byref(d)) == 0
+            assert D.omr_ar_plan_create(d, L.n, B, L.num_lanes, 8, ctypes.byref(plan)) == 0
+            st = torch.cuda.Stream()
+            assert D.omr_sparse_round_f32(plan, x.data_ptr(), out.data_ptr(), None, None, None, 1, None, None,
+                                          st.cuda_stream) == 0, D.omr_dist_last_error()
+            torch.cuda.synchronize()
+            outs[r] = out.cpu().numpy()
+            D.omr_ar_plan_destroy(plan)
+            D.omr_dist_destroy(d)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    D.omr_local_board_destroy(board)
+    assert not errs, errs
+    bounds = [s * L.rows // world for s in range(world + 1)]
+    for r in range(world):
+        full = bufs[r].copy()
+        oracle.block_sum(bufs, L.n, B, L.num_lanes, 8, uf, full)
+        exp = bufs[r].copy()
+        lo, hi = bounds[r] * L.num_lanes * B, bounds[r + 1] * L.num_lanes * B
+        exp[lo:hi] = full[lo:hi]
+        assert (outs[r].view(np.uint32) == exp.view(np.uint32)).all(), f"rank {r}"
 
 
 def _run(cmd, timeout=300):

@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, B, density, mode, use_gpu, errq):
+def _worker(rank, world, port, n, B, density, mode, use_gpu, errq, round_mode=0):
     try:
         sys.path[:0] = [HERE, os.path.join(HERE, "..", "oracle"), os.path.join(HERE, "..", "omnireduce-rdma-demo_amd")]
         import oracle
@@ -45,6 +45,24 @@ def _worker(rank, world, port, n, B, density, mode, use_gpu, errq):
         else:
             x = torch.from_numpy(bufs[rank].copy())
             eng = odist.SparseAllreduce(L, device="cpu", backend=CpuBackend(L, world), comm=odist.TorchComm())
+        if round_mode == 1:  # reduce-scatter: own shard of the write set gets the sums, the rest is untouched
+            out = x.clone()
+            res = eng.run(x, out=out, mode=1)
+            if use_gpu:
+                torch.cuda.synchronize()
+            flags = [oracle.flags_from_data(b, B) for b in bufs]
+            uf = oracle.union_flags(flags)
+            full = bufs[rank].copy()
+            oracle.block_sum(bufs, L.n, B, L.num_lanes, L.num_threads, uf, full)
+            r0, r1 = eng.bounds[rank], eng.bounds[rank + 1]
+            exp = bufs[rank].copy()
+            lo, hi = r0 * L.num_lanes * B, r1 * L.num_lanes * B
+            exp[lo:hi] = full[lo:hi]
+            got = out.cpu().numpy()
+            assert (got.view(np.uint32) == exp.view(np.uint32)).all(), f"rank {rank}: reduce-scatter mismatch"
+            dist.barrier()
+            dist.destroy_process_group()
+            return
         for it in range(2):  # second round: results feed the next round's scan (values change, masks do not)
             res = eng.run(x)
             if use_gpu:
@@ -74,11 +92,11 @@ def _worker(rank, world, port, n, B, density, mode, use_gpu, errq):
         raise
 
 
-def _run(world, n, B, density, mode, use_gpu=False):
+def _run(world, n, B, density, mode, use_gpu=False, round_mode=0):
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, B, density, mode, use_gpu, errq))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, B, density, mode, use_gpu, errq, round_mode))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -102,6 +120,11 @@ def _run(world, n, B, density, mode, use_gpu=False):
 ])
 def test_sparse_allreduce_cpu(world, B, density, mode):
     _run(world, 1 << 20, B, density, mode)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sparse_reduce_scatter_cpu(world):
+    _run(world, 1 << 20, 256, 0.3, 1, round_mode=1)
 
 
 def test_sparse_allreduce_all_zero_cpu():
