@@ -5,13 +5,16 @@
 //   aggregator sum server.cc:83-99 (block_next_offset / min_next bookkeeping :84-96, the add :97-98)
 //   layout         common.h:27-42 (BLOCK_SIZE, NUM_BLOCKS lanes, NUM_THREADS partitions)
 //   generator      client.cc:396-421
-// Design: the hot path is HBM-bound integer/byte work plus one fp32 add per element; no MFMA.
-//   k_scan1 / k_scanm : one wave per 64 KiB row (num_lanes blocks).  Every block is read once with
-//                       16-byte-per-lane coalesced loads (a 256-float block is exactly one wave-wide
-//                       dwordx4 load), the non-zero flag is a wavefront ballot, and the aggregator sum is
-//                       fused into the same pass so non-zero blocks are written straight from registers.
-//   k_next            : next-offset chains from the uint64 row masks (tiny: 8 B per 64 KiB row);
-//                       one workgroup per 64-row segment, lane columns transposed with ballots.
+// Design: the hot path is HBM-bound byte/integer work plus one fp32 add per element; no MFMA.
+//   k_scan1f          : the single-pass m = 1 worker step.  A workgroup owns one (partition, lane) column — one
+//                       reference next-offset chain — streams its 1 KiB blocks (16 dwordx4 loads per wave in
+//                       flight), ballots the flags, stores the aggregated non-zero blocks write-through, and
+//                       resolves every next offset from the column's bit vector in LDS (segments of a column, when
+//                       there are few columns, meet through device-scope atomics).
+//   k_scan1 / k_scanm : two-pass variant (plus row masks for the multi-GPU exchange) and the m-worker sum;
+//                       16 KiB chunks / rows swept grid-stride, same loads, ballots and stores.
+//   k_next            : next-offset chains from uint64 row masks (64x64 wave bit transposes).
+//   exchange kernels  : mask union, popcount prefixes, compaction, block gather/scatter, sparse shard sum.
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
