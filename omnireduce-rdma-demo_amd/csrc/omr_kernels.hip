@@ -191,15 +191,23 @@ __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
 //
 // One launch for the whole m = 1 worker step.  Work is split by COLUMN instead of by address: a workgroup owns
 // one lane l of one partition p (or a segment of its rows, when there are too few columns to fill the chip),
-// i.e. exactly the blocks one find_next_nonzero_block chain walks (client.cc:19-31).  Each wave streams batches
-// of 16 dwordx4 loads (16 rows of the column: 1 KiB each, 64 KiB apart — measured as fast as contiguous
-// chunks), ballots the flags, stores the aggregated non-zero blocks, and ORs the flag bits into the column's
-// bit vector in LDS.  Next offsets then need no other workgroup: every row's successor is a ctz over the LDS
-// bit vector (plus a suffix "next non-zero word" index).  With K > 1 segments per column, each segment
-// publishes {first, last} non-zero row through device-scope atomics; the segment whose arrival count completes
-// the column fills in the rows whose successor lies in a later segment (tail rows).  Workgroup -> (p, l, k) is
-// permuted so that one partition's columns share an XCD, letting the L2 merge their 4-byte flag/next stores
-// into whole lines (speed only, never correctness).
+// i.e. exactly the blocks one find_next_nonzero_block chain walks (client.cc:19-31).  Each wave owns a
+// CONTIGUOUS range of the segment's rows and streams it last batch first, LOADS dwordx4 loads per lane in flight
+// (RB rows of the column: 1 KiB pieces 64 KiB apart at B=256), ballots the flags and stores the aggregated
+// non-zero blocks write-through.  Because the rows are visited backwards, every row's successor lies either in
+// its own batch (a ctz over the batch's ballot bits) or among the wave's already-scanned rows (a running carry
+// = first non-zero row seen so far), so next offsets are stored as the stream goes, with no epilogue pass.
+// Only the wave's tail rows (at and after its last non-zero row) need a later wave's first non-zero row: one
+// barrier and one store per wave.  With K > 1 segments per column, each segment publishes {first, last}
+// non-zero row through device-scope atomics; the segment whose arrival count completes the column writes the
+// rows whose successor lies in a later segment.  Workgroup -> (p, l, k) is permuted so that one partition's
+// columns share an XCD, letting the L2 merge their 4-byte flag/next stores into whole lines (speed only).
+//
+// Stores: every row issues its stores; a zero block's are pointed past the descriptor's range and discarded by
+// the buffer range check.  The number of memory operations per batch is then static, so the compiler's vmcnt
+// wait for a load never includes a younger, data-dependent store (tools/tune_fused.py: 2-4 % faster than
+// branching around the stores; write-through sc0 sc1 beat plain, sc1-only and nt stores).
+// ABL (timing-only builds, csrc/tune/): bit 0 drops the data stores, bit 1 the flag/next stores.
 struct FusedArgs {
   const float* x;
   float* out;
@@ -207,36 +215,39 @@ struct FusedArgs {
   uint32_t* next;
   uint32_t* cnt;       // [parts*lanes] arrival counters (K > 1), zero between launches
   uint64_t* summary;   // [parts*lanes*K] {first << 32 | last} per segment (K > 1)
-  uint32_t lanes, rpp, K, S, block, sentinel, nwords;
+  uint32_t lanes, rpp, K, S, block, sentinel;
 };
 
-template <int VEC, int WAVES, int LOADS = 16, bool XCD_MAP = true>
+constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
+
+template <int VEC, int WAVES, int LOADS = 16, int ABL = 0>
 __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
-  constexpr int RB = LOADS / VEC;  // rows per batch: LOADS dwordx4 loads per lane in flight
-  extern __shared__ uint64_t s_words[];                                  // column bits, row i -> word i/64
-  uint32_t* s_nw = reinterpret_cast<uint32_t*>(s_words + a.nwords);      // first non-zero word >= w
-  __shared__ uint32_t s_first, s_last;
+  constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
+  static_assert(RB >= 1 && RB <= 32, "batch bits are 32-bit");
+  __shared__ uint32_t s_wfirst[WAVES], s_wlast[WAVES];
   __shared__ int s_fix;
   __shared__ uint32_t s_carry[64];
   __shared__ uint32_t s_seg_last[64];
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t T = gridDim.x, bid = blockIdx.x;
-  const uint32_t lin = (XCD_MAP && T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
   const uint32_t k = lin % a.K, col = lin / a.K;
   const uint32_t l = col % a.lanes, p = col / a.lanes;
   const uint32_t r0 = k * a.S;                                  // segment's first row within the partition
   const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;  // its global row
-  for (uint32_t w = threadIdx.x; w < a.nwords; w += blockDim.x) s_words[w] = 0;
-  if (threadIdx.x == 0) {
-    s_first = kNone;
-    s_last = 0;
-  }
-  __syncthreads();
   const uint32_t row_bytes = a.lanes * a.block * 4;
-  for (uint32_t j = wave; j * RB < a.S; j += WAVES) {
-    const uint32_t rr = j * RB;
-    const uint32_t nrow = (a.S - rr < static_cast<uint32_t>(RB)) ? a.S - rr : RB;
+  const uint32_t lane_b = l * a.block;
+  const uint32_t row_stride = a.lanes * a.block;
+  const bool last_seg = (k + 1 == a.K);
+  // the wave's rows [lo, hi) of the segment: whole batches, except possibly the last nonempty wave's top one
+  const uint32_t rw = ((a.S + WAVES * RB - 1) / (WAVES * RB)) * RB;
+  const uint32_t lo = wave * rw < a.S ? wave * rw : a.S;
+  const uint32_t hi = lo + rw < a.S ? lo + rw : a.S;
+  uint32_t carry = kNone, wlast = kNone;
+  for (uint32_t nb_ = (hi - lo + RB - 1) / RB; nb_ > 0; --nb_) {
+    const uint32_t rr = lo + (nb_ - 1) * RB;
+    const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
     const uint64_t blk0 = (row0 + rr) * a.lanes + l;  // block of the batch's first row
     const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, nrow * row_bytes);
     v4f v[RB][VEC];
@@ -246,7 +257,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
       for (int q = 0; q < VEC; ++q)
         v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
                                               src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
-    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + blk0 * a.block, a.out != nullptr ? nrow * row_bytes : 0u);
+    const __amdgpu_buffer_rsrc_t dst =
+        chunk_rsrc(a.out + blk0 * a.block, (a.out != nullptr && !(ABL & 1)) ? nrow * row_bytes : 0u);
     uint32_t bits = 0;
 #pragma unroll
     for (int s = 0; s < RB; ++s) {
@@ -256,70 +268,51 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
       const bool nz = wave_ballot(o != 0) != 0 && static_cast<uint32_t>(s) < nrow;
       bits |= static_cast<uint32_t>(nz) << s;
       const bool head = (r0 + rr + s) == 0;  // lane head: row 0 of the partition, always sent (client.cc:201-205)
-      if (a.out != nullptr && (nz || (head && static_cast<uint32_t>(s) < nrow))) {
+      // aggregated block 0.0f + x (server.cc:148-150 zero, :97-98 add), written in place (client.cc:89)
+      const uint32_t drop = (nz || head) ? 0u : kDropStore;
 #pragma unroll
-        for (int q = 0; q < VEC; ++q)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
-                                                 dst, s * row_bytes + (q * 64 + lane) * 16, 0, kStoreAux);
-      }
+      for (int q = 0; q < VEC; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])), dst,
+                                               (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, kStoreAux);
     }
-    if (a.flags != nullptr && static_cast<uint32_t>(lane) < nrow)
-      a.flags[blk0 + static_cast<uint64_t>(lane) * a.lanes] = static_cast<int32_t>((bits >> lane) & 1u);
-    if (lane == 0 && bits != 0) atomicOr(reinterpret_cast<unsigned long long*>(&s_words[rr / 64]),
-                                         static_cast<unsigned long long>(bits) << (rr % 64));
+    if (!(ABL & 2) && static_cast<uint32_t>(lane) < nrow) {
+      const uint64_t blk = blk0 + static_cast<uint64_t>(lane) * a.lanes;
+      if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>((bits >> lane) & 1u);
+      // successor of row rr+lane: next set bit above it in this batch, else the carry (client.cc:19-31)
+      const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
+      const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : carry;
+      if (nr != kNone) a.next[blk] = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+    }
+    if (bits != 0) {
+      if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
+      carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
+    }
+  }
+  if (lane == 0) {
+    s_wfirst[wave] = carry;  // first non-zero row of the wave's range (kNone: all zero)
+    s_wlast[wave] = wlast;   // last one
   }
   __syncthreads();
-  // suffix index of the first non-zero word (log-step min scan; nwords <= blockDim by launch construction)
-  const uint32_t w = threadIdx.x;
-  uint32_t nwv = (w < a.nwords && s_words[w] != 0) ? w : kNone;
-  if (w < a.nwords) {
-    s_nw[w] = nwv;
-    if (s_words[w] != 0) {
-      atomicMin(&s_first, w * 64 + static_cast<uint32_t>(__builtin_ctzll(s_words[w])));
-      atomicMax(&s_last, w * 64 + 63 - static_cast<uint32_t>(__builtin_clzll(s_words[w])));
+  // tail rows [wlast or lo, hi): successor = first non-zero row of a later wave, else of a later segment
+  uint32_t succ = kNone;
+  for (uint32_t w2 = wave + 1; w2 < WAVES; ++w2)
+    if (s_wfirst[w2] != kNone) {
+      succ = s_wfirst[w2];
+      break;
     }
-  }
-  if (w == 0) s_nw[a.nwords] = kNone;
-  __syncthreads();
-  for (uint32_t off = 1; off < a.nwords; off <<= 1) {
-    const uint32_t other = (w + off < a.nwords) ? s_nw[w + off] : kNone;
-    __syncthreads();
-    if (w < a.nwords && other < nwv) {
-      nwv = other;
-      s_nw[w] = nwv;
-    }
-    __syncthreads();
-  }
-  // next offsets of the segment's rows (client.cc:19-31: first non-zero block after row i in lane l)
-  const uint32_t lane_b = l * a.block;
-  const uint32_t row_stride = a.lanes * a.block;
-  const bool last_seg = (k + 1 == a.K);
-  for (uint32_t i = threadIdx.x; i < a.S; i += blockDim.x) {
-    const uint32_t j = i + 1;
-    uint32_t nr = kNone;
-    if (j < a.S) {
-      const uint64_t m = s_words[j / 64] >> (j % 64);
-      if (m != 0) {
-        nr = j + static_cast<uint32_t>(__builtin_ctzll(m));
-      } else if (j / 64 + 1 < a.nwords) {
-        const uint32_t w2 = s_nw[j / 64 + 1];
-        if (w2 != kNone) nr = w2 * 64 + static_cast<uint32_t>(__builtin_ctzll(s_words[w2]));
-      }
-    }
-    uint32_t val;
-    if (nr != kNone) {
-      val = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
-    } else if (last_seg) {
-      val = a.sentinel + lane_b;
-    } else {
-      continue;  // successor in a later segment: written by the column's finishing segment below
-    }
-    a.next[(row0 + i) * a.lanes + l] = val;
+  if (!(ABL & 2) && (succ != kNone || last_seg)) {
+    const uint32_t val = succ != kNone ? static_cast<uint32_t>(row0 + succ) * row_stride + lane_b : a.sentinel + lane_b;
+    for (uint32_t i = (wlast == kNone ? lo : wlast) + lane; i < hi; i += 64) a.next[(row0 + i) * a.lanes + l] = val;
   }
   if (a.K == 1) return;
   // multi-segment column: publish {first, last}, count arrivals; the last arriver fixes every tail row
   if (threadIdx.x == 0) {
-    const uint64_t sm = (static_cast<uint64_t>(s_first) << 32) | (s_first == kNone ? kNone : s_last);
+    uint32_t first = kNone, last = 0;
+    for (int w2 = 0; w2 < WAVES; ++w2) {
+      if (first == kNone) first = s_wfirst[w2];
+      if (s_wlast[w2] != kNone) last = s_wlast[w2];
+    }
+    const uint64_t sm = (static_cast<uint64_t>(first) << 32) | (first == kNone ? kNone : last);
     (void)__hip_atomic_exchange(&a.summary[static_cast<uint64_t>(col) * a.K + k], sm, __ATOMIC_RELAXED,
                                 __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -844,12 +837,13 @@ int launch_next(const Layout& L, const uint64_t* masks, uint32_t count, uint32_t
 #endif
 constexpr bool kNT = OMR_SCAN_NT != 0;
 
-// Column split of the single-pass kernel: K segments per (partition, lane) column, enough workgroups to give
-// every CU one (>= 256: tools/tune_fused.py measured K = 1 best at 512 columns (B=256) and K = 2 best at 128
-// columns (B=1024)), each segment small enough for one LDS bit-index scan.
-constexpr int kFusedWaves = 8;
+// Column split of the single-pass kernel: K segments per (partition, lane) column, at least one 16-wave
+// workgroup per CU (>= 256: tools/tune_fused.py measured K = 1 at 512 columns (B=256) and K = 2 at 128 columns
+// (B=1024) best, profiles/r01/tune_fused_*.log), segments of at least 64 rows, K <= 64 (the fix-up's LDS).
+constexpr int kFusedWaves = 16;
+constexpr int kFusedLoads = 16;
 struct FusedShape {
-  uint32_t K = 0, S = 0, nwords = 0;
+  uint32_t K = 0, S = 0;
 };
 
 FusedShape fused_shape(const Layout& L) {
@@ -857,14 +851,8 @@ FusedShape fused_shape(const Layout& L) {
   const uint64_t cols = static_cast<uint64_t>(L.parts) * L.lanes;
   uint32_t K = 1;
   while (cols * K < 256 && L.rows_per_part % (2 * K) == 0 && L.rows_per_part / (2 * K) >= 64 && 2 * K <= 64) K *= 2;
-  while ((L.rows_per_part / K + 63) / 64 > 64u * kFusedWaves && L.rows_per_part % (2 * K) == 0 && 2 * K <= 64)
-    K *= 2;
-  const uint32_t S = L.rows_per_part / K;
-  const uint32_t nwords = (S + 63) / 64;
-  if (L.rows_per_part % K != 0 || nwords > 64u * kFusedWaves) return f;  // not representable: K = 0
   f.K = K;
-  f.S = S;
-  f.nwords = nwords;
+  f.S = L.rows_per_part / K;
   return f;
 }
 
@@ -891,14 +879,12 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
   a.S = f.S;
   a.block = L.block;
   a.sentinel = omr_sentinel(L.block, L.lanes);
-  a.nwords = f.nwords;
   const unsigned grid = static_cast<unsigned>(cols * f.K);
-  const size_t lds = f.nwords * sizeof(uint64_t) + (f.nwords + 1) * sizeof(uint32_t);
   constexpr int T = 64 * kFusedWaves;
   switch (L.vec) {
-    case 1: k_scan1f<1, kFusedWaves><<<grid, T, lds, st>>>(a); break;
-    case 2: k_scan1f<2, kFusedWaves><<<grid, T, lds, st>>>(a); break;
-    default: k_scan1f<4, kFusedWaves><<<grid, T, lds, st>>>(a); break;
+    case 1: k_scan1f<1, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
+    case 2: k_scan1f<2, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
+    default: k_scan1f<4, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
   }
   return launch_status("k_scan1f");
 }

@@ -273,12 +273,14 @@ def assert_fused_parity(x, L, out_init=None, reps=2):
 
 
 @pytest.mark.parametrize("n,B,parts,density", [
-    (1 << 20, 256, 8, 0.3),        # config 1 layout: 8 rows per partition, K = 1
-    (4 << 20, 256, 8, 0.095),      # K = 1, S = 32
-    (16 << 20, 256, 8, 0.01),      # K = 1, S = 128 (two LDS words)
-    (16 << 20, 1024, 8, 0.0099),   # 128 columns -> K = 2 segments
-    (64 << 20, 1024, 8, 0.0099),   # K = 4 (config 3 split)
+    (1 << 20, 256, 8, 0.3),        # config 1 layout: 8 rows per partition, K = 1, one partial batch
+    (4 << 20, 256, 8, 0.095),      # K = 1, S = 32: two of 16 waves busy
+    (16 << 20, 256, 8, 0.01),      # K = 1, S = 128
+    (16 << 20, 1024, 8, 0.0099),   # 128 columns -> K = 2 segments of 64 rows
+    (64 << 20, 1024, 8, 0.0099),   # K = 2 (config 3 split), S = 256
     (16 << 20, 1024, 1, 0.0005),   # one partition, 16 columns -> K = 16, long empty stretches
+    (800 * 16384, 256, 8, 0.095),  # S = 100: seven busy waves, the last with a 4-row partial batch
+    (20 << 20, 1024, 5, 0.2),      # 5 partitions of 256 rows, 80 columns -> K = 4, S = 64
     (8 << 20, 512, 8, 0.49),       # B = 512
     (4 << 20, 256, 8, 0.0),        # all zero: every chain is the sentinel
     (4 << 20, 256, 8, 1.0),        # dense

@@ -25,7 +25,7 @@ def run_pass(counter, outdir, bench_args):
     cmd = ["rocprofv3", "--pmc", counter, "-d", outdir, "-o", "pmc", "--output-format", "csv", "--",
            sys.executable, os.path.join(ROOT, "bench.py")] + bench_args
     env = dict(os.environ, TMPDIR="/tmp")
-    subprocess.run(cmd, check=True, env=env, cwd="/tmp", stdout=subprocess.DEVNULL)
+    subprocess.run(cmd, check=True, env=env, cwd="/tmp", stdout=subprocess.DEVNULL, timeout=180)
     files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {outdir}")
