@@ -185,6 +185,48 @@ int omr_sparse_block_sum_f32(const float* recv, const uint64_t* recv_offsets, co
                              uint32_t num_lanes, const uint32_t* block_list, uint32_t num_list,
                              uint32_t block_size, float* out, omr_stream_t stream);
 
+/* ---------------------------------------------------------------- multi-rank round, mask-addressed */
+
+/* Single-pass worker scan for a multi-rank round (client.cc:19-31 + :87-102 over the whole tensor): as
+ * omr_scan_sum_fused_f32 (flags, next offsets, and out if non-NULL), plus row masks: the bit of every non-zero
+ * block is OR-ed into row_masks (device uint64[rows], all zero on entry). */
+int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                        int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out, void* workspace,
+                        size_t workspace_bytes, omr_stream_t stream);
+
+/* The aggregator bookkeeping of a round in ONE launch (server.cc:83-96, for the whole tensor at once), from
+ * `count` workers' row masks (device, stride rows):
+ *   union_masks[r] = OR of the workers' masks (the domain of the min_next chain, server.cc:86-96);
+ *   write_set[r]   = union_masks[r], with every lane of a lane-head row (r % rows_per_part == 0) set: the blocks
+ *                    the aggregators return (lane heads are always sent: client.cc:201-205);
+ *   prefix[a*(rows+1) + r] = set bits of array a in rows [0, r), for a < count (workers) and a == count (the
+ *                    write set); r = rows gives the total;
+ *   counts[a*num_bounds + s] = prefix[a][bounds[s]] (bounds: device uint64[num_bounds], each <= rows);
+ *   zero_masks (device uint64[rows] or NULL) is cleared (the next round's omr_worker_scan_f32 target). */
+int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
+                   uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
+                   uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
+                   omr_stream_t stream);
+
+/* Block movement addressed by a row mask and its prefix (no block list): the k-th set bit of `row_masks` over
+ * rows [0, rows) minus [skip_begin, skip_end) is block k of the packed stream.
+ *   dir 0 (pack, the worker's gather of common.cc:405-407): dst packed <- src dense;
+ *   dir 1 (unpack, the worker's in-place result copy of client.cc:89): dst dense <- src packed. */
+int omr_move_blocks_f32(const float* src, float* dst, int dir, const uint64_t* row_masks, const uint32_t* prefix,
+                        uint64_t rows, uint32_t num_lanes, uint32_t block_size, uint64_t skip_begin,
+                        uint64_t skip_end, omr_stream_t stream);
+
+/* Aggregator shard sum (server.cc:83-99 with the RDMA hop replaced by the transport) over rows
+ * [row_begin, row_end) of write_set: every write-set block gets ((0.0f + x_a0) + x_a1) + ... over the workers a
+ * whose mask has it, in rank order (lane-head blocks no worker has: +0.0f).  Worker `me`'s blocks are read in
+ * place from its dense tensor `own`; worker a != me's from recv + recv_offsets[a] blocks (HOST uint64[count]):
+ * its non-zero blocks of these rows in block order.  `prefix` as omr_round_plan.  packed_out 0: out is dense
+ * (blocks written at their own positions; may alias own); 1: out is packed in write-set order of the rows. */
+int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const uint64_t* recv_offsets,
+                      const uint64_t* row_masks, uint32_t count, const uint32_t* prefix, const uint64_t* write_set,
+                      uint64_t rows, uint64_t row_begin, uint64_t row_end, uint32_t num_lanes, uint32_t block_size,
+                      int packed_out, float* out, omr_stream_t stream);
+
 /* ---------------------------------------------------------------- host-resident end-to-end path */
 
 /* The gradient lives in host memory (the reference's registered region, common.cc:873-914): H2D in row chunks,

@@ -143,15 +143,6 @@ struct LocalDist final : omr_dist {
   }
 };
 
-// prefix[a*(rows+1) + bounds[s]] for every array a and bound s -> counts[a*(N+1) + s]
-__global__ void k_gather_counts(const uint32_t* prefix, uint64_t rows, const uint64_t* bounds, uint32_t arrays,
-                                uint32_t nb, uint32_t* counts) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= arrays * nb) return;
-  const uint32_t a = i / nb, s = i % nb;
-  counts[i] = prefix[static_cast<uint64_t>(a) * (rows + 1) + bounds[s]];
-}
-
 template <typename T>
 int dev_alloc(T** p, size_t count) {
   return hip_check(hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(count, 1) * sizeof(T)), "hipMalloc");
@@ -164,31 +155,25 @@ struct omr_ar_plan {
   uint64_t n = 0, nb = 0, rows = 0;
   uint32_t B = 0, lanes = 0, parts = 0, rpp = 0;
   int N = 1, me = 0;
-  std::vector<uint64_t> bounds;
-  uint64_t shard_nb = 0;
-  uint64_t* masks_all = nullptr;  // [(N+1)][rows]: workers, then the write set
-  uint64_t* umask = nullptr;      // [rows]
-  uint32_t* prefix = nullptr;     // [(N+1)][rows+1]
-  uint32_t* my_list = nullptr;
-  uint32_t* full_list = nullptr;
-  uint32_t* shard_list = nullptr;
-  uint32_t* count = nullptr;      // [3]
-  float* packed = nullptr;        // own non-zero blocks, block order
-  float* recv = nullptr;          // this shard's contributions, worker-major
-  uint64_t* recv_off = nullptr;   // [N] block offset of each worker's stream in recv
-  float* sums = nullptr;          // this shard's sums
-  float* results = nullptr;       // every shard's sums, shard-major
+  std::vector<uint64_t> bounds;   // shard s = rows [bounds[s], bounds[s+1])
+  uint64_t shard_nb = 0;          // blocks of the largest shard
+  uint64_t* own_masks = nullptr;  // [rows] this rank's masks (the scan ORs into it; the plan kernel re-zeroes it)
+  uint64_t* masks_all = nullptr;  // [N][rows] every worker's masks (all-gather)
+  uint64_t* wset = nullptr;       // [rows] write set: union + lane heads
+  uint64_t* umask = nullptr;      // [rows] union of the workers' masks
+  uint32_t* prefix = nullptr;     // [N+1][rows+1] popcount prefixes: workers, then the write set
+  uint64_t* bounds_dev = nullptr;
+  uint32_t* counts_dev = nullptr;   // [N+1][N+1] prefix[a][bounds[s]]
+  uint32_t* counts_host = nullptr;  // pinned copy
+  float* packed = nullptr;   // own non-zero blocks of the other shards, block order
+  float* recv = nullptr;     // this shard's blocks from each peer, peer-major
+  float* results = nullptr;  // all-reduce: every shard's sums, write-set order
   int32_t* flags_ws = nullptr;
   uint32_t* next_ws = nullptr;
   uint32_t* unext_ws = nullptr;
-  uint64_t* bounds_dev = nullptr;
-  uint32_t* counts_dev = nullptr;
-  uint32_t* counts_host = nullptr;    // pinned
-  uint64_t* recv_off_host = nullptr;  // pinned
-  void* prefix_ws = nullptr;
-  size_t prefix_ws_bytes = 0;
-  void* compact_ws = nullptr;
-  size_t compact_ws_bytes = 0;
+  void* scan_ws = nullptr;   // omr_worker_scan_f32 segment workspace (zeroed once, self-resetting)
+  size_t scan_ws_bytes = 0;
+  hipEvent_t counts_ready = nullptr;
 };
 
 extern "C" {
@@ -241,13 +226,11 @@ int omr_dist_destroy(omr_dist* d) {
 
 int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p == nullptr) return 0;
-  void* devs[] = {p->masks_all, p->umask,    p->prefix,    p->my_list,    p->full_list,  p->shard_list,
-                  p->count,     p->packed,   p->recv_off,  p->sums,       p->results,
-                  p->flags_ws,  p->next_ws,  p->unext_ws,  p->bounds_dev, p->counts_dev, p->prefix_ws,
-                  p->compact_ws};
+  void* devs[] = {p->own_masks, p->masks_all, p->wset,    p->umask,    p->prefix,   p->bounds_dev, p->counts_dev,
+                  p->packed,    p->recv,      p->results, p->flags_ws, p->next_ws,  p->unext_ws,   p->scan_ws};
   for (void* v : devs) (void)hipFree(v);
   (void)hipHostFree(p->counts_host);
-  (void)hipHostFree(p->recv_off_host);
+  if (p->counts_ready) (void)hipEventDestroy(p->counts_ready);
   delete p;
   return 0;
 }
@@ -257,6 +240,7 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   if (d == nullptr || out == nullptr) return derr(OMR_EINVAL, "ar_plan_create: NULL");
   *out = nullptr;
   TRY(omr_check(omr_layout_check(n, block_size, num_lanes, num_parts), "omr_layout_check"));
+  if (d->world > OMR_MAX_WORKERS) return derr(OMR_EINVAL, "ar_plan_create: world %d > %d", d->world, OMR_MAX_WORKERS);
   auto* p = new omr_ar_plan();
   p->d = d;
   p->n = n;
@@ -277,35 +261,32 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   auto A = [&](int r) {
     if (rc == 0) rc = r;
   };
-  A(dev_alloc(&p->masks_all, (N + 1) * p->rows));
+  A(dev_alloc(&p->own_masks, p->rows));
+  A(dev_alloc(&p->masks_all, static_cast<size_t>(N) * p->rows));
+  A(dev_alloc(&p->wset, p->rows));
   A(dev_alloc(&p->umask, p->rows));
-  A(dev_alloc(&p->prefix, (N + 1) * (p->rows + 1)));
-  A(dev_alloc(&p->my_list, p->nb));
-  A(dev_alloc(&p->full_list, p->nb));
-  A(dev_alloc(&p->shard_list, p->shard_nb));
-  A(dev_alloc(&p->count, 3));
-  // one allocation: packed own blocks, then the peers' streams, so the shard sum addresses the rank's own
-  // contribution in place (no copy into the receive area)
-  A(dev_alloc(&p->packed, n + static_cast<size_t>(N) * p->shard_nb * block_size));
-  if (rc == 0) p->recv = p->packed + n;
-  A(dev_alloc(&p->recv_off, N));
-  A(dev_alloc(&p->sums, p->shard_nb * block_size));
+  A(dev_alloc(&p->prefix, static_cast<size_t>(N + 1) * (p->rows + 1)));
+  A(dev_alloc(&p->bounds_dev, N + 1));
+  A(dev_alloc(&p->counts_dev, static_cast<size_t>(N + 1) * (N + 1)));
+  if (N > 1) {
+    A(dev_alloc(&p->packed, n));
+    A(dev_alloc(&p->recv, static_cast<size_t>(N - 1) * p->shard_nb * block_size));
+  }
   A(dev_alloc(&p->results, n));
   A(dev_alloc(&p->flags_ws, p->nb));
   A(dev_alloc(&p->next_ws, p->nb));
   A(dev_alloc(&p->unext_ws, p->nb));
-  A(dev_alloc(&p->bounds_dev, N + 1));
-  A(dev_alloc(&p->counts_dev, (N + 1) * (N + 1)));
-  p->prefix_ws_bytes = omr_prefix_workspace_bytes(p->rows, N + 1);
-  p->compact_ws_bytes = omr_compact_workspace_bytes(p->rows);
-  A(dev_alloc(reinterpret_cast<char**>(&p->prefix_ws), p->prefix_ws_bytes));
-  A(dev_alloc(reinterpret_cast<char**>(&p->compact_ws), p->compact_ws_bytes));
+  p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
+  A(dev_alloc(reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), (N + 1) * (N + 1) * sizeof(uint32_t)),
               "hipHostMalloc"));
-  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->recv_off_host), N * sizeof(uint64_t)), "hipHostMalloc"));
+  A(hip_check(hipEventCreateWithFlags(&p->counts_ready, hipEventDisableTiming), "hipEventCreate"));
+  if (rc == 0) A(hip_check(hipMemset(p->own_masks, 0, p->rows * sizeof(uint64_t)), "hipMemset own masks"));
+  if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset scan ws"));
   if (rc == 0)
     A(hip_check(hipMemcpy(p->bounds_dev, p->bounds.data(), (N + 1) * sizeof(uint64_t), hipMemcpyHostToDevice),
                 "hipMemcpy bounds"));
+  if (rc == 0) A(hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize"));
   if (rc != 0) {
     omr_ar_plan_destroy(p);
     return rc;
@@ -314,6 +295,9 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   return 0;
 }
 
+// One round: scan -> mask all-gather -> one bookkeeping launch -> block counts to the host (the
+// round's single mid-round sync: the transport needs host-side sizes) -> pack -> send/recv -> shard sums
+// [-> sums back -> unpack].  Every block movement is addressed by masks and prefixes.
 int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
                          uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
                          omr_stream_t stream) {
@@ -323,89 +307,70 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int N = p->N, me = p->me;
   const uint64_t rows = p->rows, B = p->B;
-  uint64_t* my_masks = p->masks_all + static_cast<uint64_t>(me) * rows;
+  const uint32_t NB = N + 1;
   int32_t* fl = flags ? flags : p->flags_ws;
   uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
   uint32_t* un = union_next ? union_next : p->unext_ws;
-  // 1. worker scan: flags, own row masks straight into this rank's all-gather slot, own next chain
-  const float* bufs[1] = {x};
-  TRY(omr_check(omr_scan_sum_f32(bufs, 1, p->n, p->B, p->lanes, p->parts, fl, my_masks, nx, nullptr, stream),
-                "omr_scan_sum_f32"));
-  // 2. every worker's row masks (in place)
-  TRY(p->d->allgather(my_masks, p->masks_all, rows * sizeof(uint64_t), st));
-  // 3. write set (union + lane heads), union, aggregator chain, prefixes, per-shard counts
-  uint64_t* wset = p->masks_all + static_cast<uint64_t>(N) * rows;
-  TRY(omr_check(omr_mask_union(p->masks_all, N, rows, p->rpp, p->lanes, 1, wset, stream), "omr_mask_union"));
-  TRY(omr_check(omr_mask_union(p->masks_all, N, rows, p->rpp, p->lanes, 0, p->umask, stream), "omr_mask_union"));
-  TRY(omr_check(omr_next_offsets(p->umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
-  TRY(omr_check(omr_row_prefix(p->masks_all, N + 1, rows, p->prefix, p->prefix_ws, p->prefix_ws_bytes, stream),
-                "omr_row_prefix"));
-  const uint32_t A = N + 1, NB = N + 1;
-  k_gather_counts<<<(A * NB + 255) / 256, 256, 0, st>>>(p->prefix, rows, p->bounds_dev, A, NB, p->counts_dev);
-  TRY(hip_check(hipGetLastError(), "k_gather_counts"));
-  TRY(hip_check(hipMemcpyAsync(p->counts_host, p->counts_dev, A * NB * sizeof(uint32_t), hipMemcpyDeviceToHost, st),
+  // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass
+  TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, p->own_masks, nullptr, p->scan_ws,
+                                    p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+  // 2. every worker's row masks
+  TRY(p->d->allgather(p->own_masks, p->masks_all, rows * sizeof(uint64_t), st));
+  // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for the next round
+  TRY(omr_check(omr_round_plan(p->masks_all, N, rows, p->rpp, p->lanes, p->bounds_dev, NB, p->wset, p->umask,
+                               p->prefix, p->counts_dev, p->own_masks, stream), "omr_round_plan"));
+  TRY(hip_check(hipMemcpyAsync(p->counts_host, p->counts_dev, NB * NB * sizeof(uint32_t), hipMemcpyDeviceToHost, st),
                 "hipMemcpyAsync counts"));
-  TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
+  TRY(hip_check(hipEventRecord(p->counts_ready, st), "hipEventRecord"));
+  // aggregator chain (server.cc:86-96 min_next) over the union, queued behind the counts copy
+  TRY(omr_check(omr_next_offsets(p->umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
+  TRY(hip_check(hipEventSynchronize(p->counts_ready), "hipEventSynchronize counts"));
   auto cnt = [&](int a, int s) -> uint64_t { return p->counts_host[a * NB + s]; };
   auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
-  // 4. pack own non-zero blocks (block order == shard order) and send each shard's slice to its aggregator
-  const uint64_t total_send = cnt(me, N);
-  TRY(omr_check(omr_compact(my_masks, 0, rows, p->lanes, p->my_list, p->count, p->compact_ws, p->compact_ws_bytes,
-                            stream), "omr_compact"));
-  TRY(omr_check(omr_gather_blocks_f32(x, p->my_list, static_cast<uint32_t>(total_send), p->B, p->packed, stream),
-                "omr_gather_blocks_f32"));
-  // stream offsets (in blocks) from p->packed: peers' streams in the receive area, this rank's own slice
-  // where the gather left it
-  std::vector<uint64_t> roff(N);
-  uint64_t acc = 0;
-  for (int w = 0; w < N; ++w) {
-    roff[w] = acc;
-    if (w != me) acc += per(w, me);
-    p->recv_off_host[w] = (w == me) ? cnt(me, me) : p->n / p->B + roff[w];
-  }
-  std::vector<Slice> sends(N), recvs(N);
-  for (int s = 0; s < N; ++s) {
-    sends[s] = Slice{p->packed + cnt(me, s) * B, s == me ? 0 : per(me, s) * B * sizeof(float)};
-    recvs[s] = Slice{p->recv + roff[s] * B, s == me ? 0 : per(s, me) * B * sizeof(float)};
-  }
-  TRY(hip_check(hipMemcpyAsync(p->recv_off, p->recv_off_host, N * sizeof(uint64_t), hipMemcpyHostToDevice, st),
-                "hipMemcpyAsync recv_off"));
-  TRY(p->d->exchange(sends, recvs, st));
-  // 5. aggregator: rank-order sums of this shard's write set
   const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
-  const uint64_t nres_me = per(N, me);
-  TRY(omr_check(omr_compact(wset, r0, r1, p->lanes, p->shard_list, p->count + 1, p->compact_ws,
-                            p->compact_ws_bytes, stream), "omr_compact shard"));
-  TRY(omr_check(omr_sparse_block_sum_f32(p->packed, p->recv_off, p->masks_all, N, rows, p->prefix, r0, p->lanes,
-                                         p->shard_list, static_cast<uint32_t>(nres_me), p->B, p->sums, stream),
-                "omr_sparse_block_sum_f32"));
-  if (mode == OMR_ROUND_REDUCE_SCATTER) {  // aggregator keeps its shard: sums written in place into `out`
-    TRY(omr_check(omr_scatter_blocks_f32(p->sums, p->shard_list, static_cast<uint32_t>(nres_me), p->B, out, stream),
-                  "omr_scatter_blocks_f32 shard"));
-    TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
-    if (sent_blocks) *sent_blocks = total_send - per(me, me);
-    if (union_blocks) *union_blocks = nres_me;
-    return 0;
+  const uint64_t own_shard = per(me, me);
+  const uint64_t total_send = cnt(me, N) - own_shard;
+  // 4. pack own non-zero blocks of the other shards (block order == shard order), send each slice to its
+  //    aggregator (common.cc:405-407, :449); receive this shard's blocks from every peer
+  std::vector<uint64_t> roff(N, 0);
+  if (N > 1) {
+    if (total_send)
+      TRY(omr_check(omr_move_blocks_f32(x, p->packed, 0, p->masks_all + static_cast<uint64_t>(me) * rows,
+                                        p->prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
+                                        r1, stream), "omr_move_blocks_f32 pack"));
+    std::vector<Slice> sends(N), recvs(N);
+    uint64_t acc = 0;
+    for (int s = 0; s < N; ++s) {
+      const uint64_t k0 = cnt(me, s) - (s > me ? own_shard : 0);
+      sends[s] = Slice{p->packed + k0 * B, s == me ? 0 : per(me, s) * B * sizeof(float)};
+      roff[s] = acc;
+      recvs[s] = Slice{p->recv + acc * B, s == me ? 0 : per(s, me) * B * sizeof(float)};
+      if (s != me) acc += per(s, me);
+    }
+    TRY(p->d->exchange(sends, recvs, st));
   }
-  // 6. sums back to every worker, scattered in place
-  std::vector<Slice> rs(N), rr(N);
-  for (int s = 0; s < N; ++s) {
-    rs[s] = Slice{p->sums, s == me ? 0 : nres_me * B * sizeof(float)};
-    rr[s] = Slice{p->results + cnt(N, s) * B, per(N, s) * B * sizeof(float)};
+  // 5. aggregator: rank-order shard sums (server.cc:97-98), own contribution read in place
+  const bool rs_mode = mode == OMR_ROUND_REDUCE_SCATTER;
+  float* sums = rs_mode ? out : p->results + cnt(N, me) * B;
+  TRY(omr_check(omr_shard_sum_f32(x, static_cast<uint32_t>(me), p->recv, roff.data(), p->masks_all, N, p->prefix,
+                                  p->wset, rows, r0, r1, p->lanes, p->B, rs_mode ? 0 : 1, sums, stream),
+                "omr_shard_sum_f32"));
+  if (!rs_mode) {
+    // 6. sums back to every worker (server.cc:162), scattered in place (client.cc:89)
+    if (N > 1) {
+      std::vector<Slice> ss(N), sr(N);
+      for (int s = 0; s < N; ++s) {
+        ss[s] = Slice{sums, s == me ? 0 : per(N, me) * B * sizeof(float)};
+        sr[s] = Slice{p->results + cnt(N, s) * B, s == me ? 0 : per(N, s) * B * sizeof(float)};
+      }
+      TRY(p->d->exchange(ss, sr, st));
+    }
+    TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, p->wset, p->prefix + static_cast<uint64_t>(N) * (rows + 1),
+                                      rows, p->lanes, p->B, 0, 0, stream), "omr_move_blocks_f32 unpack"));
   }
-  if (nres_me)
-    TRY(hip_check(hipMemcpyAsync(rr[me].ptr, p->sums, nres_me * B * sizeof(float), hipMemcpyDeviceToDevice, st),
-                  "hipMemcpyAsync own sums"));
-  rr[me].bytes = 0;
-  TRY(p->d->exchange(rs, rr, st));
-  const uint64_t total_res = cnt(N, N);
-  TRY(omr_check(omr_compact(wset, 0, rows, p->lanes, p->full_list, p->count + 2, p->compact_ws, p->compact_ws_bytes,
-                            stream), "omr_compact full"));
-  TRY(omr_check(omr_scatter_blocks_f32(p->results, p->full_list, static_cast<uint32_t>(total_res), p->B, out, stream),
-                "omr_scatter_blocks_f32"));
   TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
-  if (sent_blocks) *sent_blocks = total_send - per(me, me);
-  if (union_blocks) *union_blocks = total_res;
+  if (sent_blocks) *sent_blocks = total_send;
+  if (union_blocks) *union_blocks = rs_mode ? per(N, me) : cnt(N, N);
   return 0;
 }
 

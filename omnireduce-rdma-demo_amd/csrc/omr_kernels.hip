@@ -215,6 +215,7 @@ struct FusedArgs {
   uint32_t* next;
   uint32_t* cnt;       // [parts*lanes] arrival counters (K > 1), zero between launches
   uint64_t* summary;   // [parts*lanes*K] {first << 32 | last} per segment (K > 1)
+  uint64_t* masks;     // [rows] row masks, zero on entry, non-zero blocks OR-ed in (multi-rank round), or null
   uint32_t lanes, rpp, K, S, block, sentinel;
 };
 
@@ -282,6 +283,8 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
       const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
       const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : carry;
       if (nr != kNone) a.next[blk] = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+      if (a.masks != nullptr && ((bits >> lane) & 1u))
+        (void)__hip_atomic_fetch_or(&a.masks[row0 + rr + lane], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (bits != 0) {
       if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
@@ -744,6 +747,253 @@ __global__ __launch_bounds__(kWGThreads) void k_list_sum(WorkerPtrs in, uint32_t
   }
 }
 
+// ---------------------------------------------------------------- multi-rank round kernels (mask-addressed)
+//
+// The round's block movement is addressed straight from row masks and their popcount prefixes, with no block
+// lists: the k-th set bit of a mask (in block order) is block k of that mask's packed stream.  Work unit = one
+// wave per (row, group of SL lanes): at B=256 eight 1 KiB blocks, all loaded before any is stored, absent
+// blocks' loads/stores pointed past the descriptor range (dropped), so every wave has SL*VEC loads in flight
+// and a static memory-operation count.
+template <int VEC>
+constexpr int move_slots() {
+  return (8 / VEC) < 2 ? 2 : 8 / VEC;
+}
+
+__device__ __forceinline__ uint64_t below(uint32_t l) { return l >= 64 ? ~0ull : ((1ull << l) - 1ull); }
+
+// One workgroup per mask array (count worker arrays + the write set), 1024 threads, each a contiguous run of
+// rows: popcounts -> block-wide exclusive scan -> prefix[a][r]; counts[a][s] = prefix[a][bounds[s]].  The
+// write-set workgroup also forms union = OR of the workers (the aggregator's min_next domain, server.cc:86-96)
+// and write set = union | lane heads (every lane head is sent and returned: client.cc:201-205), and clears the
+// next round's own-mask buffer.
+constexpr int kPlanThreads = 1024;
+
+__device__ __forceinline__ uint64_t plan_row(const uint64_t* masks, uint32_t a, uint32_t count, uint64_t rows,
+                                             uint64_t r, uint32_t rpp, uint64_t all_lanes, uint64_t* uni) {
+  if (a < count) return masks[static_cast<uint64_t>(a) * rows + r];
+  uint64_t u = 0;
+  for (uint32_t c = 0; c < count; ++c) u |= masks[static_cast<uint64_t>(c) * rows + r];
+  *uni = u;
+  return (r % rpp == 0) ? (u | all_lanes) : u;
+}
+
+struct PlanArgs {
+  const uint64_t* masks;
+  uint32_t count, rpp, lanes, nbounds;
+  uint64_t rows;
+  const uint64_t* bounds;
+  uint64_t* write_set;
+  uint64_t* union_masks;
+  uint32_t* prefix;
+  uint32_t* counts;
+  uint64_t* zero_masks;
+};
+
+__global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
+  __shared__ uint32_t s_wave[kPlanThreads / 64];
+  const uint32_t arr = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint64_t all_lanes = a.lanes >= 64 ? ~0ull : ((1ull << a.lanes) - 1ull);
+  const uint64_t per = (a.rows + kPlanThreads - 1) / kPlanThreads;
+  const uint64_t rb = t * per < a.rows ? t * per : a.rows;
+  const uint64_t re = rb + per < a.rows ? rb + per : a.rows;
+  const bool ws = arr == a.count;
+  uint32_t sum = 0;
+  for (uint64_t r = rb; r < re; ++r) {
+    uint64_t u = 0;
+    const uint64_t v = plan_row(a.masks, arr, a.count, a.rows, r, a.rpp, all_lanes, &u);
+    if (ws) {
+      a.write_set[r] = v;
+      a.union_masks[r] = u;
+      if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
+    }
+    sum += static_cast<uint32_t>(__builtin_popcountll(v));
+  }
+  // block-wide exclusive scan of the per-thread sums (wave shuffles, then the 16 wave totals)
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if (lane >= static_cast<uint32_t>(d)) inc += o;
+  }
+  if (lane == 63) s_wave[wave] = inc;
+  __syncthreads();
+  uint32_t wbase = 0, total = 0;
+  for (uint32_t w = 0; w < kPlanThreads / 64; ++w) {
+    if (w < wave) wbase += s_wave[w];
+    total += s_wave[w];
+  }
+  uint32_t run = wbase + inc - sum;  // exclusive prefix at row rb
+  uint32_t* pre = a.prefix + static_cast<uint64_t>(arr) * (a.rows + 1);
+  for (uint64_t r = rb; r < re; ++r) {
+    for (uint32_t s = 0; s < a.nbounds; ++s)
+      if (a.bounds[s] == r) a.counts[arr * a.nbounds + s] = run;
+    pre[r] = run;
+    uint64_t u = 0;
+    run += static_cast<uint32_t>(__builtin_popcountll(
+        ws ? a.write_set[r] : plan_row(a.masks, arr, a.count, a.rows, r, a.rpp, all_lanes, &u)));
+  }
+  if (t == 0) {
+    pre[a.rows] = total;
+    for (uint32_t s = 0; s < a.nbounds; ++s)
+      if (a.bounds[s] >= a.rows) a.counts[arr * a.nbounds + s] = total;
+  }
+}
+
+// Dense <-> packed block movement over the set bits of one mask array (dir 0: pack, the worker's gather of
+// common.cc:405-407; dir 1: unpack, the worker's in-place result copy of client.cc:89).  Rows [skip_b, skip_e)
+// are skipped and do not occupy the packed stream.
+struct MoveArgs {
+  const float* src;
+  float* dst;
+  const uint64_t* masks;
+  const uint32_t* prefix;  // exclusive popcount prefix of `masks`, rows + 1 entries
+  uint64_t rows, skip_b, skip_e;
+  uint32_t lanes, block, dir;
+};
+
+template <int VEC>
+__global__ __launch_bounds__(kWGThreads) void k_move(MoveArgs a) {
+  constexpr int SL = move_slots<VEC>();
+  const int lane = threadIdx.x & 63;
+  const uint32_t groups = a.lanes / SL;
+  const uint32_t bbytes = a.block * 4;
+  const uint64_t units = a.rows * groups;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
+  const uint32_t skip_cnt = a.prefix[a.skip_e] - a.prefix[a.skip_b];
+  for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+       u < units; u += nw) {
+    const uint64_t r = u / groups;
+    const uint32_t l0 = static_cast<uint32_t>(u % groups) * SL;
+    if (r >= a.skip_b && r < a.skip_e) continue;
+    const uint64_t m = a.masks[r];
+    const uint32_t bits = static_cast<uint32_t>(m >> l0) & ((1u << SL) - 1u);
+    if (bits == 0) continue;
+    const uint64_t k0 = a.prefix[r] + static_cast<uint64_t>(__builtin_popcountll(m & below(l0))) -
+                        (r >= a.skip_e ? skip_cnt : 0u);
+    const uint32_t nk = static_cast<uint32_t>(__builtin_popcount(bits));
+    float* dense = const_cast<float*>(a.dir == 0 ? a.src : a.dst) + (r * a.lanes + l0) * a.block;
+    float* packed = const_cast<float*>(a.dir == 0 ? a.dst : a.src) + k0 * a.block;
+    const __amdgpu_buffer_rsrc_t rd = chunk_rsrc(dense, SL * bbytes);
+    const __amdgpu_buffer_rsrc_t rp = chunk_rsrc(packed, nk * bbytes);
+    const __amdgpu_buffer_rsrc_t rs = a.dir == 0 ? rd : rp;
+    const __amdgpu_buffer_rsrc_t rt = a.dir == 0 ? rp : rd;
+    v4f v[SL][VEC];
+#pragma unroll
+    for (int j = 0; j < SL; ++j) {
+      const bool has = (bits >> j) & 1u;
+      const uint32_t kj = static_cast<uint32_t>(__builtin_popcount(bits & ((1u << j) - 1u)));
+      const uint32_t off = (a.dir == 0 ? j : kj) * bbytes;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rs, (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0,
+                                              kLoadAux));
+    }
+#pragma unroll
+    for (int j = 0; j < SL; ++j) {
+      const bool has = (bits >> j) & 1u;
+      const uint32_t kj = static_cast<uint32_t>(__builtin_popcount(bits & ((1u << j) - 1u)));
+      const uint32_t off = (a.dir == 0 ? kj : j) * bbytes;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v[j][q]), rt,
+                                               (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0, 0);
+    }
+  }
+}
+
+// Aggregator shard sum over rows [r0, r1) of the write set (server.cc:83-99 with the RDMA hop replaced by the
+// transport): for every write-set block, ((0.0f + x_a0) + x_a1) + ... over the workers whose mask has it, in
+// rank order.  Worker `me`'s contribution is read in place from its dense tensor `own`; worker a's from its
+// received stream at recv + recv_off[a] blocks (its shard blocks in block order).  Output dense (block
+// position, in place) or packed (write-set order of the shard, for the sums' return trip).
+struct ShardArgs {
+  const float* own;
+  const float* recv;
+  uint64_t recv_off[OMR_MAX_WORKERS];
+  const uint64_t* masks;  // [count][rows]
+  const uint32_t* prefix;  // [count + 1][rows + 1]; index count = write set
+  const uint64_t* write_set;
+  float* out;
+  uint64_t rows, r0, r1;
+  uint32_t count, me, lanes, block, packed_out;
+};
+
+template <int VEC>
+__global__ __launch_bounds__(kWGThreads) void k_shard_sum(ShardArgs a) {
+  constexpr int SL = move_slots<VEC>();
+  const int lane = threadIdx.x & 63;
+  const uint32_t groups = a.lanes / SL;
+  const uint32_t bbytes = a.block * 4;
+  const uint64_t units = (a.r1 - a.r0) * groups;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
+  const uint32_t* pws = a.prefix + static_cast<uint64_t>(a.count) * (a.rows + 1);
+  for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+       u < units; u += nw) {
+    const uint64_t r = a.r0 + u / groups;
+    const uint32_t l0 = static_cast<uint32_t>(u % groups) * SL;
+    const uint64_t w = a.write_set[r];
+    const uint32_t bits = static_cast<uint32_t>(w >> l0) & ((1u << SL) - 1u);
+    if (bits == 0) continue;
+    // lane c < count: worker c's mask and the first packed block of this group in its stream
+    uint64_t mc = 0, kc = 0;
+    if (static_cast<uint32_t>(lane) < a.count) {
+      mc = a.masks[static_cast<uint64_t>(lane) * a.rows + r];
+      const uint32_t* pc = a.prefix + static_cast<uint64_t>(lane) * (a.rows + 1);
+      kc = a.recv_off[lane] + (pc[r] - pc[a.r0]) + static_cast<uint64_t>(__builtin_popcountll(mc & below(l0)));
+    }
+    const uint32_t gbits = static_cast<uint32_t>(mc >> l0) & bits;  // lane c: its blocks in this group
+    v4f acc[SL][VEC];
+#pragma unroll
+    for (int j = 0; j < SL; ++j)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc[j][q] = v4f{0.f, 0.f, 0.f, 0.f};
+    // contributors of the group, rank order: one worker at a time, all of its (up to SL) blocks loaded at once
+    uint64_t cont = __ballot(gbits != 0) & (a.count >= 64 ? ~0ull : ((1ull << a.count) - 1ull));
+    while (cont != 0) {
+      const uint32_t c = static_cast<uint32_t>(__builtin_ctzll(cont));
+      cont &= cont - 1;
+      const uint32_t cb = __builtin_amdgcn_readlane(gbits, c);
+      const __amdgpu_buffer_rsrc_t src =
+          c == a.me ? chunk_rsrc(a.own + (r * a.lanes + l0) * a.block, SL * bbytes)
+                    : chunk_rsrc(a.recv + (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(kc), c)) |
+                                           (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(kc >> 32), c)) << 32)) *
+                                              a.block,
+                                 static_cast<uint32_t>(__builtin_popcount(cb)) * bbytes);
+      v4f v[SL][VEC];
+#pragma unroll
+      for (int j = 0; j < SL; ++j) {
+        const bool has = (cb >> j) & 1u;
+        const uint32_t off = (c == a.me ? j : static_cast<uint32_t>(__builtin_popcount(cb & ((1u << j) - 1u)))) * bbytes;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q)
+          v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                                src, (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0,
+                                                kLoadAux));
+      }
+#pragma unroll
+      for (int j = 0; j < SL; ++j)
+        if ((cb >> j) & 1u) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) acc[j][q] = add4(acc[j][q], v[j][q]);
+        }
+    }
+    const uint64_t kw = pws[r] - pws[a.r0] + static_cast<uint64_t>(__builtin_popcountll(w & below(l0)));
+    float* obase = a.packed_out ? a.out + kw * a.block : a.out + (r * a.lanes + l0) * a.block;
+    const __amdgpu_buffer_rsrc_t dst =
+        chunk_rsrc(obase, (a.packed_out ? static_cast<uint32_t>(__builtin_popcount(bits)) : SL) * bbytes);
+#pragma unroll
+    for (int j = 0; j < SL; ++j) {
+      const bool has = (bits >> j) & 1u;
+      const uint32_t off = (a.packed_out ? static_cast<uint32_t>(__builtin_popcount(bits & ((1u << j) - 1u))) : j) * bbytes;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[j][q]), dst,
+                                               (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0, 0);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- synthetic fill (client.cc:401-419)
 
 __device__ __forceinline__ float hash_uniform(uint64_t idx, uint32_t seed) {
@@ -863,7 +1113,7 @@ size_t fused_workspace_bytes(const Layout& L, const FusedShape& f) {
 }
 
 int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* out, int32_t* flags, uint32_t* next,
-                 void* ws, hipStream_t st) {
+                 void* ws, hipStream_t st, uint64_t* masks = nullptr) {
   FusedArgs a;
   a.x = x;
   a.out = out;
@@ -879,6 +1129,7 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
   a.S = f.S;
   a.block = L.block;
   a.sentinel = omr_sentinel(L.block, L.lanes);
+  a.masks = masks;
   const unsigned grid = static_cast<unsigned>(cols * f.K);
   constexpr int T = 64 * kFusedWaves;
   switch (L.vec) {
@@ -1239,6 +1490,132 @@ int omr_scatter_blocks_f32(const float* packed, const uint32_t* block_list, uint
     default: k_scatter<4><<<g, kWGThreads, 0, st>>>(packed, block_list, num_list, dst); break;
   }
   return launch_status("k_scatter");
+}
+
+// ---------------------------------------------------------------- multi-rank round (mask-addressed)
+
+int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                        int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out, void* workspace,
+                        size_t workspace_bytes, omr_stream_t stream) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  if (buf == nullptr || next_offsets == nullptr || row_masks == nullptr)
+    return fail("worker_scan: buf, next_offsets and row_masks are required");
+  if (reinterpret_cast<uintptr_t>(buf) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 16 != 0)
+    return fail("worker_scan: buffers must be 16-byte aligned");
+  const FusedShape f = fused_shape(L);
+  const size_t need = fused_workspace_bytes(L, f);
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need))
+    return fail("worker_scan: needs a zero-initialised workspace of %zu bytes", need);
+  return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks);
+}
+
+int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
+                   uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
+                   uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
+                   omr_stream_t stream) {
+  if (count == 0 || count > OMR_MAX_WORKERS) return fail("round_plan: count %u out of range", count);
+  if (rows == 0 || rows_per_part == 0 || rows % rows_per_part != 0) return fail("round_plan: bad rows");
+  if (num_lanes == 0 || num_lanes > 64) return fail("round_plan: num_lanes %u out of range", num_lanes);
+  if (row_masks == nullptr || write_set == nullptr || union_masks == nullptr || prefix == nullptr ||
+      (num_bounds > 0 && (bounds == nullptr || counts == nullptr)))
+    return fail("round_plan: NULL pointer");
+  if (rows > 0xFFFFFFFFull / 64) return fail("round_plan: too many rows");
+  PlanArgs a;
+  a.masks = row_masks;
+  a.count = count;
+  a.rpp = rows_per_part;
+  a.lanes = num_lanes;
+  a.nbounds = num_bounds;
+  a.rows = rows;
+  a.bounds = bounds;
+  a.write_set = write_set;
+  a.union_masks = union_masks;
+  a.prefix = prefix;
+  a.counts = counts;
+  a.zero_masks = zero_masks;
+  k_round_plan<<<count + 1, kPlanThreads, 0, S(stream)>>>(a);
+  return launch_status("k_round_plan");
+}
+
+int omr_move_blocks_f32(const float* src, float* dst, int dir, const uint64_t* row_masks, const uint32_t* prefix,
+                        uint64_t rows, uint32_t num_lanes, uint32_t block_size, uint64_t skip_begin,
+                        uint64_t skip_end, omr_stream_t stream) {
+  if (dir != 0 && dir != 1) return fail("move_blocks: dir must be 0 (pack) or 1 (unpack)");
+  if (block_size != 256 && block_size != 512 && block_size != 1024)
+    return fail("move_blocks: block_size %u unsupported", block_size);
+  const uint32_t vec = block_size / 256;
+  const uint32_t sl = vec == 1 ? 8u : (vec == 2 ? 4u : 2u);
+  if (num_lanes == 0 || num_lanes > 64 || num_lanes % sl != 0) return fail("move_blocks: num_lanes %u", num_lanes);
+  if (skip_begin > skip_end || skip_end > rows) return fail("move_blocks: bad skip range");
+  if (rows == 0) return 0;
+  if (src == nullptr || dst == nullptr || row_masks == nullptr || prefix == nullptr)
+    return fail("move_blocks: NULL pointer");
+  if (reinterpret_cast<uintptr_t>(src) % 16 != 0 || reinterpret_cast<uintptr_t>(dst) % 16 != 0)
+    return fail("move_blocks: buffers must be 16-byte aligned");
+  MoveArgs a;
+  a.src = src;
+  a.dst = dst;
+  a.masks = row_masks;
+  a.prefix = prefix;
+  a.rows = rows;
+  a.skip_b = skip_begin;
+  a.skip_e = skip_end;
+  a.lanes = num_lanes;
+  a.block = block_size;
+  a.dir = static_cast<uint32_t>(dir);
+  const unsigned g = grid_for(rows * (num_lanes / sl));
+  hipStream_t st = S(stream);
+  switch (vec) {
+    case 1: k_move<1><<<g, kWGThreads, 0, st>>>(a); break;
+    case 2: k_move<2><<<g, kWGThreads, 0, st>>>(a); break;
+    default: k_move<4><<<g, kWGThreads, 0, st>>>(a); break;
+  }
+  return launch_status("k_move");
+}
+
+int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const uint64_t* recv_offsets,
+                      const uint64_t* row_masks, uint32_t count, const uint32_t* prefix, const uint64_t* write_set,
+                      uint64_t rows, uint64_t row_begin, uint64_t row_end, uint32_t num_lanes, uint32_t block_size,
+                      int packed_out, float* out, omr_stream_t stream) {
+  if (count == 0 || count > OMR_MAX_WORKERS) return fail("shard_sum: count %u out of range", count);
+  if (block_size != 256 && block_size != 512 && block_size != 1024)
+    return fail("shard_sum: block_size %u unsupported", block_size);
+  const uint32_t vec = block_size / 256;
+  const uint32_t sl = vec == 1 ? 8u : (vec == 2 ? 4u : 2u);
+  if (num_lanes == 0 || num_lanes > 64 || num_lanes % sl != 0) return fail("shard_sum: num_lanes %u", num_lanes);
+  if (row_begin > row_end || row_end > rows) return fail("shard_sum: bad row range");
+  if (row_end == row_begin) return 0;
+  if (row_masks == nullptr || prefix == nullptr || write_set == nullptr || out == nullptr ||
+      (me < count && own == nullptr) || (count > 1 && recv == nullptr) || recv_offsets == nullptr)
+    return fail("shard_sum: NULL pointer");
+  if (reinterpret_cast<uintptr_t>(out) % 16 != 0 || reinterpret_cast<uintptr_t>(own) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(recv) % 16 != 0)
+    return fail("shard_sum: buffers must be 16-byte aligned");
+  ShardArgs a;
+  a.own = own;
+  a.recv = recv;
+  for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) a.recv_off[c] = c < count ? recv_offsets[c] : 0;
+  a.masks = row_masks;
+  a.prefix = prefix;
+  a.write_set = write_set;
+  a.out = out;
+  a.rows = rows;
+  a.r0 = row_begin;
+  a.r1 = row_end;
+  a.count = count;
+  a.me = me;
+  a.lanes = num_lanes;
+  a.block = block_size;
+  a.packed_out = packed_out ? 1u : 0u;
+  const unsigned g = grid_for((row_end - row_begin) * (num_lanes / sl));
+  hipStream_t st = S(stream);
+  switch (vec) {
+    case 1: k_shard_sum<1><<<g, kWGThreads, 0, st>>>(a); break;
+    case 2: k_shard_sum<2><<<g, kWGThreads, 0, st>>>(a); break;
+    default: k_shard_sum<4><<<g, kWGThreads, 0, st>>>(a); break;
+  }
+  return launch_status("k_shard_sum");
 }
 
 }  // extern "C"

@@ -1,0 +1,198 @@
+"""GPU parity of the mask-addressed multi-rank round kernels, called through the C ABI (include/omr.h):
+omr_worker_scan_f32 (scan + row masks), omr_round_plan (union / write set / prefixes / shard counts, the
+aggregator bookkeeping of server.cc:83-96), omr_move_blocks_f32 (pack common.cc:405-407 / unpack client.cc:89)
+and omr_shard_sum_f32 (server.cc:97-98 in rank order).  Checked against the oracle (flags, masks, next chains,
+block sums) and plain numpy restatements of the index arithmetic.  Bar: bit-exact (integer work and rank-order
+fp32 sums, 0 ulp)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from omr import Layout, _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def popc(a):
+    a = a.astype(np.uint64)
+    return np.array([bin(int(v)).count("1") for v in a.ravel()], dtype=np.int64).reshape(a.shape)
+
+
+def np_prefix(masks):
+    c = popc(masks)
+    return np.concatenate([[0], np.cumsum(c)]).astype(np.uint32)
+
+
+def np_write_set(masks, rpp, lanes):
+    u = np.bitwise_or.reduce(masks, axis=0) if len(masks) else np.zeros(masks.shape[1], np.uint64)
+    w = u.copy()
+    allm = np.uint64((1 << lanes) - 1) if lanes < 64 else np.uint64(0xFFFFFFFFFFFFFFFF)
+    w[::rpp] |= allm
+    return u, w
+
+
+def set_blocks(mask_rows, lanes, r0=0, r1=None, skip=None):
+    """Global block indices of the set bits of rows [r0, r1) in block order (optionally skipping a row range)."""
+    r1 = len(mask_rows) if r1 is None else r1
+    out = []
+    for r in range(r0, r1):
+        if skip is not None and skip[0] <= r < skip[1]:
+            continue
+        m = int(mask_rows[r])
+        out += [r * lanes + l for l in range(lanes) if (m >> l) & 1]
+    return np.array(out, dtype=np.int64)
+
+
+@pytest.mark.parametrize("n,B,density", [(1 << 20, 256, 0.3), (4 << 20, 256, 0.095), (16 << 20, 1024, 0.0099),
+                                         (8 << 20, 512, 0.49), (20 << 20, 1024, 0.2)])
+def test_worker_scan_masks(gpu, n, B, density):
+    L = Layout(n=n, block_size=B, num_threads=8 if n != 20 << 20 else 5)
+    x = oracle.fill(oracle.gen_bitmap(2, density, L.nb), B, mode=1, seed=3)
+    lib = _lib.load()
+    xd = torch.from_numpy(x).to(gpu)
+    flags = torch.zeros(L.nb, dtype=torch.int32, device=gpu)
+    nxt = torch.zeros(L.nb, dtype=torch.int32, device=gpu)
+    masks = torch.zeros(L.rows, dtype=torch.int64, device=gpu)
+    wsb = lib.omr_scan_workspace_bytes(L.n, B, L.num_lanes, L.num_threads)
+    ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=gpu)
+    for _ in range(2):  # twice: the segment counters reset themselves; masks re-zeroed by the caller
+        masks.zero_()
+        assert lib.omr_worker_scan_f32(P(xd), L.n, B, L.num_lanes, L.num_threads, P(flags), P(nxt), P(masks), None,
+                                       P(ws), wsb, stream()) == 0, lib.omr_last_error()
+        torch.cuda.synchronize()
+        f = oracle.flags_from_data(x, B)
+        assert (flags.cpu().numpy() == f).all()
+        assert (masks.cpu().numpy().view(np.uint64) == oracle.row_masks(f, L.num_lanes)).all()
+        assert (nxt.cpu().numpy().view(np.uint32) == oracle.next_offsets(f, L.n, B, L.num_lanes, L.num_threads)).all()
+    assert torch.equal(xd, torch.from_numpy(x).to(gpu))  # out = NULL: the tensor is not written
+
+
+@pytest.mark.parametrize("count,rows,rpp,lanes", [(1, 64, 8, 64), (3, 512, 64, 64), (8, 4096, 512, 64),
+                                                   (5, 1280, 256, 16), (16, 100, 25, 32)])
+def test_round_plan(gpu, count, rows, rpp, lanes):
+    rng = np.random.default_rng(count * 1000 + rows)
+    lane_mask = (1 << lanes) - 1 if lanes < 64 else (1 << 64) - 1
+    dens = rng.random(count) * 0.5
+    masks = np.zeros((count, rows), dtype=np.uint64)
+    for c in range(count):
+        bits = rng.random((rows, lanes)) < dens[c]
+        masks[c] = (bits.astype(np.uint64) << np.arange(lanes, dtype=np.uint64)).sum(axis=1).astype(np.uint64)
+        masks[c] &= np.uint64(lane_mask)
+    N = max(1, min(count, 8))
+    bounds = np.array([s * rows // N for s in range(N + 1)], dtype=np.uint64)
+    lib = _lib.load()
+    md = torch.from_numpy(masks.view(np.int64)).to(gpu)
+    bd = torch.from_numpy(bounds.view(np.int64)).to(gpu)
+    wset = torch.zeros(rows, dtype=torch.int64, device=gpu)
+    umask = torch.zeros(rows, dtype=torch.int64, device=gpu)
+    prefix = torch.zeros((count + 1) * (rows + 1), dtype=torch.int32, device=gpu)
+    counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int32, device=gpu)
+    zero = torch.full((rows,), -1, dtype=torch.int64, device=gpu)
+    assert lib.omr_round_plan(P(md), count, rows, rpp, lanes, P(bd), N + 1, P(wset), P(umask), P(prefix), P(counts),
+                              P(zero), stream()) == 0, lib.omr_last_error()
+    torch.cuda.synchronize()
+    u, w = np_write_set(masks, rpp, lanes)
+    assert (umask.cpu().numpy().view(np.uint64) == u).all()
+    assert (wset.cpu().numpy().view(np.uint64) == w).all()
+    pre = prefix.cpu().numpy().view(np.uint32).reshape(count + 1, rows + 1)
+    cn = counts.cpu().numpy().view(np.uint32).reshape(count + 1, N + 1)
+    for a in range(count + 1):
+        exp = np_prefix(masks[a] if a < count else w)
+        assert (pre[a] == exp).all(), a
+        assert (cn[a] == exp[bounds.astype(np.int64)]).all(), a
+    assert int(zero.count_nonzero()) == 0
+
+
+@pytest.mark.parametrize("B,rows,skip", [(256, 512, (0, 0)), (256, 512, (128, 256)), (512, 256, (200, 256)),
+                                         (1024, 300, (0, 100)), (256, 64, (0, 64))])
+def test_move_blocks_pack_unpack(gpu, B, rows, skip):
+    lanes = 16384 // B
+    rng = np.random.default_rng(rows + B)
+    bits = rng.random((rows, lanes)) < 0.3
+    masks = (bits.astype(np.uint64) << np.arange(lanes, dtype=np.uint64)).sum(axis=1).astype(np.uint64)
+    pre = np_prefix(masks)
+    n = rows * lanes * B
+    x = rng.standard_normal(n).astype(np.float32)
+    lib = _lib.load()
+    xd = torch.from_numpy(x).to(gpu)
+    md = torch.from_numpy(masks.view(np.int64)).to(gpu)
+    pd = torch.from_numpy(pre.view(np.int32)).to(gpu)
+    blocks = set_blocks(masks, lanes, skip=skip)
+    packed = torch.full((max(len(blocks), 1) * B,), np.nan, dtype=torch.float32, device=gpu)
+    assert lib.omr_move_blocks_f32(P(xd), P(packed), 0, P(md), P(pd), rows, lanes, B, skip[0], skip[1],
+                                   stream()) == 0, lib.omr_last_error()
+    torch.cuda.synchronize()
+    exp = x.reshape(-1, B)[blocks].ravel()
+    assert (packed.cpu().numpy()[: len(exp)].view(np.uint32) == exp.view(np.uint32)).all()
+    # unpack back into a fresh dense buffer: listed blocks restored, everything else untouched
+    dense = torch.full((n,), -7.0, dtype=torch.float32, device=gpu)
+    assert lib.omr_move_blocks_f32(P(packed), P(dense), 1, P(md), P(pd), rows, lanes, B, skip[0], skip[1],
+                                   stream()) == 0, lib.omr_last_error()
+    torch.cuda.synchronize()
+    want = np.full(n, -7.0, dtype=np.float32).reshape(-1, B)
+    want[blocks] = x.reshape(-1, B)[blocks]
+    assert (dense.cpu().numpy().view(np.uint32) == want.ravel().view(np.uint32)).all()
+
+
+@pytest.mark.parametrize("count,me,B,packed_out", [(1, 0, 256, 0), (3, 1, 256, 0), (3, 2, 256, 1), (8, 5, 256, 1),
+                                                   (4, 0, 1024, 0), (2, 1, 512, 1), (16, 7, 256, 0)])
+def test_shard_sum(gpu, count, me, B, packed_out):
+    L = Layout(n=(2 << 20) if B == 256 else (4 << 20), block_size=B)
+    lanes, rows = L.num_lanes, L.rows
+    xs = [oracle.fill(oracle.gen_bitmap(c, 0.2, L.nb), B, mode=1, seed=11 + c) for c in range(count)]
+    flags = [oracle.flags_from_data(x, B) for x in xs]
+    masks = np.stack([oracle.row_masks(f, lanes) for f in flags])
+    u, wset = np_write_set(masks, L.rows_per_part, lanes)
+    N = 4
+    r0, r1 = rows // N, 3 * rows // N  # a two-shard-wide row range
+    # worker c != me sends its non-zero blocks of [r0, r1) in block order; streams concatenated in rank order
+    streams, roff, acc = [], [], 0
+    for c in range(count):
+        roff.append(acc)
+        if c != me:
+            bl = set_blocks(masks[c], lanes, r0, r1)
+            streams.append(xs[c].reshape(-1, B)[bl])
+            acc += len(bl)
+    recv = np.concatenate(streams).ravel() if streams and acc else np.zeros(B, np.float32)
+    prefix = np.concatenate([np_prefix(masks[c]) for c in range(count)] + [np_prefix(wset)])
+    lib = _lib.load()
+    own = torch.from_numpy(xs[me]).to(gpu)
+    recvd = torch.from_numpy(recv.astype(np.float32)).to(gpu)
+    md = torch.from_numpy(masks.view(np.int64).ravel()).to(gpu)
+    pd = torch.from_numpy(prefix.view(np.int32)).to(gpu)
+    wd = torch.from_numpy(wset.view(np.int64)).to(gpu)
+    roff_h = (ctypes.c_uint64 * count)(*roff)
+    wblocks = set_blocks(wset, lanes, r0, r1)
+    if packed_out:
+        out = torch.full((len(wblocks) * B,), np.nan, dtype=torch.float32, device=gpu)
+    else:
+        out = own.clone()  # dense, in place semantics: other blocks keep x_me
+    assert lib.omr_shard_sum_f32(P(own), me, P(recvd), roff_h, P(md), count, P(pd), P(wd), rows, r0, r1, lanes, B,
+                                 packed_out, P(out), stream()) == 0, lib.omr_last_error()
+    torch.cuda.synchronize()
+    # expected: rank-order sums from +0.0 over the workers that flag the block (server.cc:97-98, :148-150)
+    exp_blocks = np.zeros((len(wblocks), B), dtype=np.float32)
+    for i, b in enumerate(wblocks):
+        s = np.zeros(B, dtype=np.float32)
+        for c in range(count):
+            if flags[c][b]:
+                s = (s + xs[c].reshape(-1, B)[b]).astype(np.float32)
+        exp_blocks[i] = s
+    got = out.cpu().numpy()
+    if packed_out:
+        assert (got.view(np.uint32) == exp_blocks.ravel().view(np.uint32)).all()
+    else:
+        want = xs[me].copy().reshape(-1, B)
+        want[wblocks] = exp_blocks
+        assert (got.view(np.uint32) == want.ravel().view(np.uint32)).all()
