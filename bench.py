@@ -104,8 +104,9 @@ def fused_bytes(L: Layout, bm) -> int:
 
 
 def scan_only_bytes(L: Layout) -> int:
-    """Worker scan without the fused sum (N>1): read S, write int32 flags and row masks."""
-    return L.nbytes + L.nb * 4 + L.rows * 8
+    """The round's worker scan (N>1, omr_worker_scan_f32, no sum): read S, write int32 flags, uint32 next
+    offsets and uint64 row masks."""
+    return L.nbytes + L.nb * 8 + L.rows * 8
 
 
 def step_algorithmic_bytes(L: Layout, bitmaps, m: int) -> int:
@@ -254,14 +255,16 @@ def main():
     kernel_name = ("k_scan1f (single pass: scan + sum + next)" if (m == 1 and args.kernel == "fused") else
                    ("k_scan1" if m == 1 else "k_scanm"))
     if dist_mode:
-        kernel_name = "k_scan1 (worker scan, no out)"
+        kernel_name = ("k_scan1f (round worker scan: flags + next + row masks, no out)" if args.dist_impl == "cpp"
+                       else "k_scan1 (worker scan, no out)")
     if dist_mode and args.dist_impl == "cpp":
         # the C++ round is one call; time its worker-scan kernel in its own event-bracketed loop, same data
-        plan1 = ops.ScanSumPlan(L, 1, with_next=False, device=dev)
+        # (masks not re-zeroed between launches: same atomics, timing only)
+        plan1 = ops.ScanSumPlan(L, 1, device=dev, fused=True, row_masks=True)
         for i in range(min(args.steps, 50)):
             xs, _ = sets[i % len(sets)]
             kev[i][0].record(stream)
-            plan1.run(xs, None, with_next=False)
+            plan1.run(xs, None, zero_masks=False)
             kev[i][1].record(stream)
         torch.cuda.synchronize()
         kev = kev[:min(args.steps, 50)]

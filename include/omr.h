@@ -202,11 +202,14 @@ int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint3
  *   prefix[a*(rows+1) + r] = set bits of array a in rows [0, r), for a < count (workers) and a == count (the
  *                    write set); r = rows gives the total;
  *   counts[a*num_bounds + s] = prefix[a][bounds[s]] (bounds: device uint64[num_bounds], each <= rows);
- *   zero_masks (device uint64[rows] or NULL) is cleared (the next round's omr_worker_scan_f32 target). */
+ *   zero_masks (device uint64[rows] or NULL) is cleared (the next round's omr_worker_scan_f32 target).
+ * Completion notice (both NULL, or both set): once every count is visible system-wide, *done_flag = seq.  `arrive`
+ * is a device uint32 zeroed once by the caller and left zeroed; done_flag may be pinned host memory (mapped), so
+ * a host can poll it instead of synchronising the stream (the multi-rank round does). */
 int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                    uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
                    uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                   omr_stream_t stream);
+                   uint32_t* arrive, uint32_t* done_flag, uint32_t seq, omr_stream_t stream);
 
 /* Block movement addressed by a row mask and its prefix (no block list): the k-th set bit of `row_masks` over
  * rows [0, rows) minus [skip_begin, skip_end) is block k of the packed stream.

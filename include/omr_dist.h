@@ -59,7 +59,9 @@ int omr_ar_plan_destroy(omr_ar_plan* plan);
  * result, otherwise it must already hold x's values outside that set.  flags / next_offsets / union_next (device,
  * nb entries each, may be NULL) receive the worker's flags, its next-offset chain and the aggregator chain.
  * *sent_blocks / *union_blocks (host, may be NULL) receive this rank's off-rank sent blocks and the write-set size.
- * Synchronises `stream` once (block counts for the transport) and on return. */
+ * Waits once mid-round for the block counts (the transport needs host-side sizes; the bookkeeping kernel stores
+ * them straight into pinned host memory) and returns with the rest of the round enqueued on `stream`:
+ * synchronise `stream` before reading out / flags / next_offsets / union_next. */
 int omr_sparse_allreduce_f32(omr_ar_plan* plan, const float* x, float* out, int32_t* flags,
                              uint32_t* next_offsets, uint32_t* union_next, uint64_t* sent_blocks,
                              uint64_t* union_blocks, omr_stream_t stream);

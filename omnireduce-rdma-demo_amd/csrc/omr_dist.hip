@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -143,6 +144,25 @@ struct LocalDist final : omr_dist {
   }
 };
 
+// Spin until the plan kernel's completion notice (the round's sequence number) lands in pinned memory: the host
+// learns the block counts about a microsecond after the kernel ends, without an event or a stream sync.  Bails
+// out if the stream drains without the notice (a failed launch) or after a minute (a stuck peer).
+int wait_flag(const uint32_t* flag, uint32_t seq, hipStream_t st) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 1;; ++spin) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return 0;
+    if ((spin & 4095) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q != hipSuccess && q != hipErrorNotReady) return hip_check(q, "round plan");
+      if (q == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq)
+        return derr(OMR_EINVAL, "round plan: stream idle but no completion notice (seq %u)", seq);
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+        return derr(OMR_EINVAL, "round plan: no completion notice after 60 s (seq %u)", seq);
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 template <typename T>
 int dev_alloc(T** p, size_t count) {
   return hip_check(hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(count, 1) * sizeof(T)), "hipMalloc");
@@ -163,8 +183,8 @@ struct omr_ar_plan {
   uint64_t* umask = nullptr;      // [rows] union of the workers' masks
   uint32_t* prefix = nullptr;     // [N+1][rows+1] popcount prefixes: workers, then the write set
   uint64_t* bounds_dev = nullptr;
-  uint32_t* counts_dev = nullptr;   // [N+1][N+1] prefix[a][bounds[s]]
-  uint32_t* counts_host = nullptr;  // pinned copy
+  uint32_t* counts_host = nullptr;  // [N+1][N+1] prefix[a][bounds[s]], pinned host memory the plan kernel writes
+  uint32_t* counts_map = nullptr;   // its device-side address
   float* packed = nullptr;   // own non-zero blocks of the other shards, block order
   float* recv = nullptr;     // this shard's blocks from each peer, peer-major
   float* results = nullptr;  // all-reduce: every shard's sums, write-set order
@@ -173,7 +193,10 @@ struct omr_ar_plan {
   uint32_t* unext_ws = nullptr;
   void* scan_ws = nullptr;   // omr_worker_scan_f32 segment workspace (zeroed once, self-resetting)
   size_t scan_ws_bytes = 0;
-  hipEvent_t counts_ready = nullptr;
+  uint32_t* arrive = nullptr;     // device arrival counter of the plan kernel's completion notice
+  uint32_t* flag_host = nullptr;  // pinned: the plan kernel stores the round's sequence number here
+  uint32_t* flag_map = nullptr;   // its device-side address
+  uint32_t seq = 0;
 };
 
 extern "C" {
@@ -226,11 +249,12 @@ int omr_dist_destroy(omr_dist* d) {
 
 int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p == nullptr) return 0;
-  void* devs[] = {p->own_masks, p->masks_all, p->wset,    p->umask,    p->prefix,   p->bounds_dev, p->counts_dev,
+  void* devs[] = {p->own_masks, p->masks_all, p->wset,    p->umask,    p->prefix,   p->bounds_dev,
                   p->packed,    p->recv,      p->results, p->flags_ws, p->next_ws,  p->unext_ws,   p->scan_ws};
   for (void* v : devs) (void)hipFree(v);
   (void)hipHostFree(p->counts_host);
-  if (p->counts_ready) (void)hipEventDestroy(p->counts_ready);
+  (void)hipHostFree(p->flag_host);
+  (void)hipFree(p->arrive);
   delete p;
   return 0;
 }
@@ -267,7 +291,6 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   A(dev_alloc(&p->umask, p->rows));
   A(dev_alloc(&p->prefix, static_cast<size_t>(N + 1) * (p->rows + 1)));
   A(dev_alloc(&p->bounds_dev, N + 1));
-  A(dev_alloc(&p->counts_dev, static_cast<size_t>(N + 1) * (N + 1)));
   if (N > 1) {
     A(dev_alloc(&p->packed, n));
     A(dev_alloc(&p->recv, static_cast<size_t>(N - 1) * p->shard_nb * block_size));
@@ -278,9 +301,20 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   A(dev_alloc(&p->unext_ws, p->nb));
   p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
   A(dev_alloc(reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
-  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), (N + 1) * (N + 1) * sizeof(uint32_t)),
-              "hipHostMalloc"));
-  A(hip_check(hipEventCreateWithFlags(&p->counts_ready, hipEventDisableTiming), "hipEventCreate"));
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), (N + 1) * (N + 1) * sizeof(uint32_t),
+                            hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
+  if (rc == 0)
+    A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->counts_map), p->counts_host, 0),
+                "hipHostGetDevicePointer"));
+  A(dev_alloc(&p->arrive, 1));
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), sizeof(uint32_t),
+                            hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
+  if (rc == 0) {
+    *p->flag_host = 0;
+    A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->flag_map), p->flag_host, 0),
+                "hipHostGetDevicePointer"));
+  }
+  if (rc == 0) A(hip_check(hipMemset(p->arrive, 0, sizeof(uint32_t)), "hipMemset arrive"));
   if (rc == 0) A(hip_check(hipMemset(p->own_masks, 0, p->rows * sizeof(uint64_t)), "hipMemset own masks"));
   if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset scan ws"));
   if (rc == 0)
@@ -317,14 +351,14 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   // 2. every worker's row masks
   TRY(p->d->allgather(p->own_masks, p->masks_all, rows * sizeof(uint64_t), st));
   // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for the next round
+  //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
+  const uint32_t seq = ++p->seq;
   TRY(omr_check(omr_round_plan(p->masks_all, N, rows, p->rpp, p->lanes, p->bounds_dev, NB, p->wset, p->umask,
-                               p->prefix, p->counts_dev, p->own_masks, stream), "omr_round_plan"));
-  TRY(hip_check(hipMemcpyAsync(p->counts_host, p->counts_dev, NB * NB * sizeof(uint32_t), hipMemcpyDeviceToHost, st),
-                "hipMemcpyAsync counts"));
-  TRY(hip_check(hipEventRecord(p->counts_ready, st), "hipEventRecord"));
-  // aggregator chain (server.cc:86-96 min_next) over the union, queued behind the counts copy
+                               p->prefix, p->counts_map, p->own_masks, p->arrive, p->flag_map, seq, stream),
+                "omr_round_plan"));
+  // aggregator chain (server.cc:86-96 min_next) over the union, queued right behind
   TRY(omr_check(omr_next_offsets(p->umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
-  TRY(hip_check(hipEventSynchronize(p->counts_ready), "hipEventSynchronize counts"));
+  TRY(wait_flag(p->flag_host, seq, st));
   auto cnt = [&](int a, int s) -> uint64_t { return p->counts_host[a * NB + s]; };
   auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
   const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
@@ -368,7 +402,6 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
     TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, p->wset, p->prefix + static_cast<uint64_t>(N) * (rows + 1),
                                       rows, p->lanes, p->B, 0, 0, stream), "omr_move_blocks_f32 unpack"));
   }
-  TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
   if (sent_blocks) *sent_blocks = total_send;
   if (union_blocks) *union_blocks = rs_mode ? per(N, me) : cnt(N, N);
   return 0;

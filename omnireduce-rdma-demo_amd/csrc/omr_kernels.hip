@@ -751,15 +751,45 @@ __global__ __launch_bounds__(kWGThreads) void k_list_sum(WorkerPtrs in, uint32_t
 //
 // The round's block movement is addressed straight from row masks and their popcount prefixes, with no block
 // lists: the k-th set bit of a mask (in block order) is block k of that mask's packed stream.  Work unit = one
-// wave per (row, group of SL lanes): at B=256 eight 1 KiB blocks, all loaded before any is stored, absent
-// blocks' loads/stores pointed past the descriptor range (dropped), so every wave has SL*VEC loads in flight
-// and a static memory-operation count.
+// wave per (row, group of `lg` lanes); the unit's SET bits are taken SL at a time, so a batch is SL present
+// blocks whatever the density (all loaded before any is stored; a short batch's spare slots are pointed past the
+// descriptor range and dropped, keeping the memory-operation count static).  lg is chosen on the host so that
+// there are enough units to fill the chip (whole rows when there are many rows).
 template <int VEC>
-constexpr int move_slots() {
+constexpr int move_slots() {  // blocks per batch for a pure move
+  return 16 / VEC;
+}
+template <int VEC>
+constexpr int sum_slots() {  // blocks per batch for the shard sum (accumulators + one worker's loads)
   return (8 / VEC) < 2 ? 2 : 8 / VEC;
 }
 
 __device__ __forceinline__ uint64_t below(uint32_t l) { return l >= 64 ? ~0ull : ((1ull << l) - 1ull); }
+
+// (the builtin returns int: go through uint32_t, or the low half would be sign-extended into the high half)
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t lane) {
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v)), lane));
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v >> 32)), lane));
+  return static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
+}
+
+// Takes up to SL set bits off `rem` (lowest first): their lane indices, how many, and their mask.
+template <int SL>
+__device__ __forceinline__ uint32_t take_bits(uint64_t& rem, uint32_t (&lj)[SL], uint64_t& bmask) {
+  uint32_t nv = 0;
+  bmask = 0;
+#pragma unroll
+  for (int j = 0; j < SL; ++j) {
+    lj[j] = 0;
+    if (rem != 0) {
+      lj[j] = static_cast<uint32_t>(__builtin_ctzll(rem));
+      bmask |= rem & (~rem + 1);
+      rem &= rem - 1;
+      nv = j + 1;
+    }
+  }
+  return nv;
+}
 
 // One workgroup per mask array (count worker arrays + the write set), 1024 threads, each a contiguous run of
 // rows: popcounts -> block-wide exclusive scan -> prefix[a][r]; counts[a][s] = prefix[a][bounds[s]].  The
@@ -787,6 +817,9 @@ struct PlanArgs {
   uint32_t* prefix;
   uint32_t* counts;
   uint64_t* zero_masks;
+  uint32_t* arrive;     // device arrival counter (zero between launches) or null
+  uint32_t* done_flag;  // receives `seq` once every workgroup's counts are visible system-wide, or null
+  uint32_t seq;
 };
 
 __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
@@ -837,6 +870,18 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
     for (uint32_t s = 0; s < a.nbounds; ++s)
       if (a.bounds[s] >= a.rows) a.counts[arr * a.nbounds + s] = total;
   }
+  if (a.arrive == nullptr) return;
+  // completion notice for a host that polls instead of waiting on an event: every workgroup publishes its counts
+  // system-wide and arrives; the last arrival stores the round's sequence number and re-arms the counter
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old == a.count) {
+      __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // Dense <-> packed block movement over the set bits of one mask array (dir 0: pack, the worker's gather of
@@ -848,14 +893,14 @@ struct MoveArgs {
   const uint64_t* masks;
   const uint32_t* prefix;  // exclusive popcount prefix of `masks`, rows + 1 entries
   uint64_t rows, skip_b, skip_e;
-  uint32_t lanes, block, dir;
+  uint32_t lanes, block, dir, lg;
 };
 
 template <int VEC>
 __global__ __launch_bounds__(kWGThreads) void k_move(MoveArgs a) {
   constexpr int SL = move_slots<VEC>();
   const int lane = threadIdx.x & 63;
-  const uint32_t groups = a.lanes / SL;
+  const uint32_t groups = a.lanes / a.lg;
   const uint32_t bbytes = a.block * 4;
   const uint64_t units = a.rows * groups;
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
@@ -863,41 +908,43 @@ __global__ __launch_bounds__(kWGThreads) void k_move(MoveArgs a) {
   for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
        u < units; u += nw) {
     const uint64_t r = u / groups;
-    const uint32_t l0 = static_cast<uint32_t>(u % groups) * SL;
+    const uint32_t g0 = static_cast<uint32_t>(u % groups) * a.lg;
     if (r >= a.skip_b && r < a.skip_e) continue;
     const uint64_t m = a.masks[r];
-    const uint32_t bits = static_cast<uint32_t>(m >> l0) & ((1u << SL) - 1u);
-    if (bits == 0) continue;
-    const uint64_t k0 = a.prefix[r] + static_cast<uint64_t>(__builtin_popcountll(m & below(l0))) -
-                        (r >= a.skip_e ? skip_cnt : 0u);
-    const uint32_t nk = static_cast<uint32_t>(__builtin_popcount(bits));
-    float* dense = const_cast<float*>(a.dir == 0 ? a.src : a.dst) + (r * a.lanes + l0) * a.block;
-    float* packed = const_cast<float*>(a.dir == 0 ? a.dst : a.src) + k0 * a.block;
-    const __amdgpu_buffer_rsrc_t rd = chunk_rsrc(dense, SL * bbytes);
-    const __amdgpu_buffer_rsrc_t rp = chunk_rsrc(packed, nk * bbytes);
-    const __amdgpu_buffer_rsrc_t rs = a.dir == 0 ? rd : rp;
-    const __amdgpu_buffer_rsrc_t rt = a.dir == 0 ? rp : rd;
-    v4f v[SL][VEC];
+    const uint32_t pr = a.prefix[r];  // issued with the mask load: one round trip before the data
+    uint64_t rem = m & (below(g0 + a.lg) & ~below(g0));
+    if (rem == 0) continue;
+    uint64_t k = pr + static_cast<uint64_t>(__builtin_popcountll(m & below(g0))) - (r >= a.skip_e ? skip_cnt : 0u);
+    float* dense = const_cast<float*>(a.dir == 0 ? a.src : a.dst) + r * a.lanes * a.block;
+    const __amdgpu_buffer_rsrc_t rd = chunk_rsrc(dense, a.lanes * bbytes);
+    while (rem != 0) {
+      uint32_t lj[SL];
+      uint64_t bm;
+      const uint32_t nv = take_bits<SL>(rem, lj, bm);
+      float* packed = const_cast<float*>(a.dir == 0 ? a.dst : a.src) + k * a.block;
+      const __amdgpu_buffer_rsrc_t rp = chunk_rsrc(packed, nv * bbytes);
+      const __amdgpu_buffer_rsrc_t rs = a.dir == 0 ? rd : rp;
+      const __amdgpu_buffer_rsrc_t rt = a.dir == 0 ? rp : rd;
+      v4f v[SL][VEC];
 #pragma unroll
-    for (int j = 0; j < SL; ++j) {
-      const bool has = (bits >> j) & 1u;
-      const uint32_t kj = static_cast<uint32_t>(__builtin_popcount(bits & ((1u << j) - 1u)));
-      const uint32_t off = (a.dir == 0 ? j : kj) * bbytes;
+      for (int j = 0; j < SL; ++j) {
+        const uint32_t off = (a.dir == 0 ? lj[j] : static_cast<uint32_t>(j)) * bbytes;
+        const uint32_t drop = static_cast<uint32_t>(j) < nv ? 0u : kDropStore;
 #pragma unroll
-      for (int q = 0; q < VEC; ++q)
-        v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
-                                              rs, (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0,
-                                              kLoadAux));
-    }
+        for (int q = 0; q < VEC; ++q)
+          v[j][q] = __builtin_bit_cast(
+              v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, (off + (q * 64 + lane) * 16) | drop, 0, kLoadAux));
+      }
 #pragma unroll
-    for (int j = 0; j < SL; ++j) {
-      const bool has = (bits >> j) & 1u;
-      const uint32_t kj = static_cast<uint32_t>(__builtin_popcount(bits & ((1u << j) - 1u)));
-      const uint32_t off = (a.dir == 0 ? kj : j) * bbytes;
+      for (int j = 0; j < SL; ++j) {
+        const uint32_t off = (a.dir == 0 ? static_cast<uint32_t>(j) : lj[j]) * bbytes;
+        const uint32_t drop = static_cast<uint32_t>(j) < nv ? 0u : kDropStore;
 #pragma unroll
-      for (int q = 0; q < VEC; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v[j][q]), rt,
-                                               (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0, 0);
+        for (int q = 0; q < VEC; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v[j][q]), rt,
+                                                 (off + (q * 64 + lane) * 16) | drop, 0, 0);
+      }
+      k += nv;
     }
   }
 }
@@ -916,80 +963,87 @@ struct ShardArgs {
   const uint64_t* write_set;
   float* out;
   uint64_t rows, r0, r1;
-  uint32_t count, me, lanes, block, packed_out;
+  uint32_t count, me, lanes, block, packed_out, lg;
 };
 
 template <int VEC>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum(ShardArgs a) {
-  constexpr int SL = move_slots<VEC>();
+  constexpr int SL = sum_slots<VEC>();
   const int lane = threadIdx.x & 63;
-  const uint32_t groups = a.lanes / SL;
+  const uint32_t groups = a.lanes / a.lg;
   const uint32_t bbytes = a.block * 4;
   const uint64_t units = (a.r1 - a.r0) * groups;
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
   const uint32_t* pws = a.prefix + static_cast<uint64_t>(a.count) * (a.rows + 1);
+  const uint64_t cmask = a.count >= 64 ? ~0ull : ((1ull << a.count) - 1ull);
   for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
        u < units; u += nw) {
     const uint64_t r = a.r0 + u / groups;
-    const uint32_t l0 = static_cast<uint32_t>(u % groups) * SL;
+    const uint32_t g0 = static_cast<uint32_t>(u % groups) * a.lg;
+    // every index load of the unit issued together (one round trip before the data loads): the write-set row and
+    // its prefix, and on lane c < count worker c's mask and stream prefixes
+    const bool cl = static_cast<uint32_t>(lane) < a.count;
+    const uint32_t* pc = a.prefix + static_cast<uint64_t>(cl ? lane : 0) * (a.rows + 1);
     const uint64_t w = a.write_set[r];
-    const uint32_t bits = static_cast<uint32_t>(w >> l0) & ((1u << SL) - 1u);
-    if (bits == 0) continue;
-    // lane c < count: worker c's mask and the first packed block of this group in its stream
-    uint64_t mc = 0, kc = 0;
-    if (static_cast<uint32_t>(lane) < a.count) {
-      mc = a.masks[static_cast<uint64_t>(lane) * a.rows + r];
-      const uint32_t* pc = a.prefix + static_cast<uint64_t>(lane) * (a.rows + 1);
-      kc = a.recv_off[lane] + (pc[r] - pc[a.r0]) + static_cast<uint64_t>(__builtin_popcountll(mc & below(l0)));
-    }
-    const uint32_t gbits = static_cast<uint32_t>(mc >> l0) & bits;  // lane c: its blocks in this group
-    v4f acc[SL][VEC];
-#pragma unroll
-    for (int j = 0; j < SL; ++j)
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) acc[j][q] = v4f{0.f, 0.f, 0.f, 0.f};
-    // contributors of the group, rank order: one worker at a time, all of its (up to SL) blocks loaded at once
-    uint64_t cont = __ballot(gbits != 0) & (a.count >= 64 ? ~0ull : ((1ull << a.count) - 1ull));
-    while (cont != 0) {
-      const uint32_t c = static_cast<uint32_t>(__builtin_ctzll(cont));
-      cont &= cont - 1;
-      const uint32_t cb = __builtin_amdgcn_readlane(gbits, c);
-      const __amdgpu_buffer_rsrc_t src =
-          c == a.me ? chunk_rsrc(a.own + (r * a.lanes + l0) * a.block, SL * bbytes)
-                    : chunk_rsrc(a.recv + (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(kc), c)) |
-                                           (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(kc >> 32), c)) << 32)) *
-                                              a.block,
-                                 static_cast<uint32_t>(__builtin_popcount(cb)) * bbytes);
-      v4f v[SL][VEC];
-#pragma unroll
-      for (int j = 0; j < SL; ++j) {
-        const bool has = (cb >> j) & 1u;
-        const uint32_t off = (c == a.me ? j : static_cast<uint32_t>(__builtin_popcount(cb & ((1u << j) - 1u)))) * bbytes;
-#pragma unroll
-        for (int q = 0; q < VEC; ++q)
-          v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
-                                                src, (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0,
-                                                kLoadAux));
-      }
+    const uint64_t mc = cl ? a.masks[static_cast<uint64_t>(lane) * a.rows + r] : 0ull;
+    const uint32_t pcr = pc[r], pcr0 = pc[a.r0];
+    const uint32_t pwr = pws[r], pwr0 = pws[a.r0];
+    uint64_t rem = w & (below(g0 + a.lg) & ~below(g0));
+    if (rem == 0) continue;
+    // lane c: the first block of row r in worker c's stream
+    const uint64_t kc0 = cl ? a.recv_off[lane] + (pcr - pcr0) : 0ull;
+    uint64_t kw = pwr - pwr0 + static_cast<uint64_t>(__builtin_popcountll(w & below(g0)));
+    float* orow = a.out + r * a.lanes * a.block;
+    while (rem != 0) {
+      uint32_t lj[SL];
+      uint64_t bm;
+      const uint32_t nv = take_bits<SL>(rem, lj, bm);
+      v4f acc[SL][VEC];
 #pragma unroll
       for (int j = 0; j < SL; ++j)
-        if ((cb >> j) & 1u) {
 #pragma unroll
-          for (int q = 0; q < VEC; ++q) acc[j][q] = add4(acc[j][q], v[j][q]);
+        for (int q = 0; q < VEC; ++q) acc[j][q] = v4f{0.f, 0.f, 0.f, 0.f};
+      // contributors of the batch in rank order; each worker's (up to SL) blocks loaded at once
+      uint64_t cont = __ballot((mc & bm) != 0) & cmask;
+      while (cont != 0) {
+        const uint32_t c = static_cast<uint32_t>(__builtin_ctzll(cont));
+        cont &= cont - 1;
+        const uint64_t m_c = readlane64(mc, c);
+        const bool mine = c == a.me;
+        const __amdgpu_buffer_rsrc_t src =
+            mine ? chunk_rsrc(a.own + r * a.lanes * a.block, a.lanes * bbytes)
+                 : chunk_rsrc(a.recv + readlane64(kc0, c) * a.block,
+                              static_cast<uint32_t>(__builtin_popcountll(m_c)) * bbytes);
+        v4f v[SL][VEC];
+#pragma unroll
+        for (int j = 0; j < SL; ++j) {
+          const bool has = static_cast<uint32_t>(j) < nv && ((m_c >> lj[j]) & 1u);
+          const uint32_t off = (mine ? lj[j] : static_cast<uint32_t>(__builtin_popcountll(m_c & below(lj[j])))) * bbytes;
+#pragma unroll
+          for (int q = 0; q < VEC; ++q)
+            v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  src, (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0,
+                                                  kLoadAux));
         }
-    }
-    const uint64_t kw = pws[r] - pws[a.r0] + static_cast<uint64_t>(__builtin_popcountll(w & below(l0)));
-    float* obase = a.packed_out ? a.out + kw * a.block : a.out + (r * a.lanes + l0) * a.block;
-    const __amdgpu_buffer_rsrc_t dst =
-        chunk_rsrc(obase, (a.packed_out ? static_cast<uint32_t>(__builtin_popcount(bits)) : SL) * bbytes);
 #pragma unroll
-    for (int j = 0; j < SL; ++j) {
-      const bool has = (bits >> j) & 1u;
-      const uint32_t off = (a.packed_out ? static_cast<uint32_t>(__builtin_popcount(bits & ((1u << j) - 1u))) : j) * bbytes;
+        for (int j = 0; j < SL; ++j)
+          if (static_cast<uint32_t>(j) < nv && ((m_c >> lj[j]) & 1u)) {
 #pragma unroll
-      for (int q = 0; q < VEC; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[j][q]), dst,
-                                               (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0, 0);
+            for (int q = 0; q < VEC; ++q) acc[j][q] = add4(acc[j][q], v[j][q]);
+          }
+      }
+      const __amdgpu_buffer_rsrc_t dst = a.packed_out ? chunk_rsrc(a.out + kw * a.block, nv * bbytes)
+                                                      : chunk_rsrc(orow, a.lanes * bbytes);
+#pragma unroll
+      for (int j = 0; j < SL; ++j) {
+        const uint32_t off = (a.packed_out ? static_cast<uint32_t>(j) : lj[j]) * bbytes;
+        const uint32_t drop = static_cast<uint32_t>(j) < nv ? 0u : kDropStore;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[j][q]), dst,
+                                                 (off + (q * 64 + lane) * 16) | drop, 0, 0);
+      }
+      kw += nv;
     }
   }
 }
@@ -1064,6 +1118,14 @@ unsigned grid_for(uint64_t work_items_per_wave_units) {
   if (g > kMaxGrid) g = kMaxGrid;
   if (g == 0) g = 1;
   return static_cast<unsigned>(g);
+}
+
+// Lanes per work unit of the mask-addressed movers: whole rows when there are enough of them to give every SIMD
+// a few units, otherwise rows split into groups (>= 4 lanes).
+uint32_t unit_lanes(uint64_t rows, uint32_t lanes) {
+  uint32_t lg = lanes;
+  while (lg > 4 && rows * (lanes / lg) < 8192) lg /= 2;
+  return lg;
 }
 
 int launch_next(const Layout& L, const uint64_t* masks, uint32_t count, uint32_t* next, hipStream_t st) {
@@ -1513,7 +1575,7 @@ int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint3
 int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                    uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
                    uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                   omr_stream_t stream) {
+                   uint32_t* arrive, uint32_t* done_flag, uint32_t seq, omr_stream_t stream) {
   if (count == 0 || count > OMR_MAX_WORKERS) return fail("round_plan: count %u out of range", count);
   if (rows == 0 || rows_per_part == 0 || rows % rows_per_part != 0) return fail("round_plan: bad rows");
   if (num_lanes == 0 || num_lanes > 64) return fail("round_plan: num_lanes %u out of range", num_lanes);
@@ -1534,6 +1596,10 @@ int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uin
   a.prefix = prefix;
   a.counts = counts;
   a.zero_masks = zero_masks;
+  if ((arrive == nullptr) != (done_flag == nullptr)) return fail("round_plan: arrive and done_flag go together");
+  a.arrive = arrive;
+  a.done_flag = done_flag;
+  a.seq = seq;
   k_round_plan<<<count + 1, kPlanThreads, 0, S(stream)>>>(a);
   return launch_status("k_round_plan");
 }
@@ -1545,8 +1611,8 @@ int omr_move_blocks_f32(const float* src, float* dst, int dir, const uint64_t* r
   if (block_size != 256 && block_size != 512 && block_size != 1024)
     return fail("move_blocks: block_size %u unsupported", block_size);
   const uint32_t vec = block_size / 256;
-  const uint32_t sl = vec == 1 ? 8u : (vec == 2 ? 4u : 2u);
-  if (num_lanes == 0 || num_lanes > 64 || num_lanes % sl != 0) return fail("move_blocks: num_lanes %u", num_lanes);
+  if (num_lanes == 0 || num_lanes > 64 || (num_lanes & (num_lanes - 1)) != 0)
+    return fail("move_blocks: num_lanes %u", num_lanes);
   if (skip_begin > skip_end || skip_end > rows) return fail("move_blocks: bad skip range");
   if (rows == 0) return 0;
   if (src == nullptr || dst == nullptr || row_masks == nullptr || prefix == nullptr)
@@ -1564,7 +1630,8 @@ int omr_move_blocks_f32(const float* src, float* dst, int dir, const uint64_t* r
   a.lanes = num_lanes;
   a.block = block_size;
   a.dir = static_cast<uint32_t>(dir);
-  const unsigned g = grid_for(rows * (num_lanes / sl));
+  a.lg = unit_lanes(rows, num_lanes);
+  const unsigned g = grid_for(rows * (num_lanes / a.lg));
   hipStream_t st = S(stream);
   switch (vec) {
     case 1: k_move<1><<<g, kWGThreads, 0, st>>>(a); break;
@@ -1582,8 +1649,8 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
   if (block_size != 256 && block_size != 512 && block_size != 1024)
     return fail("shard_sum: block_size %u unsupported", block_size);
   const uint32_t vec = block_size / 256;
-  const uint32_t sl = vec == 1 ? 8u : (vec == 2 ? 4u : 2u);
-  if (num_lanes == 0 || num_lanes > 64 || num_lanes % sl != 0) return fail("shard_sum: num_lanes %u", num_lanes);
+  if (num_lanes == 0 || num_lanes > 64 || (num_lanes & (num_lanes - 1)) != 0)
+    return fail("shard_sum: num_lanes %u", num_lanes);
   if (row_begin > row_end || row_end > rows) return fail("shard_sum: bad row range");
   if (row_end == row_begin) return 0;
   if (row_masks == nullptr || prefix == nullptr || write_set == nullptr || out == nullptr ||
@@ -1608,7 +1675,8 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
   a.lanes = num_lanes;
   a.block = block_size;
   a.packed_out = packed_out ? 1u : 0u;
-  const unsigned g = grid_for((row_end - row_begin) * (num_lanes / sl));
+  a.lg = unit_lanes(row_end - row_begin, num_lanes);
+  const unsigned g = grid_for((row_end - row_begin) * (num_lanes / a.lg));
   hipStream_t st = S(stream);
   switch (vec) {
     case 1: k_shard_sum<1><<<g, kWGThreads, 0, st>>>(a); break;

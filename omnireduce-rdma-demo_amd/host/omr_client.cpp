@@ -114,6 +114,7 @@ int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer) {
       fprintf(stderr, "failed to run the round: %s\n", omr_dist_last_error());  // client.cc:131-135
       return 1;
     }
+    HIPOK(hipStreamSynchronize(st));  // a round ends when its results are in place (client.cc:220 wait())
     if (round >= o.warmups) {  // client.cc:439-448, print_freq 1
       if (round - o.warmups > 0) {
         const auto now = std::chrono::steady_clock::now();

@@ -94,9 +94,10 @@ class ScanSumPlan:
     """
 
     def __init__(self, layout: Layout, m: int = 1, with_flags: bool = True, with_next: bool = True,
-                 device="cuda", fused: bool = False):
+                 device="cuda", fused: bool = False, row_masks: bool = False):
         """fused=True (m = 1 only): one single-pass launch (omr_scan_sum_fused_f32) producing flags, next
-        offsets and the aggregated blocks; no row masks."""
+        offsets and the aggregated blocks; with row_masks=True it is the multi-rank round's worker scan
+        (omr_worker_scan_f32), which also ORs the row masks into `masks` (zeroed before each run)."""
         if not 1 <= m <= _lib.OMR_MAX_WORKERS:
             raise ValueError(f"m={m} out of range")
         lib = _lib.load()
@@ -107,14 +108,16 @@ class ScanSumPlan:
         self.layout, self.m, self.fused = layout, m, fused
         arrays = m if m == 1 else m + 1
         self.flags = torch.empty((m, layout.nb), dtype=torch.int32, device=device) if with_flags else None
-        self.masks = None if fused else torch.empty((arrays, layout.rows), dtype=torch.int64, device=device)
+        self.row_masks = bool(fused and row_masks)
+        self.masks = (None if fused and not row_masks else
+                      torch.zeros((arrays, layout.rows), dtype=torch.int64, device=device))
         self.next_offsets = (torch.empty((arrays, layout.nb), dtype=torch.int32, device=device)
                              if with_next else None)
         ws = lib.omr_scan_workspace_bytes(layout.n, layout.block_size, layout.num_lanes, layout.num_threads)
         self.workspace = torch.zeros(max(ws, 16), dtype=torch.uint8, device=device) if fused else None
 
     def run(self, bufs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None, stream=None,
-            with_next: bool = True) -> ScanResult:
+            with_next: bool = True, zero_masks: bool = True) -> ScanResult:
         """Fused scan (+ sum into `out`) and, unless with_next=False, the next-offset chains."""
         L = self.layout
         if len(bufs) != self.m:
@@ -123,6 +126,14 @@ class ScanSumPlan:
             _check_f32(b, L.n, f"bufs[{i}]")
         if out is not None:
             _check_f32(out, L.n, "out")
+        if self.fused and self.row_masks:
+            if zero_masks:
+                self.masks.zero_()
+            _lib.check(_lib.load().omr_worker_scan_f32(
+                _ptr(bufs[0]), L.n, L.block_size, L.num_lanes, L.num_threads, _ptr(self.flags),
+                _ptr(self.next_offsets), _ptr(self.masks), _ptr(out), _ptr(self.workspace), self.workspace.numel(),
+                _stream(stream)), "omr_worker_scan_f32")
+            return ScanResult(self.flags, self.masks, self.next_offsets, out)
         if self.fused:
             _lib.check(_lib.load().omr_scan_sum_fused_f32(
                 _ptr(bufs[0]), L.n, L.block_size, L.num_lanes, L.num_threads, _ptr(self.flags),

@@ -99,9 +99,13 @@ def test_round_plan(gpu, count, rows, rpp, lanes):
     prefix = torch.zeros((count + 1) * (rows + 1), dtype=torch.int32, device=gpu)
     counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int32, device=gpu)
     zero = torch.full((rows,), -1, dtype=torch.int64, device=gpu)
-    assert lib.omr_round_plan(P(md), count, rows, rpp, lanes, P(bd), N + 1, P(wset), P(umask), P(prefix), P(counts),
-                              P(zero), stream()) == 0, lib.omr_last_error()
-    torch.cuda.synchronize()
+    arrive = torch.zeros(1, dtype=torch.int32, device=gpu)
+    done = torch.zeros(1, dtype=torch.int32, device=gpu)
+    for seq in (7, 8):  # the completion notice, twice: the arrival counter re-arms itself
+        assert lib.omr_round_plan(P(md), count, rows, rpp, lanes, P(bd), N + 1, P(wset), P(umask), P(prefix),
+                                  P(counts), P(zero), P(arrive), P(done), seq, stream()) == 0, lib.omr_last_error()
+        torch.cuda.synchronize()
+        assert int(done.item()) == seq and int(arrive.item()) == 0
     u, w = np_write_set(masks, rpp, lanes)
     assert (umask.cpu().numpy().view(np.uint64) == u).all()
     assert (wset.cpu().numpy().view(np.uint64) == w).all()
