@@ -230,6 +230,28 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
                       uint64_t rows, uint64_t row_begin, uint64_t row_end, uint32_t num_lanes, uint32_t block_size,
                       int packed_out, float* out, omr_stream_t stream);
 
+/* ---------------------------------------------------------------- message-level round (wire format) */
+
+/* The round as the reference's messages, byte for byte, for m workers on one device
+ * (the loopback stand-in for m machines): every worker message and aggregator reply of the per-slot state
+ * machines (client.cc:32-205, server.cc:13-199), with a protocol round's worker messages arriving in rank order.
+ * Wire format (common.cc:399-408, :424, :443, :542): a message occupies a slot of 2*MESSAGE_SIZE floats:
+ * `len` blocks of block_size floats, then `len` uint32 next offsets; imm = (len << 16) | global slot (gs = slot +
+ * NUM_SLOTS*partition).  Logs (device, valid for round r < rounds[gs]):
+ *   messages[(gs*cap + r)*2*MESSAGE_SIZE ...], imm[gs*cap + r]   worker `worker`'s message (imm 0: none sent)
+ *   replies [(gs*cap + r)*2*MESSAGE_SIZE ...], reply_imm[...]     the aggregator's reply (the same to every worker)
+ * outs[w] (device, may equal bufs[w]) receives worker w's buffer after the round: every reply block written at
+ * the worker's current offset of its lane (client.cc:87-90).  num_lanes must be NUM_SLOTS*MESSAGE_SIZE/block_size.
+ * omr_msg_round_f32 synchronises `stream` once (the schedule's round count sizes the logs). */
+typedef struct omr_msg_plan omr_msg_plan;
+int omr_msg_plan_create(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, uint32_t m,
+                        omr_msg_plan** plan);
+int omr_msg_plan_destroy(omr_msg_plan* plan);
+int omr_msg_round_f32(omr_msg_plan* plan, const float* const* bufs, float* const* outs, uint32_t* max_rounds,
+                      omr_stream_t stream);
+int omr_msg_logs(omr_msg_plan* plan, uint32_t worker, float** messages, uint32_t** imm, float** replies,
+                 uint32_t** reply_imm, uint32_t** rounds, uint32_t* round_capacity);
+
 /* ---------------------------------------------------------------- host-resident end-to-end path */
 
 /* The gradient lives in host memory (the reference's registered region, common.cc:873-914): H2D in row chunks,

@@ -1230,6 +1230,14 @@ int launch_scan(const Layout& L, const ScanArgs& a, hipStream_t st) {
 
 }  // namespace
 
+// internal, not in omr.h: the other translation units of libomr.so report through omr_last_error() with this
+namespace omr_detail {
+int set_error(int code, const char* msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+}  // namespace omr_detail
+
 // ================================================================ C ABI
 #ifndef OMR_NO_CAPI
 

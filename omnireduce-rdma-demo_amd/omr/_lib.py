@@ -54,6 +54,10 @@ SIGNATURES = {
     "omr_move_blocks_f32": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_u64, c_u32, c_u32, c_u64, c_u64, c_vp]),
     "omr_shard_sum_f32": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, c_vp, c_vp, c_u64, c_u64, c_u64, c_u32,
                                   c_u32, c_int, c_vp, c_vp]),
+    "omr_msg_plan_create": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u32, c_vp]),
+    "omr_msg_plan_destroy": (c_int, [c_vp]),
+    "omr_msg_round_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "omr_msg_logs": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "omr_sparse_block_sum_f32": (c_int, [c_vp, c_vp, c_vp, c_u32, c_u64, c_vp, c_u64, c_u32, c_vp, c_u32, c_u32,
                                          c_vp, c_vp]),
     "omr_host_last_error": (ctypes.c_char_p, []),

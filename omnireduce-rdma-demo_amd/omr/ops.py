@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .layout import Layout
+from .layout import MESSAGE_SIZE, NUM_SLOTS, Layout
 
 
 def _stream(stream: Optional[torch.cuda.Stream] = None) -> int:
@@ -278,4 +278,64 @@ class HostPlan:
         try:
             self.close()
         except Exception:
+            pass
+
+
+# ------------------------------------------------------------------ message-level round (wire format)
+
+class _DeviceView:
+    """A device buffer owned by the library, exposed to torch through __cuda_array_interface__ (no copy)."""
+
+    def __init__(self, ptr: int, shape, typestr: str):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (ptr, False),
+                                         "version": 3, "strides": None}
+
+
+class MessageRound:
+    """The round as the reference's messages (include/omr.h omr_msg_*): m workers on one device, every worker
+    message and aggregator reply in the wire format of common.cc:399-443, results written in place."""
+
+    def __init__(self, layout: Layout, m: int, device="cuda"):
+        lib = _lib.load()
+        self.layout, self.m, self.device = layout, m, torch.device(device)
+        self._p = ctypes.c_void_p()
+        _lib.check(lib.omr_msg_plan_create(layout.n, layout.block_size, layout.num_lanes, layout.num_threads, m,
+                                           ctypes.byref(self._p)), "omr_msg_plan_create")
+
+    def run(self, bufs: Sequence[torch.Tensor], outs: Optional[Sequence[torch.Tensor]] = None, stream=None) -> int:
+        L = self.layout
+        outs = list(bufs) if outs is None else list(outs)
+        if len(bufs) != self.m or len(outs) != self.m:
+            raise ValueError(f"expected {self.m} worker buffers")
+        for i, (b, o) in enumerate(zip(bufs, outs)):
+            _check_f32(b, L.n, f"bufs[{i}]")
+            _check_f32(o, L.n, f"outs[{i}]")
+        maxr = ctypes.c_uint32()
+        _lib.check(_lib.load().omr_msg_round_f32(self._p, _ptr_array(bufs), _ptr_array(outs), ctypes.byref(maxr),
+                                                 _stream(stream)), "omr_msg_round_f32")
+        return maxr.value
+
+    def logs(self, worker: int) -> dict:
+        """Copies of the wire logs: messages / replies [G, cap, 2*MESSAGE_SIZE] f32, imm / reply_imm [G, cap]
+        (uint32 bits in int32), rounds [G]."""
+        msg, imm, rep, rimm, rnd = (ctypes.c_void_p() for _ in range(5))
+        cap = ctypes.c_uint32()
+        _lib.check(_lib.load().omr_msg_logs(self._p, worker, ctypes.byref(msg), ctypes.byref(imm), ctypes.byref(rep),
+                                            ctypes.byref(rimm), ctypes.byref(rnd), ctypes.byref(cap)), "omr_msg_logs")
+        G, c, W = self.layout.num_threads * NUM_SLOTS, cap.value, 2 * MESSAGE_SIZE
+        torch.cuda.synchronize(self.device)
+        view = (lambda p, shape, t: torch.as_tensor(_DeviceView(p.value, shape, t), device=self.device).clone())
+        return {"messages": view(msg, (G, c, W), "<f4"), "imm": view(imm, (G, c), "<i4"),
+                "replies": view(rep, (G, c, W), "<f4"), "reply_imm": view(rimm, (G, c), "<i4"),
+                "rounds": view(rnd, (G,), "<i4"), "cap": c}
+
+    def close(self):
+        if self._p:
+            _lib.load().omr_msg_plan_destroy(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 (interpreter shutdown)
             pass

@@ -330,3 +330,161 @@ double orc_cpu_baseline(const float* x, const int32_t* bitmap, uint64_t n, uint3
   free(th);
   return rounds > 0 ? acc / rounds : 0.0;
 }
+
+/* ------------------------------------------------------------------ message-level protocol (one round)
+ *
+ * A literal restatement of the two per-slot state machines, one message at a time, with the workers' messages
+ * of a protocol round arriving in RANK order (one admissible arrival order; the reference's order is whatever
+ * the NIC delivers):
+ *   worker      client.cc:180-205 (first burst: the slot's lane heads, each with find_next_nonzero_block of
+ *               head + B*NB) and client.cc:32-152 handle_recv (per reply block: copy the sum to
+ *               buf[current_offset[bid]] (:89), current = the reply's next (:90), queue it when below the
+ *               sentinel and own bitmap == 1 (:91-96), else reset the lane and count it finished (:98-101);
+ *               send the queue if the slot is not finished (:113-127));
+ *   aggregator  server.cc:13-199 handle_recv (per received block: block_next_offset[bid][w] = next (:84-86),
+ *               min over every worker (:87-91), complete when current_offset < min_next (:92-96), add into the
+ *               slot's accumulator set (:97-98); reply when completed >= BLOCKS_PER_MESSAGE - finished
+ *               (:143): sums of the completed lanes in completion order + their min_next (:144-147), zero the
+ *               other accumulator set (:148-150); advance / reset lanes (:173-186); flip the set (:193)).
+ * Wire format (common.cc:399-407, :424, :443, :503, :522, :542): a message is `len` blocks of B floats then `len`
+ * uint32 next offsets, in a 2*MESSAGE_SIZE-float slot; imm = (len << 16) | global slot.
+ * Logs: wmsg[w][gs][r] / wimm[w][gs][r] = worker w's message of protocol round r of global slot gs (imm 0 = it
+ * sent none), rmsg[gs][r] / rimm[gs][r] = the aggregator's reply; outs[w] = worker w's buffer after the round
+ * (callers pass copies of the inputs: results are written in place, client.cc:89).  rounds[gs] = replies in
+ * slot gs.  Returns the largest round count, or -1 if rcap is too small / the state machines disagree. */
+
+#define ORC_MSG 1024u  /* MESSAGE_SIZE (common.h:31) */
+#define ORC_SLOTS 16u  /* NUM_SLOTS (common.h:34) */
+#define ORC_MAXW 16u
+
+int orc_msg_simulate(const float* const* bufs, const int32_t* const* flags, uint32_t m, uint64_t n, uint32_t B,
+                     uint32_t NB, uint32_t parts, uint32_t rcap, float* wmsg, uint32_t* wimm, float* rmsg,
+                     uint32_t* rimm, float* const* outs, uint32_t* rounds) {
+  const uint32_t BPM = ORC_MSG / B;                 /* BLOCKS_PER_MESSAGE (common.h:33) */
+  const uint32_t SLOTW = 2 * ORC_MSG;               /* floats per message slot */
+  const uint32_t P = (uint32_t)(n / parts);         /* DATA_SIZE_PER_THREAD */
+  const uint32_t sent = orc_sentinel(B, NB);        /* max_index base (client.cc:42, server.cc:16) */
+  const uint64_t G = (uint64_t)parts * ORC_SLOTS;   /* global slots */
+  if (m == 0 || m > ORC_MAXW || BPM == 0 || BPM > 4 || NB != ORC_SLOTS * BPM) return -1;
+  int maxr = 0;
+  for (uint32_t t = 0; t < parts; t++) {
+    const uint32_t start = P * t;
+    for (uint32_t s = 0; s < ORC_SLOTS; s++) {
+      const uint64_t gs = (uint64_t)t * ORC_SLOTS + s;
+      /* worker state (client.cc:35-48) and pending message */
+      uint32_t wcur[ORC_MAXW][4], wfin[ORC_MAXW], qlen[ORC_MAXW], qcur[ORC_MAXW][4], qnext[ORC_MAXW][4];
+      /* aggregator state (server.cc:14-48) */
+      uint32_t acur[4], bno[4][ORC_MAXW], minn[4], ccur[4], cnext[4], ncomp = 0, afin = 0, set = 0;
+      float acc[2][4][1024], rsum[4][1024];
+      memset(acc, 0, sizeof(acc));
+      for (uint32_t j = 0; j < BPM; j++) {
+        acur[j] = start + (s * BPM + j) * B;
+        for (uint32_t w = 0; w < m; w++) bno[j][w] = 0;
+      }
+      for (uint32_t w = 0; w < m; w++) {
+        wfin[w] = 0;
+        qlen[w] = BPM; /* first burst (client.cc:198-205): the slot's lane heads, unconditionally */
+        for (uint32_t j = 0; j < BPM; j++) {
+          wcur[w][j] = start + (s * BPM + j) * B;
+          qcur[w][j] = start + s * ORC_MSG + j * B;
+          qnext[w][j] = orc_find_next_nonzero_block(flags[w], P, B, NB, t, qcur[w][j] + B * NB);
+        }
+      }
+      uint32_t r = 0;
+      int done = 0;
+      while (!done) {
+        if (r >= rcap) return -1;
+        int replied = 0;
+        uint32_t rcur[4], rnext[4], nrep = 0; /* the round's reply, applied by the workers after the round */
+        for (uint32_t w = 0; w < m; w++) { /* rank-order arrival of the messages pending at the round start */
+          const uint32_t len = qlen[w];
+          uint32_t* imm = wimm ? wimm + ((uint64_t)w * G + gs) * rcap + r : NULL;
+          if (imm) *imm = 0;
+          if (len == 0) continue;
+          if (replied) return -1; /* a message after the round's reply: the state machines disagree */
+          float* msg = wmsg ? wmsg + (((uint64_t)w * G + gs) * rcap + r) * SLOTW : NULL;
+          for (uint32_t k = 0; k < len; k++) { /* worker pack: common.cc:405-407 blocks, :408 next offsets */
+            const float* src = bufs[w] + qcur[w][k];
+            if (msg) memcpy(msg + k * B, src, B * sizeof(float));
+          }
+          if (msg) memcpy(msg + len * B, qnext[w], len * sizeof(uint32_t));
+          if (imm) *imm = (len << 16) | (uint32_t)gs; /* common.cc:443 */
+          /* aggregator receive (server.cc:68-99) */
+          for (uint32_t k = 0; k < len; k++) {
+            const uint32_t bo = qnext[w][k];
+            const uint32_t lane = (bo / B) % NB, j = lane - s * BPM;
+            bno[j][w] = bo;
+            uint32_t mn = bno[j][0];
+            for (uint32_t v = 1; v < m; v++)
+              if (mn > bno[j][v]) mn = bno[j][v];
+            minn[j] = mn;
+            if (acur[j] < minn[j]) {
+              ccur[ncomp] = acur[j];
+              cnext[ncomp] = minn[j];
+              ncomp++;
+            }
+            const float* src = bufs[w] + qcur[w][k];
+            for (uint32_t e = 0; e < B; e++) acc[set][j][e] += src[e];
+          }
+          if (ncomp >= BPM - afin) { /* server.cc:143: reply */
+            float* rm = rmsg ? rmsg + (gs * rcap + r) * SLOTW : NULL;
+            for (uint32_t k = 0; k < ncomp; k++) {
+              const uint32_t j = (ccur[k] / B) % NB - s * BPM;
+              if (rm) memcpy(rm + k * B, acc[set][j], B * sizeof(float));
+            }
+            if (rm) memcpy(rm + ncomp * B, cnext, ncomp * sizeof(uint32_t));
+            if (rimm) rimm[gs * rcap + r] = (ncomp << 16) | (uint32_t)gs;
+            for (uint32_t k = 0; k < ncomp; k++) { /* the reply as sent: completed sums + min_next */
+              const uint32_t j = (ccur[k] / B) % NB - s * BPM;
+              rcur[k] = ccur[k];
+              rnext[k] = cnext[k];
+              memcpy(rsum[k], acc[set][j], B * sizeof(float));
+            }
+            nrep = ncomp;
+            memset(acc[set ^ 1u], 0, sizeof(acc[0])); /* server.cc:148-150 */
+            /* aggregator lane advance (server.cc:173-186) */
+            for (uint32_t k = 0; k < ncomp; k++) {
+              const uint32_t lane = (cnext[k] / B) % NB, j = lane - s * BPM;
+              acur[j] = cnext[k];
+              if (cnext[k] >= sent) {
+                acur[j] = start + lane * B;
+                for (uint32_t v = 0; v < m; v++) bno[j][v] = 0;
+                afin++;
+              }
+            }
+            ncomp = 0;
+            if (afin == BPM) done = 1; /* server.cc:187-192 */
+            set ^= 1u;                 /* server.cc:193 */
+            replied = 1;
+          }
+        }
+        if (!replied) return -1; /* every worker idle but the slot unfinished */
+        /* every worker receives the reply (client.cc:67-127) */
+        for (uint32_t v = 0; v < m; v++) {
+          uint32_t nq = 0;
+          for (uint32_t k = 0; k < nrep; k++) {
+            const uint32_t lane = (rnext[k] / B) % NB, j = lane - s * BPM;
+            memcpy(outs[v] + wcur[v][j], rsum[k], B * sizeof(float)); /* client.cc:89 */
+            wcur[v][j] = rnext[k];
+            if (wcur[v][j] < sent) {
+              if (flags[v][wcur[v][j] / B] == 1) {
+                qcur[v][nq] = wcur[v][j];
+                qnext[v][nq] = orc_find_next_nonzero_block(flags[v], P, B, NB, t, wcur[v][j] + B * NB);
+                nq++;
+              }
+            } else {
+              wcur[v][j] = start + lane * B;
+              wfin[v]++;
+            }
+          }
+          qlen[v] = wfin[v] < BPM ? nq : 0;
+        }
+        (void)rcur;
+        r++;
+      }
+      if (rounds) rounds[gs] = r;
+      if ((int)r > maxr) maxr = (int)r;
+    }
+  }
+  return maxr;
+}

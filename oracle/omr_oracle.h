@@ -21,6 +21,9 @@ void orc_block_sum(const float* const* bufs, uint32_t m, uint64_t n, uint32_t B,
                    const int32_t* uflags, float* out);
 uint32_t orc_lane_stream(const int32_t* flags, uint64_t n, uint32_t B, uint32_t NB, uint32_t parts, uint32_t tid,
                          uint32_t bid, uint32_t* cur_out, uint32_t* next_out, uint32_t cap);
+int orc_msg_simulate(const float* const* bufs, const int32_t* const* flags, uint32_t m, uint64_t n, uint32_t B,
+                     uint32_t NB, uint32_t parts, uint32_t rcap, float* wmsg, uint32_t* wimm, float* rmsg,
+                     uint32_t* rimm, float* const* outs, uint32_t* rounds);
 double orc_cpu_baseline(const float* x, const int32_t* bitmap, uint64_t n, uint32_t B, uint32_t NB,
                         uint32_t parts, uint32_t nthreads, uint32_t variant, int warmups, int rounds,
                         int32_t* flags, uint32_t* next, float* out);

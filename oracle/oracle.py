@@ -26,6 +26,7 @@ _SIG = {
     "orc_next_offsets": (None, [_vp, _u64, _u32, _u32, _u32, _vp]),
     "orc_block_sum": (None, [_vp, _u32, _u64, _u32, _u32, _u32, _vp, _vp]),
     "orc_lane_stream": (_u32, [_vp, _u64, _u32, _u32, _u32, _u32, _u32, _vp, _vp, _u32]),
+    "orc_msg_simulate": (_int, [_vp, _vp, _u32, _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orc_cpu_baseline": (_dbl, [_vp, _vp, _u64, _u32, _u32, _u32, _u32, _u32, _int, _int, _vp, _vp, _vp]),
 }
 _lib = None
@@ -128,3 +129,33 @@ def cpu_baseline(x: np.ndarray, bitmap: np.ndarray, n: int, B: int, NB: int, par
     if t < 0:
         raise ValueError("orc_cpu_baseline: nthreads must divide parts")
     return t, flags, nxt, out
+
+
+def msg_simulate(bufs, flags_list, n: int, B: int, NB: int, parts: int, rcap: int = 0, logs: bool = True):
+    """Message-level round (the reference's per-slot state machines, client.cc:32-205 / server.cc:13-199, rank-order
+    arrival).  Returns dict: outs (in-place results per worker), rounds [G], and with logs=True the wire logs
+    wmsg [m][G][rcap][2048] f32, wimm [m][G][rcap], rmsg [G][rcap][2048], rimm [G][rcap]."""
+    m = len(bufs)
+    G = parts * 16
+    if rcap <= 0:
+        rcap = (n // parts) // (B * NB) + 2
+    outs = [b.copy() for b in bufs]
+    fl = [np.ascontiguousarray(f.astype(np.int32)) for f in flags_list]
+    barr = (ctypes.c_void_p * m)(*[b.ctypes.data for b in bufs])
+    farr = (ctypes.c_void_p * m)(*[f.ctypes.data for f in fl])
+    oarr = (ctypes.c_void_p * m)(*[o.ctypes.data for o in outs])
+    rounds = np.zeros(G, dtype=np.uint32)
+    res = {"outs": outs, "rounds": rounds, "rcap": rcap}
+    if logs:
+        res["wmsg"] = np.zeros((m, G, rcap, 2048), dtype=np.float32)
+        res["wimm"] = np.zeros((m, G, rcap), dtype=np.uint32)
+        res["rmsg"] = np.zeros((G, rcap, 2048), dtype=np.float32)
+        res["rimm"] = np.zeros((G, rcap), dtype=np.uint32)
+        args = [_p(res["wmsg"]), _p(res["wimm"]), _p(res["rmsg"]), _p(res["rimm"])]
+    else:
+        args = [None, None, None, None]
+    r = lib().orc_msg_simulate(barr, farr, m, n, B, NB, parts, rcap, *args, oarr, _p(rounds))
+    if r < 0:
+        raise ValueError("orc_msg_simulate: round capacity exceeded or inconsistent state")
+    res["max_rounds"] = r
+    return res

@@ -160,3 +160,62 @@ def test_cpu_baseline_variants_agree():
     sel = visited | heads
     assert (nx0[sel] == ref[sel]).all()
     assert t0 > 0 and t1 > 0
+
+
+# ------------------------------------------------------------------ message-level state machines (orc_msg_simulate)
+
+@pytest.mark.parametrize("n,B,m,density", [(1 << 20, 256, 1, 0.095), (1 << 20, 256, 3, 0.3), (2 << 20, 512, 2, 0.1),
+                                           (4 << 20, 1024, 4, 0.2), (1 << 20, 256, 2, 1.0), (1 << 20, 256, 2, 0.0)])
+def test_msg_simulate_known_answer_and_wire_invariants(n, B, m, density):
+    """The literal per-slot state machines (client.cc:32-205, server.cc:13-199) end every worker on the dense
+    rank-order sum (the reference's CHECK, client.cc:449-465), and their wire traffic has the shape SURVEY.md
+    Appendix A states: imm = (len << 16) | gs, replies carry the union chain (server.cc:86-96 min_next), worker
+    messages carry the worker's own non-zero blocks with its own next offsets (after the lane heads)."""
+    NB, P = 16384 // B, 8
+    BPM = 1024 // B
+    bufs = [oracle.fill(oracle.gen_bitmap(w, density, n // B), B, mode=1, seed=w + 2) for w in range(m)]
+    flags = [oracle.flags_from_data(b, B) for b in bufs]
+    ref = oracle.msg_simulate(bufs, flags, n, B, NB, P)
+    uf = oracle.union_flags(flags)
+    unext = oracle.next_offsets(uf, n, B, NB, P)
+    own_next = [oracle.next_offsets(f, n, B, NB, P) for f in flags]
+    for w in range(m):
+        exp = bufs[w].copy()
+        oracle.block_sum(bufs, n, B, NB, P, uf, exp)
+        assert (ref["outs"][w].view(np.uint32) == exp.view(np.uint32)).all()
+    sent = oracle.sentinel(B, NB)
+    for gs in range(P * 16):
+        R = int(ref["rounds"][gs])
+        assert R >= 1
+        cur = {}  # lane -> the block its round carries
+        t, s = divmod(gs, 16)
+        for j in range(BPM):
+            cur[s * BPM + j] = (t * (n // P)) // B + s * BPM + j
+        for r in range(R):
+            rimm = int(ref["rimm"][gs, r])
+            ln = rimm >> 16
+            assert rimm & 0xFFFF == gs and 1 <= ln <= BPM
+            meta = ref["rmsg"][gs, r, ln * B: ln * B + ln].view(np.uint32)
+            assert sorted((int(x) // B) % NB for x in meta) == sorted(cur), "reply lanes = the active lanes"
+            for w in range(m):
+                wi = int(ref["wimm"][w, gs, r])
+                if wi == 0:
+                    continue
+                lw = wi >> 16
+                assert wi & 0xFFFF == gs
+                wmeta = ref["wmsg"][w, gs, r, lw * B: lw * B + lw].view(np.uint32)
+                for k, nx in enumerate(wmeta):
+                    lane = (int(nx) // B) % NB
+                    b = cur[lane]
+                    assert r == 0 or flags[w][b] == 1, "after the heads a worker sends only its non-zero blocks"
+                    assert int(nx) == int(own_next[w][b]), "each block travels with the worker's own next offset"
+                    blk = ref["wmsg"][w, gs, r, k * B:(k + 1) * B]
+                    assert (blk.view(np.uint32) == bufs[w][b * B:(b + 1) * B].view(np.uint32)).all()
+            nxt = {}
+            for x in meta:
+                lane = (int(x) // B) % NB
+                assert int(x) == int(unext[cur[lane]]), "min_next = the union chain"
+                if int(x) < sent:
+                    nxt[lane] = int(x) // B
+            cur = nxt
+        assert not cur, "a slot ends when every lane reaches its sentinel"
