@@ -8,6 +8,11 @@
 //       client.cc:449-465)    -I  in place (the reference writes results into res->buf, so rounds after the first
 //       start from the previous round's output)    -L k  run k workers as threads of this process over the
 //       loopback transport (no server needed)
+//   -M  (with -L k) message mode: the k workers share one GPU and the round runs as the reference's messages
+//       (omr_msg_round_f32: every worker message and aggregator reply of the per-slot state machines, in the
+//       wire format of common.cc:399-443)    -T file  (with -M) write the last round's wire trace: per message
+//       a {src, dst, imm, len} record of four uint32 (workers 0..k-1, aggregator 100) then its payload, the
+//       (B*len + len)*4 bytes an ibv_post_send would carry (common.cc:424), slot by slot, round by round
 //
 // With an aggregator list, the first entry is the ./omr_server rendezvous: it assigns this worker's ID by IP list
 // position (common.cc:123-133) and relays the RCCL unique id; the round itself is omr_sparse_allreduce_f32 over
@@ -40,7 +45,8 @@ struct Opts {
   uint32_t block = 256;
   int warmups = 10, rounds = 101;  // client.cc:368-369
   int gpu = -1, local = 0;
-  bool check = false, inplace = false;
+  bool check = false, inplace = false, messages = false;
+  const char* trace = nullptr;
 };
 
 void usage(const char* argv0) {  // common.cc:1441-1457 (default port and -r text corrected: SURVEY.md §5)
@@ -54,6 +60,7 @@ void usage(const char* argv0) {  // common.cc:1441-1457 (default port and -r tex
   fprintf(stdout, " -r, --density-ratio <r> fraction of non-zero blocks, as rand()%%100/101 < r (default 1.0)\n");
   fprintf(stdout, " -n <floats> -b <block size> -W <warm-ups> -R <rounds> -G <gpu> -c (check) -I (in place)\n");
   fprintf(stdout, " -L <k> run k workers in this process over the loopback transport\n");
+  fprintf(stdout, " -M (with -L) message mode: the round as the reference's wire messages; -T <file> trace them\n");
   fprintf(stdout, " -h, --help show this help message\n");
 }
 
@@ -178,6 +185,154 @@ int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer) {
   return rc;
 }
 
+// -M: k workers on one GPU, the round as the reference's messages (omr_msg_round_f32)
+int run_messages(const Opts& o, int gpu) {
+  HIPOK(hipSetDevice(gpu));
+  const int k = o.local;
+  const uint32_t lanes = omr_num_lanes(o.block);
+  const uint64_t nb = o.n / o.block;
+  if (omr_layout_check(o.n, o.block, lanes, OMR_NUM_THREADS)) {
+    fprintf(stderr, "bad layout: %s\n", omr_last_error());
+    return 1;
+  }
+  std::vector<float*> x(k), out(k);
+  int32_t* d_bitmap = nullptr;
+  HIPOK(hipMalloc(&d_bitmap, nb * sizeof(int32_t)));
+  for (int w = 0; w < k; ++w) {
+    HIPOK(hipMalloc(&x[w], o.n * sizeof(float)));
+    HIPOK(hipMalloc(&out[w], o.n * sizeof(float)));
+    if (make_input(static_cast<uint32_t>(w), o, x[w], d_bitmap)) return 1;  // srand(myId+1) per worker
+    HIPOK(hipMemcpy(out[w], x[w], o.n * sizeof(float), hipMemcpyDeviceToDevice));
+  }
+  omr_msg_plan* plan = nullptr;
+  if (omr_msg_plan_create(o.n, o.block, lanes, OMR_NUM_THREADS, static_cast<uint32_t>(k), &plan)) {
+    fprintf(stderr, "omr_msg_plan_create: %s\n", omr_last_error());
+    return 1;
+  }
+  hipStream_t st;
+  HIPOK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  std::cout << "density: " << o.density << std::endl;  // client.cc:405
+  const double gib = o.n * sizeof(float) / (1024.0 * 1024.0 * 1024.0);
+  double avg_bw = 0.0;
+  unsigned long avg_time_usec = 0;
+  int print_count = 0;
+  uint32_t maxr = 0;
+  std::vector<const float*> in(x.begin(), x.end());
+  auto start = std::chrono::steady_clock::now();
+  for (int round = 0; round < o.warmups + o.rounds; ++round) {
+    std::vector<float*> dst = o.inplace ? x : out;
+    if (omr_msg_round_f32(plan, in.data(), dst.data(), &maxr, st)) {
+      fprintf(stderr, "failed to run the round: %s\n", omr_last_error());
+      return 1;
+    }
+    HIPOK(hipStreamSynchronize(st));
+    if (round >= o.warmups) {
+      if (round - o.warmups > 0) {
+        const auto now = std::chrono::steady_clock::now();
+        const unsigned long us =
+            static_cast<unsigned long>(std::chrono::duration_cast<std::chrono::microseconds>(now - start).count());
+        const double bw = gib / (us / 1e6);
+        ++print_count;
+        avg_time_usec += us;
+        avg_bw += bw;
+        fprintf(stdout, "data size: %lu Bytes; time: %lu us; alg bw: %f GB/s\n",
+                static_cast<unsigned long>(o.n * sizeof(float)), us, bw);
+      }
+      start = std::chrono::steady_clock::now();
+    }
+  }
+  std::cout << "protocol rounds (largest slot): " << maxr << std::endl;
+  int rc = 0;
+  if (o.trace) {  // the last round's wire traffic, SURVEY.md Appendix B.6 record layout
+    FILE* f = fopen(o.trace, "wb");
+    if (!f) {
+      fprintf(stderr, "cannot open %s\n", o.trace);
+      return 1;
+    }
+    const uint32_t G = OMR_NUM_THREADS * OMR_NUM_SLOTS, W = 2 * OMR_MESSAGE_SIZE;
+    float *dm = nullptr, *drep = nullptr;
+    uint32_t *dimm = nullptr, *drimm = nullptr, *drounds = nullptr, cap = 0;
+    std::vector<std::vector<float>> msg(k);
+    std::vector<std::vector<uint32_t>> imm(k);
+    std::vector<float> rep;
+    std::vector<uint32_t> rimm, rounds(G);
+    for (int w = 0; w < k; ++w) {
+      omr_msg_logs(plan, static_cast<uint32_t>(w), &dm, &dimm, &drep, &drimm, &drounds, &cap);
+      msg[w].resize(static_cast<size_t>(G) * cap * W);
+      imm[w].resize(static_cast<size_t>(G) * cap);
+      HIPOK(hipMemcpy(msg[w].data(), dm, msg[w].size() * sizeof(float), hipMemcpyDeviceToHost));
+      HIPOK(hipMemcpy(imm[w].data(), dimm, imm[w].size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    }
+    rep.resize(static_cast<size_t>(G) * cap * W);
+    rimm.resize(static_cast<size_t>(G) * cap);
+    HIPOK(hipMemcpy(rep.data(), drep, rep.size() * sizeof(float), hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(rimm.data(), drimm, rimm.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(rounds.data(), drounds, G * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    uint64_t records = 0;
+    auto put = [&](uint32_t src, uint32_t dst, uint32_t word, const float* payload) {
+      const uint32_t len = word >> 16;
+      const uint32_t rec[4] = {src, dst, word, len};
+      fwrite(rec, sizeof(rec), 1, f);
+      fwrite(payload, sizeof(float), static_cast<size_t>(o.block) * len + len, f);  // common.cc:424
+      ++records;
+    };
+    for (uint32_t gs = 0; gs < G; ++gs)
+      for (uint32_t r = 0; r < rounds[gs]; ++r) {
+        const size_t u = static_cast<size_t>(gs) * cap + r;
+        for (int w = 0; w < k; ++w)
+          if (imm[w][u]) put(static_cast<uint32_t>(w), 100, imm[w][u], &msg[w][u * W]);
+        for (int w = 0; w < k; ++w) put(100, static_cast<uint32_t>(w), rimm[u], &rep[u * W]);
+      }
+    fclose(f);
+    std::cout << "trace: " << records << " messages -> " << o.trace << std::endl;
+  }
+  if (o.check) {  // every worker must hold the rank-order sum of every input (client.cc:449-465, done right)
+    float* d_exp = nullptr;
+    uint64_t* d_masks = nullptr;
+    HIPOK(hipMalloc(&d_exp, o.n * sizeof(float)));
+    HIPOK(hipMalloc(&d_masks, (k + 1) * (nb / lanes) * sizeof(uint64_t)));
+    std::vector<float*> orig(k);
+    for (int w = 0; w < k; ++w) {
+      HIPOK(hipMalloc(&orig[w], o.n * sizeof(float)));
+      if (make_input(static_cast<uint32_t>(w), o, orig[w], d_bitmap)) return 1;
+    }
+    std::vector<const float*> cb(orig.begin(), orig.end());
+    std::vector<float> got(o.n), exp(o.n);
+    for (int w = 0; w < k && rc == 0; ++w) {
+      HIPOK(hipMemcpy(d_exp, orig[w], o.n * sizeof(float), hipMemcpyDeviceToDevice));
+      if (omr_scan_sum_f32(cb.data(), k, o.n, o.block, lanes, OMR_NUM_THREADS, nullptr, d_masks, nullptr, d_exp,
+                           nullptr)) {
+        fprintf(stderr, "check skipped: %s\n", omr_last_error());
+        break;
+      }
+      HIPOK(hipDeviceSynchronize());
+      HIPOK(hipMemcpy(got.data(), o.inplace ? x[w] : out[w], o.n * sizeof(float), hipMemcpyDeviceToHost));
+      HIPOK(hipMemcpy(exp.data(), d_exp, o.n * sizeof(float), hipMemcpyDeviceToHost));
+      for (uint64_t i = 0; i < o.n; ++i)
+        if (memcmp(&got[i], &exp[i], sizeof(float)) != 0) {
+          std::cout << "error: " << exp[i] << "<---->" << got[i] << std::endl;  // client.cc:453-456
+          rc = 1;
+          break;
+        }
+    }
+    if (rc == 0) std::cout << "check OK" << std::endl;
+    for (float* b : orig) (void)hipFree(b);
+    (void)hipFree(d_exp);
+    (void)hipFree(d_masks);
+  }
+  if (print_count > 0)  // client.cc:473
+    fprintf(stdout, "data size: %lu Bytes; average time: %lu us; average alg bw: %f GB/s\n",
+            static_cast<unsigned long>(o.n * sizeof(float)), avg_time_usec / print_count, avg_bw / print_count);
+  omr_msg_plan_destroy(plan);
+  (void)hipStreamDestroy(st);
+  for (int w = 0; w < k; ++w) {
+    (void)hipFree(x[w]);
+    (void)hipFree(out[w]);
+  }
+  (void)hipFree(d_bitmap);
+  return rc;
+}
+
 }  // namespace
 
 int main(int argc, char* argv[]) {
@@ -187,7 +342,7 @@ int main(int argc, char* argv[]) {
                               {"service-level", 1, nullptr, 's'}, {"density-ratio", 1, nullptr, 'r'},
                               {"help", 0, nullptr, 'h'},          {nullptr, 0, nullptr, 0}};
   while (true) {
-    int c = getopt_long(argc, argv, "p:d:i:g:s:r:n:b:W:R:G:L:cIh", longopts, nullptr);
+    int c = getopt_long(argc, argv, "p:d:i:g:s:r:n:b:W:R:G:L:T:cIMh", longopts, nullptr);
     if (c == -1) break;
     switch (c) {
       case 'p': o.port = static_cast<int>(strtoul(optarg, nullptr, 0)); break;
@@ -207,6 +362,8 @@ int main(int argc, char* argv[]) {
       case 'L': o.local = atoi(optarg); break;
       case 'c': o.check = true; break;
       case 'I': o.inplace = true; break;
+      case 'M': o.messages = true; break;
+      case 'T': o.trace = optarg; break;
       default: usage(argv[0]); return 1;
     }
   }
@@ -219,6 +376,18 @@ int main(int argc, char* argv[]) {
   std::vector<std::string> aggs = omrnet::split_list(optind == argc - 1 ? argv[optind] : nullptr);
   omrnet::print_config(false, aggs, o.port, o.dev, o.ib_port, o.gid, o.sl);
   int rc = 0;
+  if (o.messages) {  // message mode: k workers on one GPU, the round as the reference's wire messages
+    if (o.local <= 0 || o.local > OMR_MAX_WORKERS) {
+      fprintf(stderr, "-M needs -L k with 1 <= k <= %d\n", OMR_MAX_WORKERS);
+      return 1;
+    }
+    std::cout << "Number of aggregators: 1; Number of workers is " << o.local << " (message mode, one GPU)"
+              << std::endl;
+    printf("Connected.\n");
+    rc = run_messages(o, o.gpu >= 0 ? o.gpu : 0);
+    fprintf(stdout, "\ntest result is %d\n", rc);
+    return rc;
+  }
   if (o.local > 0) {  // loopback: k workers as threads, GPUs round-robin
     omr_local_board* board = omr_local_board_create(o.local);
     std::vector<int> rcs(o.local, 0);

@@ -160,3 +160,42 @@ def test_server_client_rccl_one_worker(gpu):
     assert rc == 0, out
     assert "check OK" in out and "My ID is 0" in out
     assert srv.returncode == 0 and "test result is 0" in sout, sout
+
+
+def test_client_message_mode_trace(gpu, tmp_path):
+    """./omr_client -L 3 -M: the round as the reference's messages; the -T wire trace (SURVEY.md Appendix B.6
+    record layout) must equal, record for record and byte for byte, the oracle's literal state machines run on the
+    reference generator's inputs (srand(myId+1), 0.01f blocks: client.cc:396-421)."""
+    n, B, k, r = 1 << 20, 256, 3, 0.2
+    trace = str(tmp_path / "wire.bin")
+    rc, out = _run([os.path.join(BIN, "omr_client"), "-L", str(k), "-M", "-n", str(n), "-r", str(r), "-W", "1",
+                    "-R", "2", "-c", "-T", trace])
+    assert rc == 0, out
+    assert "check OK" in out and "test result is 0" in out
+    L = Layout(n=n, block_size=B)
+    bufs = [oracle.fill(oracle.gen_bitmap(w, r, L.nb), B) for w in range(k)]
+    flags = [oracle.flags_from_data(b, B) for b in bufs]
+    ref = oracle.msg_simulate(bufs, flags, n, B, L.num_lanes, L.num_threads)
+    exp = []
+    for gs in range(L.num_threads * 16):
+        for rr in range(int(ref["rounds"][gs])):
+            for w in range(k):
+                imm = int(ref["wimm"][w, gs, rr])
+                if imm:
+                    ln = imm >> 16
+                    exp.append((w, 100, imm, ln, ref["wmsg"][w, gs, rr, :ln * B + ln].tobytes()))
+            imm = int(ref["rimm"][gs, rr])
+            ln = imm >> 16
+            for w in range(k):
+                exp.append((100, w, imm, ln, ref["rmsg"][gs, rr, :ln * B + ln].tobytes()))
+    data = open(trace, "rb").read()
+    got, pos = [], 0
+    while pos < len(data):
+        src, dst, imm, ln = np.frombuffer(data, dtype=np.uint32, count=4, offset=pos)
+        pos += 16
+        nbytes = (B * int(ln) + int(ln)) * 4
+        got.append((int(src), int(dst), int(imm), int(ln), data[pos:pos + nbytes]))
+        pos += nbytes
+    assert len(got) == len(exp)
+    for i, (g, e) in enumerate(zip(got, exp)):
+        assert g == e, f"record {i}: {g[:4]} vs {e[:4]}"
