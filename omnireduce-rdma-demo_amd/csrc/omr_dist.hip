@@ -197,6 +197,8 @@ struct omr_ar_plan {
   uint32_t* flag_host = nullptr;  // pinned: the plan kernel stores the round's sequence number here
   uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
+  hipStream_t side = nullptr;      // the union chain runs here, beside the host's wait and the exchange
+  hipEvent_t plan_done = nullptr, chain_done = nullptr;
 };
 
 extern "C" {
@@ -255,6 +257,9 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   (void)hipHostFree(p->counts_host);
   (void)hipHostFree(p->flag_host);
   (void)hipFree(p->arrive);
+  if (p->plan_done) (void)hipEventDestroy(p->plan_done);
+  if (p->chain_done) (void)hipEventDestroy(p->chain_done);
+  if (p->side) (void)hipStreamDestroy(p->side);
   delete p;
   return 0;
 }
@@ -315,6 +320,9 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
                 "hipHostGetDevicePointer"));
   }
   if (rc == 0) A(hip_check(hipMemset(p->arrive, 0, sizeof(uint32_t)), "hipMemset arrive"));
+  A(hip_check(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking), "hipStreamCreate"));
+  A(hip_check(hipEventCreateWithFlags(&p->plan_done, hipEventDisableTiming), "hipEventCreate"));
+  A(hip_check(hipEventCreateWithFlags(&p->chain_done, hipEventDisableTiming), "hipEventCreate"));
   if (rc == 0) A(hip_check(hipMemset(p->own_masks, 0, p->rows * sizeof(uint64_t)), "hipMemset own masks"));
   if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset scan ws"));
   if (rc == 0)
@@ -356,8 +364,11 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   TRY(omr_check(omr_round_plan(p->masks_all, N, rows, p->rpp, p->lanes, p->bounds_dev, NB, p->wset, p->umask,
                                p->prefix, p->counts_map, p->own_masks, p->arrive, p->flag_map, seq, stream),
                 "omr_round_plan"));
-  // aggregator chain (server.cc:86-96 min_next) over the union, queued right behind
-  TRY(omr_check(omr_next_offsets(p->umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
+  // aggregator chain (server.cc:86-96 min_next) over the union, on the side stream (joined before returning)
+  TRY(hip_check(hipEventRecord(p->plan_done, st), "hipEventRecord"));
+  TRY(hip_check(hipStreamWaitEvent(p->side, p->plan_done, 0), "hipStreamWaitEvent"));
+  TRY(omr_check(omr_next_offsets(p->umask, 1, p->n, p->B, p->lanes, p->parts, un, p->side), "omr_next_offsets"));
+  TRY(hip_check(hipEventRecord(p->chain_done, p->side), "hipEventRecord"));
   TRY(wait_flag(p->flag_host, seq, st));
   auto cnt = [&](int a, int s) -> uint64_t { return p->counts_host[a * NB + s]; };
   auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
@@ -402,6 +413,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
     TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, p->wset, p->prefix + static_cast<uint64_t>(N) * (rows + 1),
                                       rows, p->lanes, p->B, 0, 0, stream), "omr_move_blocks_f32 unpack"));
   }
+  TRY(hip_check(hipStreamWaitEvent(st, p->chain_done, 0), "hipStreamWaitEvent"));
   if (sent_blocks) *sent_blocks = total_send;
   if (union_blocks) *union_blocks = rs_mode ? per(N, me) : cnt(N, N);
   return 0;
