@@ -207,7 +207,8 @@ __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
 // the buffer range check.  The number of memory operations per batch is then static, so the compiler's vmcnt
 // wait for a load never includes a younger, data-dependent store (tools/tune_fused.py: 2-4 % faster than
 // branching around the stores; write-through sc0 sc1 beat plain, sc1-only and nt stores).
-// ABL (timing-only builds, csrc/tune/): bit 0 drops the data stores, bit 1 the flag/next stores.
+// ABL (timing-only builds, csrc/tune/): bit 0 drops the data stores, bit 1 the flag/next stores.  MINW: the
+// amdgpu_waves_per_eu floor (occupancy study; 1 = the compiler's choice).
 struct FusedArgs {
   const float* x;
   float* out;
@@ -221,8 +222,8 @@ struct FusedArgs {
 
 constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
 
-template <int VEC, int WAVES, int LOADS = 16, int ABL = 0>
-__global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
+template <int VEC, int WAVES, int LOADS = 16, int ABL = 0, int MINW = 1>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW))) void k_scan1f(FusedArgs a) {
   constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
   static_assert(RB >= 1 && RB <= 32, "batch bits are 32-bit");
   __shared__ uint32_t s_wfirst[WAVES], s_wlast[WAVES];
@@ -1176,7 +1177,7 @@ size_t fused_workspace_bytes(const Layout& L, const FusedShape& f) {
 
 int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* out, int32_t* flags, uint32_t* next,
                  void* ws, hipStream_t st, uint64_t* masks = nullptr) {
-  FusedArgs a;
+  FusedArgs a{};
   a.x = x;
   a.out = out;
   a.flags = flags;

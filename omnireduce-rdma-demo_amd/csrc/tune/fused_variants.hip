@@ -1,14 +1,177 @@
-// fused_variants.hip — tuning harness (not the product): k_scan1f shapes (waves per workgroup, loads in flight)
-// and timing-only ablations (ABL bit 0: no data stores, bit 1: no flag/next stores) from the product source,
-// timed side by side by tools/tune_fused.py.
+// fused_variants.hip — tuning harness (not the product): k_scan1f shapes (waves per workgroup, loads in flight,
+// occupancy floor), timing-only ablations (ABL bit 0: no data stores, bit 1: no flag/next stores) from the product
+// source, and the split-batch study kernel k_scan1s, timed side by side by tools/tune_fused.py
+// (profiles/r01/tune_round1_session4.md).
 #define OMR_NO_CAPI
 #include "../omr_kernels.hip"
 
 namespace {
+// k_scan1s — k_scan1f with SPLIT batch ownership (study): batch j (RB rows of the column segment) belongs to wave
+// j % WAVES, so the batches in flight at any moment are one contiguous stretch of every column (csrc/tune/
+// stream_probe.hip: "col split" read 2-3 % faster than the contiguous per-wave ranges).  In-batch successors
+// are stored in stream; every batch's tail (rows at and after its last non-zero row) gets its successor after
+// one barrier, from an LDS bitmap of non-empty batches (ds_or_b64) and the batches' 16-bit row masks.
+template <int VEC, int WAVES, int LOADS = 16, int ABL = 0>
+__global__ __launch_bounds__(64 * WAVES) void k_scan1s(FusedArgs a) {
+  constexpr int RB = LOADS / VEC;  // rows per batch
+  static_assert(RB >= 1 && RB <= 16, "batch bits are 16-bit");
+  constexpr uint32_t kMaxBatches = 4096;
+  __shared__ uint16_t s_bits[kMaxBatches];
+  __shared__ uint64_t s_ne[kMaxBatches / 64];
+  __shared__ int s_fix;
+  __shared__ uint32_t s_carry[64];
+  __shared__ uint32_t s_seg_last[64];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t k = lin % a.K, col = lin / a.K;
+  const uint32_t l = col % a.lanes, p = col / a.lanes;
+  const uint32_t r0 = k * a.S;
+  const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  const uint32_t lane_b = l * a.block;
+  const uint32_t row_stride = a.lanes * a.block;
+  const bool last_seg = (k + 1 == a.K);
+  const uint32_t nbt = (a.S + RB - 1) / RB;  // host: nbt <= kMaxBatches
+  const uint32_t nw = (nbt + 63) / 64;
+  for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) s_ne[i] = 0;
+  __syncthreads();
+  for (uint32_t j = wave; j < nbt; j += WAVES) {
+    const uint32_t rr = j * RB;
+    const uint32_t nrow = (a.S - rr < static_cast<uint32_t>(RB)) ? a.S - rr : RB;
+    const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+    const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, nrow * row_bytes);
+    v4f v[RB][VEC];
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                              src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
+    const __amdgpu_buffer_rsrc_t dst =
+        chunk_rsrc(a.out + blk0 * a.block, (a.out != nullptr && !(ABL & 1)) ? nrow * row_bytes : 0u);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
+      const bool nz = wave_ballot(o != 0) != 0 && static_cast<uint32_t>(s) < nrow;
+      bits |= static_cast<uint32_t>(nz) << s;
+      const bool head = (r0 + rr + s) == 0;
+      const uint32_t drop = (nz || head) ? 0u : kDropStore;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])), dst,
+                                               (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, kStoreAux);
+    }
+    if (!(ABL & 2) && static_cast<uint32_t>(lane) < nrow) {
+      const uint64_t blk = blk0 + static_cast<uint64_t>(lane) * a.lanes;
+      if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>((bits >> lane) & 1u);
+      const uint32_t above = bits >> (lane + 1);
+      if (above != 0)
+        a.next[blk] = static_cast<uint32_t>(row0 + rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above))) *
+                          row_stride + lane_b;
+      if (a.masks != nullptr && ((bits >> lane) & 1u))
+        (void)__hip_atomic_fetch_or(&a.masks[row0 + rr + lane], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      s_bits[j] = static_cast<uint16_t>(bits);
+      if (bits != 0)
+        (void)__hip_atomic_fetch_or(&s_ne[j / 64], 1ull << (j % 64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+  // batch tails: successor = first non-zero row of a later batch of the segment (else a later segment's)
+  for (uint32_t j = wave; j < nbt; j += WAVES) {
+    const uint32_t rr = j * RB;
+    const uint32_t nrow = (a.S - rr < static_cast<uint32_t>(RB)) ? a.S - rr : RB;
+    const uint32_t bits = s_bits[j];
+    uint32_t succ = kNone;
+    uint32_t wi = (j + 1) / 64;
+    uint64_t m = wi < nw ? s_ne[wi] & (~0ull << ((j + 1) % 64)) : 0ull;
+    while (wi < nw) {
+      if (m != 0) {
+        const uint32_t j2 = wi * 64 + static_cast<uint32_t>(__builtin_ctzll(m));
+        succ = j2 * RB + static_cast<uint32_t>(__builtin_ctz(static_cast<uint32_t>(s_bits[j2])));
+        break;
+      }
+      if (++wi < nw) m = s_ne[wi];
+    }
+    const uint32_t t0 = bits != 0 ? 31u - static_cast<uint32_t>(__builtin_clz(bits)) : 0u;
+    if (!(ABL & 2) && (succ != kNone || last_seg) && static_cast<uint32_t>(lane) >= t0 &&
+        static_cast<uint32_t>(lane) < nrow) {
+      const uint32_t val = succ != kNone ? static_cast<uint32_t>(row0 + succ) * row_stride + lane_b : a.sentinel + lane_b;
+      a.next[(row0 + rr + lane) * a.lanes + l] = val;
+    }
+  }
+  if (a.K == 1) return;
+  if (threadIdx.x == 0) {
+    uint32_t first = kNone, last = kNone;
+    for (uint32_t wi = 0; wi < nw; ++wi)
+      if (s_ne[wi] != 0) {
+        const uint32_t j2 = wi * 64 + static_cast<uint32_t>(__builtin_ctzll(s_ne[wi]));
+        first = j2 * RB + static_cast<uint32_t>(__builtin_ctz(static_cast<uint32_t>(s_bits[j2])));
+        break;
+      }
+    for (uint32_t wi = nw; wi-- > 0;)
+      if (s_ne[wi] != 0) {
+        const uint32_t j2 = wi * 64 + 63u - static_cast<uint32_t>(__builtin_clzll(s_ne[wi]));
+        last = j2 * RB + 31u - static_cast<uint32_t>(__builtin_clz(static_cast<uint32_t>(s_bits[j2])));
+        break;
+      }
+    const uint64_t sm = (static_cast<uint64_t>(first) << 32) | last;
+    (void)__hip_atomic_exchange(&a.summary[static_cast<uint64_t>(col) * a.K + k], sm, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&a.cnt[col], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_fix = (old == a.K - 1);
+  }
+  __syncthreads();
+  if (!s_fix) return;
+  if (threadIdx.x < a.K) {
+    const uint64_t sm = __hip_atomic_fetch_or(&a.summary[static_cast<uint64_t>(col) * a.K + threadIdx.x], 0ull,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_carry[threadIdx.x] = static_cast<uint32_t>(sm >> 32);
+    s_seg_last[threadIdx.x] = static_cast<uint32_t>(sm);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = kNone;
+    for (int kk = static_cast<int>(a.K) - 1; kk >= 0; --kk) {
+      const uint32_t first = s_carry[kk];
+      s_carry[kk] = c;
+      if (first != kNone) c = static_cast<uint32_t>(kk) * a.S + first;
+    }
+    __hip_atomic_store(&a.cnt[col], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint64_t part_row0 = static_cast<uint64_t>(p) * a.rpp;
+  const uint32_t tail_total = (a.K - 1) * a.S;
+  for (uint32_t t = threadIdx.x; t < tail_total; t += blockDim.x) {
+    const uint32_t kk = t / a.S, i = t % a.S;
+    const uint32_t last = s_seg_last[kk];
+    if (last != kNone && i < last) continue;
+    const uint32_t c = s_carry[kk];
+    const uint32_t val = (c != kNone) ? static_cast<uint32_t>(part_row0 + c) * row_stride + lane_b
+                                      : a.sentinel + lane_b;
+    a.next[(part_row0 + static_cast<uint64_t>(kk) * a.S + i) * a.lanes + l] = val;
+  }
+}
+
 template <int VEC, int W, int LOADS, int ABL>
+void go_s(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(L.parts) * L.lanes * f.K);
+  k_scan1s<VEC, W, LOADS, ABL><<<grid, 64 * W, 0, st>>>(a);
+}
+}  // namespace
+
+namespace {
+template <int VEC, int W, int LOADS, int ABL, int MINW = 1>
 void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(L.parts) * L.lanes * f.K);
-  k_scan1f<VEC, W, LOADS, ABL><<<grid, 64 * W, 0, st>>>(a);
+  k_scan1f<VEC, W, LOADS, ABL, MINW><<<grid, 64 * W, 0, st>>>(a);
 }
 
 struct Variant {
@@ -19,13 +182,14 @@ struct Variant {
 };
 
 #define VF(W, LD, A) go_f<1, W, LD, A>, go_f<4, W, LD, A>
+#define VS(W, LD, A) go_s<1, W, LD, A>, go_s<4, W, LD, A>
+#define VO(W, LD, A, O) go_f<1, W, LD, A, O>, go_f<4, W, LD, A, O>
 const Variant kVariants[] = {
-    {"w16 L16", true, VF(16, 16, 0)},
     {"w16 L8", true, VF(16, 8, 0)},
-    {"w8 L16", true, VF(8, 16, 0)},
-    {"w8 L8", true, VF(8, 8, 0)},
-    {"w4 L16", true, VF(4, 16, 0)},
-    {"w16 L32", true, VF(16, 32, 0)},
+    {"w16 L8 occ8", true, VO(16, 8, 0, 8)},
+    {"split w16 L16", true, VS(16, 16, 0)},
+    {"split w16 L16 -data-meta", false, VS(16, 16, 3)},
+    {"w16 L16", true, VF(16, 16, 0)},
     {"w16 L16 -data", false, VF(16, 16, 1)},
     {"w16 L16 -meta", false, VF(16, 16, 2)},
     {"w16 L16 -data-meta", false, VF(16, 16, 3)},
@@ -48,7 +212,7 @@ int tune_fused(int v, const float* x, float* out, int32_t* flags, uint32_t* next
   FusedShape f;
   f.K = K;
   f.S = L.rows_per_part / K;
-  FusedArgs a;
+  FusedArgs a{};  // every field zero: masks = nullptr unless set (k_scan1f ORs row masks when non-null)
   a.x = x; a.out = out; a.flags = flags; a.next = next;
   const uint64_t cols = static_cast<uint64_t>(L.parts) * L.lanes;
   a.cnt = static_cast<uint32_t*>(ws);

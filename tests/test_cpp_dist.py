@@ -38,7 +38,8 @@ def dist_lib():
     return L
 
 
-@pytest.mark.parametrize("world,B,density", [(2, 256, 0.095), (3, 1024, 0.0099), (4, 512, 0.49)])
+@pytest.mark.parametrize("world,B,density", [(2, 256, 0.095), (3, 1024, 0.0099), (4, 512, 0.49),
+                                                   (8, 256, 0.095)])
 def test_cpp_round_loopback(gpu, world, B, density):
     L = Layout(n=2 << 20, block_size=B)
     D = dist_lib()
@@ -90,8 +91,11 @@ def test_cpp_round_loopback(gpu, world, B, density):
         assert (unx == un).all()
 
 
-def test_cpp_reduce_scatter_loopback(gpu):
-    world, B = 3, 256
+@pytest.mark.parametrize("world,rounds", [(3, 1), (8, 3)])
+def test_cpp_reduce_scatter_loopback(gpu, world, rounds):
+    """Reduce-scatter mode (the bench's N>1 step); world 8 = the driver's 8-GPU scale run as threads on one GPU,
+    several rounds back to back (the plan's per-round state must reset)."""
+    B = 256
     L = Layout(n=2 << 20, block_size=B)
     D = dist_lib()
     bufs = [oracle.fill(oracle.gen_bitmap(w, 0.2, L.nb), B, mode=1, seed=w + 3) for w in range(world)]
@@ -108,8 +112,9 @@ def test_cpp_reduce_scatter_loopback(gpu):
             assert D.omr_dist_create_local(board, r, ctypes.byref(d)) == 0
             assert D.omr_ar_plan_create(d, L.n, B, L.num_lanes, 8, ctypes.byref(plan)) == 0
             st = torch.cuda.Stream()
-            assert D.omr_sparse_round_f32(plan, x.data_ptr(), out.data_ptr(), None, None, None, 1, None, None,
-                                          st.cuda_stream) == 0, D.omr_dist_last_error()
+            for _ in range(rounds):  # x is never written: every round writes the same shard sums into out
+                assert D.omr_sparse_round_f32(plan, x.data_ptr(), out.data_ptr(), None, None, None, 1, None, None,
+                                              st.cuda_stream) == 0, D.omr_dist_last_error()
             torch.cuda.synchronize()
             outs[r] = out.cpu().numpy()
             D.omr_ar_plan_destroy(plan)
