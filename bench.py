@@ -3,17 +3,17 @@
 
 Workload at N=1 (BASELINE.json configs[1]): a 256 MiB fp32 gradient, BLOCK_SIZE=256 (64 lanes, 8 partitions),
 reference generator at -r 0.095 (10 % of blocks non-zero = 90 % block-sparse), one worker, already resident
-in HBM.  One step = one pass of the hot path over it: the fused worker scan + aggregator sum kernel
-(flags, row masks, summed non-zero blocks written back in place, as client.cc:89 does) and the next-offset
-kernel.  (0.0f + x == x for the generator's data, so every step sees the same input.)  Four input/output buffer sets are
-rotated so that no step re-reads data the 256 MiB Infinity Cache still holds from the previous use.
+in HBM.  One step = one pass of the hot path over it: one launch of the single-pass kernel k_scan1f (per-block
+flags, next offsets, and the aggregated non-zero blocks written back in place, as client.cc:89 does).
+(0.0f + x == x for the generator's data, so every step sees the same input.)  Four input buffer sets are rotated
+so that no step re-reads data the 256 MiB Infinity Cache still holds from the previous use.
 N>1 (torch.distributed.run, one rank per GPU): each rank is worker r with its own 256 MiB tensor (seed r+1) and
-aggregator for shard r; a step is the full sparse all-reduce (omr.dist): local scan, RCCL exchange of the
-non-zero blocks over xGMI, rank-order shard sums, RCCL all-gather of the sums, in-place scatter.
-
+aggregator for shard r; a step is one OmniReduce round driven from C++ (libomr_dist.so over RCCL): worker scan,
+row-mask all-gather, round plan, pack, grouped send/recv of the non-zero blocks over xGMI, rank-order shard sums
+(reduce-scatter, BASELINE config 4; --dist-mode allreduce also returns every shard's sums to every worker).
 value   = bytes of gradient processed by all ranks per second (decimal GB/s, logical tensor bytes; the
           reference's "alg bw" divides the same quantity by 2^30: client.cc:445)
-roofline= the dominant kernel (k_scan1) timed with HIP events on its own stream inside the timed region;
+roofline= the dominant kernel (k_scan1f) timed with HIP events on its own stream inside the timed region;
           achieved = its algorithmic bytes per launch / its mean duration
 cpu_baseline = the oracle's C restatement of the reference loop (client.cc:19-31 + server.cc:83-99) on this
           host, 8 pthreads one per partition as client.cc:384-392, rank 0 at N=1 only.
@@ -118,16 +118,16 @@ def step_algorithmic_bytes(L: Layout, bitmaps, m: int) -> int:
     return m * L.nbytes + int(np.count_nonzero(union)) * L.block_size * 4 + m * nb * 8
 
 
-def read_pmc(path: str, workload: str, kernel: str):
+def read_pmc(path: str, workload: str, dist_mode: bool):
+    """HBM bytes per launch from a tools/pmc_traffic.py summary, when it was measured on this workload in this
+    mode (the round's worker scan writes no aggregated blocks, so single-GPU traffic does not describe it)."""
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("workload") == workload and kernel.startswith(d.get("kernel", "?") + " ") or \
-                (d.get("workload") == workload and kernel == d.get("kernel")):
-            return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None
+    same_mode = ("--force-dist" in d.get("bench_args", [])) == dist_mode
+    return d.get("hbm_bytes_per_launch") if d.get("workload") == workload and same_mode else None
 
 
 def cpu_baseline(L: Layout, bm: np.ndarray, args):
@@ -282,7 +282,7 @@ def main():
         else:
             kbytes = algorithmic_scan_bytes(L, bitmaps, m)
         achieved = kbytes / (kms * 1e-3) / 1e9
-        traffic = read_pmc(args.pmc, workload, kernel_name)
+        traffic = read_pmc(args.pmc, workload, dist_mode)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                     "kernel": kernel_name,
@@ -321,7 +321,7 @@ def main():
                    "num_lanes": L.num_lanes, "num_threads": L.num_threads, "density_r": args.density,
                    "nonzero_fraction": round(float(np.mean([bm.mean() for bm in bitmaps])), 5),
                    "workers_per_gpu": m, "rotating_buffer_sets": len(sets),
-                   "parallelism": "single GPU" if n_gpus == 1 else
+                   "parallelism": "single GPU" if not dist_mode else
                    f"dp{n_gpus} sparse {'all-reduce' if args.dist_mode == 'allreduce' else 'reduce-scatter'} over "
                    f"RCCL ({args.dist_impl} round driver)"},
         "alg_bw_GiBps_reference_style": round(total_bytes / (ms_per_step * 1e-3) / 2 ** 30, 2),

@@ -197,8 +197,6 @@ struct omr_ar_plan {
   uint32_t* flag_host = nullptr;  // pinned: the plan kernel stores the round's sequence number here
   uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
-  hipStream_t side = nullptr;      // the union chain runs here, beside the host's wait and the exchange
-  hipEvent_t plan_done = nullptr, chain_done = nullptr;
 };
 
 extern "C" {
@@ -257,9 +255,6 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   (void)hipHostFree(p->counts_host);
   (void)hipHostFree(p->flag_host);
   (void)hipFree(p->arrive);
-  if (p->plan_done) (void)hipEventDestroy(p->plan_done);
-  if (p->chain_done) (void)hipEventDestroy(p->chain_done);
-  if (p->side) (void)hipStreamDestroy(p->side);
   delete p;
   return 0;
 }
@@ -320,9 +315,6 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
                 "hipHostGetDevicePointer"));
   }
   if (rc == 0) A(hip_check(hipMemset(p->arrive, 0, sizeof(uint32_t)), "hipMemset arrive"));
-  A(hip_check(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking), "hipStreamCreate"));
-  A(hip_check(hipEventCreateWithFlags(&p->plan_done, hipEventDisableTiming), "hipEventCreate"));
-  A(hip_check(hipEventCreateWithFlags(&p->chain_done, hipEventDisableTiming), "hipEventCreate"));
   if (rc == 0) A(hip_check(hipMemset(p->own_masks, 0, p->rows * sizeof(uint64_t)), "hipMemset own masks"));
   if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset scan ws"));
   if (rc == 0)
@@ -364,25 +356,24 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   TRY(omr_check(omr_round_plan(p->masks_all, N, rows, p->rpp, p->lanes, p->bounds_dev, NB, p->wset, p->umask,
                                p->prefix, p->counts_map, p->own_masks, p->arrive, p->flag_map, seq, stream),
                 "omr_round_plan"));
-  // aggregator chain (server.cc:86-96 min_next) over the union, on the side stream (joined before returning)
-  TRY(hip_check(hipEventRecord(p->plan_done, st), "hipEventRecord"));
-  TRY(hip_check(hipStreamWaitEvent(p->side, p->plan_done, 0), "hipStreamWaitEvent"));
-  TRY(omr_check(omr_next_offsets(p->umask, 1, p->n, p->B, p->lanes, p->parts, un, p->side), "omr_next_offsets"));
-  TRY(hip_check(hipEventRecord(p->chain_done, p->side), "hipEventRecord"));
+  // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407), then the
+  //     aggregator chain (server.cc:86-96 min_next) over the union: both addressed by device-side data only, so
+  //     they are queued before the host learns the counts and run while it waits.  (Every host API call costs
+  //     microseconds; a round that spends them on side streams and events is host-bound.)
+  const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
+  if (N > 1)
+    TRY(omr_check(omr_move_blocks_f32(x, p->packed, 0, p->masks_all + static_cast<uint64_t>(me) * rows,
+                                      p->prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
+                                      r1, stream), "omr_move_blocks_f32 pack"));
+  TRY(omr_check(omr_next_offsets(p->umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
   TRY(wait_flag(p->flag_host, seq, st));
   auto cnt = [&](int a, int s) -> uint64_t { return p->counts_host[a * NB + s]; };
   auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
-  const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
   const uint64_t own_shard = per(me, me);
   const uint64_t total_send = cnt(me, N) - own_shard;
-  // 4. pack own non-zero blocks of the other shards (block order == shard order), send each slice to its
-  //    aggregator (common.cc:405-407, :449); receive this shard's blocks from every peer
+  // 4b. send each slice to its aggregator (common.cc:449); receive this shard's blocks from every peer
   std::vector<uint64_t> roff(N, 0);
   if (N > 1) {
-    if (total_send)
-      TRY(omr_check(omr_move_blocks_f32(x, p->packed, 0, p->masks_all + static_cast<uint64_t>(me) * rows,
-                                        p->prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
-                                        r1, stream), "omr_move_blocks_f32 pack"));
     std::vector<Slice> sends(N), recvs(N);
     uint64_t acc = 0;
     for (int s = 0; s < N; ++s) {
@@ -413,7 +404,6 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
     TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, p->wset, p->prefix + static_cast<uint64_t>(N) * (rows + 1),
                                       rows, p->lanes, p->B, 0, 0, stream), "omr_move_blocks_f32 unpack"));
   }
-  TRY(hip_check(hipStreamWaitEvent(st, p->chain_done, 0), "hipStreamWaitEvent"));
   if (sent_blocks) *sent_blocks = total_send;
   if (union_blocks) *union_blocks = rs_mode ? per(N, me) : cnt(N, N);
   return 0;

@@ -792,12 +792,15 @@ __device__ __forceinline__ uint32_t take_bits(uint64_t& rem, uint32_t (&lj)[SL],
   return nv;
 }
 
-// One workgroup per mask array (count worker arrays + the write set), 1024 threads, each a contiguous run of
-// rows: popcounts -> block-wide exclusive scan -> prefix[a][r]; counts[a][s] = prefix[a][bounds[s]].  The
+// One workgroup per mask array (count worker arrays + the write set), 1024 threads.  Pass 1 reads the array's
+// rows coalesced (row r by thread r mod 1024, four rows in flight per thread) and keeps them in LDS; the
 // write-set workgroup also forms union = OR of the workers (the aggregator's min_next domain, server.cc:86-96)
 // and write set = union | lane heads (every lane head is sent and returned: client.cc:201-205), and clears the
-// next round's own-mask buffer.
+// next round's own-mask buffer.  Pass 2 gives each thread a contiguous run of rows: popcounts -> block-wide
+// exclusive scan -> prefix[a][r]; counts[a][s] = prefix[a][bounds[s]].  (Arrays of more than kPlanLdsRows rows
+// are re-read in pass 2 instead of kept in LDS.)
 constexpr int kPlanThreads = 1024;
+constexpr uint64_t kPlanLdsRows = 8192;  // 64 KiB of dynamic LDS
 
 __device__ __forceinline__ uint64_t plan_row(const uint64_t* masks, uint32_t a, uint32_t count, uint64_t rows,
                                              uint64_t r, uint32_t rpp, uint64_t all_lanes, uint64_t* uni) {
@@ -816,7 +819,7 @@ struct PlanArgs {
   uint64_t* write_set;
   uint64_t* union_masks;
   uint32_t* prefix;
-  uint32_t* counts;
+  uint32_t* counts;     // device or host-mapped memory: stored at system scope
   uint64_t* zero_masks;
   uint32_t* arrive;     // device arrival counter (zero between launches) or null
   uint32_t* done_flag;  // receives `seq` once every workgroup's counts are visible system-wide, or null
@@ -824,24 +827,45 @@ struct PlanArgs {
 };
 
 __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
+  extern __shared__ uint64_t s_val[];  // [rows] when rows <= kPlanLdsRows
   __shared__ uint32_t s_wave[kPlanThreads / 64];
+  __shared__ uint64_t s_bounds[OMR_MAX_WORKERS + 2];
   const uint32_t arr = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint64_t all_lanes = a.lanes >= 64 ? ~0ull : ((1ull << a.lanes) - 1ull);
+  const bool ws = arr == a.count;
+  const bool keep = a.rows <= kPlanLdsRows;
+  if (t < a.nbounds) s_bounds[t] = a.bounds[t];
+  // pass 1: coalesced row reads, 4 rows per thread per step
+  for (uint64_t r0 = t; r0 < a.rows; r0 += 4 * kPlanThreads) {
+    uint64_t v[4], u[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t r = r0 + static_cast<uint64_t>(i) * kPlanThreads;
+      v[i] = r < a.rows ? plan_row(a.masks, arr, a.count, a.rows, r, a.rpp, all_lanes, &u[i]) : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t r = r0 + static_cast<uint64_t>(i) * kPlanThreads;
+      if (r >= a.rows) break;
+      if (keep) s_val[r] = v[i];
+      if (ws) {
+        a.write_set[r] = v[i];
+        a.union_masks[r] = u[i];
+        if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
+      }
+    }
+  }
+  __syncthreads();  // LDS rows (and, when re-read, this workgroup's write-set stores) visible to every thread
   const uint64_t per = (a.rows + kPlanThreads - 1) / kPlanThreads;
   const uint64_t rb = t * per < a.rows ? t * per : a.rows;
   const uint64_t re = rb + per < a.rows ? rb + per : a.rows;
-  const bool ws = arr == a.count;
+  auto row = [&](uint64_t r) -> uint64_t {
+    if (keep) return s_val[r];
+    if (ws) return a.write_set[r];
+    return a.masks[static_cast<uint64_t>(arr) * a.rows + r];
+  };
   uint32_t sum = 0;
-  for (uint64_t r = rb; r < re; ++r) {
-    uint64_t u = 0;
-    const uint64_t v = plan_row(a.masks, arr, a.count, a.rows, r, a.rpp, all_lanes, &u);
-    if (ws) {
-      a.write_set[r] = v;
-      a.union_masks[r] = u;
-      if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
-    }
-    sum += static_cast<uint32_t>(__builtin_popcountll(v));
-  }
+  for (uint64_t r = rb; r < re; ++r) sum += static_cast<uint32_t>(__builtin_popcountll(row(r)));
   // block-wide exclusive scan of the per-thread sums (wave shuffles, then the 16 wave totals)
   uint32_t inc = sum;
 #pragma unroll
@@ -860,27 +884,29 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
   uint32_t* pre = a.prefix + static_cast<uint64_t>(arr) * (a.rows + 1);
   for (uint64_t r = rb; r < re; ++r) {
     for (uint32_t s = 0; s < a.nbounds; ++s)
-      if (a.bounds[s] == r) a.counts[arr * a.nbounds + s] = run;
+      if (s_bounds[s] == r)
+        __hip_atomic_store(&a.counts[arr * a.nbounds + s], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     pre[r] = run;
-    uint64_t u = 0;
-    run += static_cast<uint32_t>(__builtin_popcountll(
-        ws ? a.write_set[r] : plan_row(a.masks, arr, a.count, a.rows, r, a.rpp, all_lanes, &u)));
+    run += static_cast<uint32_t>(__builtin_popcountll(row(r)));
   }
   if (t == 0) {
     pre[a.rows] = total;
     for (uint32_t s = 0; s < a.nbounds; ++s)
-      if (a.bounds[s] >= a.rows) a.counts[arr * a.nbounds + s] = total;
+      if (s_bounds[s] >= a.rows)
+        __hip_atomic_store(&a.counts[arr * a.nbounds + s], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (a.arrive == nullptr) return;
-  // completion notice for a host that polls instead of waiting on an event: every workgroup publishes its counts
-  // system-wide and arrives; the last arrival stores the round's sequence number and re-arms the counter
-  __threadfence_system();
+  // completion notice for a host that polls instead of waiting on an event.  The counts went out as system-scope
+  // (write-through) stores; once every thread has seen them acknowledged (vmcnt(0)) and passed the barrier, the
+  // workgroup arrives, and the last arrival stores the round's sequence number and re-arms the counter.  No L2
+  // write-back is needed: nothing the host reads sits in an L2.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == a.count) {
       __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -1592,6 +1618,7 @@ int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uin
       (num_bounds > 0 && (bounds == nullptr || counts == nullptr)))
     return fail("round_plan: NULL pointer");
   if (rows > 0xFFFFFFFFull / 64) return fail("round_plan: too many rows");
+  if (num_bounds > OMR_MAX_WORKERS + 2) return fail("round_plan: %u bounds > %d", num_bounds, OMR_MAX_WORKERS + 2);
   PlanArgs a;
   a.masks = row_masks;
   a.count = count;
@@ -1609,7 +1636,8 @@ int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uin
   a.arrive = arrive;
   a.done_flag = done_flag;
   a.seq = seq;
-  k_round_plan<<<count + 1, kPlanThreads, 0, S(stream)>>>(a);
+  const size_t lds = rows <= kPlanLdsRows ? rows * sizeof(uint64_t) : 0;
+  k_round_plan<<<count + 1, kPlanThreads, lds, S(stream)>>>(a);
   return launch_status("k_round_plan");
 }
 

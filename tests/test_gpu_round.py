@@ -79,8 +79,10 @@ def test_worker_scan_masks(gpu, n, B, density):
 
 
 @pytest.mark.parametrize("count,rows,rpp,lanes", [(1, 64, 8, 64), (3, 512, 64, 64), (8, 4096, 512, 64),
-                                                   (5, 1280, 256, 16), (16, 100, 25, 32)])
+                                                   (5, 1280, 256, 16), (16, 100, 25, 32),
+                                                   (2, 8192, 1024, 64), (3, 20480, 2560, 16)])
 def test_round_plan(gpu, count, rows, rpp, lanes):
+    """Rows <= 8192 stay in LDS between the two passes; more are re-read (the last case)."""
     rng = np.random.default_rng(count * 1000 + rows)
     lane_mask = (1 << lanes) - 1 if lanes < 64 else (1 << 64) - 1
     dens = rng.random(count) * 0.5
