@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--dist-mode", choices=("reduce", "allreduce"), default="reduce",
                    help="N>1 step: workers -> aggregators reduce-scatter (BASELINE config 4, default) or the full "
                         "all-reduce (sums back to every worker)")
+    p.add_argument("--dist-sync", action="store_true",
+                   help="N>1, C++ driver: keep each round's exchange on the caller's stream (default: OMR_ROUND_ASYNC, "
+                        "round k's exchange over xGMI overlaps round k+1's worker scan)")
     p.add_argument("--dist-impl", choices=("cpp", "torch"), default="cpp",
                    help="N>1 round driver: C++ (libomr_dist.so, RCCL from C++) or Python (omr.dist over "
                         "torch.distributed); same protocol and kernels")
@@ -201,10 +204,14 @@ def main():
         for xs, out in sets:  # out-of-place result buffers keep every step's input pristine
             out.copy_(xs[0])
 
+        pipelined = args.dist_impl == "cpp" and not args.dist_sync
+
         def step(i, ev=None):
             xs, out = sets[i % len(sets)]
-            engine.run(xs[0], out=out, ev=None if args.dist_impl == "cpp" else ev,
-                       mode=0 if args.dist_mode == "allreduce" else 1)
+            if args.dist_impl == "cpp":
+                engine.run(xs[0], out=out, mode=0 if args.dist_mode == "allreduce" else 1, async_=pipelined)
+            else:
+                engine.run(xs[0], out=out, ev=ev, mode=0 if args.dist_mode == "allreduce" else 1)
     else:
         fused = m == 1 and args.kernel == "fused"
         plan = ops.ScanSumPlan(L, m, device=dev, fused=fused)
@@ -221,8 +228,13 @@ def main():
             if not fused:
                 plan.resolve_next()
 
+    def join():  # asynchronous rounds: the caller's stream waits for the last one (the device sync below covers it too)
+        if dist_mode and args.dist_impl == "cpp":
+            engine.join(stream)
+
     for i in range(args.warmup):
         step(i)
+    join()
     torch.cuda.synchronize()
     if dist_mode:
         torch.distributed.barrier()
@@ -240,6 +252,7 @@ def main():
         step(args.warmup + i, None if one_kernel else (kev[i] if i % every == 0 else None))
     if one_kernel:
         span[1].record(stream)
+    join()
     torch.cuda.synchronize()
     if dist_mode:
         torch.distributed.barrier()
@@ -323,7 +336,8 @@ def main():
                    "workers_per_gpu": m, "rotating_buffer_sets": len(sets),
                    "parallelism": "single GPU" if not dist_mode else
                    f"dp{n_gpus} sparse {'all-reduce' if args.dist_mode == 'allreduce' else 'reduce-scatter'} over "
-                   f"RCCL ({args.dist_impl} round driver)"},
+                   f"RCCL ({args.dist_impl} round driver"
+                   f"{', rounds pipelined: exchange k beside scan k+1' if dist_mode and args.dist_impl == 'cpp' and not args.dist_sync else ''})"},
         "alg_bw_GiBps_reference_style": round(total_bytes / (ms_per_step * 1e-3) / 2 ** 30, 2),
         "roofline": roofline,
         "cpu_baseline": None,

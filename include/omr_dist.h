@@ -73,9 +73,19 @@ int omr_sparse_allreduce_f32(omr_ar_plan* plan, const float* x, float* out, int3
  *                             *union_blocks = this shard's write-set size. */
 #define OMR_ROUND_ALLREDUCE 0
 #define OMR_ROUND_REDUCE_SCATTER 1
+/* OR-ed into `mode`: the round's exchange and aggregation (send/recv, shard sums [, sums back, unpack]) go on the
+ * plan's own communication stream instead of `stream`, so the next call's worker scan overlaps this round's
+ * transfer over xGMI (the bucket pipeline of a training step).  flags / next_offsets / union_next are ready in
+ * `stream` order as usual; `out` is ready once omr_ar_plan_join() has made a stream wait for the round (or after
+ * a device-wide synchronise).  Two consecutive rounds use alternating plan buffers; a round waits for the one two
+ * calls back before reusing its buffers.  x and out must stay untouched (and must not be a later round's input)
+ * until the round is joined. */
+#define OMR_ROUND_ASYNC 0x100
 int omr_sparse_round_f32(omr_ar_plan* plan, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
                          uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
                          omr_stream_t stream);
+/* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
+int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -67,9 +67,14 @@ struct omr_dist {
 
 namespace {
 
+// Two communicators over the same ranks: `comm` carries the mask all-gather, `xcomm` the block exchange, so an
+// asynchronous round's exchange (on the plan's communication stream) may run beside the next round's all-gather
+// (on the caller's stream) — RCCL forbids concurrent use of ONE communicator from two streams.  Each is used in
+// the same order on every rank.
 struct RcclDist final : omr_dist {
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr, xcomm = nullptr;
   ~RcclDist() override {
+    if (xcomm) (void)ncclCommDestroy(xcomm);
     if (comm) (void)ncclCommDestroy(comm);
   }
   int allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
@@ -79,8 +84,8 @@ struct RcclDist final : omr_dist {
     TRY(nccl_check(ncclGroupStart(), "ncclGroupStart"));
     for (int p = 0; p < world; ++p) {
       if (p == rank) continue;
-      if (recvs[p].bytes) TRY(nccl_check(ncclRecv(recvs[p].ptr, recvs[p].bytes, ncclUint8, p, comm, st), "ncclRecv"));
-      if (sends[p].bytes) TRY(nccl_check(ncclSend(sends[p].ptr, sends[p].bytes, ncclUint8, p, comm, st), "ncclSend"));
+      if (recvs[p].bytes) TRY(nccl_check(ncclRecv(recvs[p].ptr, recvs[p].bytes, ncclUint8, p, xcomm, st), "ncclRecv"));
+      if (sends[p].bytes) TRY(nccl_check(ncclSend(sends[p].ptr, sends[p].bytes, ncclUint8, p, xcomm, st), "ncclSend"));
     }
     return nccl_check(ncclGroupEnd(), "ncclGroupEnd");
   }
@@ -178,14 +183,24 @@ struct omr_ar_plan {
   std::vector<uint64_t> bounds;   // shard s = rows [bounds[s], bounds[s+1])
   uint64_t shard_nb = 0;          // blocks of the largest shard
   uint64_t* own_masks = nullptr;  // [rows] this rank's masks (the scan ORs into it; the plan kernel re-zeroes it)
-  uint64_t* masks_all = nullptr;  // [N][rows] every worker's masks (all-gather)
-  uint64_t* wset = nullptr;       // [rows] write set: union + lane heads
-  uint64_t* umask = nullptr;      // [rows] union of the workers' masks
-  uint32_t* prefix = nullptr;     // [N+1][rows+1] popcount prefixes: workers, then the write set
+  // per-round state, two sets used alternately (an asynchronous round's exchange still reads its set while the
+  // next round fills the other)
+  struct Set {
+    uint64_t* masks_all = nullptr;  // [N][rows] every worker's masks (all-gather)
+    uint64_t* wset = nullptr;       // [rows] write set: union + lane heads
+    uint64_t* umask = nullptr;      // [rows] union of the workers' masks
+    uint32_t* prefix = nullptr;     // [N+1][rows+1] popcount prefixes: workers, then the write set
+    float* packed = nullptr;        // own non-zero blocks of the other shards, block order
+    hipEvent_t ready = nullptr;     // recorded on the caller's stream once the set is filled (async rounds)
+    hipEvent_t done = nullptr;      // recorded on the communication stream once the round is through with it
+    bool pending = false;           // `done` recorded and not yet waited for by a refill
+  } set[2];
+  int cur = 0;                      // the set the next round fills
+  int last_async = -1;              // set of the last asynchronous round (for join)
+  hipStream_t cs = nullptr;         // communication stream of asynchronous rounds
   uint64_t* bounds_dev = nullptr;
   uint32_t* counts_host = nullptr;  // [N+1][N+1] prefix[a][bounds[s]], pinned host memory the plan kernel writes
   uint32_t* counts_map = nullptr;   // its device-side address
-  float* packed = nullptr;   // own non-zero blocks of the other shards, block order
   float* recv = nullptr;     // this shard's blocks from each peer, peer-major
   float* results = nullptr;  // all-reduce: every shard's sums, write-set order
   int32_t* flags_ws = nullptr;
@@ -217,7 +232,9 @@ int omr_dist_create_rccl(const void* id, int rank, int world, omr_dist** out) {
   d->world = world;
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof(uid));
-  if (int rc = nccl_check(ncclCommInitRank(&d->comm, world, uid, rank), "ncclCommInitRank")) {
+  int rc = nccl_check(ncclCommInitRank(&d->comm, world, uid, rank), "ncclCommInitRank");
+  if (rc == 0) rc = nccl_check(ncclCommSplit(d->comm, 0, rank, &d->xcomm, nullptr), "ncclCommSplit");
+  if (rc != 0) {
     delete d;
     return rc;
   }
@@ -249,9 +266,16 @@ int omr_dist_destroy(omr_dist* d) {
 
 int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p == nullptr) return 0;
-  void* devs[] = {p->own_masks, p->masks_all, p->wset,    p->umask,    p->prefix,   p->bounds_dev,
-                  p->packed,    p->recv,      p->results, p->flags_ws, p->next_ws,  p->unext_ws,   p->scan_ws};
+  void* devs[] = {p->own_masks, p->bounds_dev, p->recv,    p->results,
+                  p->flags_ws,  p->next_ws,    p->unext_ws, p->scan_ws};
   for (void* v : devs) (void)hipFree(v);
+  for (auto& st : p->set) {
+    void* sv[] = {st.masks_all, st.wset, st.umask, st.prefix, st.packed};
+    for (void* v : sv) (void)hipFree(v);
+    if (st.ready) (void)hipEventDestroy(st.ready);
+    if (st.done) (void)hipEventDestroy(st.done);
+  }
+  if (p->cs) (void)hipStreamDestroy(p->cs);
   (void)hipHostFree(p->counts_host);
   (void)hipHostFree(p->flag_host);
   (void)hipFree(p->arrive);
@@ -286,15 +310,18 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
     if (rc == 0) rc = r;
   };
   A(dev_alloc(&p->own_masks, p->rows));
-  A(dev_alloc(&p->masks_all, static_cast<size_t>(N) * p->rows));
-  A(dev_alloc(&p->wset, p->rows));
-  A(dev_alloc(&p->umask, p->rows));
-  A(dev_alloc(&p->prefix, static_cast<size_t>(N + 1) * (p->rows + 1)));
-  A(dev_alloc(&p->bounds_dev, N + 1));
-  if (N > 1) {
-    A(dev_alloc(&p->packed, n));
-    A(dev_alloc(&p->recv, static_cast<size_t>(N - 1) * p->shard_nb * block_size));
+  for (auto& st : p->set) {
+    A(dev_alloc(&st.masks_all, static_cast<size_t>(N) * p->rows));
+    A(dev_alloc(&st.wset, p->rows));
+    A(dev_alloc(&st.umask, p->rows));
+    A(dev_alloc(&st.prefix, static_cast<size_t>(N + 1) * (p->rows + 1)));
+    if (N > 1) A(dev_alloc(&st.packed, n));
+    A(hip_check(hipEventCreateWithFlags(&st.ready, hipEventDisableTiming), "hipEventCreate"));
+    A(hip_check(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "hipEventCreate"));
   }
+  A(hip_check(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking), "hipStreamCreate"));
+  A(dev_alloc(&p->bounds_dev, N + 1));
+  if (N > 1) A(dev_alloc(&p->recv, static_cast<size_t>(N - 1) * p->shard_nb * block_size));
   A(dev_alloc(&p->results, n));
   A(dev_alloc(&p->flags_ws, p->nb));
   A(dev_alloc(&p->next_ws, p->nb));
@@ -336,6 +363,8 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
                          uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
                          omr_stream_t stream) {
   if (p == nullptr || x == nullptr || out == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL");
+  const bool async = (mode & OMR_ROUND_ASYNC) != 0;
+  mode &= ~OMR_ROUND_ASYNC;
   if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER)
     return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -345,16 +374,24 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   int32_t* fl = flags ? flags : p->flags_ws;
   uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
   uint32_t* un = union_next ? union_next : p->unext_ws;
+  const int si = p->cur;
+  omr_ar_plan::Set& S = p->set[si];
+  p->cur ^= 1;
   // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass
   TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, p->own_masks, nullptr, p->scan_ws,
                                     p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+  // the set is refilled from here on: an asynchronous round two calls back must be through with it
+  if (S.pending) {
+    TRY(hip_check(hipStreamWaitEvent(st, S.done, 0), "hipStreamWaitEvent"));
+    S.pending = false;
+  }
   // 2. every worker's row masks
-  TRY(p->d->allgather(p->own_masks, p->masks_all, rows * sizeof(uint64_t), st));
+  TRY(p->d->allgather(p->own_masks, S.masks_all, rows * sizeof(uint64_t), st));
   // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for the next round
   //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
   const uint32_t seq = ++p->seq;
-  TRY(omr_check(omr_round_plan(p->masks_all, N, rows, p->rpp, p->lanes, p->bounds_dev, NB, p->wset, p->umask,
-                               p->prefix, p->counts_map, p->own_masks, p->arrive, p->flag_map, seq, stream),
+  TRY(omr_check(omr_round_plan(S.masks_all, N, rows, p->rpp, p->lanes, p->bounds_dev, NB, S.wset, S.umask,
+                               S.prefix, p->counts_map, p->own_masks, p->arrive, p->flag_map, seq, stream),
                 "omr_round_plan"));
   // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407), then the
   //     aggregator chain (server.cc:86-96 min_next) over the union: both addressed by device-side data only, so
@@ -362,10 +399,18 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   //     microseconds; a round that spends them on side streams and events is host-bound.)
   const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
   if (N > 1)
-    TRY(omr_check(omr_move_blocks_f32(x, p->packed, 0, p->masks_all + static_cast<uint64_t>(me) * rows,
-                                      p->prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
+    TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * rows,
+                                      S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
                                       r1, stream), "omr_move_blocks_f32 pack"));
-  TRY(omr_check(omr_next_offsets(p->umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
+  TRY(omr_check(omr_next_offsets(S.umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
+  // the rest goes on the communication stream for an asynchronous round, behind everything queued so far
+  hipStream_t xs = st;
+  if (async) {
+    TRY(hip_check(hipEventRecord(S.ready, st), "hipEventRecord"));
+    TRY(hip_check(hipStreamWaitEvent(p->cs, S.ready, 0), "hipStreamWaitEvent"));
+    xs = p->cs;
+  }
+  const omr_stream_t xstream = reinterpret_cast<omr_stream_t>(xs);
   TRY(wait_flag(p->flag_host, seq, st));
   auto cnt = [&](int a, int s) -> uint64_t { return p->counts_host[a * NB + s]; };
   auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
@@ -378,18 +423,18 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
     uint64_t acc = 0;
     for (int s = 0; s < N; ++s) {
       const uint64_t k0 = cnt(me, s) - (s > me ? own_shard : 0);
-      sends[s] = Slice{p->packed + k0 * B, s == me ? 0 : per(me, s) * B * sizeof(float)};
+      sends[s] = Slice{S.packed + k0 * B, s == me ? 0 : per(me, s) * B * sizeof(float)};
       roff[s] = acc;
       recvs[s] = Slice{p->recv + acc * B, s == me ? 0 : per(s, me) * B * sizeof(float)};
       if (s != me) acc += per(s, me);
     }
-    TRY(p->d->exchange(sends, recvs, st));
+    TRY(p->d->exchange(sends, recvs, xs));
   }
   // 5. aggregator: rank-order shard sums (server.cc:97-98), own contribution read in place
   const bool rs_mode = mode == OMR_ROUND_REDUCE_SCATTER;
   float* sums = rs_mode ? out : p->results + cnt(N, me) * B;
-  TRY(omr_check(omr_shard_sum_f32(x, static_cast<uint32_t>(me), p->recv, roff.data(), p->masks_all, N, p->prefix,
-                                  p->wset, rows, r0, r1, p->lanes, p->B, rs_mode ? 0 : 1, sums, stream),
+  TRY(omr_check(omr_shard_sum_f32(x, static_cast<uint32_t>(me), p->recv, roff.data(), S.masks_all, N, S.prefix,
+                                  S.wset, rows, r0, r1, p->lanes, p->B, rs_mode ? 0 : 1, sums, xstream),
                 "omr_shard_sum_f32"));
   if (!rs_mode) {
     // 6. sums back to every worker (server.cc:162), scattered in place (client.cc:89)
@@ -399,13 +444,27 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
         ss[s] = Slice{sums, s == me ? 0 : per(N, me) * B * sizeof(float)};
         sr[s] = Slice{p->results + cnt(N, s) * B, s == me ? 0 : per(N, s) * B * sizeof(float)};
       }
-      TRY(p->d->exchange(ss, sr, st));
+      TRY(p->d->exchange(ss, sr, xs));
     }
-    TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, p->wset, p->prefix + static_cast<uint64_t>(N) * (rows + 1),
-                                      rows, p->lanes, p->B, 0, 0, stream), "omr_move_blocks_f32 unpack"));
+    TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, S.wset, S.prefix + static_cast<uint64_t>(N) * (rows + 1),
+                                      rows, p->lanes, p->B, 0, 0, xstream), "omr_move_blocks_f32 unpack"));
+  }
+  if (async) {
+    TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
+    S.pending = true;
+    p->last_async = si;
   }
   if (sent_blocks) *sent_blocks = total_send;
   if (union_blocks) *union_blocks = rs_mode ? per(N, me) : cnt(N, N);
+  return 0;
+}
+
+int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
+  if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_join: NULL");
+  if (p->last_async < 0) return 0;
+  // the communication stream runs rounds in issue order: waiting for the last one covers every earlier one
+  TRY(hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), p->set[p->last_async].done, 0),
+                "hipStreamWaitEvent"));
   return 0;
 }
 

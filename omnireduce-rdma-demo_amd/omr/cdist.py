@@ -46,6 +46,7 @@ def load():
         "omr_ar_plan_destroy": (i, [vp]),
         "omr_sparse_allreduce_f32": (i, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "omr_sparse_round_f32": (i, [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]),
+        "omr_ar_plan_join": (i, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -82,12 +83,15 @@ class CppSparseAllreduce:
                "omr_ar_plan_create")
         self.rank, self.world = rank, world
 
-    ALLREDUCE, REDUCE_SCATTER = 0, 1
+    ALLREDUCE, REDUCE_SCATTER, ASYNC = 0, 1, 0x100
 
     def run(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, ev=None, flags=None, next_offsets=None,
-            union_next=None, mode: int = 0):
+            union_next=None, mode: int = 0, async_: bool = False):
         """mode 0: all-reduce (every worker gets every shard's sums); 1: reduce-scatter (stop at the
-        aggregators: `out` gets this rank's shard sums only)."""
+        aggregators: `out` gets this rank's shard sums only).  async_: the exchange and the sums run on the plan's
+        communication stream, overlapping the next call's worker scan; `out` is ready after join()."""
+        if async_:
+            mode |= self.ASYNC
         out = x if out is None else out
         sent, uni = ctypes.c_uint64(), ctypes.c_uint64()
         st = torch.cuda.current_stream(self.device)
@@ -100,6 +104,11 @@ class CppSparseAllreduce:
         if ev is not None:
             ev[1].record(st)
         return sent.value, uni.value
+
+    def join(self, stream=None):
+        """Make `stream` (default: the current stream) wait for every asynchronous round issued so far."""
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(load().omr_ar_plan_join(self._p, st.cuda_stream), "omr_ar_plan_join")
 
     def close(self):
         D = load()

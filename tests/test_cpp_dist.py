@@ -34,6 +34,7 @@ def dist_lib():
     L.omr_ar_plan_destroy.argtypes = [vp]
     L.omr_sparse_allreduce_f32.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.omr_sparse_round_f32.argtypes = [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]
+    L.omr_ar_plan_join.argtypes = [vp, vp]
     L.omr_dist_last_error.restype = ctypes.c_char_p
     return L
 
@@ -137,6 +138,62 @@ def test_cpp_reduce_scatter_loopback(gpu, world, rounds):
         lo, hi = bounds[r] * L.num_lanes * B, bounds[r + 1] * L.num_lanes * B
         exp[lo:hi] = full[lo:hi]
         assert (outs[r].view(np.uint32) == exp.view(np.uint32)).all(), f"rank {r}"
+
+
+@pytest.mark.parametrize("world,mode", [(3, 1), (8, 1), (4, 0)])
+def test_cpp_async_rounds_loopback(gpu, world, mode):
+    """OMR_ROUND_ASYNC: the exchange and sums of round k run on the plan's communication stream while round k+1
+    scans; rounds take different inputs and outputs (the bench's rotation), use the two plan buffer sets in
+    turn (five rounds: each set refilled twice), and are joined once at the end."""
+    B, rounds = 256, 5
+    L = Layout(n=2 << 20, block_size=B)
+    D = dist_lib()
+    bufs = [[oracle.fill(oracle.gen_bitmap(w + 10 * k, 0.15, L.nb), B, mode=1, seed=w + 10 * k + 1)
+             for w in range(world)] for k in range(rounds)]
+    board = D.omr_local_board_create(world)
+    errs, outs = [], [[None] * rounds for _ in range(world)]
+
+    def rank(r):
+        try:
+            torch.cuda.set_device(0)
+            xs = [torch.from_numpy(bufs[k][r].copy()).cuda() for k in range(rounds)]
+            os_ = [x.clone() for x in xs]
+            d, plan = ctypes.c_void_p(), ctypes.c_void_p()
+            assert D.omr_dist_create_local(board, r, ctypes.byref(d)) == 0
+            assert D.omr_ar_plan_create(d, L.n, B, L.num_lanes, 8, ctypes.byref(plan)) == 0
+            st = torch.cuda.Stream()
+            for k in range(rounds):
+                assert D.omr_sparse_round_f32(plan, xs[k].data_ptr(), os_[k].data_ptr(), None, None, None,
+                                              mode | 0x100, None, None, st.cuda_stream) == 0, D.omr_dist_last_error()
+            assert D.omr_ar_plan_join(plan, st.cuda_stream) == 0
+            st.synchronize()
+            for k in range(rounds):
+                outs[r][k] = os_[k].cpu().numpy()
+            D.omr_ar_plan_destroy(plan)
+            D.omr_dist_destroy(d)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    D.omr_local_board_destroy(board)
+    assert not errs, errs
+    bounds = [s * L.rows // world for s in range(world + 1)]
+    for k in range(rounds):
+        uf = oracle.union_flags([oracle.flags_from_data(b, B) for b in bufs[k]])
+        for r in range(world):
+            full = bufs[k][r].copy()
+            oracle.block_sum(bufs[k], L.n, B, L.num_lanes, 8, uf, full)
+            if mode == 1:
+                exp = bufs[k][r].copy()
+                lo, hi = bounds[r] * L.num_lanes * B, bounds[r + 1] * L.num_lanes * B
+                exp[lo:hi] = full[lo:hi]
+            else:
+                exp = full
+            assert (outs[r][k].view(np.uint32) == exp.view(np.uint32)).all(), f"round {k} rank {r}"
 
 
 def _run(cmd, timeout=300):
