@@ -267,6 +267,12 @@ int omr_host_plan_create(uint64_t n, uint32_t block_size, uint32_t num_lanes, ui
 int omr_host_plan_destroy(omr_host_plan* plan);
 int omr_host_scan_sum_f32(omr_host_plan* plan, float* host_buf, int32_t* host_flags, uint32_t* host_next,
                           double* seconds);
+/* The same round without staging copies: the single-pass kernel (omr_scan_sum_fused_f32) reads the pinned host
+ * buffer over PCIe and writes the aggregated blocks (non-zero blocks + lane heads) straight back into it, in place
+ * (client.cc:89); only the flag / next arrays travel as copies.  The link carries S one way and the written blocks
+ * the other, at once.  host_buf must be pinned (omr_host_register or hipHostMalloc), else OMR_EINVAL. */
+int omr_host_scan_sum_zero_copy_f32(omr_host_plan* plan, float* host_buf, int32_t* host_flags, uint32_t* host_next,
+                                    double* seconds);
 
 #ifdef __cplusplus
 }

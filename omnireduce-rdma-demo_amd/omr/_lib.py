@@ -66,6 +66,7 @@ SIGNATURES = {
     "omr_host_plan_create": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u64, c_vp]),
     "omr_host_plan_destroy": (c_int, [c_vp]),
     "omr_host_scan_sum_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "omr_host_scan_sum_zero_copy_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

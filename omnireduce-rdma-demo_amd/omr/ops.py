@@ -254,19 +254,22 @@ class HostPlan:
             raise _lib.OmrError(f"omr_host_plan_create rc={rc}: {_lib.load().omr_host_last_error().decode()}")
 
     def run(self, host_buf: torch.Tensor, flags: Optional[torch.Tensor] = None,
-            next_offsets: Optional[torch.Tensor] = None) -> float:
+            next_offsets: Optional[torch.Tensor] = None, zero_copy: bool = False) -> float:
+        """zero_copy: the single-pass kernel reads and writes the pinned buffer in place over PCIe instead of
+        staging it through HBM (omr_host_scan_sum_zero_copy_f32)."""
         L = self.layout
         for t, n, dt in ((host_buf, L.n, torch.float32), (flags, L.nb, torch.int32),
                          (next_offsets, L.nb, torch.int32)):
             if t is not None and (t.is_cuda or t.dtype != dt or t.numel() != n or not t.is_contiguous()):
                 raise ValueError("host tensors must be contiguous CPU tensors of the layout's size")
         secs = ctypes.c_double()
-        rc = _lib.load().omr_host_scan_sum_f32(self._p, host_buf.data_ptr(),
-                                               flags.data_ptr() if flags is not None else None,
-                                               next_offsets.data_ptr() if next_offsets is not None else None,
-                                               ctypes.byref(secs))
+        lib = _lib.load()
+        fn = lib.omr_host_scan_sum_zero_copy_f32 if zero_copy else lib.omr_host_scan_sum_f32
+        rc = fn(self._p, host_buf.data_ptr(), flags.data_ptr() if flags is not None else None,
+                next_offsets.data_ptr() if next_offsets is not None else None, ctypes.byref(secs))
         if rc != 0:
-            raise _lib.OmrError(f"omr_host_scan_sum_f32 rc={rc}: {_lib.load().omr_host_last_error().decode()}")
+            raise _lib.OmrError(f"omr_host_scan_sum{'_zero_copy' if zero_copy else ''}_f32 rc={rc}: "
+                                f"{lib.omr_host_last_error().decode()}")
         return secs.value
 
     def close(self):

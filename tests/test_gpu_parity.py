@@ -13,7 +13,7 @@ import pytest
 import torch
 
 import oracle
-from omr import Layout, ops
+from omr import Layout, _lib, ops
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -229,25 +229,38 @@ def test_full_size_properties(gpu, nbytes, B, r):
     assert int(torch.count_nonzero(ob[~sel])) == 0
 
 
-@pytest.mark.parametrize("chunk_rows", [7, 64, 4096])
-def test_host_resident_pipeline(gpu, chunk_rows):
-    """Pinned-host round: H2D chunks, in-place scan+aggregate, D2H (ragged last chunk with chunk_rows=7)."""
-    L = Layout(n=4 << 20, block_size=256)
+@pytest.mark.parametrize("chunk_rows,zero_copy,B", [(7, False, 256), (64, False, 256), (4096, False, 256),
+                                                    (512, True, 256), (512, True, 1024)])
+def test_host_resident_pipeline(gpu, chunk_rows, zero_copy, B):
+    """Pinned-host round: H2D chunks, in-place scan+aggregate, D2H (ragged last chunk with chunk_rows=7); or
+    zero-copy, the single-pass kernel reading and writing the pinned buffer over PCIe (B=1024: K=2 segments)."""
+    L = Layout(n=4 << 20, block_size=B)
     x = _rand_sparse(L, 0.3, 51)[0]
-    x[5 * 256:6 * 256] = -0.0
+    x[5 * B:6 * B] = -0.0
     host = torch.from_numpy(x.copy()).pin_memory()
     flags = torch.empty(L.nb, dtype=torch.int32).pin_memory()
     nxt = torch.empty(L.nb, dtype=torch.int32).pin_memory()
     plan = ops.HostPlan(L, chunk_rows=chunk_rows)
-    secs = plan.run(host, flags, nxt)
+    for _ in range(2 if zero_copy else 1):  # twice: the kernel's segment counters re-arm themselves
+        host.copy_(torch.from_numpy(x))
+        secs = plan.run(host, flags, nxt, zero_copy=zero_copy)
     plan.close()
-    f = oracle.flags_from_data(x, 256)
+    NB = L.num_lanes
+    f = oracle.flags_from_data(x, B)
     exp = x.copy()
-    oracle.block_sum([x], L.n, 256, 64, 8, f, exp)
+    oracle.block_sum([x], L.n, B, NB, 8, f, exp)
     assert secs > 0
     assert (flags.numpy() == f).all()
-    assert (nxt.numpy().view(np.uint32) == oracle.next_offsets(f, L.n, 256, 64, 8)).all()
+    assert (nxt.numpy().view(np.uint32) == oracle.next_offsets(f, L.n, B, NB, 8)).all()
     assert (host.numpy().view(np.uint32) == exp.view(np.uint32)).all()
+
+
+def test_host_zero_copy_rejects_pageable(gpu):
+    L = Layout(n=1 << 20, block_size=256)
+    plan = ops.HostPlan(L)
+    with pytest.raises(_lib.OmrError, match="not pinned"):
+        plan.run(torch.zeros(L.n), zero_copy=True)
+    plan.close()
 
 
 # ------------------------------------------------------------------ single-pass fused kernel (k_scan1f)

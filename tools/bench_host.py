@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Host-resident end-to-end rate (north_star: the gradient starts and ends in host memory): a pinned host tensor
 goes H2D in row chunks, is scanned + aggregated in place on the GPU, and comes back D2H (omr_host_plan, three
-overlapped HIP streams), next to the plain H2D / D2H copy rates and the device-resident kernel rate.
+overlapped HIP streams), next to the plain H2D / D2H copy rates, the device-resident kernel rate, and a zero-copy
+leg (the single-pass kernel reading and writing the pinned host tensor in place over PCIe).
 usage: python tools/bench_host.py [--size-mib 4096] [--density 0.49] [--chunk-rows 512] [--reps 5]"""
 import argparse
 import json
@@ -57,12 +58,27 @@ def main():
         dplan.run([xd], out)
     torch.cuda.synchronize()
     dev_t = (time.perf_counter() - t0) / a.reps
+    # zero-copy leg: the single-pass kernel reads the pinned host tensor over PCIe and writes the aggregated
+    # blocks straight back into it (out = the same host pointer, client.cc:89's in-place result): S crosses the
+    # link once each way only for the non-zero blocks, no staging copies; flags / next land in HBM and follow
+    # with one D2H copy each
+    fl_h = torch.empty(L.nb, dtype=torch.int32).pin_memory()
+    nx_h = torch.empty(L.nb, dtype=torch.int32).pin_memory()
+    zc = []
+    for r in range(a.reps + 1):
+        host.copy_(pristine)
+        t = plan.run(host, fl_h, nx_h, zero_copy=True)  # omr_host_scan_sum_zero_copy_f32
+        if r:
+            zc.append(t)
+    zc_ok = bool((fl_h.numpy() == bm).all()) and bool(torch.equal(host, pristine))  # 0.0f + x == x here
     S = L.nbytes
     res = {"tensor_bytes": S, "block_size": L.block_size, "density_r": a.density,
            "nonzero_fraction": float(bm.mean()), "chunk_rows": a.chunk_rows, "flags_ok": ok,
            "e2e_ms": 1e3 * float(np.median(e2e)), "e2e_GBps": S / float(np.median(e2e)) / 1e9,
            "h2d_GBps": S / float(np.median(h2d)) / 1e9, "d2h_GBps": S / float(np.median(d2h)) / 1e9,
-           "device_resident_ms": dev_t * 1e3, "device_resident_GBps": S / dev_t / 1e9}
+           "device_resident_ms": dev_t * 1e3, "device_resident_GBps": S / dev_t / 1e9,
+           "zero_copy_ms": 1e3 * float(np.median(zc)), "zero_copy_GBps": S / float(np.median(zc)) / 1e9,
+           "zero_copy_ok": zc_ok}
     print(json.dumps(res))
 
 
