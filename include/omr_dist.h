@@ -1,6 +1,6 @@
 /*
  * omr_dist.h — C ABI of the multi-rank sparse all-reduce (one OmniReduce round across ranks), host side in C++
- * (omnireduce-rdma-demo_amd/csrc/omr_dist.cpp, library libomr_dist.so, on top of libomr.so).
+ * (omnireduce-rdma-demo_amd/csrc/omr_dist.hip, library libomr_dist.so, on top of libomr.so).
  *
  * Replaces the reference's RDMA transport and per-thread protocol loops for the hot path: every rank is worker r
  * and aggregator of shard r (README.md:13-22; common.cc:381-383 shards slots over aggregators).  One call =

@@ -1,4 +1,4 @@
-// omr_dist.cpp — C++ host side of the multi-rank sparse all-reduce (include/omr_dist.h).
+// omr_dist.hip — C++ host side of the multi-rank sparse all-reduce (include/omr_dist.h).
 //
 // The round is the one omr/dist.py drives from Python (same shard bounds, same packed-stream layout, same
 // kernels from libomr.so); this is the C++ host path the ./omr_client and ./omr_server drivers run, with either
