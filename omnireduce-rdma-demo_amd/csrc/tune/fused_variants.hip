@@ -168,6 +168,163 @@ void go_s(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
 }  // namespace
 
 namespace {
+// Pure read with k_scan1f's geometry and workgroup -> column mapping (no ballots, stores or barrier): the floor
+// the fused kernel's read stream could reach (csrc/tune/stream_probe.hip "col contig xcd").  Timing only.
+template <int VEC, int W>
+__global__ __launch_bounds__(64 * W) void k_read_geom(FusedArgs a) {
+  constexpr int RB = 16 / VEC;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t k = lin % a.K, col = lin / a.K;
+  const uint32_t l = col % a.lanes, p = col / a.lanes;
+  const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + k * a.S;
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  const uint32_t rw = ((a.S + W * RB - 1) / (W * RB)) * RB;
+  const uint32_t lo = wave * rw < a.S ? wave * rw : a.S;
+  const uint32_t hi = lo + rw < a.S ? lo + rw : a.S;
+  uint32_t acc = 0;
+  for (uint32_t nb_ = (hi - lo + RB - 1) / RB; nb_ > 0; --nb_) {
+    const uint32_t rr = lo + (nb_ - 1) * RB;
+    const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
+    const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+    const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, nrow * row_bytes);
+    v4f v[RB][VEC];
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                              src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc |= nz_bits(v[s][q]);
+  }
+  if (acc == 0x12345678u) a.next[0] = acc;  // never true for nz_bits of the generator's data; keeps the loads
+}
+
+template <int VEC, int W, int LOADS, int ABL>
+void go_r(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(L.parts) * L.lanes * f.K);
+  k_read_geom<VEC, W><<<grid, 64 * W, 0, st>>>(a);
+}
+}  // namespace
+
+namespace {
+// k_scan1p — k_scan1f with the next batch's loads issued BEFORE the current batch's stores (study).  On gfx9
+// stores count in vmcnt, so in k_scan1f the wait for batch i+1's first load also waits for batch i's stores to be
+// acknowledged; here the prefetched loads are older than those stores and the wait covers the loads only.  Two
+// register sets (LOADS x 2 dwordx4 per lane).  Same outputs as k_scan1f (next offsets in stream, K = 1 only).
+template <int VEC, int WAVES, int LOADS, int ABL>
+__global__ __launch_bounds__(64 * WAVES) void k_scan1p(FusedArgs a) {
+  constexpr int RB = LOADS / VEC;
+  static_assert(RB >= 1 && RB <= 32, "batch bits are 32-bit");
+  __shared__ uint32_t s_wfirst[WAVES], s_wlast[WAVES];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t col = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;  // K = 1
+  const uint32_t l = col % a.lanes, p = col / a.lanes;
+  const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp;
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  const uint32_t lane_b = l * a.block;
+  const uint32_t row_stride = a.lanes * a.block;
+  const uint32_t rw = ((a.S + WAVES * RB - 1) / (WAVES * RB)) * RB;
+  const uint32_t lo = wave * rw < a.S ? wave * rw : a.S;
+  const uint32_t hi = lo + rw < a.S ? lo + rw : a.S;
+  uint32_t carry = kNone, wlast = kNone;
+  auto load = [&](uint32_t nb_, v4f (&v)[RB][VEC]) {
+    const uint32_t rr = lo + (nb_ - 1) * RB;
+    const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
+    const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+    const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, nrow * row_bytes);
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                              src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
+  };
+  auto ballots = [&](uint32_t nb_, const v4f (&v)[RB][VEC]) -> uint32_t {
+    const uint32_t rr = lo + (nb_ - 1) * RB;
+    const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
+      bits |= static_cast<uint32_t>(wave_ballot(o != 0) != 0 && static_cast<uint32_t>(s) < nrow) << s;
+    }
+    return bits;
+  };
+  auto store = [&](uint32_t nb_, const v4f (&v)[RB][VEC], uint32_t bits) {
+    const uint32_t rr = lo + (nb_ - 1) * RB;
+    const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
+    const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+    const __amdgpu_buffer_rsrc_t dst =
+        chunk_rsrc(a.out + blk0 * a.block, (a.out != nullptr && !(ABL & 1)) ? nrow * row_bytes : 0u);
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+      const uint32_t drop = (((bits >> s) & 1u) || (rr + s) == 0) ? 0u : kDropStore;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])), dst,
+                                               (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, kStoreAux);
+    }
+    if (!(ABL & 2) && static_cast<uint32_t>(lane) < nrow) {
+      const uint64_t blk = blk0 + static_cast<uint64_t>(lane) * a.lanes;
+      if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>((bits >> lane) & 1u);
+      const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
+      const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : carry;
+      if (nr != kNone) a.next[blk] = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+    }
+    if (bits != 0) {
+      if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
+      carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
+    }
+  };
+  v4f va[RB][VEC], vb[RB][VEC];
+  const uint32_t nbt = (hi - lo + RB - 1) / RB;
+  if (nbt > 0) load(nbt, va);
+  for (uint32_t nb_ = nbt; nb_ > 0;) {
+    uint32_t bits = ballots(nb_, va);
+    if (nb_ > 1) load(nb_ - 1, vb);  // issued before this batch's stores
+    store(nb_, va, bits);
+    if (--nb_ == 0) break;
+    bits = ballots(nb_, vb);
+    if (nb_ > 1) load(nb_ - 1, va);
+    store(nb_, vb, bits);
+    --nb_;
+  }
+  if (lane == 0) {
+    s_wfirst[wave] = carry;
+    s_wlast[wave] = wlast;
+  }
+  __syncthreads();
+  uint32_t succ = kNone;
+  for (uint32_t w2 = wave + 1; w2 < WAVES; ++w2)
+    if (s_wfirst[w2] != kNone) {
+      succ = s_wfirst[w2];
+      break;
+    }
+  if (!(ABL & 2)) {
+    const uint32_t val = succ != kNone ? static_cast<uint32_t>(row0 + succ) * row_stride + lane_b : a.sentinel + lane_b;
+    for (uint32_t i = (wlast == kNone ? lo : wlast) + lane; i < hi; i += 64) a.next[(row0 + i) * a.lanes + l] = val;
+  }
+}
+
+template <int VEC, int W, int LOADS, int ABL>
+void go_p(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  if (f.K != 1) return;  // study kernel: one segment per column only
+  const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(L.parts) * L.lanes);
+  k_scan1p<VEC, W, LOADS, ABL><<<grid, 64 * W, 0, st>>>(a);
+}
+}  // namespace
+
+namespace {
 template <int VEC, int W, int LOADS, int ABL, int MINW = 1>
 void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(L.parts) * L.lanes * f.K);
@@ -184,11 +341,16 @@ struct Variant {
 #define VF(W, LD, A) go_f<1, W, LD, A>, go_f<4, W, LD, A>
 #define VS(W, LD, A) go_s<1, W, LD, A>, go_s<4, W, LD, A>
 #define VO(W, LD, A, O) go_f<1, W, LD, A, O>, go_f<4, W, LD, A, O>
+#define VR(W) go_r<1, W, 16, 0>, go_r<4, W, 16, 0>
+#define VP(W, LD, A) go_p<1, W, LD, A>, go_p<4, W, LD, A>
 const Variant kVariants[] = {
+    {"pipe w16 L8", true, VP(16, 8, 0)},
+    {"pipe w8 L16", true, VP(8, 16, 0)},
+    {"pipe w16 L16", true, VP(16, 16, 0)},
+    {"pipe w8 L8", true, VP(8, 8, 0)},
+    {"pipe w16 L8 -data-meta", false, VP(16, 8, 3)},
     {"w16 L8", true, VF(16, 8, 0)},
-    {"w16 L8 occ8", true, VO(16, 8, 0, 8)},
-    {"split w16 L16", true, VS(16, 16, 0)},
-    {"split w16 L16 -data-meta", false, VS(16, 16, 3)},
+    {"pure read, k_scan1f geometry", false, VR(16)},
     {"w16 L16", true, VF(16, 16, 0)},
     {"w16 L16 -data", false, VF(16, 16, 1)},
     {"w16 L16 -meta", false, VF(16, 16, 2)},

@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--size-mib", type=int, default=256)
     ap.add_argument("--density", type=float, default=0.095)
     ap.add_argument("--rounds", type=int, default=12)
-    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=20, help="launches between one pair of events")
     ap.add_argument("--variants", default="", help="comma list of variant indices (default: all)")
     ap.add_argument("--ks", default="1,2,4")
     ap.add_argument("--block-size", type=int, default=256)
@@ -71,15 +71,18 @@ def main():
         if lib.tune_fused_checked(v):
             assert torch.equal(flags, ref.flags[0]) and torch.equal(nxt, ref.next_offsets[0]), name
     times = {n: [] for n, _ in cases}
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     k = 0
-    for r in range(a.rounds):
+    for r in range(a.rounds):  # per case: one event pair around a.reps back-to-back launches (bench.py's timing)
         for name, fn in cases:
-            for e0, e1 in ev:
-                e0.record(); fn(k % 4); e1.record(); k += 1
+            e0.record()
+            for _ in range(a.reps):
+                fn(k % 4)
+                k += 1
+            e1.record()
             torch.cuda.synchronize()
             if r:
-                times[name] += [x.elapsed_time(y) for x, y in ev]
+                times[name].append(e0.elapsed_time(e1) / a.reps)
     for name, _ in sorted(cases, key=lambda c: np.median(times[c[0]])):
         t = np.array(times[name]) * 1e-3
         print(f"{name:22s} median {np.median(t)*1e6:8.2f} us  min {t.min()*1e6:8.2f} us  "
