@@ -139,6 +139,7 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
     x = oracle.fill(bm, L.block_size)
     t, _, _, _ = oracle.cpu_baseline(x, bm, L.n, L.block_size, L.num_lanes, L.num_threads, args.cpu_threads, 1,
                                      args.cpu_warmups, args.cpu_rounds)
+    cores = oracle.cpu_baseline_cores()
     t_ref, _, _, _ = oracle.cpu_baseline(x, bm, L.n, L.block_size, L.num_lanes, L.num_threads, args.cpu_threads,
                                          0, args.cpu_warmups, args.cpu_rounds)
     t1, _, _, _ = oracle.cpu_baseline(x, bm, L.n, L.block_size, L.num_lanes, L.num_threads, 1, 1, 1, 5)
@@ -154,7 +155,9 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
     return {
         "value": round(L.nbytes / t / 1e9, 3),
         "unit": "GB/s",
+        "alg_bw_GiBps_reference_style": round(L.nbytes / t / 2 ** 30, 3),
         "cores": args.cpu_threads,
+        "pinned_cores": cores,
         "kind": "port",
         "sample": (f"config 2 tensor ({L.nbytes >> 20} MiB, B={L.block_size}, -r {args.density}), data-derived "
                    f"fp32 scan + next offsets + block aggregate, {args.cpu_warmups} warm-up + {args.cpu_rounds} "

@@ -22,6 +22,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -253,10 +254,28 @@ typedef struct {
   pthread_barrier_t* start;
   pthread_barrier_t* done;
   int rounds;
+  int cpu; /* core this thread pins itself to (-1: none) */
 } orc_worker;
+
+/* Cores the last orc_cpu_baseline run pinned its threads to (the reference pins its per-partition threads,
+ * client.cc:384-392; here thread t takes the t-th core this process may run on, so it stays inside a cgroup). */
+static int g_cores[256];
+static int g_ncores = 0;
+
+int orc_cpu_baseline_cores(int* out, int cap) {
+  int k = 0;
+  for (; k < g_ncores && k < cap; k++) out[k] = g_cores[k];
+  return k;
+}
 
 static void* orc_thread(void* arg) {
   orc_worker* w = (orc_worker*)arg;
+  if (w->cpu >= 0) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(w->cpu, &set);
+    (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+  }
   for (int r = 0; r < w->rounds; r++) {
     pthread_barrier_wait(w->start);
     orc_partition(&w->job);
@@ -285,8 +304,16 @@ double orc_cpu_baseline(const float* x, const int32_t* bitmap, uint64_t n, uint3
   orc_worker* ws = (orc_worker*)calloc(nthreads, sizeof(orc_worker));
   pthread_t* th = (pthread_t*)calloc(nthreads, sizeof(pthread_t));
   uint32_t per = parts / nthreads;
+  cpu_set_t allowed;
+  int avail[256], navail = 0;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0)
+    for (int c = 0; c < CPU_SETSIZE && navail < 256; c++)
+      if (CPU_ISSET(c, &allowed)) avail[navail++] = c;
+  g_ncores = 0;
   /* each worker thread handles `per` consecutive partitions: fold them into one job per partition loop */
   for (uint32_t t = 0; t < nthreads; t++) {
+    ws[t].cpu = (per == 1 && navail > 0) ? avail[t % navail] : -1;
+    if (ws[t].cpu >= 0 && g_ncores < 256) g_cores[g_ncores++] = ws[t].cpu;
     ws[t].job.x = x;
     ws[t].job.bitmap = bitmap;
     ws[t].job.flags = flags;

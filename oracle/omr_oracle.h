@@ -27,6 +27,8 @@ int orc_msg_simulate(const float* const* bufs, const int32_t* const* flags, uint
 double orc_cpu_baseline(const float* x, const int32_t* bitmap, uint64_t n, uint32_t B, uint32_t NB,
                         uint32_t parts, uint32_t nthreads, uint32_t variant, int warmups, int rounds,
                         int32_t* flags, uint32_t* next, float* out);
+/* Cores the last orc_cpu_baseline run pinned its threads to; returns how many were written to out. */
+int orc_cpu_baseline_cores(int* out, int cap);
 
 #ifdef __cplusplus
 }

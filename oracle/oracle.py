@@ -28,6 +28,7 @@ _SIG = {
     "orc_lane_stream": (_u32, [_vp, _u64, _u32, _u32, _u32, _u32, _u32, _vp, _vp, _u32]),
     "orc_msg_simulate": (_int, [_vp, _vp, _u32, _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "orc_cpu_baseline": (_dbl, [_vp, _vp, _u64, _u32, _u32, _u32, _u32, _u32, _int, _int, _vp, _vp, _vp]),
+    "orc_cpu_baseline_cores": (_int, [_vp, _int]),
 }
 _lib = None
 
@@ -129,6 +130,13 @@ def cpu_baseline(x: np.ndarray, bitmap: np.ndarray, n: int, B: int, NB: int, par
     if t < 0:
         raise ValueError("orc_cpu_baseline: nthreads must divide parts")
     return t, flags, nxt, out
+
+
+def cpu_baseline_cores():
+    """Core IDs the last cpu_baseline run pinned its threads to (empty for the single-thread path)."""
+    buf = (ctypes.c_int * 256)()
+    k = lib().orc_cpu_baseline_cores(buf, 256)
+    return [int(buf[i]) for i in range(k)]
 
 
 def msg_simulate(bufs, flags_list, n: int, B: int, NB: int, parts: int, rcap: int = 0, logs: bool = True):
