@@ -258,7 +258,8 @@ typedef struct {
 } orc_worker;
 
 /* Cores the last orc_cpu_baseline run pinned its threads to (the reference pins its per-partition threads,
- * client.cc:384-392; here thread t takes the t-th core this process may run on, so it stays inside a cgroup). */
+ * client.cc:384-392; here the threads are spread evenly over the cores this process may run on, so they stay
+ * inside its cgroup and use every CCD's memory link). */
 static int g_cores[256];
 static int g_ncores = 0;
 
@@ -312,7 +313,8 @@ double orc_cpu_baseline(const float* x, const int32_t* bitmap, uint64_t n, uint3
   g_ncores = 0;
   /* each worker thread handles `per` consecutive partitions: fold them into one job per partition loop */
   for (uint32_t t = 0; t < nthreads; t++) {
-    ws[t].cpu = (per == 1 && navail > 0) ? avail[t % navail] : -1;
+    /* spread over the allowed cores (every CCD's memory link in use), not packed onto the first ones */
+    ws[t].cpu = (per == 1 && navail > 0) ? avail[((uint64_t)t * navail / nthreads) % navail] : -1;
     if (ws[t].cpu >= 0 && g_ncores < 256) g_cores[g_ncores++] = ws[t].cpu;
     ws[t].job.x = x;
     ws[t].job.bitmap = bitmap;
