@@ -80,12 +80,6 @@ __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;  // "no row" marker
 
-constexpr int pow2floor(int x) {
-  int r = 1;
-  while (r * 2 <= x) r *= 2;
-  return r;
-}
-
 struct ScanArgs {
   WorkerPtrs x;
   uint32_t m;
@@ -357,21 +351,26 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
 
 // ---------------------------------------------------------------- k_scanm: m >= 2 workers on one device
 //
-// Same row sweep; per sub-batch the m workers' blocks are read in rank order and accumulated from +0.0f
-// (server.cc:148-150, :97-98).  Adding a zero-flagged worker's block (all +-0.0) to an accumulator that
-// started at +0.0 never changes it, so summing every worker equals the reference, which only adds the
-// workers that sent the block.  Lane w keeps worker w's row mask (no runtime-indexed register arrays).
-template <int VEC, bool NT>
+// One wave per row, rows swept grid-stride.  Per group of SUB blocks of the row, the m workers' blocks are read in
+// rank order (buffer loads, nt; UW workers' SUB*VEC dwordx4 per lane in flight at once) and accumulated from
+// +0.0f (server.cc:148-150, :97-98); each block's ballot gives the worker's flag bit.  Adding a zero-flagged
+// worker's block (all +-0.0) to an accumulator that started at +0.0 never changes it, so summing every worker
+// equals the reference, which only adds the workers that sent the block.  The aggregated blocks go out
+// write-through with a static store schedule (a block outside the write set is pointed past the row's
+// descriptor and dropped).  Lane w keeps worker w's row mask (no runtime-indexed register arrays).
+// tools/tune_scanm.py: SUB*VEC = 16 loads per worker, UW = 1 is fastest (8 x 256 MiB: 391.5 vs 410.8 us for the
+// previous plain-load form, csrc/tune/scanm_variants.hip).
+template <int VEC, int SUB, int UW>
 __global__ __launch_bounds__(kWGThreads) void k_scanm(ScanArgs a) {
-  constexpr int B4 = 64 * VEC;
-  constexpr int SUB = pow2floor(8 / VEC);
+  constexpr uint32_t B4 = 64 * VEC;  // 16-byte vectors per block
   const int lane = threadIdx.x & 63;
-  v4f* __restrict__ out = reinterpret_cast<v4f*>(a.out);
+  const uint32_t row_bytes = a.lanes * B4 * 16;
   const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
-  for (uint64_t row = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + (threadIdx.x >> 6); row < a.rows;
-       row += nwaves) {
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint64_t row = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + wave; row < a.rows; row += nwaves) {
     const bool head = (row % a.rows_per_part) == 0;
-    const uint64_t rowbase = row * a.lanes * B4;
+    const uint64_t rowbase = row * a.lanes * B4 * 4;  // float offset of the row
+    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + rowbase, a.out != nullptr ? row_bytes : 0u);
     uint64_t lane_wm = 0;  // lane w: worker w's mask
     uint64_t um = 0;       // union mask (wave-uniform)
     for (uint32_t l0 = 0; l0 < a.lanes; l0 += SUB) {
@@ -381,39 +380,47 @@ __global__ __launch_bounds__(kWGThreads) void k_scanm(ScanArgs a) {
 #pragma unroll
         for (int q = 0; q < VEC; ++q) acc[s][q] = v4f{0.f, 0.f, 0.f, 0.f};
       uint32_t sub_any = 0;
-
-      for (uint32_t w = 0; w < a.m; ++w) {
-        const v4f* src = reinterpret_cast<const v4f*>(a.x.p[w]) + rowbase +
-                            static_cast<uint64_t>(l0) * B4 + lane;
-        v4f v[SUB][VEC];
+      for (uint32_t w = 0; w < a.m; w += UW) {
+        v4f v[UW][SUB][VEC];
 #pragma unroll
-        for (int s = 0; s < SUB; ++s)
+        for (int j = 0; j < UW; ++j) {
+          // workers past m read through an empty descriptor: zeros, no memory traffic
+          const bool live = w + j < a.m;
+          const __amdgpu_buffer_rsrc_t src =
+              chunk_rsrc(a.x.p[live ? w + j : 0] + rowbase + static_cast<uint64_t>(l0) * B4 * 4, live ? SUB * B4 * 16 : 0u);
 #pragma unroll
-          for (int q = 0; q < VEC; ++q) v[s][q] = ld4<NT>(src + s * B4 + q * 64);
-        uint32_t wbits = 0;
+          for (int s = 0; s < SUB; ++s)
 #pragma unroll
-        for (int s = 0; s < SUB; ++s) {
-          uint32_t o = 0;
-#pragma unroll
-          for (int q = 0; q < VEC; ++q) {
-            o |= nz_bits(v[s][q]);
-            acc[s][q] = add4(acc[s][q], v[s][q]);
-          }
-          wbits |= static_cast<uint32_t>(wave_ballot(o != 0) != 0) << s;
+            for (int q = 0; q < VEC; ++q)
+              v[j][s][q] = __builtin_bit_cast(
+                  v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (s * B4 + q * 64 + lane) * 16, 0, kLoadAux));
         }
-        if (lane == static_cast<int>(w)) lane_wm |= static_cast<uint64_t>(wbits) << l0;
-        sub_any |= wbits;
+        __builtin_amdgcn_sched_barrier(0);  // every load of the group in flight before the first use
+#pragma unroll
+        for (int j = 0; j < UW; ++j) {
+          uint32_t wbits = 0;
+#pragma unroll
+          for (int s = 0; s < SUB; ++s) {
+            uint32_t o = 0;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+              o |= nz_bits(v[j][s][q]);
+              acc[s][q] = add4(acc[s][q], v[j][s][q]);  // rank order: worker w+j after w+j-1 (server.cc:97-98)
+            }
+            wbits |= static_cast<uint32_t>(wave_ballot(o != 0) != 0) << s;
+          }
+          if (lane == static_cast<int>(w + j)) lane_wm |= static_cast<uint64_t>(wbits) << l0;
+          sub_any |= wbits;
+        }
       }
       um |= static_cast<uint64_t>(sub_any) << l0;
-      if (out != nullptr) {
 #pragma unroll
-        for (int s = 0; s < SUB; ++s) {
-          if (((sub_any >> s) & 1u) || head) {
-            v4f* dst = out + rowbase + static_cast<uint64_t>(l0 + s) * B4 + lane;
+      for (int s = 0; s < SUB; ++s) {
+        const uint32_t drop = (((sub_any >> s) & 1u) || head) ? 0u : kDropStore;
 #pragma unroll
-            for (int q = 0; q < VEC; ++q) dst[q * 64] = acc[s][q];
-          }
-        }
+        for (int q = 0; q < VEC; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[s][q]), dst,
+                                                 (((l0 + s) * B4 + q * 64 + lane) * 16) | drop, 0, kStoreAux);
       }
     }
     if (lane < static_cast<int>(a.m)) a.masks[static_cast<uint64_t>(lane) * a.rows + row] = lane_wm;
@@ -1171,11 +1178,6 @@ int launch_next(const Layout& L, const uint64_t* masks, uint32_t count, uint32_t
   return launch_status("k_next");
 }
 
-#ifndef OMR_SCAN_NT
-#define OMR_SCAN_NT 1
-#endif
-constexpr bool kNT = OMR_SCAN_NT != 0;
-
 // Column split of the single-pass kernel: K segments per (partition, lane) column, at least one 16-wave
 // workgroup per CU (>= 256: tools/tune_fused.py measured K = 1 at 512 columns (B=256) and K = 2 at 128 columns
 // (B=1024) best, profiles/r01/tune_fused_*.log), segments of at least 64 rows, K <= 64 (the fix-up's LDS).
@@ -1248,9 +1250,9 @@ int launch_scan(const Layout& L, const ScanArgs& a, hipStream_t st) {
     return launch_status("k_scan1");
   }
   switch (L.vec) {
-    case 1: k_scanm<1, kNT><<<g, kWGThreads, 0, st>>>(a); break;
-    case 2: k_scanm<2, kNT><<<g, kWGThreads, 0, st>>>(a); break;
-    default: k_scanm<4, kNT><<<g, kWGThreads, 0, st>>>(a); break;
+    case 1: k_scanm<1, 16, 1><<<g, kWGThreads, 0, st>>>(a); break;
+    case 2: k_scanm<2, 8, 1><<<g, kWGThreads, 0, st>>>(a); break;
+    default: k_scanm<4, 4, 1><<<g, kWGThreads, 0, st>>>(a); break;
   }
   return launch_status("k_scanm");
 }
