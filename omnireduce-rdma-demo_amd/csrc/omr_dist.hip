@@ -374,6 +374,12 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   int32_t* fl = flags ? flags : p->flags_ws;
   uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
   uint32_t* un = union_next ? union_next : p->unext_ws;
+  // a synchronous round after asynchronous ones: its exchange goes on `stream`, so the communication stream
+  // must be idle first (one communicator is never driven from two streams at once)
+  if (!async && p->last_async >= 0) {
+    TRY(hip_check(hipStreamWaitEvent(st, p->set[p->last_async].done, 0), "hipStreamWaitEvent"));
+    p->last_async = -1;
+  }
   const int si = p->cur;
   omr_ar_plan::Set& S = p->set[si];
   p->cur ^= 1;

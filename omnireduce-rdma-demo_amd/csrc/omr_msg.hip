@@ -10,7 +10,7 @@
 //             completion order (:143-147), lane advance / reset (:173-186)
 // with the workers' messages of a protocol round arriving in rank order.
 //
-// The state machines are not stepped message by message.  Their schedule has a closed form (DESIGN.md §9):
+// The state machines are not stepped message by message.  Their schedule has a closed form (DESIGN.md §3.4):
 // in protocol round r a slot's lane l carries the r-th block of its UNION chain (its head at r = 0, then the
 // union's non-zero blocks: server.cc:86-96 makes min_next the union's next); worker w sends it iff r = 0 or w
 // flags it; the lane completes on the message of the highest-ranked sender, so the reply lists the active lanes

@@ -140,11 +140,12 @@ def test_cpp_reduce_scatter_loopback(gpu, world, rounds):
         assert (outs[r].view(np.uint32) == exp.view(np.uint32)).all(), f"rank {r}"
 
 
-@pytest.mark.parametrize("world,mode", [(3, 1), (8, 1), (4, 0)])
-def test_cpp_async_rounds_loopback(gpu, world, mode):
+@pytest.mark.parametrize("world,mode,sync_rounds", [(3, 1, ()), (8, 1, ()), (4, 0, ()), (3, 1, (2, 4))])
+def test_cpp_async_rounds_loopback(gpu, world, mode, sync_rounds):
     """OMR_ROUND_ASYNC: the exchange and sums of round k run on the plan's communication stream while round k+1
     scans; rounds take different inputs and outputs (the bench's rotation), use the two plan buffer sets in
-    turn (five rounds: each set refilled twice), and are joined once at the end."""
+    turn (five rounds: each set refilled twice), and are joined once at the end.  sync_rounds: rounds issued
+    without the flag in between (they must wait for the asynchronous ones before using the stream)."""
     B, rounds = 256, 5
     L = Layout(n=2 << 20, block_size=B)
     D = dist_lib()
@@ -163,8 +164,9 @@ def test_cpp_async_rounds_loopback(gpu, world, mode):
             assert D.omr_ar_plan_create(d, L.n, B, L.num_lanes, 8, ctypes.byref(plan)) == 0
             st = torch.cuda.Stream()
             for k in range(rounds):
+                flag = 0 if k in sync_rounds else 0x100
                 assert D.omr_sparse_round_f32(plan, xs[k].data_ptr(), os_[k].data_ptr(), None, None, None,
-                                              mode | 0x100, None, None, st.cuda_stream) == 0, D.omr_dist_last_error()
+                                              mode | flag, None, None, st.cuda_stream) == 0, D.omr_dist_last_error()
             assert D.omr_ar_plan_join(plan, st.cuda_stream) == 0
             st.synchronize()
             for k in range(rounds):
