@@ -88,3 +88,17 @@ def test_layout_class():
     assert L.global_slot(2, 5) == 37
     with pytest.raises(ValueError):
         Layout(n=(1 << 20) + 256)
+
+
+def test_dist_library_exports_every_declared_symbol():
+    """libomr_dist.so (the multi-rank round, include/omr_dist.h) loads without a GPU and exports what its header
+    declares; the ctypes binding (omr/cdist.py) binds every one of them."""
+    import inspect
+    from omr import cdist
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "omr_dist.h")).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(omr_[a-z0-9_]+)\s*\(", src)))
+    lib = cdist.load()
+    for name in declared:
+        assert hasattr(lib, name), name
+    bound = set(re.findall(r'"(omr_[a-z0-9_]+)"', inspect.getsource(cdist.load)))
+    assert sorted(set(declared) - bound) == [], "omr_dist.h entry points without a ctypes binding"
