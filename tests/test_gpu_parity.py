@@ -315,10 +315,17 @@ def test_fused_edge_values(gpu):
     assert_fused_parity(x, L, out_init=np.full(L.n, -0.0, dtype=np.float32))
 
 
+MAX_N = 32767 * 8 * 16384  # the largest layout below the uint32 lane sentinel 4294934528 (client.cc:24): 16 GiB
+
+
 @pytest.mark.slow
-@pytest.mark.parametrize("nbytes,B,r", [(256 << 20, 256, 0.095), (1 << 30, 1024, 0.0099)])
+@pytest.mark.parametrize("nbytes,B,r", [(256 << 20, 256, 0.095), (1 << 30, 1024, 0.0099), (4 << 30, 256, 0.49),
+                                        (MAX_N * 4, 256, 0.01), (MAX_N * 4, 1024, 0.01)])
 def test_fused_full_size(gpu, nbytes, B, r):
-    L = Layout.from_bytes(nbytes, B)
+    """Configs 2, 3 and 5 at full size, and the largest tensor whose offsets fit the reference's uint32 chains
+    (odd rows per partition: ragged per-wave ranges; at B=1024 one segment per column): flags == the generator's
+    bitmap, next == the oracle chain from it (offsets up to ~2^32), in-place result == input."""
+    L = Layout(n=nbytes // 4, block_size=B)
     bm = ops.gen_bitmap(0, r, L.nb)
     x = ops.fill_blocks(torch.from_numpy(bm).to(gpu), L, mode=1, seed=1)
     ref = x.clone()
