@@ -22,6 +22,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <stdio.h>
 #include <sched.h>
 #include <stdlib.h>
 #include <string.h>
@@ -258,8 +259,8 @@ typedef struct {
 } orc_worker;
 
 /* Cores the last orc_cpu_baseline run pinned its threads to (the reference pins its per-partition threads,
- * client.cc:384-392; here the threads are spread evenly over the cores this process may run on, so they stay
- * inside its cgroup and use every CCD's memory link). */
+ * client.cc:384-392; here the threads are spread evenly over distinct physical cores of the package the caller
+ * runs on (orc_pick_cores), so they stay inside its cgroup, near its memory, and use every CCD's memory link). */
 static int g_cores[256];
 static int g_ncores = 0;
 
@@ -267,6 +268,44 @@ int orc_cpu_baseline_cores(int* out, int cap) {
   int k = 0;
   for (; k < g_ncores && k < cap; k++) out[k] = g_cores[k];
   return k;
+}
+
+/* sysfs topology value of a CPU (-1 if unreadable). */
+static int cpu_topo(int cpu, const char* what) {
+  char path[128];
+  snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/topology/%s", cpu, what);
+  FILE* f = fopen(path, "r");
+  if (f == NULL) return -1;
+  int v = -1;
+  if (fscanf(f, "%d", &v) != 1) v = -1;
+  fclose(f);
+  return v;
+}
+
+/* The cores the baseline's threads may use, in the order they are handed out: CPUs this process may run on, in
+ * the package of the CPU it runs on now (where its pages were first touched), one logical CPU per physical core
+ * (no SMT sibling pairs).  Falls back to every allowed CPU when the topology is unreadable. */
+static int orc_pick_cores(int* out, int cap) {
+  cpu_set_t allowed;
+  int n = 0;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return 0;
+  const int here = sched_getcpu();
+  const int pkg = here >= 0 ? cpu_topo(here, "physical_package_id") : -1;
+  int seen_core[1024], nseen = 0;
+  for (int c = 0; c < CPU_SETSIZE && n < cap; c++) {
+    if (!CPU_ISSET(c, &allowed)) continue;
+    const int cp = cpu_topo(c, "physical_package_id"), core = cpu_topo(c, "core_id");
+    if (pkg >= 0 && cp != pkg) continue;
+    int dup = 0;
+    for (int i = 0; i < nseen && core >= 0; i++) dup |= (seen_core[i] == core);
+    if (dup) continue;
+    if (core >= 0 && nseen < 1024) seen_core[nseen++] = core;
+    out[n++] = c;
+  }
+  if (n == 0)
+    for (int c = 0; c < CPU_SETSIZE && n < cap; c++)
+      if (CPU_ISSET(c, &allowed)) out[n++] = c;
+  return n;
 }
 
 static void* orc_thread(void* arg) {
@@ -305,11 +344,8 @@ double orc_cpu_baseline(const float* x, const int32_t* bitmap, uint64_t n, uint3
   orc_worker* ws = (orc_worker*)calloc(nthreads, sizeof(orc_worker));
   pthread_t* th = (pthread_t*)calloc(nthreads, sizeof(pthread_t));
   uint32_t per = parts / nthreads;
-  cpu_set_t allowed;
-  int avail[256], navail = 0;
-  if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0)
-    for (int c = 0; c < CPU_SETSIZE && navail < 256; c++)
-      if (CPU_ISSET(c, &allowed)) avail[navail++] = c;
+  int avail[256];
+  const int navail = orc_pick_cores(avail, 256);
   g_ncores = 0;
   /* each worker thread handles `per` consecutive partitions: fold them into one job per partition loop */
   for (uint32_t t = 0; t < nthreads; t++) {
