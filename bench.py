@@ -307,8 +307,8 @@ def main():
                     "timing": ("fence-free HIP events (hipEventDisableSystemFence) on the kernel's stream around "
                                "the timed launches" + (" (all K, divided by K)" if one_kernel else
                                                        f" (every {every}th step)")),
-                    "traffic_source": "rocprofv3 PMC 2*FETCH_SIZE+WRITE_SIZE per launch, profiles/pmc_r01.json"
-                    if traffic else None}
+                    "traffic_source": ("rocprofv3 PMC 2*FETCH_SIZE+WRITE_SIZE per launch, "
+                                       + os.path.relpath(args.pmc, ROOT)) if traffic else None}
         if not dist_mode:
             sbytes = step_algorithmic_bytes(L, bitmaps, m)
             roofline["step_algorithmic_bytes"] = sbytes
