@@ -7,6 +7,7 @@ multi-rank RCCL leg runs on multi-GPU nodes only.)"""
 import ctypes
 import os
 import subprocess
+import sys
 import threading
 
 import numpy as np
@@ -263,3 +264,24 @@ def test_client_message_mode_trace(gpu, tmp_path):
     assert len(got) == len(exp)
     for i, (g, e) in enumerate(zip(got, exp)):
         assert g == e, f"record {i}: {g[:4]} vs {e[:4]}"
+
+
+@pytest.mark.parametrize("extra", [[], ["--dist-sync"], ["--dist-mode", "allreduce"]])
+def test_bench_distributed_path_world1(gpu, extra):
+    """bench.py's N>1 path as the driver launches it (torch.distributed.run, RCCL, the C++ round with two
+    communicators, pipelined rounds joined before the closing sync), rehearsed at world 1."""
+    import json
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(PKG)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--force-dist", "--no-cpu",
+           "--steps", "5", "--warmup", "2", "--size-mib", "64"] + extra
+    rc, out = _run(cmd, timeout=240)
+    assert rc == 0, out[-3000:]
+    line = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0 and line["roofline"]["frac"] > 0
+    assert "RCCL" in line["config"]["parallelism"]
