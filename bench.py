@@ -60,9 +60,10 @@ def parse():
                    help="N=1, m=1: single-pass k_scan1f (default) or k_scan1 + k_next")
     p.add_argument("--force-dist", action="store_true",
                    help="take the N>1 (distributed) code path even at WORLD_SIZE=1 (rehearsal under torchrun)")
-    p.add_argument("--dist-mode", choices=("reduce", "allreduce"), default="reduce",
-                   help="N>1 step: workers -> aggregators reduce-scatter (BASELINE config 4, default) or the full "
-                        "all-reduce (sums back to every worker)")
+    p.add_argument("--dist-mode", choices=("reduce", "allreduce", "dense"), default="reduce",
+                   help="N>1 step: workers -> aggregators reduce-scatter (BASELINE config 4, default), the full "
+                        "all-reduce (sums back to every worker), or the dense stand-in (ncclReduceScatter of the "
+                        "whole tensor, C++ driver only)")
     p.add_argument("--dist-sync", action="store_true",
                    help="N>1, C++ driver: keep each round's exchange on the caller's stream (default: OMR_ROUND_ASYNC, "
                         "round k's exchange over xGMI overlaps round k+1's worker scan)")
@@ -197,6 +198,8 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
+    if dist_mode and args.dist_mode == "dense" and args.dist_impl != "cpp":
+        raise SystemExit("--dist-mode dense runs on the C++ round driver only (--dist-impl cpp)")
     if dist_mode:
         if args.dist_impl == "cpp":
             from omr import cdist
@@ -212,7 +215,8 @@ def main():
         def step(i, ev=None):
             xs, out = sets[i % len(sets)]
             if args.dist_impl == "cpp":
-                engine.run(xs[0], out=out, mode=0 if args.dist_mode == "allreduce" else 1, async_=pipelined)
+                engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
+                           async_=pipelined)
             else:
                 engine.run(xs[0], out=out, ev=ev, mode=0 if args.dist_mode == "allreduce" else 1)
     else:
@@ -338,7 +342,7 @@ def main():
                    "nonzero_fraction": round(float(np.mean([bm.mean() for bm in bitmaps])), 5),
                    "workers_per_gpu": m, "rotating_buffer_sets": len(sets),
                    "parallelism": "single GPU" if not dist_mode else
-                   f"dp{n_gpus} sparse {'all-reduce' if args.dist_mode == 'allreduce' else 'reduce-scatter'} over "
+                   f"dp{n_gpus} {dict(allreduce='sparse all-reduce', reduce='sparse reduce-scatter', dense='dense reduce-scatter (stand-in)')[args.dist_mode]} over "
                    f"RCCL ({args.dist_impl} round driver"
                    f"{', rounds pipelined: exchange k beside scan k+1' if dist_mode and args.dist_impl == 'cpp' and not args.dist_sync else ''})"},
         "alg_bw_GiBps_reference_style": round(total_bytes / (ms_per_step * 1e-3) / 2 ** 30, 2),

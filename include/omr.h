@@ -145,6 +145,11 @@ int omr_next_offsets(const uint64_t* row_masks, uint32_t count, uint64_t n, uint
 int omr_block_sum_f32(const float* const* inputs, uint32_t m, const uint32_t* block_list, uint32_t num_list,
                       uint32_t block_size, float* out, omr_stream_t stream);
 
+/* The dense stand-in aggregator: out[i] = ((0.0f + in_0[i]) + in_1[i]) + ... for every i < n (all blocks, zero
+ * or not; rank order as server.cc:97-98).  `inputs` is a HOST array of m device pointers; n a multiple of 4,
+ * pointers 16-byte aligned; out may alias an input. */
+int omr_dense_sum_f32(const float* const* inputs, uint32_t m, uint64_t n, float* out, omr_stream_t stream);
+
 /* ---------------------------------------------------------------- compaction and block movement */
 
 /* Bytes of device workspace omr_compact needs for `rows` rows. */

@@ -73,6 +73,13 @@ int omr_sparse_allreduce_f32(omr_ar_plan* plan, const float* x, float* out, int3
  *                             *union_blocks = this shard's write-set size. */
 #define OMR_ROUND_ALLREDUCE 0
 #define OMR_ROUND_REDUCE_SCATTER 1
+/*   OMR_ROUND_DENSE_REDUCE_SCATTER  the dense stand-in: the worker scan and the aggregator chain as
+ *                             usual, then the WHOLE tensor reduce-scattered (RCCL ncclReduceScatter, ncclSum;
+ *                             loopback: omr_dense_sum_f32 in rank order): `out` receives this rank's shard of the
+ *                             elementwise sum, every block, zero or not; other rows untouched.  RCCL's summation order
+ *                             is its own (results within fp32 reassociation error of the rank-order sum).  Shards
+ *                             must be equal: rows % world == 0.  Moves 7/8*S per rank at N=8 whatever the density. */
+#define OMR_ROUND_DENSE_REDUCE_SCATTER 2
 /* OR-ed into `mode`: the round's exchange and aggregation (send/recv, shard sums [, sums back, unpack]) go on the
  * plan's own communication stream instead of `stream`, so the next call's worker scan overlaps this round's
  * transfer over xGMI (the bucket pipeline of a training step).  flags / next_offsets / union_next are ready in

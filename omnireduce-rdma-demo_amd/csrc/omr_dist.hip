@@ -63,6 +63,8 @@ struct omr_dist {
   virtual int allgather(const void* in, void* out, size_t bytes, hipStream_t st) = 0;
   // sends[p] to peer p, recvs[p] from peer p (sizes agree pairwise; zero = nothing), p != rank
   virtual int exchange(const std::vector<Slice>& sends, const std::vector<Slice>& recvs, hipStream_t st) = 0;
+  // out[0 .. count) = sum over ranks p of in_p[rank*count .. (rank+1)*count)  (dense stand-in)
+  virtual int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) = 0;
 };
 
 namespace {
@@ -88,6 +90,9 @@ struct RcclDist final : omr_dist {
       if (sends[p].bytes) TRY(nccl_check(ncclSend(sends[p].ptr, sends[p].bytes, ncclUint8, p, xcomm, st), "ncclSend"));
     }
     return nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
+    return nccl_check(ncclReduceScatter(in, out, count, ncclFloat32, ncclSum, xcomm, st), "ncclReduceScatter");
   }
 };
 
@@ -144,6 +149,19 @@ struct LocalDist final : omr_dist {
                     recvs[p].bytes, p, s.bytes);
       TRY(hip_check(hipMemcpy(recvs[p].ptr, s.ptr, s.bytes, hipMemcpyDefault), "hipMemcpy"));
     }
+    b->barrier();
+    return 0;
+  }
+  int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
+    // every rank's input is addressable here (threads of one process): sum the shard in rank order
+    TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
+    b->posted[rank] = in;
+    b->barrier();
+    std::vector<const float*> ptrs(world);
+    for (int p = 0; p < world; ++p) ptrs[p] = static_cast<const float*>(b->posted[p]) + static_cast<size_t>(rank) * count;
+    TRY(omr_check(omr_dense_sum_f32(ptrs.data(), static_cast<uint32_t>(world), count, out,
+                                    reinterpret_cast<omr_stream_t>(st)), "omr_dense_sum_f32"));
+    TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));  // peers' inputs read before anyone moves on
     b->barrier();
     return 0;
   }
@@ -365,8 +383,11 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   if (p == nullptr || x == nullptr || out == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL");
   const bool async = (mode & OMR_ROUND_ASYNC) != 0;
   mode &= ~OMR_ROUND_ASYNC;
-  if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER)
+  if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
     return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
+  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && p->rows % p->N != 0)
+    return derr(OMR_EINVAL, "sparse_round: dense reduce-scatter needs equal shards (rows %llu, world %d)",
+                static_cast<unsigned long long>(p->rows), p->N);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int N = p->N, me = p->me;
   const uint64_t rows = p->rows, B = p->B;
@@ -404,7 +425,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   //     they are queued before the host learns the counts and run while it waits.  (Every host API call costs
   //     microseconds; a round that spends them on side streams and events is host-bound.)
   const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
-  if (N > 1)
+  if (N > 1 && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
     TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * rows,
                                       S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
                                       r1, stream), "omr_move_blocks_f32 pack"));
@@ -417,6 +438,20 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
     xs = p->cs;
   }
   const omr_stream_t xstream = reinterpret_cast<omr_stream_t>(xs);
+  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER) {
+    // the dense stand-in: every element of this rank's shard, reduced over all ranks by the transport
+    const uint64_t row_floats = static_cast<uint64_t>(p->lanes) * B;
+    TRY(p->d->reduce_scatter(x, out + r0 * row_floats, (r1 - r0) * row_floats, xs));
+    if (async) {
+      TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
+      S.pending = true;
+      p->last_async = si;
+    }
+    if (sent_blocks != nullptr || union_blocks != nullptr) TRY(wait_flag(p->flag_host, seq, st));
+    if (sent_blocks) *sent_blocks = (r1 - r0) * p->lanes * static_cast<uint64_t>(N - 1);
+    if (union_blocks) *union_blocks = p->counts_host[N * NB + me + 1] - p->counts_host[N * NB + me];
+    return 0;
+  }
   TRY(wait_flag(p->flag_host, seq, st));
   auto cnt = [&](int a, int s) -> uint64_t { return p->counts_host[a * NB + s]; };
   auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };

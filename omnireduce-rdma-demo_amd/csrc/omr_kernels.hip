@@ -733,6 +733,30 @@ __global__ __launch_bounds__(kWGThreads) void k_scatter(const float* packed, con
   }
 }
 
+// Dense rank-order sum of m arrays (the dense stand-in aggregator, omr_dense_sum_f32): four dwordx4 per lane
+// per worker in flight, grid-stride.
+__global__ __launch_bounds__(kWGThreads) void k_dense_sum(WorkerPtrs in, uint32_t m, uint64_t n4, float* out) {
+  constexpr int U = 4;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWGThreads;
+  for (uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kWGThreads + threadIdx.x; i0 < n4; i0 += stride * U) {
+    v4f acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (uint32_t w = 0; w < m; ++w) {
+      const v4f* src = reinterpret_cast<const v4f*>(in.p[w]);
+      v4f v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = i0 + u * stride < n4 ? src[i0 + u * stride] : v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] = add4(acc[u], v[u]);
+    }
+    v4f* dst = reinterpret_cast<v4f*>(out);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * stride < n4) dst[i0 + u * stride] = acc[u];
+  }
+}
+
 template <int VEC>
 __global__ __launch_bounds__(kWGThreads) void k_list_sum(WorkerPtrs in, uint32_t m, const uint32_t* list,
                                                          uint32_t num, float* out) {
@@ -1441,6 +1465,26 @@ int omr_next_offsets(const uint64_t* row_masks, uint32_t count, uint64_t n, uint
   if (count == 0) return 0;
   if (row_masks == nullptr || next_offsets == nullptr) return fail("next_offsets: NULL pointer");
   return launch_next(L, row_masks, count, next_offsets, S(stream));
+}
+
+int omr_dense_sum_f32(const float* const* inputs, uint32_t m, uint64_t n, float* out, omr_stream_t stream) {
+  if (m == 0 || m > OMR_MAX_WORKERS) return fail("dense_sum: m=%u out of range (1..%d)", m, OMR_MAX_WORKERS);
+  if (n % 4 != 0) return fail("dense_sum: n=%llu is not a multiple of 4", static_cast<unsigned long long>(n));
+  if (n == 0) return 0;
+  if (inputs == nullptr || out == nullptr) return fail("dense_sum: NULL pointer");
+  if (reinterpret_cast<uintptr_t>(out) % 16 != 0) return fail("dense_sum: out not 16-byte aligned");
+  WorkerPtrs in;
+  memset(&in, 0, sizeof(in));
+  for (uint32_t w = 0; w < m; ++w) {
+    if (inputs[w] == nullptr || reinterpret_cast<uintptr_t>(inputs[w]) % 16 != 0)
+      return fail("dense_sum: inputs[%u] NULL or not 16-byte aligned", w);
+    in.p[w] = inputs[w];
+  }
+  const uint64_t n4 = n / 4;
+  uint64_t g = (n4 + kWGThreads * 4 - 1) / (kWGThreads * 4);
+  if (g > kMaxGrid) g = kMaxGrid;
+  k_dense_sum<<<static_cast<unsigned>(g), kWGThreads, 0, S(stream)>>>(in, m, n4, out);
+  return launch_status("k_dense_sum");
 }
 
 int omr_block_sum_f32(const float* const* inputs, uint32_t m, const uint32_t* block_list, uint32_t num_list,

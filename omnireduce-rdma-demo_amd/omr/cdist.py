@@ -83,12 +83,13 @@ class CppSparseAllreduce:
                "omr_ar_plan_create")
         self.rank, self.world = rank, world
 
-    ALLREDUCE, REDUCE_SCATTER, ASYNC = 0, 1, 0x100
+    ALLREDUCE, REDUCE_SCATTER, DENSE_REDUCE_SCATTER, ASYNC = 0, 1, 2, 0x100
 
     def run(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, ev=None, flags=None, next_offsets=None,
             union_next=None, mode: int = 0, async_: bool = False):
         """mode 0: all-reduce (every worker gets every shard's sums); 1: reduce-scatter (stop at the
-        aggregators: `out` gets this rank's shard sums only).  async_: the exchange and the sums run on the plan's
+        aggregators: `out` gets this rank's shard sums only); 2: the dense stand-in (the whole tensor reduce-scattered
+        by RCCL, every block).  async_: the exchange and the sums run on the plan's
         communication stream, overlapping the next call's worker scan; `out` is ready after join()."""
         if async_:
             mode |= self.ASYNC

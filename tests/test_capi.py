@@ -61,6 +61,9 @@ def test_entry_points_validate_before_launching():
     assert lib.omr_block_sum_f32(None, 1, None, 0, 256, None, None) == 0  # empty list is a no-op
     assert lib.omr_compact(None, 5, 3, 64, None, None, None, 0, None) == _lib.OMR_EINVAL
     assert lib.omr_fill_blocks_f32(None, 4, 256, 7, 0, None, None) == _lib.OMR_EINVAL
+    assert lib.omr_dense_sum_f32(None, 0, 16, None, None) == _lib.OMR_EINVAL  # m out of range
+    assert lib.omr_dense_sum_f32(None, 2, 6, None, None) == _lib.OMR_EINVAL  # n not a multiple of 4
+    assert lib.omr_dense_sum_f32(None, 2, 0, None, None) == 0  # empty is a no-op
 
 
 @pytest.mark.parametrize("wid", [0, 1, 2, 7])

@@ -199,6 +199,75 @@ def test_cpp_async_rounds_loopback(gpu, world, mode, sync_rounds):
             assert (outs[r][k].view(np.uint32) == exp.view(np.uint32)).all(), f"round {k} rank {r}"
 
 
+@pytest.mark.parametrize("world,flags", [(4, 0), (8, 0x100)])
+def test_cpp_dense_reduce_scatter_loopback(gpu, world, flags):
+    """OMR_ROUND_DENSE_REDUCE_SCATTER (the dense stand-in): this rank's shard of the elementwise rank-order sum of
+    every worker's whole tensor; other rows untouched; the worker outputs as in the sparse modes."""
+    B = 256
+    L = Layout(n=2 << 20, block_size=B)
+    D = dist_lib()
+    bufs = [oracle.fill(oracle.gen_bitmap(w, 0.3, L.nb), B, mode=1, seed=w + 5) for w in range(world)]
+    dense = np.zeros(L.n, dtype=np.float32)
+    for b in bufs:
+        dense = dense + b
+    uf = oracle.union_flags([oracle.flags_from_data(b, B) for b in bufs])
+    board = D.omr_local_board_create(world)
+    errs, outs = [], [None] * world
+
+    def rank(r):
+        try:
+            torch.cuda.set_device(0)
+            x = torch.from_numpy(bufs[r].copy()).cuda()
+            out = x.clone()
+            unext = torch.empty(L.nb, dtype=torch.int32, device="cuda")
+            d, plan = ctypes.c_void_p(), ctypes.c_void_p()
+            assert D.omr_dist_create_local(board, r, ctypes.byref(d)) == 0
+            assert D.omr_ar_plan_create(d, L.n, B, L.num_lanes, 8, ctypes.byref(plan)) == 0
+            st = torch.cuda.Stream()
+            for _ in range(2):
+                assert D.omr_sparse_round_f32(plan, x.data_ptr(), out.data_ptr(), None, None, unext.data_ptr(),
+                                              2 | flags, None, None, st.cuda_stream) == 0, D.omr_dist_last_error()
+            assert D.omr_ar_plan_join(plan, st.cuda_stream) == 0
+            st.synchronize()
+            outs[r] = (out.cpu().numpy(), unext.cpu().numpy().view(np.uint32))
+            D.omr_ar_plan_destroy(plan)
+            D.omr_dist_destroy(d)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    D.omr_local_board_destroy(board)
+    assert not errs, errs
+    un = oracle.next_offsets(uf, L.n, B, L.num_lanes, 8)
+    bounds = [s * L.rows // world for s in range(world + 1)]
+    for r in range(world):
+        exp = bufs[r].copy()
+        lo, hi = bounds[r] * L.num_lanes * B, bounds[r + 1] * L.num_lanes * B
+        exp[lo:hi] = dense[lo:hi]
+        out, unx = outs[r]
+        assert (out.view(np.uint32) == exp.view(np.uint32)).all(), f"rank {r}"
+        assert (unx == un).all()
+
+
+def test_cpp_dense_reduce_scatter_needs_equal_shards(gpu):
+    D = dist_lib()
+    board = D.omr_local_board_create(3)
+    d, plan = ctypes.c_void_p(), ctypes.c_void_p()
+    assert D.omr_dist_create_local(board, 0, ctypes.byref(d)) == 0
+    L = Layout(n=2 << 20, block_size=256)  # 128 rows: not a multiple of 3
+    assert D.omr_ar_plan_create(d, L.n, 256, L.num_lanes, 8, ctypes.byref(plan)) == 0
+    x = torch.zeros(L.n, device="cuda")
+    rc = D.omr_sparse_round_f32(plan, x.data_ptr(), x.data_ptr(), None, None, None, 2, None, None, None)
+    assert rc != 0 and b"equal shards" in D.omr_dist_last_error()
+    D.omr_ar_plan_destroy(plan)
+    D.omr_dist_destroy(d)
+    D.omr_local_board_destroy(board)
+
+
 def _run(cmd, timeout=300):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
     return p.returncode, p.stdout + p.stderr
@@ -266,7 +335,7 @@ def test_client_message_mode_trace(gpu, tmp_path):
         assert g == e, f"record {i}: {g[:4]} vs {e[:4]}"
 
 
-@pytest.mark.parametrize("extra", [[], ["--dist-sync"], ["--dist-mode", "allreduce"]])
+@pytest.mark.parametrize("extra", [[], ["--dist-sync"], ["--dist-mode", "allreduce"], ["--dist-mode", "dense"]])
 def test_bench_distributed_path_world1(gpu, extra):
     """bench.py's N>1 path as the driver launches it (torch.distributed.run, RCCL, the C++ round with two
     communicators, pipelined rounds joined before the closing sync), rehearsed at world 1."""

@@ -4,6 +4,7 @@ Bar: flags, row masks, next offsets and block lists bit-exact; summed floats bit
 rank-order sum (server.cc:97-98 from a zeroed accumulator, server.cc:148-150) — tolerance 0 ulp here, because
 the GPU adds the workers in the same rank order.  Full-size configs are checked through size-independent
 properties (flags == the generator bitmap, next == the closed-form chain, out == the dense sum)."""
+import ctypes
 import hashlib
 import json
 import os
@@ -261,6 +262,23 @@ def test_host_zero_copy_rejects_pageable(gpu):
     with pytest.raises(_lib.OmrError, match="not pinned"):
         plan.run(torch.zeros(L.n), zero_copy=True)
     plan.close()
+
+
+@pytest.mark.parametrize("m,n", [(1, 4), (2, 1 << 20), (3, 12345 * 4), (8, (1 << 22) + 36), (16, 4096)])
+def test_dense_sum(gpu, m, n):
+    """omr_dense_sum_f32 (the dense stand-in aggregator): every element summed from +0.0f in rank order."""
+    rng = np.random.default_rng(m * 7 + n)
+    xs = [rng.standard_normal(n).astype(np.float32) for _ in range(m)]
+    xs[0][:3] = -0.0
+    exp = np.zeros(n, dtype=np.float32)
+    for x in xs:
+        exp = exp + x  # float32, sequential: ((0 + x0) + x1) + ...
+    xd = [torch.from_numpy(x).to(gpu) for x in xs]
+    out = torch.empty(n, dtype=torch.float32, device=gpu)
+    ptrs = (ctypes.c_void_p * m)(*[t.data_ptr() for t in xd])
+    assert _lib.load().omr_dense_sum_f32(ptrs, m, n, out.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy().view(np.uint32) == exp.view(np.uint32)).all()
 
 
 # ------------------------------------------------------------------ single-pass fused kernel (k_scan1f)
