@@ -35,6 +35,7 @@ import torch  # noqa: E402
 from omr import Layout, ops  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+XGMI_LINK_GBPS = 153.0  # one of a GPU's 7 point-to-point xGMI links (the task's hardware notes; not in the guide)
 
 
 def parse():
@@ -272,6 +273,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     roofline = None
+    exchange = None
     kernel_name = ("k_scan1f (single pass: scan + sum + next)" if (m == 1 and args.kernel == "fused") else
                    ("k_scan1" if m == 1 else "k_scanm"))
     if dist_mode:
@@ -288,6 +290,28 @@ def main():
             kev[i][1].record(stream)
         torch.cuda.synchronize()
         kev = kev[:min(args.steps, 50)]
+        # the worker -> aggregator exchange of a sample of rounds, timed with events on the stream it runs on
+        # (after the timed region: the events cost host time)
+        xs_ms, xs_out, xs_in = [], [], []
+        for i in range(min(args.steps, 20)):
+            xs, out = sets[i % len(sets)]
+            engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
+                       async_=pipelined, time_exchange=True)
+            ms_x, b_out, b_in = engine.exchange_time()
+            xs_ms.append(ms_x)
+            xs_out.append(b_out)
+            xs_in.append(b_in)
+        join()
+        torch.cuda.synchronize()
+        x_ms = float(np.mean(xs_ms))
+        exchange = {"ms_mean": round(x_ms, 5), "bytes_out_per_rank": int(np.mean(xs_out)),
+                    "bytes_in_per_rank": int(np.mean(xs_in)), "peers": ws - 1,
+                    "GBps_out_per_rank": round(float(np.mean(xs_out)) / (x_ms * 1e-3) / 1e9, 2) if x_ms > 0 else None,
+                    "GBps_out_per_peer": (round(float(np.mean(xs_out)) / (ws - 1) / (x_ms * 1e-3) / 1e9, 2)
+                                          if x_ms > 0 and ws > 1 else None),
+                    "xgmi_link_GBps_nominal": XGMI_LINK_GBPS,
+                    "timing": "HIP events around the grouped ncclSend/ncclRecv (dense: ncclReduceScatter) on the "
+                              "round's communication stream, 20 rounds after the timed region, rank 0"}
     if not (dist_mode and args.dist_impl == "cpp"):
         kev = kev[::every]
     if one_kernel:  # every step is exactly one k_scan1f launch: events around all K steps, divided by K
@@ -349,6 +373,8 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
+    if exchange is not None:
+        line["exchange"] = exchange
     if not dist_mode and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(L, bitmaps[0], args)
     print(json.dumps(line), flush=True)

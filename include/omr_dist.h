@@ -88,9 +88,16 @@ int omr_sparse_allreduce_f32(omr_ar_plan* plan, const float* x, float* out, int3
  * calls back before reusing its buffers.  x and out must stay untouched (and must not be a later round's input)
  * until the round is joined. */
 #define OMR_ROUND_ASYNC 0x100
+/* OR-ed into `mode`: bracket this round's worker -> aggregator exchange (the grouped send/recv; the dense
+ * stand-in's reduce-scatter) with timing events on the stream it runs on; read them with
+ * omr_ar_plan_exchange_time().  Measurement only: the events cost host time, so time a sample of rounds. */
+#define OMR_ROUND_TIME_EXCHANGE 0x200
 int omr_sparse_round_f32(omr_ar_plan* plan, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
                          uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
                          omr_stream_t stream);
+/* Duration of the last OMR_ROUND_TIME_EXCHANGE round's exchange (waits for it), with the bytes this rank sent
+ * to and received from its peers in it (bytes_out / bytes_in may be NULL).  OMR_EINVAL if no round was timed. */
+int omr_ar_plan_exchange_time(omr_ar_plan* plan, float* ms, uint64_t* bytes_out, uint64_t* bytes_in);
 /* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
 int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
 

@@ -230,6 +230,10 @@ struct omr_ar_plan {
   uint32_t* flag_host = nullptr;  // pinned: the plan kernel stores the round's sequence number here
   uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
+  // OMR_ROUND_TIME_EXCHANGE: events around the last timed round's worker -> aggregator exchange, and its bytes
+  hipEvent_t xt0 = nullptr, xt1 = nullptr;
+  bool xt_recorded = false;
+  uint64_t xt_out = 0, xt_in = 0;
 };
 
 extern "C" {
@@ -294,6 +298,8 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     if (st.done) (void)hipEventDestroy(st.done);
   }
   if (p->cs) (void)hipStreamDestroy(p->cs);
+  if (p->xt0) (void)hipEventDestroy(p->xt0);
+  if (p->xt1) (void)hipEventDestroy(p->xt1);
   (void)hipHostFree(p->counts_host);
   (void)hipHostFree(p->flag_host);
   (void)hipFree(p->arrive);
@@ -338,6 +344,8 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
     A(hip_check(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "hipEventCreate"));
   }
   A(hip_check(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking), "hipStreamCreate"));
+  A(hip_check(hipEventCreate(&p->xt0), "hipEventCreate"));
+  A(hip_check(hipEventCreate(&p->xt1), "hipEventCreate"));
   A(dev_alloc(&p->bounds_dev, N + 1));
   if (N > 1) A(dev_alloc(&p->recv, static_cast<size_t>(N - 1) * p->shard_nb * block_size));
   A(dev_alloc(&p->results, n));
@@ -382,7 +390,8 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
                          omr_stream_t stream) {
   if (p == nullptr || x == nullptr || out == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL");
   const bool async = (mode & OMR_ROUND_ASYNC) != 0;
-  mode &= ~OMR_ROUND_ASYNC;
+  const bool timed = (mode & OMR_ROUND_TIME_EXCHANGE) != 0;
+  mode &= ~(OMR_ROUND_ASYNC | OMR_ROUND_TIME_EXCHANGE);
   if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
     return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
   if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && p->rows % p->N != 0)
@@ -441,7 +450,14 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER) {
     // the dense stand-in: every element of this rank's shard, reduced over all ranks by the transport
     const uint64_t row_floats = static_cast<uint64_t>(p->lanes) * B;
+    if (timed) TRY(hip_check(hipEventRecord(p->xt0, xs), "hipEventRecord"));
     TRY(p->d->reduce_scatter(x, out + r0 * row_floats, (r1 - r0) * row_floats, xs));
+    if (timed) {
+      TRY(hip_check(hipEventRecord(p->xt1, xs), "hipEventRecord"));
+      // a ring reduce-scatter sends and receives (N-1)/N of the tensor per rank
+      p->xt_out = p->xt_in = static_cast<uint64_t>(N - 1) * (r1 - r0) * row_floats * sizeof(float);
+      p->xt_recorded = true;
+    }
     if (async) {
       TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
       S.pending = true;
@@ -459,6 +475,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   const uint64_t total_send = cnt(me, N) - own_shard;
   // 4b. send each slice to its aggregator (common.cc:449); receive this shard's blocks from every peer
   std::vector<uint64_t> roff(N, 0);
+  if (timed) TRY(hip_check(hipEventRecord(p->xt0, xs), "hipEventRecord"));
   if (N > 1) {
     std::vector<Slice> sends(N), recvs(N);
     uint64_t acc = 0;
@@ -470,6 +487,15 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
       if (s != me) acc += per(s, me);
     }
     TRY(p->d->exchange(sends, recvs, xs));
+  }
+  if (timed) {
+    TRY(hip_check(hipEventRecord(p->xt1, xs), "hipEventRecord"));
+    uint64_t in_blocks = 0;
+    for (int s = 0; s < N; ++s)
+      if (s != me) in_blocks += per(s, me);
+    p->xt_out = total_send * B * sizeof(float);
+    p->xt_in = in_blocks * B * sizeof(float);
+    p->xt_recorded = true;
   }
   // 5. aggregator: rank-order shard sums (server.cc:97-98), own contribution read in place
   const bool rs_mode = mode == OMR_ROUND_REDUCE_SCATTER;
@@ -506,6 +532,16 @@ int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
   // the communication stream runs rounds in issue order: waiting for the last one covers every earlier one
   TRY(hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), p->set[p->last_async].done, 0),
                 "hipStreamWaitEvent"));
+  return 0;
+}
+
+int omr_ar_plan_exchange_time(omr_ar_plan* p, float* ms, uint64_t* bytes_out, uint64_t* bytes_in) {
+  if (p == nullptr || ms == nullptr) return derr(OMR_EINVAL, "ar_plan_exchange_time: NULL");
+  if (!p->xt_recorded) return derr(OMR_EINVAL, "ar_plan_exchange_time: no OMR_ROUND_TIME_EXCHANGE round issued");
+  TRY(hip_check(hipEventSynchronize(p->xt1), "hipEventSynchronize"));
+  TRY(hip_check(hipEventElapsedTime(ms, p->xt0, p->xt1), "hipEventElapsedTime"));
+  if (bytes_out) *bytes_out = p->xt_out;
+  if (bytes_in) *bytes_in = p->xt_in;
   return 0;
 }
 

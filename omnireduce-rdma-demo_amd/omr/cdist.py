@@ -47,6 +47,7 @@ def load():
         "omr_sparse_allreduce_f32": (i, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "omr_sparse_round_f32": (i, [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]),
         "omr_ar_plan_join": (i, [vp, vp]),
+        "omr_ar_plan_exchange_time": (i, [vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -83,16 +84,19 @@ class CppSparseAllreduce:
                "omr_ar_plan_create")
         self.rank, self.world = rank, world
 
-    ALLREDUCE, REDUCE_SCATTER, DENSE_REDUCE_SCATTER, ASYNC = 0, 1, 2, 0x100
+    ALLREDUCE, REDUCE_SCATTER, DENSE_REDUCE_SCATTER, ASYNC, TIME_EXCHANGE = 0, 1, 2, 0x100, 0x200
 
     def run(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, ev=None, flags=None, next_offsets=None,
-            union_next=None, mode: int = 0, async_: bool = False):
+            union_next=None, mode: int = 0, async_: bool = False, time_exchange: bool = False):
         """mode 0: all-reduce (every worker gets every shard's sums); 1: reduce-scatter (stop at the
         aggregators: `out` gets this rank's shard sums only); 2: the dense stand-in (the whole tensor reduce-scattered
         by RCCL, every block).  async_: the exchange and the sums run on the plan's
-        communication stream, overlapping the next call's worker scan; `out` is ready after join()."""
+        communication stream, overlapping the next call's worker scan; `out` is ready after join().
+        time_exchange: bracket the worker -> aggregator exchange with timing events (read with exchange_time())."""
         if async_:
             mode |= self.ASYNC
+        if time_exchange:
+            mode |= self.TIME_EXCHANGE
         out = x if out is None else out
         sent, uni = ctypes.c_uint64(), ctypes.c_uint64()
         st = torch.cuda.current_stream(self.device)
@@ -105,6 +109,13 @@ class CppSparseAllreduce:
         if ev is not None:
             ev[1].record(st)
         return sent.value, uni.value
+
+    def exchange_time(self):
+        """(ms, bytes sent, bytes received) of the last round run with time_exchange=True (waits for it)."""
+        ms, bo, bi = ctypes.c_float(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(load().omr_ar_plan_exchange_time(self._p, ctypes.byref(ms), ctypes.byref(bo), ctypes.byref(bi)),
+               "omr_ar_plan_exchange_time")
+        return ms.value, bo.value, bi.value
 
     def join(self, stream=None):
         """Make `stream` (default: the current stream) wait for every asynchronous round issued so far."""

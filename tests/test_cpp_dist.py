@@ -36,6 +36,7 @@ def dist_lib():
     L.omr_sparse_allreduce_f32.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.omr_sparse_round_f32.argtypes = [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]
     L.omr_ar_plan_join.argtypes = [vp, vp]
+    L.omr_ar_plan_exchange_time.argtypes = [vp, vp, vp, vp]
     L.omr_dist_last_error.restype = ctypes.c_char_p
     return L
 
@@ -354,3 +355,68 @@ def test_bench_distributed_path_world1(gpu, extra):
     line = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 1 and line["value"] > 0 and line["roofline"]["frac"] > 0
     assert "RCCL" in line["config"]["parallelism"]
+    assert line["exchange"]["peers"] == 0 and line["exchange"]["ms_mean"] >= 0
+
+
+@pytest.mark.parametrize("world,mode", [(4, 1 | 0x100), (3, 0), (4, 2)])
+def test_cpp_exchange_timing_loopback(gpu, world, mode):
+    """OMR_ROUND_TIME_EXCHANGE: the timed round's result is unchanged, omr_ar_plan_exchange_time reports a
+    duration and the exchange's bytes: out = this rank's sent blocks, and what the ranks send is what they
+    receive; the dense stand-in moves (N-1)/N of the tensor each way."""
+    B = 256
+    L = Layout(n=2 << 20, block_size=B)
+    D = dist_lib()
+    bufs = [oracle.fill(oracle.gen_bitmap(w, 0.2, L.nb), B, mode=1, seed=w + 3) for w in range(world)]
+    board = D.omr_local_board_create(world)
+    errs, res = [], [None] * world
+
+    def rank(r):
+        try:
+            torch.cuda.set_device(0)
+            x = torch.from_numpy(bufs[r].copy()).cuda()
+            out = x.clone()
+            d, plan = ctypes.c_void_p(), ctypes.c_void_p()
+            assert D.omr_dist_create_local(board, r, ctypes.byref(d)) == 0
+            assert D.omr_ar_plan_create(d, L.n, B, L.num_lanes, 8, ctypes.byref(plan)) == 0
+            ms, bo, bi = ctypes.c_float(), ctypes.c_uint64(), ctypes.c_uint64()
+            assert D.omr_ar_plan_exchange_time(plan, ctypes.byref(ms), None, None) == -1  # nothing timed yet (OMR_EINVAL)
+            st = torch.cuda.Stream()
+            sent = ctypes.c_uint64()
+            assert D.omr_sparse_round_f32(plan, x.data_ptr(), out.data_ptr(), None, None, None, mode | 0x200,
+                                          ctypes.byref(sent), None, st.cuda_stream) == 0, D.omr_dist_last_error()
+            assert D.omr_ar_plan_exchange_time(plan, ctypes.byref(ms), ctypes.byref(bo), ctypes.byref(bi)) == 0
+            assert D.omr_ar_plan_join(plan, st.cuda_stream) == 0
+            st.synchronize()
+            res[r] = (ms.value, bo.value, bi.value, sent.value, out.cpu().numpy())
+            D.omr_ar_plan_destroy(plan)
+            D.omr_dist_destroy(d)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    D.omr_local_board_destroy(board)
+    assert not errs, errs
+    bounds = [s * L.rows // world for s in range(world + 1)]
+    uf = oracle.union_flags([oracle.flags_from_data(b, B) for b in bufs])
+    for r in range(world):
+        ms, bo, bi, sent, out = res[r]
+        assert ms >= 0.0
+        if (mode & 3) == 2:
+            shard = (bounds[r + 1] - bounds[r]) * L.num_lanes * B * 4
+            assert bo == bi == (world - 1) * shard
+        else:
+            assert bo == sent * B * 4
+        full = bufs[r].copy()
+        if (mode & 3) != 2:
+            oracle.block_sum(bufs, L.n, B, L.num_lanes, 8, uf, full)
+            exp = full if (mode & 3) == 0 else bufs[r].copy()
+            if (mode & 3) == 1:
+                lo, hi = bounds[r] * L.num_lanes * B, bounds[r + 1] * L.num_lanes * B
+                exp[lo:hi] = full[lo:hi]
+            assert (out.view(np.uint32) == exp.view(np.uint32)).all(), f"rank {r}"
+    if (mode & 3) != 2:
+        assert sum(x[1] for x in res) == sum(x[2] for x in res)
