@@ -65,9 +65,12 @@ def parse():
                    help="N>1 step: workers -> aggregators reduce-scatter (BASELINE config 4, default), the full "
                         "all-reduce (sums back to every worker), or the dense stand-in (ncclReduceScatter of the "
                         "whole tensor, C++ driver only)")
-    p.add_argument("--dist-sync", action="store_true",
-                   help="N>1, C++ driver: keep each round's exchange on the caller's stream (default: OMR_ROUND_ASYNC, "
-                        "round k's exchange over xGMI overlaps round k+1's worker scan)")
+    p.add_argument("--dist-pipe", choices=("sync", "async", "defer"), default="defer",
+                   help="N>1, C++ driver: sync = each round's exchange on the caller's stream; async "
+                        "(OMR_ROUND_ASYNC) = round k's exchange over xGMI overlaps round k+1's worker scan; defer "
+                        "(OMR_ROUND_DEFER, default) = as async, and round k's exchange is issued after round k+1's "
+                        "first half is queued, so the host never waits for block counts with the GPU idle")
+    p.add_argument("--dist-sync", action="store_true", help="same as --dist-pipe sync")
     p.add_argument("--dist-impl", choices=("cpp", "torch"), default="cpp",
                    help="N>1 round driver: C++ (libomr_dist.so, RCCL from C++) or Python (omr.dist over "
                         "torch.distributed); same protocol and kernels")
@@ -211,13 +214,14 @@ def main():
         for xs, out in sets:  # out-of-place result buffers keep every step's input pristine
             out.copy_(xs[0])
 
-        pipelined = args.dist_impl == "cpp" and not args.dist_sync
+        pipe = "sync" if (args.dist_sync or args.dist_impl != "cpp") else args.dist_pipe
+        pipelined = pipe != "sync"
 
         def step(i, ev=None):
             xs, out = sets[i % len(sets)]
             if args.dist_impl == "cpp":
                 engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
-                           async_=pipelined)
+                           async_=pipelined, defer=pipe == "defer")
             else:
                 engine.run(xs[0], out=out, ev=ev, mode=0 if args.dist_mode == "allreduce" else 1)
     else:
@@ -296,7 +300,8 @@ def main():
         for i in range(min(args.steps, 20)):
             xs, out = sets[i % len(sets)]
             engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
-                       async_=pipelined, time_exchange=True)
+                       async_=pipelined, defer=pipe == "defer", time_exchange=True)
+            engine.join(stream)  # (issues a deferred round's exchange)
             ms_x, b_out, b_in = engine.exchange_time()
             xs_ms.append(ms_x)
             xs_out.append(b_out)
@@ -346,6 +351,10 @@ def main():
         if dist_mode:
             torch.distributed.destroy_process_group()
         return
+    pipe_note = ""
+    if dist_mode and args.dist_impl == "cpp" and pipe != "sync":
+        pipe_note = (", rounds pipelined: exchange k beside scan k+1" +
+                     (", exchange k issued after round k+1's first half (OMR_ROUND_DEFER)" if pipe == "defer" else ""))
     total_bytes = n_gpus * m * L.nbytes
     value = total_bytes / (ms_per_step * 1e-3) / 1e9
     line = {
@@ -368,7 +377,7 @@ def main():
                    "parallelism": "single GPU" if not dist_mode else
                    f"dp{n_gpus} {dict(allreduce='sparse all-reduce', reduce='sparse reduce-scatter', dense='dense reduce-scatter (stand-in)')[args.dist_mode]} over "
                    f"RCCL ({args.dist_impl} round driver"
-                   f"{', rounds pipelined: exchange k beside scan k+1' if dist_mode and args.dist_impl == 'cpp' and not args.dist_sync else ''})"},
+                   f"{pipe_note})"},
         "alg_bw_GiBps_reference_style": round(total_bytes / (ms_per_step * 1e-3) / 2 ** 30, 2),
         "roofline": roofline,
         "cpu_baseline": None,

@@ -92,6 +92,15 @@ int omr_sparse_allreduce_f32(omr_ar_plan* plan, const float* x, float* out, int3
  * stand-in's reduce-scatter) with timing events on the stream it runs on; read them with
  * omr_ar_plan_exchange_time().  Measurement only: the events cost host time, so time a sample of rounds. */
 #define OMR_ROUND_TIME_EXCHANGE 0x200
+/* OR-ed into `mode` (implies OMR_ROUND_ASYNC): a deeper pipeline.  The call queues this round's first half
+ * (worker scan, mask all-gather, plan, pack, aggregator chain) on `stream` and only then issues the PREVIOUS
+ * deferred round's exchange and aggregation on the communication stream; this round's follow at the next call,
+ * at a call without this flag, or at omr_ar_plan_join().  The host therefore never waits for block counts with the
+ * caller's stream idle: the previous round's counts are in host memory while this round's scan runs.
+ * *sent_blocks / *union_blocks receive the values of the previous round (the one whose exchange this call
+ * issued; 0 if none).  Every rank must use the same sequence of modes; join (or a non-deferred call) before
+ * reading `out` or destroying the plan (destroy issues a pending exchange and synchronises the device). */
+#define OMR_ROUND_DEFER 0x400
 int omr_sparse_round_f32(omr_ar_plan* plan, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
                          uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
                          omr_stream_t stream);

@@ -217,7 +217,7 @@ struct omr_ar_plan {
   int last_async = -1;              // set of the last asynchronous round (for join)
   hipStream_t cs = nullptr;         // communication stream of asynchronous rounds
   uint64_t* bounds_dev = nullptr;
-  uint32_t* counts_host = nullptr;  // [N+1][N+1] prefix[a][bounds[s]], pinned host memory the plan kernel writes
+  uint32_t* counts_host = nullptr;  // [2][N+1][N+1] per set: prefix[a][bounds[s]], pinned memory the plan kernel writes
   uint32_t* counts_map = nullptr;   // its device-side address
   float* recv = nullptr;     // this shard's blocks from each peer, peer-major
   float* results = nullptr;  // all-reduce: every shard's sums, write-set order
@@ -227,14 +227,28 @@ struct omr_ar_plan {
   void* scan_ws = nullptr;   // omr_worker_scan_f32 segment workspace (zeroed once, self-resetting)
   size_t scan_ws_bytes = 0;
   uint32_t* arrive = nullptr;     // device arrival counter of the plan kernel's completion notice
-  uint32_t* flag_host = nullptr;  // pinned: the plan kernel stores the round's sequence number here
+  uint32_t* flag_host = nullptr;  // [2] pinned, per set: the plan kernel stores the round's sequence number here
   uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
   // OMR_ROUND_TIME_EXCHANGE: events around the last timed round's worker -> aggregator exchange, and its bytes
   hipEvent_t xt0 = nullptr, xt1 = nullptr;
   bool xt_recorded = false;
   uint64_t xt_out = 0, xt_in = 0;
+  // OMR_ROUND_DEFER: the round whose exchange and aggregation the next call (or join) issues
+  struct Pending {
+    bool active = false;
+    int si = 0, mode = 0;
+    bool timed = false;
+    const float* x = nullptr;
+    float* out = nullptr;
+    uint32_t seq = 0;
+    hipStream_t st = nullptr;  // the stream its first half went on (the count wait checks it for a failed launch)
+  } pend;
 };
+
+namespace {
+int flush_pending(omr_ar_plan* p, hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks);
+}  // namespace
 
 extern "C" {
 
@@ -288,6 +302,10 @@ int omr_dist_destroy(omr_dist* d) {
 
 int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p == nullptr) return 0;
+  if (p->pend.active) {  // a deferred round still owes its exchange to the peers: issue it and let it drain
+    (void)flush_pending(p, p->cs, nullptr, nullptr);
+    (void)hipDeviceSynchronize();
+  }
   void* devs[] = {p->own_masks, p->bounds_dev, p->recv,    p->results,
                   p->flags_ws,  p->next_ws,    p->unext_ws, p->scan_ws};
   for (void* v : devs) (void)hipFree(v);
@@ -354,16 +372,16 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   A(dev_alloc(&p->unext_ws, p->nb));
   p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
   A(dev_alloc(reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
-  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), (N + 1) * (N + 1) * sizeof(uint32_t),
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), 2 * (N + 1) * (N + 1) * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0)
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->counts_map), p->counts_host, 0),
                 "hipHostGetDevicePointer"));
   A(dev_alloc(&p->arrive, 1));
-  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), sizeof(uint32_t),
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), 2 * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0) {
-    *p->flag_host = 0;
+    p->flag_host[0] = p->flag_host[1] = 0;
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->flag_map), p->flag_host, 0),
                 "hipHostGetDevicePointer"));
   }
@@ -382,67 +400,23 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   return 0;
 }
 
-// One round (DESIGN.md §5): scan -> mask all-gather -> one bookkeeping launch -> block counts to the host (the
-// round's single mid-round sync: the transport needs host-side sizes) -> pack -> send/recv -> shard sums
-// [-> sums back -> unpack].  Every block movement is addressed by masks and prefixes.
-int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
-                         uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
-                         omr_stream_t stream) {
-  if (p == nullptr || x == nullptr || out == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL");
-  const bool async = (mode & OMR_ROUND_ASYNC) != 0;
-  const bool timed = (mode & OMR_ROUND_TIME_EXCHANGE) != 0;
-  mode &= ~(OMR_ROUND_ASYNC | OMR_ROUND_TIME_EXCHANGE);
-  if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
-    return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
-  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && p->rows % p->N != 0)
-    return derr(OMR_EINVAL, "sparse_round: dense reduce-scatter needs equal shards (rows %llu, world %d)",
-                static_cast<unsigned long long>(p->rows), p->N);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+}  // extern "C"
+
+namespace {
+
+// The second half of a round (steps 4b-7): wait for the plan's counts, exchange, shard sums [, sums back,
+// unpack].  `async`: on the communication stream, behind the set's `ready` event.
+int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, bool async, bool timed, uint32_t seq,
+                 hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks) {
+  omr_ar_plan::Set& S = p->set[si];
   const int N = p->N, me = p->me;
   const uint64_t rows = p->rows, B = p->B;
   const uint32_t NB = N + 1;
-  int32_t* fl = flags ? flags : p->flags_ws;
-  uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
-  uint32_t* un = union_next ? union_next : p->unext_ws;
-  // a synchronous round after asynchronous ones: its exchange goes on `stream`, so the communication stream
-  // must be idle first (one communicator is never driven from two streams at once)
-  if (!async && p->last_async >= 0) {
-    TRY(hip_check(hipStreamWaitEvent(st, p->set[p->last_async].done, 0), "hipStreamWaitEvent"));
-    p->last_async = -1;
-  }
-  const int si = p->cur;
-  omr_ar_plan::Set& S = p->set[si];
-  p->cur ^= 1;
-  // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass
-  TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, p->own_masks, nullptr, p->scan_ws,
-                                    p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
-  // the set is refilled from here on: an asynchronous round two calls back must be through with it
-  if (S.pending) {
-    TRY(hip_check(hipStreamWaitEvent(st, S.done, 0), "hipStreamWaitEvent"));
-    S.pending = false;
-  }
-  // 2. every worker's row masks
-  TRY(p->d->allgather(p->own_masks, S.masks_all, rows * sizeof(uint64_t), st));
-  // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for the next round
-  //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
-  const uint32_t seq = ++p->seq;
-  TRY(omr_check(omr_round_plan(S.masks_all, N, rows, p->rpp, p->lanes, p->bounds_dev, NB, S.wset, S.umask,
-                               S.prefix, p->counts_map, p->own_masks, p->arrive, p->flag_map, seq, stream),
-                "omr_round_plan"));
-  // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407), then the
-  //     aggregator chain (server.cc:86-96 min_next) over the union: both addressed by device-side data only, so
-  //     they are queued before the host learns the counts and run while it waits.  (Every host API call costs
-  //     microseconds; a round that spends them on side streams and events is host-bound.)
+  const uint32_t* counts = p->counts_host + static_cast<size_t>(si) * NB * NB;
+  const uint32_t* flag = p->flag_host + si;
   const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
-  if (N > 1 && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
-    TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * rows,
-                                      S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
-                                      r1, stream), "omr_move_blocks_f32 pack"));
-  TRY(omr_check(omr_next_offsets(S.umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
-  // the rest goes on the communication stream for an asynchronous round, behind everything queued so far
   hipStream_t xs = st;
   if (async) {
-    TRY(hip_check(hipEventRecord(S.ready, st), "hipEventRecord"));
     TRY(hip_check(hipStreamWaitEvent(p->cs, S.ready, 0), "hipStreamWaitEvent"));
     xs = p->cs;
   }
@@ -463,13 +437,13 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
       S.pending = true;
       p->last_async = si;
     }
-    if (sent_blocks != nullptr || union_blocks != nullptr) TRY(wait_flag(p->flag_host, seq, st));
+    if (sent_blocks != nullptr || union_blocks != nullptr) TRY(wait_flag(flag, seq, st));
     if (sent_blocks) *sent_blocks = (r1 - r0) * p->lanes * static_cast<uint64_t>(N - 1);
-    if (union_blocks) *union_blocks = p->counts_host[N * NB + me + 1] - p->counts_host[N * NB + me];
+    if (union_blocks) *union_blocks = counts[N * NB + me + 1] - counts[N * NB + me];
     return 0;
   }
-  TRY(wait_flag(p->flag_host, seq, st));
-  auto cnt = [&](int a, int s) -> uint64_t { return p->counts_host[a * NB + s]; };
+  TRY(wait_flag(flag, seq, st));
+  auto cnt = [&](int a, int s) -> uint64_t { return counts[a * NB + s]; };
   auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
   const uint64_t own_shard = per(me, me);
   const uint64_t total_send = cnt(me, N) - own_shard;
@@ -526,8 +500,106 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   return 0;
 }
 
+// Issue the deferred round's second half, if there is one.
+int flush_pending(omr_ar_plan* p, hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks) {
+  if (sent_blocks) *sent_blocks = 0;
+  if (union_blocks) *union_blocks = 0;
+  if (!p->pend.active) return 0;
+  const omr_ar_plan::Pending q = p->pend;
+  p->pend.active = false;
+  (void)st;
+  return round_finish(p, q.si, q.x, q.out, q.mode, true, q.timed, q.seq, q.st, sent_blocks, union_blocks);
+}
+
+}  // namespace
+
+extern "C" {
+
+// One round (DESIGN.md §5): scan -> mask all-gather -> one bookkeeping launch -> block counts to the host (the
+// round's single mid-round sync: the transport needs host-side sizes) -> pack -> send/recv -> shard sums
+// [-> sums back -> unpack].  Every block movement is addressed by masks and prefixes.
+int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
+                         uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
+                         omr_stream_t stream) {
+  if (p == nullptr || x == nullptr || out == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL");
+  const bool defer = (mode & OMR_ROUND_DEFER) != 0;
+  const bool async = defer || (mode & OMR_ROUND_ASYNC) != 0;
+  const bool timed = (mode & OMR_ROUND_TIME_EXCHANGE) != 0;
+  mode &= ~(OMR_ROUND_ASYNC | OMR_ROUND_DEFER | OMR_ROUND_TIME_EXCHANGE);
+  if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
+    return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
+  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && p->rows % p->N != 0)
+    return derr(OMR_EINVAL, "sparse_round: dense reduce-scatter needs equal shards (rows %llu, world %d)",
+                static_cast<unsigned long long>(p->rows), p->N);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int N = p->N, me = p->me;
+  const uint64_t rows = p->rows;
+  const uint32_t NB = N + 1;
+  int32_t* fl = flags ? flags : p->flags_ws;
+  uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
+  uint32_t* un = union_next ? union_next : p->unext_ws;
+  // a round that is not deferred finishes a deferred one first (rounds complete in call order)
+  if (!defer) TRY(flush_pending(p, st, nullptr, nullptr));
+  // a synchronous round after asynchronous ones: its exchange goes on `stream`, so the communication stream
+  // must be idle first (one communicator is never driven from two streams at once)
+  if (!async && p->last_async >= 0) {
+    TRY(hip_check(hipStreamWaitEvent(st, p->set[p->last_async].done, 0), "hipStreamWaitEvent"));
+    p->last_async = -1;
+  }
+  const int si = p->cur;
+  omr_ar_plan::Set& S = p->set[si];
+  p->cur ^= 1;
+  // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass
+  TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, p->own_masks, nullptr, p->scan_ws,
+                                    p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+  // the set is refilled from here on: an asynchronous round two calls back must be through with it
+  // (skipped when the host already sees the event complete: a stream-wait packet costs the GPU a few
+  // microseconds of dispatch even when its event has long fired)
+  if (S.pending) {
+    const hipError_t q = hipEventQuery(S.done);
+    if (q == hipErrorNotReady) TRY(hip_check(hipStreamWaitEvent(st, S.done, 0), "hipStreamWaitEvent"));
+    else TRY(hip_check(q, "hipEventQuery"));
+    S.pending = false;
+  }
+  // 2. every worker's row masks
+  TRY(p->d->allgather(p->own_masks, S.masks_all, rows * sizeof(uint64_t), st));
+  // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for the next round
+  //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
+  const uint32_t seq = ++p->seq;
+  TRY(omr_check(omr_round_plan(S.masks_all, N, rows, p->rpp, p->lanes, p->bounds_dev, NB, S.wset, S.umask,
+                               S.prefix, p->counts_map + static_cast<size_t>(si) * NB * NB, p->own_masks, p->arrive,
+                               p->flag_map + si, seq, stream),
+                "omr_round_plan"));
+  // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407), then the
+  //     aggregator chain (server.cc:86-96 min_next) over the union: both addressed by device-side data only, so
+  //     they are queued before the host learns the counts and run while it waits.  (Every host API call costs
+  //     microseconds; a round that spends them on side streams and events is host-bound.)
+  const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
+  if (N > 1 && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
+    TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * rows,
+                                      S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
+                                      r1, stream), "omr_move_blocks_f32 pack"));
+  TRY(omr_check(omr_next_offsets(S.umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
+  // the rest goes on the communication stream for an asynchronous round, behind everything queued so far
+  if (async) TRY(hip_check(hipEventRecord(S.ready, st), "hipEventRecord"));
+  if (!defer) return round_finish(p, si, x, out, mode, async, timed, seq, st, sent_blocks, union_blocks);
+  // deferred: this round's first half is queued; now issue the previous round's exchange, whose counts have long
+  // been in host memory, so the host neither waits nor leaves the caller's stream idle
+  TRY(flush_pending(p, st, sent_blocks, union_blocks));
+  p->pend.active = true;
+  p->pend.si = si;
+  p->pend.mode = mode;
+  p->pend.timed = timed;
+  p->pend.x = x;
+  p->pend.out = out;
+  p->pend.seq = seq;
+  p->pend.st = st;
+  return 0;
+}
+
 int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_join: NULL");
+  TRY(flush_pending(p, reinterpret_cast<hipStream_t>(stream), nullptr, nullptr));
   if (p->last_async < 0) return 0;
   // the communication stream runs rounds in issue order: waiting for the last one covers every earlier one
   TRY(hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), p->set[p->last_async].done, 0),

@@ -84,15 +84,20 @@ class CppSparseAllreduce:
                "omr_ar_plan_create")
         self.rank, self.world = rank, world
 
-    ALLREDUCE, REDUCE_SCATTER, DENSE_REDUCE_SCATTER, ASYNC, TIME_EXCHANGE = 0, 1, 2, 0x100, 0x200
+    ALLREDUCE, REDUCE_SCATTER, DENSE_REDUCE_SCATTER, ASYNC, TIME_EXCHANGE, DEFER = 0, 1, 2, 0x100, 0x200, 0x400
 
     def run(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, ev=None, flags=None, next_offsets=None,
-            union_next=None, mode: int = 0, async_: bool = False, time_exchange: bool = False):
+            union_next=None, mode: int = 0, async_: bool = False, time_exchange: bool = False,
+            defer: bool = False):
         """mode 0: all-reduce (every worker gets every shard's sums); 1: reduce-scatter (stop at the
         aggregators: `out` gets this rank's shard sums only); 2: the dense stand-in (the whole tensor reduce-scattered
         by RCCL, every block).  async_: the exchange and the sums run on the plan's
         communication stream, overlapping the next call's worker scan; `out` is ready after join().
-        time_exchange: bracket the worker -> aggregator exchange with timing events (read with exchange_time())."""
+        time_exchange: bracket the worker -> aggregator exchange with timing events (read with exchange_time()).
+        defer: OMR_ROUND_DEFER, this round's exchange is issued by the next call (or join()), after the next
+        round's worker scan is queued; the returned counts are the previous round's."""
+        if defer:
+            mode |= self.DEFER
         if async_:
             mode |= self.ASYNC
         if time_exchange:

@@ -142,12 +142,20 @@ def test_cpp_reduce_scatter_loopback(gpu, world, rounds):
         assert (outs[r].view(np.uint32) == exp.view(np.uint32)).all(), f"rank {r}"
 
 
-@pytest.mark.parametrize("world,mode,sync_rounds", [(3, 1, ()), (8, 1, ()), (4, 0, ()), (3, 1, (2, 4))])
-def test_cpp_async_rounds_loopback(gpu, world, mode, sync_rounds):
+A, D_ = 0x100, 0x400  # OMR_ROUND_ASYNC, OMR_ROUND_DEFER
+
+
+@pytest.mark.parametrize("world,mode,round_flags", [
+    (3, 1, (A,) * 5), (8, 1, (A,) * 5), (4, 0, (A,) * 5), (3, 1, (A, A, 0, A, 0)),
+    (3, 1, (D_,) * 5), (8, 1, (D_,) * 5), (4, 0, (D_,) * 5), (4, 2, (D_,) * 5),
+    (3, 1, (D_, D_, 0, D_, A)), (4, 0, (A, D_, D_, A, D_))])
+def test_cpp_async_rounds_loopback(gpu, world, mode, round_flags):
     """OMR_ROUND_ASYNC: the exchange and sums of round k run on the plan's communication stream while round k+1
     scans; rounds take different inputs and outputs (the bench's rotation), use the two plan buffer sets in
-    turn (five rounds: each set refilled twice), and are joined once at the end.  sync_rounds: rounds issued
-    without the flag in between (they must wait for the asynchronous ones before using the stream)."""
+    turn (five rounds: each set refilled twice), and are joined once at the end.  OMR_ROUND_DEFER: round k's
+    exchange is issued by call k+1 (or the join), after round k+1's first half.  Rounds issued without a flag in
+    between must first finish a deferred round and wait for the asynchronous ones before using the stream."""
+    sync_rounds = ()
     B, rounds = 256, 5
     L = Layout(n=2 << 20, block_size=B)
     D = dist_lib()
@@ -166,7 +174,7 @@ def test_cpp_async_rounds_loopback(gpu, world, mode, sync_rounds):
             assert D.omr_ar_plan_create(d, L.n, B, L.num_lanes, 8, ctypes.byref(plan)) == 0
             st = torch.cuda.Stream()
             for k in range(rounds):
-                flag = 0 if k in sync_rounds else 0x100
+                flag = round_flags[k]
                 assert D.omr_sparse_round_f32(plan, xs[k].data_ptr(), os_[k].data_ptr(), None, None, None,
                                               mode | flag, None, None, st.cuda_stream) == 0, D.omr_dist_last_error()
             assert D.omr_ar_plan_join(plan, st.cuda_stream) == 0
@@ -191,7 +199,7 @@ def test_cpp_async_rounds_loopback(gpu, world, mode, sync_rounds):
         for r in range(world):
             full = bufs[k][r].copy()
             oracle.block_sum(bufs[k], L.n, B, L.num_lanes, 8, uf, full)
-            if mode == 1:
+            if mode in (1, 2):  # reduce-scatter, sparse or dense: this shard's sums, other rows untouched
                 exp = bufs[k][r].copy()
                 lo, hi = bounds[r] * L.num_lanes * B, bounds[r + 1] * L.num_lanes * B
                 exp[lo:hi] = full[lo:hi]
@@ -336,7 +344,8 @@ def test_client_message_mode_trace(gpu, tmp_path):
         assert g == e, f"record {i}: {g[:4]} vs {e[:4]}"
 
 
-@pytest.mark.parametrize("extra", [[], ["--dist-sync"], ["--dist-mode", "allreduce"], ["--dist-mode", "dense"]])
+@pytest.mark.parametrize("extra", [[], ["--dist-sync"], ["--dist-pipe", "async"], ["--dist-mode", "allreduce"],
+                                   ["--dist-mode", "dense"]])
 def test_bench_distributed_path_world1(gpu, extra):
     """bench.py's N>1 path as the driver launches it (torch.distributed.run, RCCL, the C++ round with two
     communicators, pipelined rounds joined before the closing sync), rehearsed at world 1."""
@@ -358,7 +367,7 @@ def test_bench_distributed_path_world1(gpu, extra):
     assert line["exchange"]["peers"] == 0 and line["exchange"]["ms_mean"] >= 0
 
 
-@pytest.mark.parametrize("world,mode", [(4, 1 | 0x100), (3, 0), (4, 2)])
+@pytest.mark.parametrize("world,mode", [(4, 1 | 0x100), (3, 0), (4, 2), (4, 1 | 0x400), (3, 0x400)])
 def test_cpp_exchange_timing_loopback(gpu, world, mode):
     """OMR_ROUND_TIME_EXCHANGE: the timed round's result is unchanged, omr_ar_plan_exchange_time reports a
     duration and the exchange's bytes: out = this rank's sent blocks, and what the ranks send is what they
@@ -384,8 +393,8 @@ def test_cpp_exchange_timing_loopback(gpu, world, mode):
             sent = ctypes.c_uint64()
             assert D.omr_sparse_round_f32(plan, x.data_ptr(), out.data_ptr(), None, None, None, mode | 0x200,
                                           ctypes.byref(sent), None, st.cuda_stream) == 0, D.omr_dist_last_error()
+            assert D.omr_ar_plan_join(plan, st.cuda_stream) == 0  # (a deferred round's exchange is issued here)
             assert D.omr_ar_plan_exchange_time(plan, ctypes.byref(ms), ctypes.byref(bo), ctypes.byref(bi)) == 0
-            assert D.omr_ar_plan_join(plan, st.cuda_stream) == 0
             st.synchronize()
             res[r] = (ms.value, bo.value, bi.value, sent.value, out.cpu().numpy())
             D.omr_ar_plan_destroy(plan)
@@ -409,7 +418,7 @@ def test_cpp_exchange_timing_loopback(gpu, world, mode):
             shard = (bounds[r + 1] - bounds[r]) * L.num_lanes * B * 4
             assert bo == bi == (world - 1) * shard
         else:
-            assert bo == sent * B * 4
+            assert bo == sent * B * 4 or (mode & 0x400)  # deferred: the call reports the previous round (none)
         full = bufs[r].copy()
         if (mode & 3) != 2:
             oracle.block_sum(bufs, L.n, B, L.num_lanes, 8, uf, full)
