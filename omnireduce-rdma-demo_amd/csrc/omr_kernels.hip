@@ -202,7 +202,8 @@ __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
 // wait for a load never includes a younger, data-dependent store (tools/tune_fused.py: 2-4 % faster than
 // branching around the stores; write-through sc0 sc1 beat plain, sc1-only and nt stores).
 // ABL (timing-only builds, csrc/tune/): bit 0 drops the data stores, bit 1 the flag/next stores.  MINW: the
-// amdgpu_waves_per_eu floor (occupancy study; 1 = the compiler's choice).
+// amdgpu_waves_per_eu floor (occupancy study; 1 = the compiler's choice).  SAUX: the block stores' cache policy
+// (store-policy study; the product's is kStoreAux).
 struct FusedArgs {
   const float* x;
   float* out;
@@ -216,7 +217,7 @@ struct FusedArgs {
 
 constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
 
-template <int VEC, int WAVES, int LOADS = 16, int ABL = 0, int MINW = 1>
+template <int VEC, int WAVES, int LOADS = 16, int ABL = 0, int MINW = 1, int SAUX = kStoreAux>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW))) void k_scan1f(FusedArgs a) {
   constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
   static_assert(RB >= 1 && RB <= 32, "batch bits are 32-bit");
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
 #pragma unroll
       for (int q = 0; q < VEC; ++q)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])), dst,
-                                               (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, kStoreAux);
+                                               (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, SAUX);
     }
     if (!(ABL & 2) && static_cast<uint32_t>(lane) < nrow) {
       const uint64_t blk = blk0 + static_cast<uint64_t>(lane) * a.lanes;

@@ -325,10 +325,10 @@ void go_p(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
 }  // namespace
 
 namespace {
-template <int VEC, int W, int LOADS, int ABL, int MINW = 1>
+template <int VEC, int W, int LOADS, int ABL, int MINW = 1, int SAUX = kStoreAux>
 void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(L.parts) * L.lanes * f.K);
-  k_scan1f<VEC, W, LOADS, ABL, MINW><<<grid, 64 * W, 0, st>>>(a);
+  k_scan1f<VEC, W, LOADS, ABL, MINW, SAUX><<<grid, 64 * W, 0, st>>>(a);
 }
 
 struct Variant {
@@ -343,6 +343,7 @@ struct Variant {
 #define VO(W, LD, A, O) go_f<1, W, LD, A, O>, go_f<4, W, LD, A, O>
 #define VR(W) go_r<1, W, 16, 0>, go_r<4, W, 16, 0>
 #define VP(W, LD, A) go_p<1, W, LD, A>, go_p<4, W, LD, A>
+#define VA(SA) go_f<1, 16, 16, 0, 1, SA>, go_f<4, 16, 16, 0, 1, SA>
 const Variant kVariants[] = {
     {"pipe w16 L8", true, VP(16, 8, 0)},
     {"pipe w8 L16", true, VP(8, 16, 0)},
@@ -355,6 +356,11 @@ const Variant kVariants[] = {
     {"w16 L16 -data", false, VF(16, 16, 1)},
     {"w16 L16 -meta", false, VF(16, 16, 2)},
     {"w16 L16 -data-meta", false, VF(16, 16, 3)},
+    {"w16 L16 st plain", true, VA(0)},
+    {"w16 L16 st sc0", true, VA(1)},
+    {"w16 L16 st sc1", true, VA(16)},
+    {"w16 L16 st nt", true, VA(2)},
+    {"w16 L16 st sc0sc1nt", true, VA(19)},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 }  // namespace
