@@ -19,6 +19,8 @@ def _ensure_built():
     have_hipcc = shutil.which("hipcc") or os.path.exists("/opt/rocm/bin/hipcc")
     if have_hipcc and not os.path.exists(os.path.join(PKG, "omr", "libomr.so")):
         subprocess.run(["make", "-C", PKG, "-s"], check=True)
+    if have_hipcc and not os.path.exists(os.path.join(PKG, "bin", "omr_client")):
+        subprocess.run(["make", "-C", PKG, "-s", "host"], check=True)  # ./omr_client, ./omr_server
 
 
 def pytest_configure(config):
