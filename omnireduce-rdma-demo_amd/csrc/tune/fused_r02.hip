@@ -1,0 +1,384 @@
+// fused_r02.hip — tuning harness (not the product), round 2: the decoupled-store single-pass kernel k_scan1d
+// (stores issued after the next batch's loads) against the product k_scan1f, with timing-only ablations (ABL bit 0:
+// no data stores, bit 1: no flag/next stores) and the pure read of the same geometry.  Timed side by side, in
+// place, by tools/tune_r02.py.
+#define OMR_NO_CAPI
+#include "../omr_kernels.hip"
+
+namespace {
+// k_scan1d — k_scan1f with decoupled stores (study; slower on MI355X: profiles/r02/tune_r02_*.log).
+//
+// Same work split, outputs and next-offset resolution as k_scan1f; only the ORDER of the memory operations differs.
+// On gfx9 a wave's vmcnt counts loads and stores together and retires them in issue order, so in k_scan1f the wait
+// for batch i+1's first load also waits for batch i's stores (data and flag/next) to be acknowledged — and a
+// write-through store queued behind a saturating read stream is acknowledged late (the memory side favours reads).
+// Here the blocks a batch must write (non-zero blocks and lane heads) are copied into P spare register slots, the
+// NEXT batch's loads are issued, and only then are the batch's stores issued: the next wait covers the loads alone.
+// A batch with more than P blocks to write stores the extra ones before the next loads (k_scan1f's behaviour, for
+// those batches only).  Every store slot is issued every batch (unused slots and masked lanes are pointed past their
+// descriptor's range and dropped), so the number of memory operations after each batch's loads is static and the
+// compiler's vmcnt for a load never includes a younger store.
+template <int VEC, int WAVES, int LOADS = 16, int P = 4, bool MASKS = false, int ABL = 0>
+__global__ __launch_bounds__(64 * WAVES) void k_scan1d(FusedArgs a) {
+  constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
+  static_assert(RB >= 1 && RB <= 32, "batch bits are 32-bit");
+  static_assert(P >= 1 && P <= RB, "spare slots");
+  __shared__ uint32_t s_wfirst[WAVES], s_wlast[WAVES];
+  __shared__ int s_fix;
+  __shared__ uint32_t s_carry[64];
+  __shared__ uint32_t s_seg_last[64];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t k = lin % a.K, col = lin / a.K;
+  const uint32_t l = col % a.lanes, p = col / a.lanes;
+  const uint32_t r0 = k * a.S;                                  // segment's first row within the partition
+  const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;  // its global row
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  const uint32_t lane_b = l * a.block;
+  const uint32_t row_stride = a.lanes * a.block;
+  const uint32_t meta_stride = a.lanes * 4;  // bytes between one column's consecutive flag / next entries
+  const bool last_seg = (k + 1 == a.K);
+  const uint32_t rw = ((a.S + WAVES * RB - 1) / (WAVES * RB)) * RB;
+  const uint32_t lo = wave * rw < a.S ? wave * rw : a.S;
+  const uint32_t hi = lo + rw < a.S ? lo + rw : a.S;
+  const uint32_t nbt = (hi - lo + RB - 1) / RB;
+  const uint32_t lane16 = static_cast<uint32_t>(lane) * 16u;
+  const bool data_out = a.out != nullptr && !(ABL & 1);
+  uint32_t carry = kNone, wlast = kNone;
+
+  v4f v[RB][VEC];
+  auto load_batch = [&](uint32_t nb_) {
+    const uint32_t rr = lo + (nb_ - 1) * RB;
+    const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
+    const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + ((row0 + rr) * a.lanes + l) * a.block, nrow * row_bytes);
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        v[s][q] = __builtin_bit_cast(
+            v4f, __builtin_amdgcn_raw_buffer_load_b128(src, s * row_bytes + q * 1024 + lane16, 0, kLoadAux));
+  };
+
+  // the previous batch's stores, issued after the next batch's loads
+  v4f sp[P][VEC];
+  uint32_t sp_row[P];  // wave-uniform: row of slot j within its batch, kNone = slot unused
+  __amdgpu_buffer_rsrc_t p_dst = chunk_rsrc(a.out, 0u);
+  __amdgpu_buffer_rsrc_t p_flags = __builtin_amdgcn_make_buffer_rsrc(a.flags, 0, 0, 0x00020000);
+  __amdgpu_buffer_rsrc_t p_next = __builtin_amdgcn_make_buffer_rsrc(a.next, 0, 0, 0x00020000);
+  uint32_t p_flag_off = kDropStore, p_next_off = kDropStore, p_flag = 0, p_next_val = 0;
+  uint64_t p_mask_row = 0;
+  bool p_mask = false;
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    sp_row[j] = kNone;
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) sp[j][q] = v4f{0.f, 0.f, 0.f, 0.f};  // defined data: the prologue's stores stay
+  }
+  auto issue_stores = [&]() {
+    if constexpr (MASKS) {
+      if (p_mask) (void)__hip_atomic_fetch_or(&a.masks[p_mask_row], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_raw_buffer_store_b32(p_flag, p_flags, p_flag_off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(p_next_val, p_next, p_next_off, 0, 0);
+#pragma unroll
+    for (int j = 0; j < P; ++j)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(v4u, sp[j][q]), p_dst,
+            (sp_row[j] != kNone ? sp_row[j] * row_bytes : kDropStore + j * VEC * 1024) + q * 1024 + lane16, 0,
+            kStoreAux);
+  };
+
+  if (nbt > 0) load_batch(nbt);
+  issue_stores();  // every slot dropped: the same operation count follows every batch's loads
+  for (uint32_t nb_ = nbt; nb_ > 0; --nb_) {
+    const uint32_t rr = lo + (nb_ - 1) * RB;
+    const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
+    const uint64_t blk0 = (row0 + rr) * a.lanes + l;  // block of the batch's first row
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
+      bits |= static_cast<uint32_t>(wave_ballot(o != 0) != 0 && static_cast<uint32_t>(s) < nrow) << s;
+    }
+    // blocks to write: non-zero ones and the lane head (row 0 of the partition, always sent: client.cc:201-205);
+    // aggregated block 0.0f + x (server.cc:148-150 zero, :97-98 add), in place (client.cc:89)
+    const uint32_t need = bits | ((r0 + rr) == 0 ? 1u : 0u);
+    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + blk0 * a.block, data_out ? nrow * row_bytes : 0u);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < P; ++j) sp_row[j] = kNone;
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+      if ((need >> s) & 1u) {
+        if (cnt < static_cast<uint32_t>(P)) {
+#pragma unroll
+          for (int j = 0; j < P; ++j)
+            if (cnt == static_cast<uint32_t>(j)) {
+#pragma unroll
+              for (int q = 0; q < VEC; ++q) sp[j][q] = add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q]);
+              sp_row[j] = static_cast<uint32_t>(s);
+            }
+          ++cnt;
+        } else {  // more blocks than spare slots: stored before the next loads
+#pragma unroll
+          for (int q = 0; q < VEC; ++q)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
+                                                   dst, s * row_bytes + q * 1024 + lane16, 0, kStoreAux);
+        }
+      }
+    }
+    // flag and next offset of row rr+lane: successor = next set bit above it in this batch, else the carry
+    // (client.cc:19-31)
+    const bool mine = static_cast<uint32_t>(lane) < nrow && !(ABL & 2);
+    const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
+    const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : carry;
+    p_flag = (bits >> lane) & 1u;
+    p_flag_off = (mine && a.flags != nullptr) ? static_cast<uint32_t>(lane) * meta_stride : kDropStore;
+    p_next_val = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+    p_next_off = (mine && nr != kNone) ? static_cast<uint32_t>(lane) * meta_stride : kDropStore;
+    p_flags = __builtin_amdgcn_make_buffer_rsrc(a.flags + blk0, 0, a.flags != nullptr ? static_cast<int>(nrow * meta_stride) : 0,
+                                                0x00020000);
+    p_next = __builtin_amdgcn_make_buffer_rsrc(a.next + blk0, 0, static_cast<int>(nrow * meta_stride), 0x00020000);
+    p_dst = dst;
+    if constexpr (MASKS) {
+      p_mask = mine && ((bits >> lane) & 1u);
+      p_mask_row = row0 + rr + lane;
+    }
+    if (bits != 0) {
+      if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
+      carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
+    }
+    if (nb_ > 1) load_batch(nb_ - 1);
+    issue_stores();
+  }
+  if (lane == 0) {
+    s_wfirst[wave] = carry;  // first non-zero row of the wave's range (kNone: all zero)
+    s_wlast[wave] = wlast;   // last one
+  }
+  __syncthreads();
+  // tail rows [wlast or lo, hi): successor = first non-zero row of a later wave, else of a later segment
+  uint32_t succ = kNone;
+  for (uint32_t w2 = wave + 1; w2 < WAVES; ++w2)
+    if (s_wfirst[w2] != kNone) {
+      succ = s_wfirst[w2];
+      break;
+    }
+  if (!(ABL & 2) && (succ != kNone || last_seg)) {
+    const uint32_t val = succ != kNone ? static_cast<uint32_t>(row0 + succ) * row_stride + lane_b : a.sentinel + lane_b;
+    for (uint32_t i = (wlast == kNone ? lo : wlast) + lane; i < hi; i += 64) a.next[(row0 + i) * a.lanes + l] = val;
+  }
+  if (a.K == 1) return;
+  // multi-segment column: publish {first, last}, count arrivals; the last arriver fixes every tail row
+  if (threadIdx.x == 0) {
+    uint32_t first = kNone, last = 0;
+    for (int w2 = 0; w2 < WAVES; ++w2) {
+      if (first == kNone) first = s_wfirst[w2];
+      if (s_wlast[w2] != kNone) last = s_wlast[w2];
+    }
+    const uint64_t sm = (static_cast<uint64_t>(first) << 32) | (first == kNone ? kNone : last);
+    (void)__hip_atomic_exchange(&a.summary[static_cast<uint64_t>(col) * a.K + k], sm, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&a.cnt[col], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_fix = (old == a.K - 1);
+  }
+  __syncthreads();
+  if (!s_fix) return;
+  if (threadIdx.x < a.K) {  // read every segment's summary at the coherence point (atomic RMW), K <= 64
+    const uint64_t sm = __hip_atomic_fetch_or(&a.summary[static_cast<uint64_t>(col) * a.K + threadIdx.x], 0ull,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_carry[threadIdx.x] = static_cast<uint32_t>(sm >> 32);  // first (temporarily)
+    s_seg_last[threadIdx.x] = static_cast<uint32_t>(sm);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // carry[k'] = first non-zero row (partition-relative) in segments after k'
+    uint32_t c = kNone;
+    for (int kk = static_cast<int>(a.K) - 1; kk >= 0; --kk) {
+      const uint32_t first = s_carry[kk];
+      s_carry[kk] = c;
+      if (first != kNone) c = static_cast<uint32_t>(kk) * a.S + first;
+    }
+    __hip_atomic_store(&a.cnt[col], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+  }
+  __syncthreads();
+  const uint64_t part_row0 = static_cast<uint64_t>(p) * a.rpp;
+  const uint32_t tail_total = (a.K - 1) * a.S;
+  for (uint32_t t = threadIdx.x; t < tail_total; t += blockDim.x) {
+    const uint32_t kk = t / a.S, i = t % a.S;
+    const uint32_t last = s_seg_last[kk];  // kNone when the segment is all zero
+    if (last != kNone && i < last) continue;  // a later non-zero row of its own segment follows: done locally
+    const uint32_t c = s_carry[kk];
+    const uint32_t val = (c != kNone) ? static_cast<uint32_t>(part_row0 + c) * row_stride + lane_b
+                                      : a.sentinel + lane_b;
+    a.next[(part_row0 + static_cast<uint64_t>(kk) * a.S + i) * a.lanes + l] = val;
+  }
+}
+
+// Pure read with k_scan1f's geometry and workgroup -> column mapping: the floor of the fused kernel's read stream.
+template <int VEC, int W>
+__global__ __launch_bounds__(64 * W) void k_read_geom2(FusedArgs a) {
+  constexpr int RB = 16 / VEC;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t k = lin % a.K, col = lin / a.K;
+  const uint32_t l = col % a.lanes, p = col / a.lanes;
+  const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + k * a.S;
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  const uint32_t rw = ((a.S + W * RB - 1) / (W * RB)) * RB;
+  const uint32_t lo = wave * rw < a.S ? wave * rw : a.S;
+  const uint32_t hi = lo + rw < a.S ? lo + rw : a.S;
+  uint32_t acc = 0;
+  for (uint32_t nb_ = (hi - lo + RB - 1) / RB; nb_ > 0; --nb_) {
+    const uint32_t rr = lo + (nb_ - 1) * RB;
+    const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
+    const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+    const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, nrow * row_bytes);
+    v4f v[RB][VEC];
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                              src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc |= nz_bits(v[s][q]);
+  }
+  if (acc == 0x12345678u) a.next[0] = acc;  // never true for the generator's data; keeps the loads
+}
+
+// Mixed read/write ceiling probes (timing only): what the HBM gives for the kernel's byte mix without any of its
+// logic.  Every probe is one grid-stride kernel of 256-thread workgroups, 16 one-KiB pieces in flight per wave.
+//   MODE 0  write only: the blocks whose flag is set (the kernel's scattered 1 KiB writes), nothing read but flags
+//   MODE 1  write only: the same number of 1 KiB blocks, packed into the first tenth of the buffer (contiguous)
+//   MODE 2  read everything + write the flagged blocks (flat address order: the cheapest schedule of the same bytes)
+//   MODE 3  read everything, write nothing (flat address order)
+template <int MODE, int SAUX = kStoreAux>
+__global__ __launch_bounds__(256) void k_mix_probe(FusedArgs a, uint64_t nb) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * 4;
+  const uint64_t w0 = static_cast<uint64_t>(blockIdx.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const v4f val = v4f{0.01f, 0.01f, 0.01f, 0.01f};
+  for (uint64_t c = w0; c * 16 < nb; c += nw) {  // chunk c = blocks [16c, 16c + 16)
+    const uint64_t b0 = c * 16;
+    uint32_t fl = 0;
+    if (lane < 16) fl = a.flags[b0 + lane] != 0 ? 1u : 0u;
+    const uint32_t fbits = static_cast<uint32_t>(__ballot(fl != 0));
+    if constexpr (MODE >= 2) {
+      const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + b0 * 256, 16 * 1024);
+      v4f v[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+        v[s] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, s * 1024 + lane * 16, 0, kLoadAux));
+      uint32_t acc = 0;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc |= nz_bits(v[s]);
+      if constexpr (MODE == 2) {
+        const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + b0 * 256, 16 * 1024);
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v[s]), dst,
+                                                 (((fbits >> s) & 1u) ? 0u : kDropStore) + s * 1024 + lane * 16, 0,
+                                                 SAUX);
+      }
+      if (acc == 0x12345678u) a.next[0] = acc;  // keeps the loads
+    } else {
+      const uint64_t wb = MODE == 0 ? b0 : b0 / 10;  // MODE 1: flagged block b goes to block b / 10
+      const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + wb * 256, 16 * 1024);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const uint32_t off = MODE == 0 ? s * 1024 : static_cast<uint32_t>((b0 + s) / 10 - b0 / 10) * 1024;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, val), dst,
+                                               (((fbits >> s) & 1u) ? 0u : kDropStore) + off + lane * 16, 0,
+                                               kStoreAux);
+      }
+    }
+  }
+}
+
+using Launch = void (*)(const Layout&, const FusedShape&, FusedArgs, hipStream_t);
+
+unsigned grid_of(const Layout& L, const FusedShape& f) {
+  return static_cast<unsigned>(static_cast<uint64_t>(L.parts) * L.lanes * f.K);
+}
+template <int VEC, int W, int LD, int ABL>
+void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  k_scan1f<VEC, W, LD, ABL><<<grid_of(L, f), 64 * W, 0, st>>>(a);
+}
+template <int VEC, int W, int LD, int P, int ABL>
+void go_d(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  k_scan1d<VEC, W, LD, P, false, ABL><<<grid_of(L, f), 64 * W, 0, st>>>(a);
+}
+template <int VEC, int W>
+void go_r(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  k_read_geom2<VEC, W><<<grid_of(L, f), 64 * W, 0, st>>>(a);
+}
+template <int MODE, int SAUX = kStoreAux>
+void go_m(const Layout& L, const FusedShape&, FusedArgs a, hipStream_t st) {
+  if (L.block != 256) return;  // B = 256 probes only
+  k_mix_probe<MODE, SAUX><<<2048, 256, 0, st>>>(a, L.nb);
+}
+
+struct Variant {
+  const char* name;
+  bool checked;  // produces the full outputs (ablations do not)
+  Launch v1, v4;
+};
+const Variant kVariants[] = {
+    {"f w16 L16 (product)", true, go_f<1, 16, 16, 0>, go_f<4, 16, 16, 0>},
+    {"pure read", false, go_r<1, 16>, go_r<4, 16>},
+    {"d w16 L16 P4/P2", true, go_d<1, 16, 16, 4, 0>, go_d<4, 16, 16, 2, 0>},
+    {"d w16 L16 P2/P1", true, go_d<1, 16, 16, 2, 0>, go_d<4, 16, 16, 1, 0>},
+    {"d w16 L16 P4/P2 -data", false, go_d<1, 16, 16, 4, 1>, go_d<4, 16, 16, 2, 1>},
+    {"f w16 L16 -data-meta", false, go_f<1, 16, 16, 3>, go_f<4, 16, 16, 3>},
+    {"f w16 L16 -data", false, go_f<1, 16, 16, 1>, go_f<4, 16, 16, 1>},
+    {"f w16 L16 -meta", false, go_f<1, 16, 16, 2>, go_f<4, 16, 16, 2>},
+    {"probe write scattered flagged blocks", false, go_m<0>, go_m<0>},
+    {"probe write same count contiguous", false, go_m<1>, go_m<1>},
+    {"probe flat read + write flagged", false, go_m<2>, go_m<2>},
+    {"probe flat read", false, go_m<3>, go_m<3>},
+    {"probe flat read + write flagged, plain st", false, go_m<2, 0>, go_m<2, 0>},
+    {"probe flat read + write flagged, nt st", false, go_m<2, 2>, go_m<2, 2>},
+    {"probe flat read + write flagged, sc1 st", false, go_m<2, 16>, go_m<2, 16>},
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+}  // namespace
+
+extern "C" {
+uint32_t omr_sentinel(uint32_t block_size, uint32_t num_lanes) {  // the product's, compiled out by OMR_NO_CAPI
+  return (UINT32_MAX / block_size / num_lanes - 1u) * num_lanes * block_size;
+}
+int tune_count(void) { return kNumVariants; }
+const char* tune_name(int v) { return (v >= 0 && v < kNumVariants) ? kVariants[v].name : "?"; }
+int tune_checked(int v) { return (v >= 0 && v < kNumVariants) ? kVariants[v].checked : 0; }
+int tune_run(int v, const float* x, float* out, int32_t* flags, uint32_t* next, void* ws, uint64_t n, uint32_t B,
+             uint32_t K, void* stream) {
+  Layout L;
+  if (v < 0 || v >= kNumVariants) return -3;
+  if (make_layout(n, B, 16384 / B, 8, &L)) return -1;
+  FusedShape f;
+  f.K = K;
+  f.S = L.rows_per_part / K;
+  FusedArgs a{};
+  a.x = x; a.out = out; a.flags = flags; a.next = next;
+  const uint64_t cols = static_cast<uint64_t>(L.parts) * L.lanes;
+  a.cnt = static_cast<uint32_t*>(ws);
+  a.summary = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + ((cols * 4 + 15) / 16) * 16);
+  a.lanes = L.lanes; a.rpp = L.rows_per_part; a.K = f.K; a.S = f.S; a.block = L.block;
+  a.sentinel = omr_sentinel(L.block, L.lanes);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (L.vec == 4) kVariants[v].v4(L, f, a, st);
+  else if (L.vec == 1) kVariants[v].v1(L, f, a, st);
+  else return -2;
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+}
