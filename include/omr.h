@@ -125,6 +125,16 @@ int omr_scan_sum_fused_f32(const float* buf, uint64_t n, uint32_t block_size, ui
                            uint32_t num_parts, int32_t* flags, uint32_t* next_offsets, float* out, void* workspace,
                            size_t workspace_bytes, omr_stream_t stream);
 
+/* The single-pass worker step for ONE partition `part` (< num_parts) of the tensor: the per-thread seam of the
+ * reference, where worker thread `res->threadId` walks only its own DATA_SIZE_PER_THREAD slice (client.cc:22-29,
+ * :168-223; threads started at client.cc:384-392).  Writes flags / next_offsets / out for that partition's blocks
+ * only (global block indexing, global float offsets in next_offsets); other partitions are untouched.  Calls on
+ * different partitions may run concurrently on different streams and may share one workspace (each partition uses
+ * its own counters in it): omr_scan_workspace_bytes(n, ...) bytes, zero-filled once, left zeroed. */
+int omr_scan_partition_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                           uint32_t part, int32_t* flags, uint32_t* next_offsets, float* out, void* workspace,
+                           size_t workspace_bytes, omr_stream_t stream);
+
 /* The m = 1 fused scan + aggregate over rows [row_begin, row_end) only (a pipelined piece of the tensor, e.g.
  * the part that has landed from host memory); `buf`, `out`, `flags`, `row_masks` are whole-tensor arrays indexed
  * by global block/row.  Next offsets need every row: run omr_next_offsets once all pieces are scanned. */

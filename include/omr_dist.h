@@ -40,6 +40,16 @@ const char* omr_dist_last_error(void);
 int omr_dist_unique_id(void* id /* OMR_UNIQUE_ID_BYTES */);
 int omr_dist_create_rccl(const void* id, int rank, int world, omr_dist** out);
 
+/* Cross-process transport over HIP IPC: `world` ranks as separate processes of one node (any GPUs; several may
+ * share one, which RCCL refuses), the stand-in for the reference's separate worker and aggregator machines.  One
+ * rank calls omr_dist_ipc_unique_id and shares the id out of band (the ./omr_server rendezvous does); every rank
+ * then calls omr_dist_create_ipc, which returns once all have joined.  Data moves device to device (each receiver
+ * copies out of the sender's IPC-mapped buffer); ordering is carried on the device by IPC events, so calls return
+ * without synchronising any stream, as with RCCL.  Buffers handed to a round must stay allocated while the
+ * transport lives (their IPC mappings are cached).  Destroy is collective. */
+int omr_dist_ipc_unique_id(void* id /* OMR_UNIQUE_ID_BYTES */);
+int omr_dist_create_ipc(const void* id, int rank, int world, omr_dist** out);
+
 omr_local_board* omr_local_board_create(int world);
 void omr_local_board_destroy(omr_local_board* board);
 int omr_dist_create_local(omr_local_board* board, int rank, omr_dist** out);

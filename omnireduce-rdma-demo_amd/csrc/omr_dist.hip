@@ -6,13 +6,24 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <array>
+#include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -51,6 +62,7 @@ struct Slice {
   void* ptr;
   size_t bytes;
 };
+using Slices = std::vector<Slice>;  // several pieces to or from one peer, matched in order (zero-byte ones skipped)
 
 }  // namespace
 
@@ -61,8 +73,9 @@ struct omr_dist {
   virtual ~omr_dist() = default;
   // out[p*bytes .. (p+1)*bytes) = rank p's `in`; `in` may alias out + rank*bytes
   virtual int allgather(const void* in, void* out, size_t bytes, hipStream_t st) = 0;
-  // sends[p] to peer p, recvs[p] from peer p (sizes agree pairwise; zero = nothing), p != rank
-  virtual int exchange(const std::vector<Slice>& sends, const std::vector<Slice>& recvs, hipStream_t st) = 0;
+  // sends[p] to peer p, recvs[p] from peer p, p != rank: the k-th non-empty send piece to a peer pairs with that
+  // peer's k-th non-empty receive piece from this rank (equal sizes); every rank calls it, possibly with nothing
+  virtual int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) = 0;
   // out[0 .. count) = sum over ranks p of in_p[rank*count .. (rank+1)*count)  (dense stand-in)
   virtual int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) = 0;
 };
@@ -82,12 +95,14 @@ struct RcclDist final : omr_dist {
   int allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
     return nccl_check(ncclAllGather(in, out, bytes, ncclUint8, comm, st), "ncclAllGather");
   }
-  int exchange(const std::vector<Slice>& sends, const std::vector<Slice>& recvs, hipStream_t st) override {
+  int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
     TRY(nccl_check(ncclGroupStart(), "ncclGroupStart"));
     for (int p = 0; p < world; ++p) {
       if (p == rank) continue;
-      if (recvs[p].bytes) TRY(nccl_check(ncclRecv(recvs[p].ptr, recvs[p].bytes, ncclUint8, p, xcomm, st), "ncclRecv"));
-      if (sends[p].bytes) TRY(nccl_check(ncclSend(sends[p].ptr, sends[p].bytes, ncclUint8, p, xcomm, st), "ncclSend"));
+      for (const Slice& r : recvs[p])
+        if (r.bytes) TRY(nccl_check(ncclRecv(r.ptr, r.bytes, ncclUint8, p, xcomm, st), "ncclRecv"));
+      for (const Slice& t : sends[p])
+        if (t.bytes) TRY(nccl_check(ncclSend(t.ptr, t.bytes, ncclUint8, p, xcomm, st), "ncclSend"));
     }
     return nccl_check(ncclGroupEnd(), "ncclGroupEnd");
   }
@@ -104,9 +119,9 @@ struct omr_local_board {
   std::condition_variable cv;
   int arrived = 0;
   uint64_t generation = 0;
-  std::vector<const void*> posted;               // allgather inputs
-  std::vector<std::vector<Slice>> posted_sends;  // [rank][peer]
-  explicit omr_local_board(int w) : world(w), posted(w), posted_sends(w, std::vector<Slice>(w, Slice{nullptr, 0})) {}
+  std::vector<const void*> posted;                // allgather inputs
+  std::vector<std::vector<Slices>> posted_sends;  // [rank][peer]
+  explicit omr_local_board(int w) : world(w), posted(w), posted_sends(w, std::vector<Slices>(w)) {}
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
     const uint64_t gen = generation;
@@ -137,20 +152,30 @@ struct LocalDist final : omr_dist {
     b->barrier();
     return 0;
   }
-  int exchange(const std::vector<Slice>& sends, const std::vector<Slice>& recvs, hipStream_t st) override {
+  int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
     TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
     b->posted_sends[rank] = sends;
     b->barrier();
-    for (int p = 0; p < world; ++p) {
-      if (p == rank || recvs[p].bytes == 0) continue;
-      const Slice& s = b->posted_sends[p][rank];
-      if (s.bytes != recvs[p].bytes)
-        return derr(OMR_EINVAL, "local exchange: rank %d expects %zu bytes from %d, peer posted %zu", rank,
-                    recvs[p].bytes, p, s.bytes);
-      TRY(hip_check(hipMemcpy(recvs[p].ptr, s.ptr, s.bytes, hipMemcpyDefault), "hipMemcpy"));
+    int rc = 0;
+    for (int p = 0; p < world && rc == 0; ++p) {
+      if (p == rank) continue;
+      const Slices& from = b->posted_sends[p][rank];
+      size_t k = 0;
+      for (const Slice& r : recvs[p]) {
+        if (r.bytes == 0) continue;
+        while (k < from.size() && from[k].bytes == 0) ++k;
+        if (k == from.size() || from[k].bytes != r.bytes) {
+          rc = derr(OMR_EINVAL, "local exchange: rank %d expects %zu bytes from %d, peer posted %zu", rank, r.bytes, p,
+                    k < from.size() ? from[k].bytes : size_t{0});
+          break;
+        }
+        rc = hip_check(hipMemcpy(r.ptr, from[k].ptr, r.bytes, hipMemcpyDefault), "hipMemcpy");
+        if (rc) break;
+        ++k;
+      }
     }
-    b->barrier();
-    return 0;
+    b->barrier();  // every rank leaves together, even on an error (no peer is left waiting)
+    return rc;
   }
   int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
     // every rank's input is addressable here (threads of one process): sum the shard in rank order
@@ -164,6 +189,329 @@ struct LocalDist final : omr_dist {
     TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));  // peers' inputs read before anyone moves on
     b->barrier();
     return 0;
+  }
+};
+
+// ---------------------------------------------------------------- cross-process transport (HIP IPC)
+//
+// Ranks are separate processes on one node, any GPUs (several may share one), the stand-in for the reference's
+// separate worker / aggregator machines (README.md:13-22) where RCCL cannot run (two ranks on one GPU).  A
+// /dev/shm board holds, per rank: its IPC event handles, and per operation the IPC memory handles + offsets of what
+// it offers.  Data moves device-to-device: each receiver pulls from the sender's buffer (mapped once with
+// hipIpcOpenMemHandle) on its own stream.  Ordering is on the device, as with RCCL: the sender records a "ready"
+// IPC event behind the producing work, the receiver's stream waits on it before copying, then records "done", and
+// every rank's stream waits for all peers' "done" before it runs on (so a sender does not overwrite a buffer a peer
+// is still reading).  The hosts only exchange sequence numbers (no stream synchronisation).  Two channels, as
+// RcclDist's two communicators: 0 carries the all-gather, 1 the exchange and the dense reduce-scatter; every rank
+// issues each channel's operations in the same order.
+constexpr uint32_t kIpcMagic = 0x4f4d5249;  // "OMRI"
+constexpr int kIpcChans = 2, kIpcRing = 2, kIpcMaxRanks = 2 * OMR_MAX_WORKERS, kIpcMaxHandles = 32;
+constexpr int kIpcMaxEntries = 4096;
+constexpr uint32_t kIpcAll = 0xFFFFFFFFu;  // an entry every peer reads (all-gather / reduce-scatter input)
+
+struct IpcEntry {
+  uint32_t peer, hidx;  // destination rank (kIpcAll: everyone), index into the post's handle table
+  uint64_t off, bytes;  // piece = allocation(hidx) + off, bytes
+};
+struct IpcPost {
+  uint32_t nent, nh;
+  hipIpcMemHandle_t h[kIpcMaxHandles];
+  IpcEntry e[kIpcMaxEntries];
+};
+struct IpcRank {
+  std::atomic<uint64_t> posted[kIpcChans], done[kIpcChans];
+  std::atomic<uint32_t> joined, left;
+  hipIpcEventHandle_t ready[kIpcChans][kIpcRing], rdone[kIpcChans][kIpcRing];
+};
+struct IpcBoard {
+  std::atomic<uint32_t> magic;
+  uint32_t world;
+  std::atomic<uint32_t> attached;
+  IpcRank rank[kIpcMaxRanks];
+  IpcPost post[kIpcChans][kIpcRing][kIpcMaxRanks];
+};
+
+std::string ipc_board_name(const void* id) {
+  const unsigned char* c = static_cast<const unsigned char*>(id);
+  char buf[48] = "/omr_";
+  for (int i = 0; i < 12; ++i) snprintf(buf + 5 + 2 * i, 3, "%02x", c[i]);
+  return buf;
+}
+
+// bounded spin on a host condition (peers are other processes: yield the core)
+template <typename F>
+int ipc_spin(F ready, const char* what, int rank) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t i = 0;; ++i) {
+    if (ready()) return 0;
+    if ((i & 1023) == 1023) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+        return derr(OMR_EINVAL, "ipc transport: rank %d waited 120 s for %s", rank, what);
+      sched_yield();
+    }
+  }
+}
+
+struct IpcDist final : omr_dist {
+  IpcBoard* b = nullptr;
+  std::string name;
+  hipEvent_t ready[kIpcChans][kIpcRing] = {}, rdone[kIpcChans][kIpcRing] = {};
+  std::vector<std::array<hipEvent_t, kIpcChans * kIpcRing>> pready, prdone;  // peers' events, opened
+  uint64_t seq[kIpcChans] = {0, 0};
+  std::map<std::pair<uintptr_t, size_t>, hipIpcMemHandle_t> own;  // allocation (base, size) -> its handle
+  std::map<std::string, char*> opened;                               // peer handle bytes -> mapped base
+
+  ~IpcDist() override {
+    if (b != nullptr) {
+      // every rank's device work (copies out of its peers' buffers, waits on their events) ends before anyone
+      // closes a mapping or an event
+      (void)hipDeviceSynchronize();
+      b->rank[rank].left.store(1, std::memory_order_release);
+      for (int p = 0; p < world; ++p)
+        (void)ipc_spin([&] { return b->rank[p].left.load(std::memory_order_acquire) != 0; }, "peers to leave", rank);
+      for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
+      for (auto& v : pready)
+        for (hipEvent_t e : v)
+          if (e) (void)hipEventDestroy(e);
+      for (auto& v : prdone)
+        for (hipEvent_t e : v)
+          if (e) (void)hipEventDestroy(e);
+    }
+    for (int c = 0; c < kIpcChans; ++c)
+      for (int k = 0; k < kIpcRing; ++k) {
+        if (ready[c][k]) (void)hipEventDestroy(ready[c][k]);
+        if (rdone[c][k]) (void)hipEventDestroy(rdone[c][k]);
+      }
+    if (b != nullptr) {
+      const bool last = b->attached.fetch_sub(1) == 1;
+      munmap(b, sizeof(IpcBoard));
+      if (last) shm_unlink(name.c_str());
+    }
+  }
+
+  int attach(const void* id) {
+    name = ipc_board_name(id);
+    const size_t bytes = sizeof(IpcBoard);
+    int fd = -1;
+    if (rank == 0) {
+      shm_unlink(name.c_str());
+      fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd < 0 || ftruncate(fd, static_cast<off_t>(bytes)) != 0) {
+        if (fd >= 0) close(fd);
+        return derr(OMR_EINVAL, "ipc transport: cannot create %s: %s", name.c_str(), strerror(errno));
+      }
+    } else {
+      TRY(ipc_spin([&] {
+            if (fd < 0) fd = shm_open(name.c_str(), O_RDWR, 0600);
+            struct stat stt;
+            return fd >= 0 && fstat(fd, &stt) == 0 && static_cast<size_t>(stt.st_size) == bytes;
+          }, "the board", rank));
+    }
+    void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) return derr(OMR_EINVAL, "ipc transport: mmap %s: %s", name.c_str(), strerror(errno));
+    b = static_cast<IpcBoard*>(m);
+    if (rank == 0) {
+      b->world = static_cast<uint32_t>(world);  // the rest is zero (a fresh shm object)
+      b->magic.store(kIpcMagic, std::memory_order_release);
+    }
+    TRY(ipc_spin([&] { return b->magic.load(std::memory_order_acquire) == kIpcMagic; }, "the board's owner", rank));
+    if (b->world != static_cast<uint32_t>(world))
+      return derr(OMR_EINVAL, "ipc transport: board world %u, this rank says %d", b->world, world);
+    b->attached.fetch_add(1);
+    IpcRank& me = b->rank[rank];
+    for (int c = 0; c < kIpcChans; ++c)
+      for (int k = 0; k < kIpcRing; ++k) {
+        TRY(hip_check(hipEventCreateWithFlags(&ready[c][k], hipEventDisableTiming | hipEventInterprocess),
+                      "hipEventCreate"));
+        TRY(hip_check(hipEventCreateWithFlags(&rdone[c][k], hipEventDisableTiming | hipEventInterprocess),
+                      "hipEventCreate"));
+        TRY(hip_check(hipIpcGetEventHandle(&me.ready[c][k], ready[c][k]), "hipIpcGetEventHandle"));
+        TRY(hip_check(hipIpcGetEventHandle(&me.rdone[c][k], rdone[c][k]), "hipIpcGetEventHandle"));
+      }
+    me.joined.store(1, std::memory_order_release);
+    pready.assign(world, {});
+    prdone.assign(world, {});
+    for (int p = 0; p < world; ++p) {
+      TRY(ipc_spin([&] { return b->rank[p].joined.load(std::memory_order_acquire) != 0; }, "peers to join", rank));
+      if (p == rank) continue;
+      for (int c = 0; c < kIpcChans; ++c)
+        for (int k = 0; k < kIpcRing; ++k) {
+          TRY(hip_check(hipIpcOpenEventHandle(&pready[p][c * kIpcRing + k], b->rank[p].ready[c][k]),
+                        "hipIpcOpenEventHandle"));
+          TRY(hip_check(hipIpcOpenEventHandle(&prdone[p][c * kIpcRing + k], b->rank[p].rdone[c][k]),
+                        "hipIpcOpenEventHandle"));
+        }
+    }
+    return 0;
+  }
+
+  // the IPC handle of the allocation holding `ptr`, and ptr's offset in it
+  int handle_of(const void* ptr, hipIpcMemHandle_t* h, uint64_t* off) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    TRY(hip_check(hipMemGetAddressRange(&base, &size, const_cast<void*>(ptr)), "hipMemGetAddressRange"));
+    const auto key = std::make_pair(reinterpret_cast<uintptr_t>(base), size);
+    auto it = own.find(key);
+    if (it == own.end()) {
+      hipIpcMemHandle_t nh;
+      TRY(hip_check(hipIpcGetMemHandle(&nh, base), "hipIpcGetMemHandle"));
+      it = own.emplace(key, nh).first;
+    }
+    *h = it->second;
+    *off = static_cast<uint64_t>(static_cast<const char*>(ptr) - static_cast<const char*>(base));
+    return 0;
+  }
+
+  int map(const IpcPost& post, const IpcEntry& e, char** out) {
+    if (e.hidx >= post.nh) return derr(OMR_EINVAL, "ipc transport: bad handle index");
+    const hipIpcMemHandle_t& h = post.h[e.hidx];
+    std::string key(reinterpret_cast<const char*>(&h), sizeof(h));
+    auto it = opened.find(key);
+    if (it == opened.end()) {
+      void* p = nullptr;
+      TRY(hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle"));
+      it = opened.emplace(key, static_cast<char*>(p)).first;
+    }
+    *out = it->second + e.off;
+    return 0;
+  }
+
+  // post the pieces this rank offers for operation `s` of channel c, behind everything queued on st; then wait for
+  // every peer to post the same operation
+  int begin(int c, hipStream_t st, const std::vector<std::pair<uint32_t, Slice>>& items, uint64_t* s_out) {
+    const uint64_t s = ++seq[c];
+    const int k = static_cast<int>(s % kIpcRing);
+    IpcPost& P = b->post[c][k][rank];
+    P.nent = P.nh = 0;
+    for (const auto& it : items) {
+      if (it.second.bytes == 0) continue;
+      if (P.nent == kIpcMaxEntries) return derr(OMR_EINVAL, "ipc transport: more than %d pieces", kIpcMaxEntries);
+      hipIpcMemHandle_t h;
+      uint64_t off = 0;
+      TRY(handle_of(it.second.ptr, &h, &off));
+      uint32_t hi = 0;
+      while (hi < P.nh && memcmp(&P.h[hi], &h, sizeof(h)) != 0) ++hi;
+      if (hi == P.nh) {
+        if (P.nh == kIpcMaxHandles) return derr(OMR_EINVAL, "ipc transport: more than %d buffers", kIpcMaxHandles);
+        P.h[P.nh++] = h;
+      }
+      P.e[P.nent++] = IpcEntry{it.first, hi, off, it.second.bytes};
+    }
+    TRY(hip_check(hipEventRecord(ready[c][k], st), "hipEventRecord"));
+    b->rank[rank].posted[c].store(s, std::memory_order_release);
+    for (int p = 0; p < world; ++p)
+      TRY(ipc_spin([&] { return b->rank[p].posted[c].load(std::memory_order_acquire) >= s; }, "a peer's post",
+                   rank));
+    *s_out = s;
+    return 0;
+  }
+  // st waits until peer p's offered pieces are ready on the device
+  int wait_ready(int c, uint64_t s, int p, hipStream_t st) {
+    return hip_check(hipStreamWaitEvent(st, pready[p][c * kIpcRing + s % kIpcRing], 0), "hipStreamWaitEvent");
+  }
+  // this rank is through reading its peers; st then waits until every peer is through reading this rank
+  int end(int c, uint64_t s, hipStream_t st) {
+    const int k = static_cast<int>(s % kIpcRing);
+    TRY(hip_check(hipEventRecord(rdone[c][k], st), "hipEventRecord"));
+    b->rank[rank].done[c].store(s, std::memory_order_release);
+    for (int p = 0; p < world; ++p) {
+      if (p == rank) continue;
+      TRY(ipc_spin([&] { return b->rank[p].done[c].load(std::memory_order_acquire) >= s; }, "a peer's copies",
+                   rank));
+      TRY(hip_check(hipStreamWaitEvent(st, prdone[p][c * kIpcRing + k], 0), "hipStreamWaitEvent"));
+    }
+    return 0;
+  }
+  const IpcPost& post_of(int c, uint64_t s, int p) const { return b->post[c][s % kIpcRing][p]; }
+
+  int allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
+    uint64_t s = 0;
+    TRY(begin(0, st, {{kIpcAll, Slice{const_cast<void*>(in), bytes}}}, &s));
+    int rc = 0;
+    for (int p = 0; p < world && rc == 0; ++p) {
+      char* dst = static_cast<char*>(out) + static_cast<size_t>(p) * bytes;
+      if (p == rank) {
+        if (dst != in) rc = hip_check(hipMemcpyAsync(dst, in, bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+        continue;
+      }
+      const IpcPost& P = post_of(0, s, p);
+      char* src = nullptr;
+      if (bytes == 0) continue;
+      if (P.nent != 1 || P.e[0].bytes != bytes) {
+        rc = derr(OMR_EINVAL, "ipc allgather: rank %d offered %u pieces", p, P.nent);
+        break;
+      }
+      rc = map(P, P.e[0], &src);
+      if (rc == 0) rc = wait_ready(0, s, p, st);
+      if (rc == 0) rc = hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+    }
+    const int rc2 = end(0, s, st);  // always: peers wait for it
+    return rc ? rc : rc2;
+  }
+
+  int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
+    std::vector<std::pair<uint32_t, Slice>> items;
+    for (int p = 0; p < world; ++p)
+      if (p != rank)
+        for (const Slice& t : sends[p]) items.push_back({static_cast<uint32_t>(p), t});
+    uint64_t s = 0;
+    TRY(begin(1, st, items, &s));
+    int rc = 0;
+    for (int p = 0; p < world && rc == 0; ++p) {
+      if (p == rank) continue;
+      const IpcPost& P = post_of(1, s, p);
+      uint32_t k = 0;
+      bool waited = false;
+      for (const Slice& r : recvs[p]) {
+        if (r.bytes == 0) continue;
+        while (k < P.nent && P.e[k].peer != static_cast<uint32_t>(rank)) ++k;
+        if (k == P.nent || P.e[k].bytes != r.bytes) {
+          rc = derr(OMR_EINVAL, "ipc exchange: rank %d expects %zu bytes from %d, peer offered %llu", rank, r.bytes,
+                    p, k < P.nent ? static_cast<unsigned long long>(P.e[k].bytes) : 0ull);
+          break;
+        }
+        char* src = nullptr;
+        rc = map(P, P.e[k], &src);
+        if (rc == 0 && !waited) {
+          rc = wait_ready(1, s, p, st);
+          waited = true;
+        }
+        if (rc == 0) rc = hip_check(hipMemcpyAsync(r.ptr, src, r.bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+        if (rc) break;
+        ++k;
+      }
+    }
+    const int rc2 = end(1, s, st);
+    return rc ? rc : rc2;
+  }
+
+  int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
+    uint64_t s = 0;
+    TRY(begin(1, st, {{kIpcAll, Slice{const_cast<float*>(in), count * world * sizeof(float)}}}, &s));
+    std::vector<const float*> ptrs(world);
+    int rc = 0;
+    for (int p = 0; p < world && rc == 0; ++p) {
+      if (p == rank) {
+        ptrs[p] = in + static_cast<size_t>(rank) * count;
+        continue;
+      }
+      const IpcPost& P = post_of(1, s, p);
+      char* src = nullptr;
+      if (P.nent != 1) {
+        rc = derr(OMR_EINVAL, "ipc reduce_scatter: rank %d offered %u pieces", p, P.nent);
+        break;
+      }
+      rc = map(P, P.e[0], &src);
+      if (rc == 0) rc = wait_ready(1, s, p, st);
+      ptrs[p] = reinterpret_cast<const float*>(src) + static_cast<size_t>(rank) * count;
+    }
+    // the shard of every rank's input summed in rank order (the loopback stand-in's order, server.cc:97-98)
+    if (rc == 0)
+      rc = omr_check(omr_dense_sum_f32(ptrs.data(), static_cast<uint32_t>(world), count, out,
+                                       reinterpret_cast<omr_stream_t>(st)), "omr_dense_sum_f32");
+    const int rc2 = end(1, s, st);
+    return rc ? rc : rc2;
   }
 };
 
@@ -271,6 +619,37 @@ int omr_dist_create_rccl(const void* id, int rank, int world, omr_dist** out) {
   int rc = nccl_check(ncclCommInitRank(&d->comm, world, uid, rank), "ncclCommInitRank");
   if (rc == 0) rc = nccl_check(ncclCommSplit(d->comm, 0, rank, &d->xcomm, nullptr), "ncclCommSplit");
   if (rc != 0) {
+    delete d;
+    return rc;
+  }
+  *out = d;
+  return 0;
+}
+
+int omr_dist_ipc_unique_id(void* id) {
+  if (id == nullptr) return derr(OMR_EINVAL, "ipc unique id: NULL");
+  unsigned char* c = static_cast<unsigned char*>(id);
+  memset(c, 0, OMR_UNIQUE_ID_BYTES);
+  int fd = open("/dev/urandom", O_RDONLY);
+  ssize_t got = fd >= 0 ? read(fd, c, 16) : -1;
+  if (fd >= 0) close(fd);
+  if (got != 16) {  // no urandom: time and pid still make the board name unique on this host
+    const uint64_t t = static_cast<uint64_t>(std::chrono::steady_clock::now().time_since_epoch().count());
+    const uint32_t pid = static_cast<uint32_t>(getpid());
+    memcpy(c, &t, sizeof(t));
+    memcpy(c + 8, &pid, sizeof(pid));
+  }
+  return 0;
+}
+
+int omr_dist_create_ipc(const void* id, int rank, int world, omr_dist** out) {
+  if (id == nullptr || out == nullptr || world < 1 || world > kIpcMaxRanks || rank < 0 || rank >= world)
+    return derr(OMR_EINVAL, "create_ipc: bad arguments (world 1..%d)", kIpcMaxRanks);
+  *out = nullptr;
+  auto* d = new IpcDist();
+  d->rank = rank;
+  d->world = world;
+  if (int rc = d->attach(id)) {
     delete d;
     return rc;
   }
@@ -451,13 +830,13 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
   std::vector<uint64_t> roff(N, 0);
   if (timed) TRY(hip_check(hipEventRecord(p->xt0, xs), "hipEventRecord"));
   if (N > 1) {
-    std::vector<Slice> sends(N), recvs(N);
+    std::vector<Slices> sends(N), recvs(N);
     uint64_t acc = 0;
     for (int s = 0; s < N; ++s) {
       const uint64_t k0 = cnt(me, s) - (s > me ? own_shard : 0);
-      sends[s] = Slice{S.packed + k0 * B, s == me ? 0 : per(me, s) * B * sizeof(float)};
+      sends[s] = {Slice{S.packed + k0 * B, s == me ? 0 : per(me, s) * B * sizeof(float)}};
       roff[s] = acc;
-      recvs[s] = Slice{p->recv + acc * B, s == me ? 0 : per(s, me) * B * sizeof(float)};
+      recvs[s] = {Slice{p->recv + acc * B, s == me ? 0 : per(s, me) * B * sizeof(float)}};
       if (s != me) acc += per(s, me);
     }
     TRY(p->d->exchange(sends, recvs, xs));
@@ -480,10 +859,10 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
   if (!rs_mode) {
     // 6. sums back to every worker (server.cc:162), scattered in place (client.cc:89)
     if (N > 1) {
-      std::vector<Slice> ss(N), sr(N);
+      std::vector<Slices> ss(N), sr(N);
       for (int s = 0; s < N; ++s) {
-        ss[s] = Slice{sums, s == me ? 0 : per(N, me) * B * sizeof(float)};
-        sr[s] = Slice{p->results + cnt(N, s) * B, s == me ? 0 : per(N, s) * B * sizeof(float)};
+        ss[s] = {Slice{sums, s == me ? 0 : per(N, me) * B * sizeof(float)}};
+        sr[s] = {Slice{p->results + cnt(N, s) * B, s == me ? 0 : per(N, s) * B * sizeof(float)}};
       }
       TRY(p->d->exchange(ss, sr, xs));
     }

@@ -213,6 +213,7 @@ struct FusedArgs {
   uint64_t* summary;   // [parts*lanes*K] {first << 32 | last} per segment (K > 1)
   uint64_t* masks;     // [rows] row masks, zero on entry, non-zero blocks OR-ed in (multi-rank round), or null
   uint32_t lanes, rpp, K, S, block, sentinel;
+  uint32_t part0;      // first partition of the launch (a per-partition call scans partitions [part0, part0 + grid))
 };
 
 constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t T = gridDim.x, bid = blockIdx.x;
   const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
-  const uint32_t k = lin % a.K, col = lin / a.K;
+  const uint32_t k = lin % a.K, col = lin / a.K + a.part0 * a.lanes;  // col: global (partition, lane) index
   const uint32_t l = col % a.lanes, p = col / a.lanes;
   const uint32_t r0 = k * a.S;                                  // segment's first row within the partition
   const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;  // its global row
@@ -1229,8 +1230,11 @@ size_t fused_workspace_bytes(const Layout& L, const FusedShape& f) {
 }
 
 int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* out, int32_t* flags, uint32_t* next,
-                 void* ws, hipStream_t st, uint64_t* masks = nullptr) {
+                 void* ws, hipStream_t st, uint64_t* masks = nullptr, uint32_t part_begin = 0,
+                 uint32_t part_count = 0) {
+  if (part_count == 0) part_count = L.parts - part_begin;
   FusedArgs a{};
+  a.part0 = part_begin;
   a.x = x;
   a.out = out;
   a.flags = flags;
@@ -1246,7 +1250,7 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
   a.block = L.block;
   a.sentinel = omr_sentinel(L.block, L.lanes);
   a.masks = masks;
-  const unsigned grid = static_cast<unsigned>(cols * f.K);
+  const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(part_count) * L.lanes * f.K);
   constexpr int T = 64 * kFusedWaves;
   switch (L.vec) {
     case 1: k_scan1f<1, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
@@ -1450,6 +1454,22 @@ int omr_scan_sum_fused_f32(const float* buf, uint64_t n, uint32_t block_size, ui
   if (need > 0 && (workspace == nullptr || workspace_bytes < need))
     return fail("scan_sum_fused: needs a zero-initialised workspace of %zu bytes", need);
   return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream));
+}
+
+int omr_scan_partition_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                           uint32_t part, int32_t* flags, uint32_t* next_offsets, float* out, void* workspace,
+                           size_t workspace_bytes, omr_stream_t stream) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  if (part >= L.parts) return fail("scan_partition: part %u out of range (num_parts %u)", part, L.parts);
+  if (buf == nullptr || next_offsets == nullptr) return fail("scan_partition: buf and next_offsets are required");
+  if (reinterpret_cast<uintptr_t>(buf) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 16 != 0)
+    return fail("scan_partition: buffers must be 16-byte aligned");
+  const FusedShape f = fused_shape(L);
+  const size_t need = fused_workspace_bytes(L, f);
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need))
+    return fail("scan_partition: needs a zero-initialised workspace of %zu bytes", need);
+  return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), nullptr, part, 1);
 }
 
 int omr_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,

@@ -38,6 +38,8 @@ SIGNATURES = {
     "omr_scan_sum_f32": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "omr_scan_workspace_bytes": (c_size, [c_u64, c_u32, c_u32, c_u32]),
     "omr_scan_sum_fused_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "omr_scan_partition_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_size,
+                                       c_vp]),
     "omr_scan_sum_rows_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_u64, c_u64, c_vp, c_vp, c_vp, c_vp]),
     "omr_next_offsets": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp]),
     "omr_block_sum_f32": (c_int, [c_vp, c_u32, c_vp, c_u32, c_u32, c_vp, c_vp]),

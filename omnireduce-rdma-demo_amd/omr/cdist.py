@@ -36,6 +36,8 @@ def load():
         "omr_dist_last_error": (ctypes.c_char_p, []),
         "omr_dist_unique_id": (i, [vp]),
         "omr_dist_create_rccl": (i, [vp, i, i, vp]),
+        "omr_dist_ipc_unique_id": (i, [vp]),
+        "omr_dist_create_ipc": (i, [vp, i, i, vp]),
         "omr_local_board_create": (vp, [i]),
         "omr_local_board_destroy": (None, [vp]),
         "omr_dist_create_local": (i, [vp, i, vp]),
@@ -61,24 +63,39 @@ def _check(rc: int, what: str):
         raise _lib.OmrError(f"{what} failed (rc={rc}): {load().omr_dist_last_error().decode(errors='replace')}")
 
 
-class CppSparseAllreduce:
-    """One rank of the C++ round over RCCL; the torch.distributed default group supplies rank/world and the
-    unique-id broadcast."""
+def ipc_unique_id() -> bytes:
+    """A fresh id for omr_dist_create_ipc (names the shared board); hand it to every rank out of band."""
+    uid = (ctypes.c_ubyte * UNIQUE_ID_BYTES)()
+    _check(load().omr_dist_ipc_unique_id(uid), "omr_dist_ipc_unique_id")
+    return bytes(uid)
 
-    def __init__(self, L: Layout, device, group=None):
+
+class CppSparseAllreduce:
+    """One rank of the C++ round.  transport "rccl" (default): one process per GPU, the torch.distributed default
+    group supplies rank/world and the unique-id broadcast.  transport "ipc": ranks are processes of one node sharing
+    any GPUs (omr_dist_create_ipc); rank, world and the id (ipc_unique_id() of one rank) are passed in."""
+
+    def __init__(self, L: Layout, device, group=None, transport: str = "rccl", uid: Optional[bytes] = None,
+                 rank: Optional[int] = None, world: Optional[int] = None):
         D = load()
         self.L = L
         self.device = torch.device(device)
-        rank, world = dist.get_rank(group), dist.get_world_size(group)
-        uid = torch.zeros(UNIQUE_ID_BYTES, dtype=torch.uint8)
-        if rank == 0:
-            _check(D.omr_dist_unique_id(uid.data_ptr()), "omr_dist_unique_id")
-        bdev = self.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
-        t = uid.to(bdev)
-        dist.broadcast(t, 0, group=group)
-        uid.copy_(t.cpu())
         self._d = ctypes.c_void_p()
-        _check(D.omr_dist_create_rccl(uid.data_ptr(), rank, world, ctypes.byref(self._d)), "omr_dist_create_rccl")
+        if transport == "ipc":
+            if uid is None or rank is None or world is None:
+                raise ValueError("the ipc transport needs uid, rank and world")
+            buf = (ctypes.c_ubyte * UNIQUE_ID_BYTES).from_buffer_copy(uid.ljust(UNIQUE_ID_BYTES, b"\0"))
+            _check(D.omr_dist_create_ipc(buf, rank, world, ctypes.byref(self._d)), "omr_dist_create_ipc")
+        else:
+            rank, world = dist.get_rank(group), dist.get_world_size(group)
+            uidt = torch.zeros(UNIQUE_ID_BYTES, dtype=torch.uint8)
+            if rank == 0:
+                _check(D.omr_dist_unique_id(uidt.data_ptr()), "omr_dist_unique_id")
+            bdev = self.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+            t = uidt.to(bdev)
+            dist.broadcast(t, 0, group=group)
+            uidt.copy_(t.cpu())
+            _check(D.omr_dist_create_rccl(uidt.data_ptr(), rank, world, ctypes.byref(self._d)), "omr_dist_create_rccl")
         self._p = ctypes.c_void_p()
         _check(D.omr_ar_plan_create(self._d, L.n, L.block_size, L.num_lanes, L.num_threads, ctypes.byref(self._p)),
                "omr_ar_plan_create")

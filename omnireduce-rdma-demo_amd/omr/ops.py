@@ -158,6 +158,30 @@ class ScanSumPlan:
         return self.next_offsets
 
 
+def scan_workspace(layout: Layout, device="cuda") -> torch.Tensor:
+    """Zeroed workspace for the single-pass kernels (omr_scan_workspace_bytes; one per concurrently running whole-
+    tensor call, or ONE shared by concurrent per-partition calls)."""
+    ws = _lib.load().omr_scan_workspace_bytes(layout.n, layout.block_size, layout.num_lanes, layout.num_threads)
+    return torch.zeros(max(ws, 16), dtype=torch.uint8, device=device)
+
+
+def scan_partition(buf: torch.Tensor, layout: Layout, part: int, flags: Optional[torch.Tensor],
+                   next_offsets: torch.Tensor, out: Optional[torch.Tensor], workspace: torch.Tensor,
+                   stream=None) -> None:
+    """The single-pass worker step for partition `part` only (omr_scan_partition_f32): the reference's per-thread
+    seam, worker thread res->threadId walking its own DATA_SIZE_PER_THREAD slice (client.cc:19-31, :168-223).
+    flags / next_offsets / out are whole-tensor arrays (global indexing); only the partition's entries are written.
+    Safe to call from several host threads at once, one partition and one stream each (ctypes drops the GIL)."""
+    _check_f32(buf, layout.n, "buf")
+    if out is not None:
+        _check_f32(out, layout.n, "out")
+    lib = _lib.load()
+    rc = lib.omr_scan_partition_f32(_ptr(buf), layout.n, layout.block_size, layout.num_lanes, layout.num_threads,
+                                    part, _ptr(flags), _ptr(next_offsets), _ptr(out), _ptr(workspace),
+                                    workspace.numel(), _stream(stream))
+    _lib.check(rc, "omr_scan_partition_f32")
+
+
 def scan(buf: torch.Tensor, layout: Layout, stream=None) -> ScanResult:
     """Worker-side scan (client.cc:19-31): flags, row masks and next offsets of one gradient buffer."""
     return ScanSumPlan(layout, 1, device=buf.device).run([buf], None, stream)

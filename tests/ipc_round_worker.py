@@ -1,0 +1,57 @@
+"""One rank of the product's C++ round (libomr_dist.so) in its own process, over the HIP-IPC transport: launched
+by tests/test_gpu_ipc.py, several of these share the one GPU.  Writes this rank's outputs to an .npz file."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "omnireduce-rdma-demo_amd"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import oracle  # noqa: E402  (the generator's inputs only; the round itself runs in libomr_dist.so)
+from omr import Layout, cdist  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--uid", required=True, help="hex of the board id")
+    ap.add_argument("--n", type=int, required=True)
+    ap.add_argument("--block", type=int, default=256)
+    ap.add_argument("--density", type=float, default=0.1)
+    ap.add_argument("--mode", type=int, default=0, help="OMR_ROUND_* (0 all-reduce, 1 reduce-scatter, 2 dense)")
+    ap.add_argument("--pipe", choices=("sync", "async", "defer"), default="sync")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    L = Layout(n=a.n, block_size=a.block)
+    eng = cdist.CppSparseAllreduce(L, dev, transport="ipc", uid=bytes.fromhex(a.uid), rank=a.rank, world=a.world)
+    # a different input per round (seed = rank, round): the pipelined rounds must not mix their buffers
+    xs, outs = [], []
+    for r in range(a.rounds):
+        x = oracle.fill(oracle.gen_bitmap(a.rank + 10 * r, a.density, L.nb), a.block, mode=1, seed=a.rank + 7 + 31 * r)
+        xs.append(torch.from_numpy(x).to(dev))
+        outs.append(xs[-1].clone())
+    flags = torch.empty(L.nb, dtype=torch.int32, device=dev)
+    nxt = torch.empty(L.nb, dtype=torch.int32, device=dev)
+    unx = torch.empty(L.nb, dtype=torch.int32, device=dev)
+    for r in range(a.rounds):
+        eng.run(xs[r], out=outs[r], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
+                async_=a.pipe != "sync", defer=a.pipe == "defer")
+    eng.join()
+    torch.cuda.synchronize()
+    np.savez(a.out, **{f"out{r}": outs[r].cpu().numpy() for r in range(a.rounds)},
+             flags=flags.cpu().numpy(), next=nxt.cpu().numpy().view(np.uint32),
+             unext=unx.cpu().numpy().view(np.uint32))
+    eng.close()
+    print(f"rank {a.rank} ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()

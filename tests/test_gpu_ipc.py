@@ -1,0 +1,87 @@
+"""The product's C++ multi-rank round (libomr_dist.so) with its ranks in SEPARATE PROCESSES sharing the one GPU,
+over the HIP-IPC transport (omr_dist_create_ipc): device-side ordering between the ranks' streams (IPC events), no
+stream synchronisation in the transport, in the synchronous, asynchronous (OMR_ROUND_ASYNC: the exchange on the
+plan's second stream and second channel) and deferred (OMR_ROUND_DEFER) pipelines, every round a different input.
+Each rank's outputs are checked bit for bit against the oracle: the rank-order block sums (server.cc:97-98), its
+flags and next chain (client.cc:19-31) and the aggregator's union chain (server.cc:86-96)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+from omr import Layout, cdist
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "ipc_round_worker.py")
+
+
+def run_ranks(tmp_path, world, n, B, density, mode, pipe, rounds=3):
+    uid = cdist.ipc_unique_id().hex()
+    procs, outs = [], []
+    for r in range(world):
+        out = str(tmp_path / f"rank{r}.npz")
+        outs.append(out)
+        cmd = [sys.executable, WORKER, "--rank", str(r), "--world", str(world), "--uid", uid, "--n", str(n),
+               "--block", str(B), "--density", str(density), "--mode", str(mode), "--pipe", pipe,
+               "--rounds", str(rounds), "--out", out]
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=150)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("an IPC rank hung:\n" + "\n".join(q.communicate()[0] or "" for q in procs))
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{logs[r]}"
+    return [np.load(o) for o in outs]
+
+
+@pytest.mark.parametrize("world,pipe,mode,B,density", [
+    (2, "sync", 0, 256, 0.095),
+    (3, "async", 0, 1024, 0.05),
+    (4, "defer", 0, 256, 0.3),
+    (4, "sync", 1, 512, 0.095),
+    (3, "defer", 1, 256, 0.5),
+    (2, "async", 2, 256, 0.2),
+    (4, "defer", 2, 256, 0.095),
+])
+def test_cpp_round_processes(gpu, tmp_path, world, pipe, mode, B, density):
+    L = Layout(n=2 << 20, block_size=B)
+    rounds = 3
+    res = run_ranks(tmp_path, world, L.n, B, density, mode, pipe, rounds)
+    NB, P = L.num_lanes, L.num_threads
+    bounds = [s * L.rows // world for s in range(world + 1)]
+    for rd in range(rounds):
+        bufs = [oracle.fill(oracle.gen_bitmap(w + 10 * rd, density, L.nb), B, mode=1, seed=w + 7 + 31 * rd)
+                for w in range(world)]
+        flags = [oracle.flags_from_data(b, B) for b in bufs]
+        uf = oracle.union_flags(flags)
+        for r in range(world):
+            got = res[r][f"out{rd}"]
+            if mode == 2:  # dense stand-in: every element of the rank's shard, rank-order sum
+                exp = bufs[r].copy()
+                lo, hi = bounds[r] * NB * B, bounds[r + 1] * NB * B
+                acc = np.zeros(hi - lo, dtype=np.float32)
+                for b in bufs:
+                    acc = acc + b[lo:hi]
+                exp[lo:hi] = acc
+            else:
+                full = bufs[r].copy()
+                oracle.block_sum(bufs, L.n, B, NB, P, uf, full)
+                if mode == 0:
+                    exp = full
+                else:  # reduce-scatter: the sums land in the rank's own shard only
+                    exp = bufs[r].copy()
+                    lo, hi = bounds[r] * NB * B, bounds[r + 1] * NB * B
+                    exp[lo:hi] = full[lo:hi]
+            assert (got.view(np.uint32) == exp.view(np.uint32)).all(), f"round {rd} rank {r} out"
+            if rd == rounds - 1:
+                assert (res[r]["flags"] == flags[r]).all(), f"rank {r} flags"
+                assert (res[r]["next"] == oracle.next_offsets(flags[r], L.n, B, NB, P)).all(), f"rank {r} next"
+                assert (res[r]["unext"] == oracle.next_offsets(uf, L.n, B, NB, P)).all(), f"rank {r} union next"
