@@ -55,6 +55,11 @@ def parse():
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
                    help="rocprofv3 PMC summary giving HBM traffic per launch (optional)")
     p.add_argument("--print-workload", action="store_true", help="print the workload string and exit")
+    p.add_argument("--host-resident", action="store_true",
+                   help="BASELINE config 5's end-to-end path: the gradient in pinned host memory, reduced in place by "
+                        "omr_sparse_buckets_f32 (H2D / scan / exchange / D2H overlapped per bucket); e.g. "
+                        "--host-resident --size-mib 4096 --density 0.49")
+    p.add_argument("--bucket-mib", type=int, default=256, help="--host-resident: bucket (one round) size")
     p.add_argument("--event-every", type=int, default=10,
                    help="bracket every k-th timed step's kernel with (fence-free) HIP events")
     p.add_argument("--kernel", choices=("fused", "twopass"), default="fused",
@@ -176,9 +181,78 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
     }
 
 
+def host_resident(args, ws, rank, local):
+    """Config 5: a size-mib gradient per rank in pinned host memory, all-reduced in place bucket by bucket; one step
+    = one omr_sparse_buckets_f32 call, which returns when the host buffer holds the result (PCIe both ways
+    included).  N=1: a one-rank group (no peers); N>1: RCCL over xGMI between the ranks' staged buckets."""
+    from omr import cdist
+    dist_mode = ws > 1
+    if dist_mode:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if dist_mode else 0)
+    Lb = Layout.from_bytes(args.bucket_mib << 20, args.block_size)
+    total = Layout.from_bytes(args.size_mib << 20, args.block_size)
+    bm = ops.gen_bitmap(rank, args.density, total.nb)
+    host = ops.fill_blocks(torch.from_numpy(bm).to(dev), total).cpu().pin_memory()
+    eng = cdist.CppSparseAllreduce(Lb, dev, transport="rccl" if dist_mode else "local1")
+    step = lambda: eng.run_buckets(host, mode=cdist.CppSparseAllreduce.ALLREDUCE)  # noqa: E731
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist_mode:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist_mode:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist_mode:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # the link's own ceiling on this box: one plain pinned H2D and one D2H of a bucket
+    dbuf = torch.empty(Lb.n, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record(); dbuf.copy_(host[:Lb.n], non_blocking=True); ev[1].record()
+    ev[2].record(); host[:Lb.n].copy_(dbuf, non_blocking=True); ev[3].record()
+    torch.cuda.synchronize()
+    h2d = Lb.nbytes / (ev[0].elapsed_time(ev[1]) * 1e-3) / 1e9
+    d2h = Lb.nbytes / (ev[2].elapsed_time(ev[3]) * 1e-3) / 1e9
+    eng.close()
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        n_gpus = max(ws, 1)
+        value = n_gpus * total.nbytes / (ms * 1e-3) / 1e9
+        nz = float(bm.mean())
+        print(json.dumps({
+            "metric": (f"GB/s end-to-end sparse all-reduce from pinned host memory, {args.size_mib} MiB fp32 @ "
+                       f"{round(100 * (1 - nz))}% block-sparse per rank (H2D + D2H included)"),
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic (reference generator client.cc:396-421: srand(rank+1), -r {args.density}, 0.01f)",
+            "config": {"workload": (f"{args.size_mib} MiB fp32 per rank in pinned host memory, block_size="
+                                    f"{args.block_size}, -r {args.density}, buckets of {args.bucket_mib} MiB, "
+                                    f"all-reduce in place (BASELINE config 5)"),
+                       "parallelism": f"dp{n_gpus}", "nonzero_fraction": round(nz, 5)},
+            "roofline": None,
+            "pcie": {"per_rank_GBps": round(total.nbytes / (ms * 1e-3) / 1e9, 2),
+                     "plain_h2d_GBps": round(h2d, 2), "plain_d2h_GBps": round(d2h, 2),
+                     "spec_GBps": 63.0, "note": "per rank: S in + S out over its own PCIe Gen5 x16 link"},
+            "cpu_baseline": None}), flush=True)
+    if dist_mode:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
+    if args.host_resident:
+        host_resident(args, ws, rank, local)
+        return
     dist_mode = ws > 1 or args.force_dist
     if args.print_workload:
         print(workload_string(args, args.workers if ws == 1 else 1))

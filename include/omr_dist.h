@@ -117,6 +117,16 @@ int omr_sparse_round_f32(omr_ar_plan* plan, const float* x, float* out, int32_t*
 /* Duration of the last OMR_ROUND_TIME_EXCHANGE round's exchange (waits for it), with the bytes this rank sent
  * to and received from its peers in it (bytes_out / bytes_in may be NULL).  OMR_EINVAL if no round was timed. */
 int omr_ar_plan_exchange_time(omr_ar_plan* plan, float* ms, uint64_t* bytes_out, uint64_t* bytes_in);
+/* A whole gradient of total_n floats (a multiple of the plan's n: one bucket), reduced in place bucket by bucket,
+ * one round per bucket with the next bucket's worker scan queued before the previous bucket's exchange
+ * (OMR_ROUND_DEFER).  mode: OMR_ROUND_ALLREDUCE or OMR_ROUND_REDUCE_SCATTER (the rank's shard of every bucket).
+ * buf is device memory, or PINNED HOST memory (the reference's registered region res->buf, common.cc:873-914, that
+ * the worker fills and gets the results back in: client.cc:89, :401-421): then buckets are staged through a ring of
+ * three device buffers, H2D of bucket k+1 and D2H of bucket k-2 on two copy streams beside bucket k's scan and
+ * bucket k-1's exchange, and the call returns once the host buffer holds the result.  Device memory: returns with
+ * the work enqueued on `stream` (joined).  *sent_blocks / *union_blocks: sums over the buckets. */
+int omr_sparse_buckets_f32(omr_ar_plan* plan, float* buf, uint64_t total_n, int mode, uint64_t* sent_blocks,
+                           uint64_t* union_blocks, omr_stream_t stream);
 /* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
 int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
 

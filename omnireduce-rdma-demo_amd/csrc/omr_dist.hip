@@ -138,19 +138,24 @@ struct omr_local_board {
 namespace {
 
 // Loopback transport: ranks are threads of one process; each posts its buffers, waits at a barrier, and pulls
-// what its peers posted with device-to-device copies (any pair of devices; UVA peer or staged copies).
+// what its peers posted with device-to-device copies on its own stream (any pair of devices; UVA peer or staged
+// copies), synchronised before the closing barrier: a device-to-device hipMemcpy may return before the copy is done,
+// and a peer must not touch its buffers again until every reader is through.
 struct LocalDist final : omr_dist {
   omr_local_board* b = nullptr;
   int allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
     TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
     b->posted[rank] = in;
     b->barrier();
-    for (int p = 0; p < world; ++p) {
+    int rc = 0;
+    for (int p = 0; p < world && rc == 0; ++p) {
       char* dst = static_cast<char*>(out) + static_cast<size_t>(p) * bytes;
-      if (b->posted[p] != dst) TRY(hip_check(hipMemcpy(dst, b->posted[p], bytes, hipMemcpyDefault), "hipMemcpy"));
+      if (b->posted[p] != dst)
+        rc = hip_check(hipMemcpyAsync(dst, b->posted[p], bytes, hipMemcpyDefault, st), "hipMemcpyAsync");
     }
+    if (rc == 0) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
     b->barrier();
-    return 0;
+    return rc;
   }
   int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
     TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
@@ -169,11 +174,12 @@ struct LocalDist final : omr_dist {
                     k < from.size() ? from[k].bytes : size_t{0});
           break;
         }
-        rc = hip_check(hipMemcpy(r.ptr, from[k].ptr, r.bytes, hipMemcpyDefault), "hipMemcpy");
+        rc = hip_check(hipMemcpyAsync(r.ptr, from[k].ptr, r.bytes, hipMemcpyDefault, st), "hipMemcpyAsync");
         if (rc) break;
         ++k;
       }
     }
+    if (rc == 0) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
     b->barrier();  // every rank leaves together, even on an error (no peer is left waiting)
     return rc;
   }
@@ -592,6 +598,16 @@ struct omr_ar_plan {
     uint32_t seq = 0;
     hipStream_t st = nullptr;  // the stream its first half went on (the count wait checks it for a failed launch)
   } pend;
+  // rounds issued on different streams run in call order: the plan's arrival counter, own-mask buffer and scan
+  // workspace are shared by every round
+  hipStream_t last_st = nullptr;
+  hipEvent_t st_ev = nullptr;
+  // omr_sparse_buckets_f32 on a pinned-host gradient: a ring of device staging buckets and two copy streams
+  static constexpr int kStage = 3;
+  float* stage[kStage] = {nullptr, nullptr, nullptr};
+  hipStream_t s_in = nullptr, s_out = nullptr;
+  hipEvent_t ev_in[kStage] = {}, ev_round[kStage] = {}, ev_out[kStage] = {};
+  bool out_used[kStage] = {false, false, false};
 };
 
 namespace {
@@ -695,6 +711,14 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     if (st.done) (void)hipEventDestroy(st.done);
   }
   if (p->cs) (void)hipStreamDestroy(p->cs);
+  for (int r = 0; r < omr_ar_plan::kStage; ++r) {
+    (void)hipFree(p->stage[r]);
+    for (hipEvent_t e : {p->ev_in[r], p->ev_round[r], p->ev_out[r]})
+      if (e) (void)hipEventDestroy(e);
+  }
+  if (p->s_in) (void)hipStreamDestroy(p->s_in);
+  if (p->s_out) (void)hipStreamDestroy(p->s_out);
+  if (p->st_ev) (void)hipEventDestroy(p->st_ev);
   if (p->xt0) (void)hipEventDestroy(p->xt0);
   if (p->xt1) (void)hipEventDestroy(p->xt1);
   (void)hipHostFree(p->counts_host);
@@ -741,6 +765,7 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
     A(hip_check(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "hipEventCreate"));
   }
   A(hip_check(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking), "hipStreamCreate"));
+  A(hip_check(hipEventCreateWithFlags(&p->st_ev, hipEventDisableTiming), "hipEventCreate"));
   A(hip_check(hipEventCreate(&p->xt0), "hipEventCreate"));
   A(hip_check(hipEventCreate(&p->xt1), "hipEventCreate"));
   A(dev_alloc(&p->bounds_dev, N + 1));
@@ -917,6 +942,12 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   int32_t* fl = flags ? flags : p->flags_ws;
   uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
   uint32_t* un = union_next ? union_next : p->unext_ws;
+  // a stream other than the previous round's starts behind it (plan-wide state is shared by every round)
+  if (p->last_st != nullptr && p->last_st != st) {
+    TRY(hip_check(hipEventRecord(p->st_ev, p->last_st), "hipEventRecord"));
+    TRY(hip_check(hipStreamWaitEvent(st, p->st_ev, 0), "hipStreamWaitEvent"));
+  }
+  p->last_st = st;
   // a round that is not deferred finishes a deferred one first (rounds complete in call order)
   if (!defer) TRY(flush_pending(p, st, nullptr, nullptr));
   // a synchronous round after asynchronous ones: its exchange goes on `stream`, so the communication stream
@@ -973,6 +1004,99 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   p->pend.out = out;
   p->pend.seq = seq;
   p->pend.st = st;
+  return 0;
+}
+
+int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mode, uint64_t* sent_blocks,
+                           uint64_t* union_blocks, omr_stream_t stream) {
+  if (p == nullptr || buf == nullptr) return derr(OMR_EINVAL, "sparse_buckets: NULL");
+  if (total_n == 0 || total_n % p->n != 0)
+    return derr(OMR_EINVAL, "sparse_buckets: total_n %llu is not a multiple of the plan's bucket of %llu floats",
+                static_cast<unsigned long long>(total_n), static_cast<unsigned long long>(p->n));
+  if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER)
+    return derr(OMR_EINVAL, "sparse_buckets: mode %d (OMR_ROUND_ALLREDUCE or OMR_ROUND_REDUCE_SCATTER)", mode);
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, buf) != hipSuccess) {
+    (void)hipGetLastError();
+    return derr(OMR_EINVAL, "sparse_buckets: buf is neither device memory nor pinned host memory "
+                            "(register it: omr_host_register / hipHostRegister)");
+  }
+  if (attr.type != hipMemoryTypeHost && attr.type != hipMemoryTypeDevice)
+    return derr(OMR_EINVAL, "sparse_buckets: buf is neither device memory nor pinned host memory (memory type %d): "
+                            "register it (omr_host_register / hipHostRegister)", static_cast<int>(attr.type));
+  const bool host = attr.type == hipMemoryTypeHost;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint64_t K = total_n / p->n, bytes = p->n * sizeof(float);
+  const int rmode = mode | OMR_ROUND_DEFER;
+  uint64_t sent = 0, uni = 0, s1 = 0, u1 = 0;
+  auto acc = [&] {
+    sent += s1;
+    uni += u1;
+  };
+  if (!host) {  // device-resident: one deferred round per bucket, in place
+    for (uint64_t k = 0; k < K; ++k) {
+      float* b = buf + k * p->n;
+      TRY(omr_sparse_round_f32(p, b, b, nullptr, nullptr, nullptr, rmode, &s1, &u1, stream));
+      acc();
+    }
+    TRY(flush_pending(p, st, &s1, &u1));
+    acc();
+    TRY(omr_ar_plan_join(p, stream));
+    if (sent_blocks) *sent_blocks = sent;
+    if (union_blocks) *union_blocks = uni;
+    return 0;
+  }
+  // pinned host: H2D(k+1) on s_in || scan(k) on stream || exchange + sums(k-1) on the plan's stream || D2H(k-2)
+  constexpr int R = omr_ar_plan::kStage;
+  if (p->s_in == nullptr) {
+    for (int r = 0; r < R; ++r) {
+      TRY(dev_alloc(&p->stage[r], p->n));
+      TRY(hip_check(hipEventCreateWithFlags(&p->ev_in[r], hipEventDisableTiming), "hipEventCreate"));
+      TRY(hip_check(hipEventCreateWithFlags(&p->ev_round[r], hipEventDisableTiming), "hipEventCreate"));
+      TRY(hip_check(hipEventCreateWithFlags(&p->ev_out[r], hipEventDisableTiming), "hipEventCreate"));
+    }
+    TRY(hip_check(hipStreamCreateWithFlags(&p->s_in, hipStreamNonBlocking), "hipStreamCreate"));
+    TRY(hip_check(hipStreamCreateWithFlags(&p->s_out, hipStreamNonBlocking), "hipStreamCreate"));
+  }
+  float* hbuf = static_cast<float*>(attr.hostPointer ? attr.hostPointer : buf);
+  // reduce-scatter returns only this rank's shard: only those rows travel back
+  const uint64_t row_floats = static_cast<uint64_t>(p->lanes) * p->B;
+  const bool rs = mode == OMR_ROUND_REDUCE_SCATTER;
+  const uint64_t back0 = rs ? p->bounds[p->me] * row_floats : 0;
+  const uint64_t back_n = rs ? (p->bounds[p->me + 1] - p->bounds[p->me]) * row_floats : p->n;
+  auto h2d = [&](uint64_t k) -> int {
+    const int r = static_cast<int>(k % R);
+    if (p->out_used[r]) TRY(hip_check(hipStreamWaitEvent(p->s_in, p->ev_out[r], 0), "hipStreamWaitEvent"));
+    TRY(hip_check(hipMemcpyAsync(p->stage[r], hbuf + k * p->n, bytes, hipMemcpyHostToDevice, p->s_in),
+                  "hipMemcpyAsync H2D"));
+    return hip_check(hipEventRecord(p->ev_in[r], p->s_in), "hipEventRecord");
+  };
+  auto d2h = [&](uint64_t k) -> int {  // after round k's second half, which is queued on the plan's stream
+    const int r = static_cast<int>(k % R);
+    TRY(hip_check(hipEventRecord(p->ev_round[r], p->cs), "hipEventRecord"));
+    TRY(hip_check(hipStreamWaitEvent(p->s_out, p->ev_round[r], 0), "hipStreamWaitEvent"));
+    if (back_n)
+      TRY(hip_check(hipMemcpyAsync(hbuf + k * p->n + back0, p->stage[r] + back0, back_n * sizeof(float),
+                                   hipMemcpyDeviceToHost, p->s_out), "hipMemcpyAsync D2H"));
+    p->out_used[r] = true;
+    return hip_check(hipEventRecord(p->ev_out[r], p->s_out), "hipEventRecord");
+  };
+  TRY(h2d(0));
+  for (uint64_t k = 0; k < K; ++k) {
+    const int r = static_cast<int>(k % R);
+    TRY(hip_check(hipStreamWaitEvent(st, p->ev_in[r], 0), "hipStreamWaitEvent"));
+    TRY(omr_sparse_round_f32(p, p->stage[r], p->stage[r], nullptr, nullptr, nullptr, rmode, &s1, &u1, stream));
+    acc();  // (the previous bucket's counts: its second half was issued by this call)
+    if (k >= 1) TRY(d2h(k - 1));
+    if (k + 1 < K) TRY(h2d(k + 1));
+  }
+  TRY(flush_pending(p, st, &s1, &u1));
+  acc();
+  TRY(d2h(K - 1));
+  TRY(hip_check(hipStreamSynchronize(p->s_out), "hipStreamSynchronize"));  // the host buffer holds the result
+  TRY(omr_ar_plan_join(p, stream));
+  if (sent_blocks) *sent_blocks = sent;
+  if (union_blocks) *union_blocks = uni;
   return 0;
 }
 

@@ -43,6 +43,15 @@ int herr(hipError_t e, const char* what) {
     if (int _rc = herr((call), #call)) return _rc;     \
   } while (0)
 
+// A library call failed partway through a pipelined round: copies already queued keep running into the host
+// buffer and the device buffer, so let them drain before returning, and report the library's message here.
+int fail_drain(omr_host_plan* p, int rc, const char* what) {
+  snprintf(g_host_err, sizeof(g_host_err), "%s: %s", what, omr_last_error());
+  for (hipStream_t s : {p->s_in, p->s_cmp, p->s_out})
+    if (s) (void)hipStreamSynchronize(s);
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -120,7 +129,10 @@ int omr_host_plan_create(uint64_t n, uint32_t block_size, uint32_t num_lanes, ui
 
 int omr_host_scan_sum_f32(omr_host_plan* p, float* host_buf, int32_t* host_flags, uint32_t* host_next,
                           double* seconds) {
-  if (p == nullptr || host_buf == nullptr) return OMR_EINVAL;
+  if (p == nullptr || host_buf == nullptr) {
+    snprintf(g_host_err, sizeof(g_host_err), "host_scan_sum: NULL plan or buffer");
+    return OMR_EINVAL;
+  }
   const auto t0 = std::chrono::steady_clock::now();
   const uint64_t row_floats = static_cast<uint64_t>(p->lanes) * p->block;
   for (uint64_t k = 0; k < p->nchunks; ++k) {
@@ -133,12 +145,13 @@ int omr_host_scan_sum_f32(omr_host_plan* p, float* host_buf, int32_t* host_flags
     OMR_HIP(hipStreamWaitEvent(p->s_cmp, p->ev_in[k], 0));
     if (int rc = omr_scan_sum_rows_f32(p->d_buf, p->n, p->block, p->lanes, p->parts, r0, r1, p->d_flags,
                                        p->d_masks, p->d_buf, p->s_cmp))
-      return rc;
+      return fail_drain(p, rc, "omr_scan_sum_rows_f32");
     OMR_HIP(hipEventRecord(p->ev_cmp[k], p->s_cmp));
     OMR_HIP(hipStreamWaitEvent(p->s_out, p->ev_cmp[k], 0));
     OMR_HIP(hipMemcpyAsync(host_buf + off, p->d_buf + off, bytes, hipMemcpyDeviceToHost, p->s_out));
   }
-  if (int rc = omr_next_offsets(p->d_masks, 1, p->n, p->block, p->lanes, p->parts, p->d_next, p->s_cmp)) return rc;
+  if (int rc = omr_next_offsets(p->d_masks, 1, p->n, p->block, p->lanes, p->parts, p->d_next, p->s_cmp))
+    return fail_drain(p, rc, "omr_next_offsets");
   if (host_flags != nullptr)
     OMR_HIP(hipMemcpyAsync(host_flags, p->d_flags, p->nb * sizeof(int32_t), hipMemcpyDeviceToHost, p->s_cmp));
   if (host_next != nullptr)
@@ -152,7 +165,10 @@ int omr_host_scan_sum_f32(omr_host_plan* p, float* host_buf, int32_t* host_flags
 
 int omr_host_scan_sum_zero_copy_f32(omr_host_plan* p, float* host_buf, int32_t* host_flags, uint32_t* host_next,
                                     double* seconds) {
-  if (p == nullptr || host_buf == nullptr) return OMR_EINVAL;
+  if (p == nullptr || host_buf == nullptr) {
+    snprintf(g_host_err, sizeof(g_host_err), "host_scan_sum_zero_copy: NULL plan or buffer");
+    return OMR_EINVAL;
+  }
   const auto t0 = std::chrono::steady_clock::now();
   // the buffer's address in the GPU's space (pinned memory only: pageable memory has none)
   void* dev = nullptr;

@@ -108,6 +108,15 @@ int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer) {
   }
   hipStream_t st;
   HIPOK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  // -c with -I: every round starts from the generator's input, as the reference's CHECK restores res.buf = input
+  // after each checked round (client.cc:463-464); without it the in-place rounds would compound
+  const bool restore = o.check && o.inplace;
+  float* d_in = nullptr;
+  if (restore) {
+    HIPOK(hipMalloc(&d_in, o.n * sizeof(float)));
+    HIPOK(hipMemcpyAsync(d_in, d_x, o.n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    HIPOK(hipStreamSynchronize(st));
+  }
   if (printer) std::cout << "density: " << o.density << std::endl;  // client.cc:405
   const double gib = o.n * sizeof(float) / (1024.0 * 1024.0 * 1024.0);
   double avg_bw = 0.0;
@@ -137,7 +146,13 @@ int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer) {
       }
       start = std::chrono::steady_clock::now();
     }
+    if (restore && round + 1 < o.warmups + o.rounds) {  // res.buf = input (client.cc:463-464), outside the timing
+      HIPOK(hipMemcpyAsync(d_x, d_in, o.n * sizeof(float), hipMemcpyDeviceToDevice, st));
+      HIPOK(hipStreamSynchronize(st));
+      start = std::chrono::steady_clock::now();
+    }
   }
+  (void)hipFree(d_in);
   int rc = 0;
   if (o.check) {  // the CHECK of client.cc:449-465, done right: expected = rank-order sum of every input
     std::vector<float*> bufs(world);
@@ -218,8 +233,22 @@ int run_messages(const Opts& o, int gpu) {
   int print_count = 0;
   uint32_t maxr = 0;
   std::vector<const float*> in(x.begin(), x.end());
+  const bool restore = o.check && o.inplace;  // client.cc:463-464, as in run_worker
+  std::vector<float*> pristine(k, nullptr);
+  if (restore)
+    for (int w = 0; w < k; ++w) {
+      HIPOK(hipMalloc(&pristine[w], o.n * sizeof(float)));
+      HIPOK(hipMemcpyAsync(pristine[w], x[w], o.n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    }
+  HIPOK(hipStreamSynchronize(st));
   auto start = std::chrono::steady_clock::now();
   for (int round = 0; round < o.warmups + o.rounds; ++round) {
+    if (restore && round > 0) {  // res.buf = input before every round after the first (client.cc:463-464)
+      for (int w = 0; w < k; ++w)
+        HIPOK(hipMemcpyAsync(x[w], pristine[w], o.n * sizeof(float), hipMemcpyDeviceToDevice, st));
+      HIPOK(hipStreamSynchronize(st));
+      start = std::chrono::steady_clock::now();
+    }
     std::vector<float*> dst = o.inplace ? x : out;
     if (omr_msg_round_f32(plan, in.data(), dst.data(), &maxr, st)) {
       fprintf(stderr, "failed to run the round: %s\n", omr_last_error());
@@ -241,6 +270,7 @@ int run_messages(const Opts& o, int gpu) {
       start = std::chrono::steady_clock::now();
     }
   }
+  for (float* b : pristine) (void)hipFree(b);
   std::cout << "protocol rounds (largest slot): " << maxr << std::endl;
   int rc = 0;
   if (o.trace) {  // the last round's wire traffic, SURVEY.md Appendix B.6 record layout

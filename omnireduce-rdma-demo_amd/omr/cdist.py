@@ -49,6 +49,7 @@ def load():
         "omr_sparse_allreduce_f32": (i, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "omr_sparse_round_f32": (i, [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]),
         "omr_ar_plan_join": (i, [vp, vp]),
+        "omr_sparse_buckets_f32": (i, [vp, vp, u64, i, vp, vp, vp]),
         "omr_ar_plan_exchange_time": (i, [vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
@@ -73,7 +74,8 @@ def ipc_unique_id() -> bytes:
 class CppSparseAllreduce:
     """One rank of the C++ round.  transport "rccl" (default): one process per GPU, the torch.distributed default
     group supplies rank/world and the unique-id broadcast.  transport "ipc": ranks are processes of one node sharing
-    any GPUs (omr_dist_create_ipc); rank, world and the id (ipc_unique_id() of one rank) are passed in."""
+    any GPUs (omr_dist_create_ipc); rank, world and the id (ipc_unique_id() of one rank) are passed in.  transport
+    "local1": a group of one rank (the round with no peers), e.g. for the single-GPU host-resident bench."""
 
     def __init__(self, L: Layout, device, group=None, transport: str = "rccl", uid: Optional[bytes] = None,
                  rank: Optional[int] = None, world: Optional[int] = None):
@@ -81,7 +83,12 @@ class CppSparseAllreduce:
         self.L = L
         self.device = torch.device(device)
         self._d = ctypes.c_void_p()
-        if transport == "ipc":
+        self._board = None
+        if transport == "local1":  # a one-rank group (loopback transport): the round without peers
+            rank, world = 0, 1
+            self._board = D.omr_local_board_create(1)
+            _check(D.omr_dist_create_local(self._board, 0, ctypes.byref(self._d)), "omr_dist_create_local")
+        elif transport == "ipc":
             if uid is None or rank is None or world is None:
                 raise ValueError("the ipc transport needs uid, rank and world")
             buf = (ctypes.c_ubyte * UNIQUE_ID_BYTES).from_buffer_copy(uid.ljust(UNIQUE_ID_BYTES, b"\0"))
@@ -132,6 +139,20 @@ class CppSparseAllreduce:
             ev[1].record(st)
         return sent.value, uni.value
 
+    def run_buckets(self, buf: torch.Tensor, mode: int = 0, stream=None):
+        """The whole tensor `buf` (numel a multiple of the layout's n) reduced in place, one pipelined round per
+        bucket of L.n floats (omr_sparse_buckets_f32).  buf on the device, or in pinned host memory (staged: returns
+        when the host buffer holds the result).  Returns (sent blocks, union blocks) summed over the buckets."""
+        if buf.dtype != torch.float32 or not buf.is_contiguous() or buf.numel() % self.L.n:
+            raise ValueError("buf must be a contiguous float32 tensor of a multiple of the bucket's n")
+        if not buf.is_cuda and not buf.is_pinned():
+            raise ValueError("a host buffer must be pinned (pin_memory())")
+        sent, uni = ctypes.c_uint64(), ctypes.c_uint64()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(load().omr_sparse_buckets_f32(self._p, buf.data_ptr(), buf.numel(), mode, ctypes.byref(sent),
+                                             ctypes.byref(uni), st.cuda_stream), "omr_sparse_buckets_f32")
+        return sent.value, uni.value
+
     def exchange_time(self):
         """(ms, bytes sent, bytes received) of the last round run with time_exchange=True (waits for it)."""
         ms, bo, bi = ctypes.c_float(), ctypes.c_uint64(), ctypes.c_uint64()
@@ -152,3 +173,6 @@ class CppSparseAllreduce:
         if self._d:
             D.omr_dist_destroy(self._d)
             self._d = ctypes.c_void_p()
+        if self._board:
+            D.omr_local_board_destroy(self._board)
+            self._board = None

@@ -289,6 +289,16 @@ def test_client_loopback_cli(gpu):
     assert "check OK" in out and "average alg bw" in out and "test result is 0" in out
 
 
+@pytest.mark.parametrize("mode", [[], ["-M"]])
+def test_client_loopback_check_in_place(gpu, mode):
+    """-c with -I: the in-place rounds would compound (0.01 -> 0.03 -> 0.09 at three workers), so each round starts
+    from the generator's input again, as the reference's CHECK restores res.buf = input (client.cc:463-464)."""
+    rc, out = _run([os.path.join(BIN, "omr_client"), "-L", "3", "-n", str(1 << 20), "-r", "0.3", "-W", "2",
+                    "-R", "3", "-c", "-I"] + mode)
+    assert rc == 0, out
+    assert "check OK" in out and "test result is 0" in out
+
+
 def test_server_client_rccl_one_worker(gpu):
     port = "19877"
     srv = subprocess.Popen([os.path.join(BIN, "omr_server"), "-p", port, "127.0.0.1"], stdout=subprocess.PIPE,
