@@ -267,6 +267,35 @@ int omr_msg_round_f32(omr_msg_plan* plan, const float* const* bufs, float* const
 int omr_msg_logs(omr_msg_plan* plan, uint32_t worker, float** messages, uint32_t** imm, float** replies,
                  uint32_t** reply_imm, uint32_t** rounds, uint32_t* round_capacity);
 
+/* The same round split into its message primitives, for workers and aggregators in different processes (the
+ * reference's separate ./client and ./server machines, common.cc:374-476 -> server.cc:56-199), all on device
+ * buffers; a transport moves the logs (omr_dist.h: omr_msgd_*).  Log layout as above: message (gs, r) at
+ * [(gs*round_capacity + r) * 2*MESSAGE_SIZE] floats, imm at [gs*round_capacity + r]; gs < num_parts*NUM_SLOTS.
+ *   omr_msg_schedule  per slot, the protocol rounds' blocks, message and reply orders (sched: omr_msg_sched_bytes()
+ *                     per (slot, round)), rounds[gs], and *max_rounds (device uint32; > round_capacity means the logs
+ *                     are too small: redo with a larger capacity), from the m workers' row masks (device [m][rows])
+ *                     and the union's next offsets (the aggregator's min_next chain, server.cc:86-96);
+ *   omr_msg_pack_f32  one worker's messages of every slot (client.cc:180-205, :113-127; common.cc:399-408);
+ *   omr_msg_aggregate_f32  the replies of the slots one aggregator owns: gs % num_aggregators == aggregator
+ *                     (common.cc:381-383), from the m workers' logs (HOST arrays of device pointers, rank order):
+ *                     rank-order sums from +0.0f (server.cc:97-98, :148-150), completion order, min_next
+ *                     (server.cc:143-147);
+ *   omr_msg_unpack_f32  a worker applies every reply in place (client.cc:87-90). */
+size_t omr_msg_sched_bytes(void);
+int omr_msg_schedule(const uint64_t* row_masks, uint32_t m, const uint32_t* union_next, uint64_t n, uint32_t block_size,
+                     uint32_t num_lanes, uint32_t num_parts, uint32_t round_capacity, void* sched, uint32_t* rounds,
+                     uint32_t* max_rounds, omr_stream_t stream);
+int omr_msg_pack_f32(const float* x, const int32_t* flags, const uint32_t* next_offsets, const void* sched,
+                     const uint32_t* rounds, uint32_t num_parts, uint32_t round_capacity, uint32_t block_size,
+                     float* messages, uint32_t* imm, omr_stream_t stream);
+int omr_msg_aggregate_f32(const float* const* messages, const uint32_t* const* imm, uint32_t m, const void* sched,
+                          const uint32_t* rounds, const uint32_t* union_next, uint32_t num_parts,
+                          uint32_t round_capacity, uint32_t block_size, uint32_t num_lanes, uint32_t num_aggregators,
+                          uint32_t aggregator, float* replies, uint32_t* reply_imm, omr_stream_t stream);
+int omr_msg_unpack_f32(const float* replies, const uint32_t* reply_imm, const void* sched, const uint32_t* rounds,
+                       uint32_t num_parts, uint32_t round_capacity, uint32_t block_size, uint32_t num_lanes,
+                       float* buf, omr_stream_t stream);
+
 /* ---------------------------------------------------------------- host-resident end-to-end path */
 
 /* The gradient lives in host memory (the reference's registered region, common.cc:873-914): H2D in row chunks,

@@ -63,6 +63,20 @@ int omr_dist_destroy(omr_dist* d);
 int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
                        omr_ar_plan** out);
 int omr_ar_plan_destroy(omr_ar_plan* plan);
+/* The same with roles (the reference's m workers and n aggregators, README.md:13-22): ranks [0, num_workers) are
+ * workers; if num_workers < world the other ranks are dedicated aggregators — the ./omr_server processes, holding no
+ * tensor — aggregator j = rank num_workers + j owning row shard j of n = world - num_workers (rows [j*rows/n,
+ * (j+1)*rows/n)); num_workers == world is omr_ar_plan_create (every rank a worker and the aggregator of its own
+ * shard).  A dedicated aggregator calls omr_sparse_round_f32 with x = out = NULL in the same sequence of modes as the
+ * workers; in all-reduce mode its sums go back to every worker, in reduce-scatter mode they stay with it
+ * (omr_ar_plan_shard).  The dense stand-in needs every rank to be a worker. */
+int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint32_t block_size, uint32_t num_lanes,
+                             uint32_t num_parts, omr_ar_plan** out);
+/* This rank's aggregator shard: *shard (-1: none), its rows [*row_begin, *row_end), and for a dedicated aggregator the
+ * last round's sums (device, write-set order of the shard rows: union blocks and lane heads in block order, as the
+ * reply of server.cc:143-147) and their count; NULL / 0 for a co-located rank (its sums are written in place). */
+int omr_ar_plan_shard(omr_ar_plan* plan, int* shard, uint64_t* row_begin, uint64_t* row_end, const float** sums,
+                      uint64_t* num_blocks);
 
 /* One round on this rank.  x: the rank's gradient (device, n floats).  out: receives the all-reduced tensor
  * (rank-order sums over the union of non-zero blocks plus lane heads); may equal x for the reference's in-place
@@ -129,6 +143,27 @@ int omr_sparse_buckets_f32(omr_ar_plan* plan, float* buf, uint64_t total_n, int 
                            uint64_t* union_blocks, omr_stream_t stream);
 /* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
 int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
+
+/* ---------------------------------------------------------------- the round as wire messages between processes
+ *
+ * The reference's message protocol between separate worker and aggregator processes: each
+ * worker packs its messages of every global slot gs (client.cc:180-205, :113-127; wire format common.cc:399-443)
+ * and sends them to aggregator gs % n (common.cc:381-383); aggregator j replies to its slots (server.cc:56-199,
+ * rank-order sums from +0.0f) and sends the replies to every worker, which applies them in place (client.cc:87-90).
+ * Roles as omr_ar_plan_create_roles (num_workers == world: every rank also aggregates; n = world; otherwise ranks
+ * >= num_workers are the n = world - num_workers aggregators).  num_lanes must be NUM_SLOTS*MESSAGE_SIZE/block_size.
+ * Logs: one 2*MESSAGE_SIZE-float message per (slot, protocol round), grown to the longest slot (about num_parts*16 *
+ * rows_per_part * 8 KiB per worker log at worst: a fidelity path for small tensors).  omr_msgd_round_f32
+ * synchronises `stream` once (the schedule's round counts size the transfers); an aggregator passes x = out = NULL.
+ * omr_msgd_logs: a worker's own log (worker == its rank) or, on an aggregator, the log it received from `worker`;
+ * the replies it holds (a worker: every slot's; an aggregator: its own slots'). */
+typedef struct omr_msgd_plan omr_msgd_plan;
+int omr_msgd_plan_create(omr_dist* d, uint32_t num_workers, uint64_t n, uint32_t block_size, uint32_t num_lanes,
+                         uint32_t num_parts, omr_msgd_plan** out);
+int omr_msgd_plan_destroy(omr_msgd_plan* plan);
+int omr_msgd_round_f32(omr_msgd_plan* plan, const float* x, float* out, uint32_t* max_rounds, omr_stream_t stream);
+int omr_msgd_logs(omr_msgd_plan* plan, uint32_t worker, float** messages, uint32_t** imm, float** replies,
+                  uint32_t** reply_imm, uint32_t** rounds, uint32_t* round_capacity);
 
 #ifdef __cplusplus
 }

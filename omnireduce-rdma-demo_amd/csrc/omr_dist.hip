@@ -552,6 +552,14 @@ struct omr_ar_plan {
   uint64_t n = 0, nb = 0, rows = 0;
   uint32_t B = 0, lanes = 0, parts = 0, rpp = 0;
   int N = 1, me = 0;
+  // roles: ranks [0, M) are workers; A aggregator shards.  Co-located (M == N): rank r is worker r AND the
+  // aggregator of shard r.  Dedicated (M < N): ranks M..N-1 aggregate shards 0..A-1 (A = N - M) and hold no tensor,
+  // the reference's separate ./server processes (README.md:13-22)
+  int M = 1, A = 1;
+  bool colocated = true;
+  int shard = 0;                  // this rank's shard, -1 for a worker that aggregates none
+  int agg_rank(int s) const { return colocated ? s : M + s; }
+  bool worker() const { return me < M; }
   std::vector<uint64_t> bounds;   // shard s = rows [bounds[s], bounds[s+1])
   uint64_t shard_nb = 0;          // blocks of the largest shard
   uint64_t* own_masks = nullptr;  // [rows] this rank's masks (the scan ORs into it; the plan kernel re-zeroes it)
@@ -574,7 +582,8 @@ struct omr_ar_plan {
   uint32_t* counts_host = nullptr;  // [2][N+1][N+1] per set: prefix[a][bounds[s]], pinned memory the plan kernel writes
   uint32_t* counts_map = nullptr;   // its device-side address
   float* recv = nullptr;     // this shard's blocks from each peer, peer-major
-  float* results = nullptr;  // all-reduce: every shard's sums, write-set order
+  float* results = nullptr;  // all-reduce: every shard's sums, write-set order (a dedicated aggregator: its own)
+  uint64_t last_sums_blocks = 0;  // a dedicated aggregator: blocks of its last round's shard sums in `results`
   int32_t* flags_ws = nullptr;
   uint32_t* next_ws = nullptr;
   uint32_t* unext_ws = nullptr;
@@ -730,11 +739,24 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
 
 int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
                        omr_ar_plan** out) {
+  if (d == nullptr) return derr(OMR_EINVAL, "ar_plan_create: NULL");
+  return omr_ar_plan_create_roles(d, static_cast<uint32_t>(d->world), n, block_size, num_lanes, num_parts, out);
+}
+
+int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint32_t block_size, uint32_t num_lanes,
+                             uint32_t num_parts, omr_ar_plan** out) {
   if (d == nullptr || out == nullptr) return derr(OMR_EINVAL, "ar_plan_create: NULL");
   *out = nullptr;
   TRY(omr_check(omr_layout_check(n, block_size, num_lanes, num_parts), "omr_layout_check"));
-  if (d->world > OMR_MAX_WORKERS) return derr(OMR_EINVAL, "ar_plan_create: world %d > %d", d->world, OMR_MAX_WORKERS);
+  if (num_workers == 0 || num_workers > static_cast<uint32_t>(d->world) || num_workers > OMR_MAX_WORKERS)
+    return derr(OMR_EINVAL, "ar_plan_create: %u workers in a world of %d (at most %d workers)", num_workers, d->world,
+                OMR_MAX_WORKERS);
+  const int naggs = num_workers == static_cast<uint32_t>(d->world) ? d->world : d->world - static_cast<int>(num_workers);
+  if (naggs > OMR_MAX_WORKERS) return derr(OMR_EINVAL, "ar_plan_create: %d aggregators > %d", naggs, OMR_MAX_WORKERS);
   auto* p = new omr_ar_plan();
+  p->M = static_cast<int>(num_workers);
+  p->A = naggs;
+  p->colocated = num_workers == static_cast<uint32_t>(d->world);
   p->d = d;
   p->n = n;
   p->B = block_size;
@@ -745,10 +767,11 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   p->rpp = static_cast<uint32_t>(p->rows / num_parts);
   p->N = d->world;
   p->me = d->rank;
-  const int N = p->N;
-  for (int s = 0; s <= N; ++s) p->bounds.push_back(static_cast<uint64_t>(s) * p->rows / N);
+  p->shard = p->colocated ? p->me : (p->me >= p->M ? p->me - p->M : -1);
+  const int N = p->N, M = p->M, NA = p->A;
+  for (int s = 0; s <= NA; ++s) p->bounds.push_back(static_cast<uint64_t>(s) * p->rows / NA);
   uint64_t max_rows = 0;
-  for (int s = 0; s < N; ++s) max_rows = std::max(max_rows, p->bounds[s + 1] - p->bounds[s]);
+  for (int s = 0; s < NA; ++s) max_rows = std::max(max_rows, p->bounds[s + 1] - p->bounds[s]);
   p->shard_nb = max_rows * num_lanes;
   int rc = 0;
   auto A = [&](int r) {
@@ -759,8 +782,8 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
     A(dev_alloc(&st.masks_all, static_cast<size_t>(N) * p->rows));
     A(dev_alloc(&st.wset, p->rows));
     A(dev_alloc(&st.umask, p->rows));
-    A(dev_alloc(&st.prefix, static_cast<size_t>(N + 1) * (p->rows + 1)));
-    if (N > 1) A(dev_alloc(&st.packed, n));
+    A(dev_alloc(&st.prefix, static_cast<size_t>(M + 1) * (p->rows + 1)));
+    if (N > 1 && p->worker()) A(dev_alloc(&st.packed, n));
     A(hip_check(hipEventCreateWithFlags(&st.ready, hipEventDisableTiming), "hipEventCreate"));
     A(hip_check(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "hipEventCreate"));
   }
@@ -768,15 +791,15 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, hipEventDisableTiming), "hipEventCreate"));
   A(hip_check(hipEventCreate(&p->xt0), "hipEventCreate"));
   A(hip_check(hipEventCreate(&p->xt1), "hipEventCreate"));
-  A(dev_alloc(&p->bounds_dev, N + 1));
-  if (N > 1) A(dev_alloc(&p->recv, static_cast<size_t>(N - 1) * p->shard_nb * block_size));
+  A(dev_alloc(&p->bounds_dev, NA + 1));
+  if (N > 1 && p->shard >= 0) A(dev_alloc(&p->recv, static_cast<size_t>(M) * p->shard_nb * block_size));
   A(dev_alloc(&p->results, n));
   A(dev_alloc(&p->flags_ws, p->nb));
   A(dev_alloc(&p->next_ws, p->nb));
   A(dev_alloc(&p->unext_ws, p->nb));
   p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
   A(dev_alloc(reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
-  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), 2 * (N + 1) * (N + 1) * sizeof(uint32_t),
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), 2 * (M + 1) * (NA + 1) * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0)
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->counts_map), p->counts_host, 0),
@@ -793,7 +816,7 @@ int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t nu
   if (rc == 0) A(hip_check(hipMemset(p->own_masks, 0, p->rows * sizeof(uint64_t)), "hipMemset own masks"));
   if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset scan ws"));
   if (rc == 0)
-    A(hip_check(hipMemcpy(p->bounds_dev, p->bounds.data(), (N + 1) * sizeof(uint64_t), hipMemcpyHostToDevice),
+    A(hip_check(hipMemcpy(p->bounds_dev, p->bounds.data(), (NA + 1) * sizeof(uint64_t), hipMemcpyHostToDevice),
                 "hipMemcpy bounds"));
   if (rc == 0) A(hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize"));
   if (rc != 0) {
@@ -813,20 +836,22 @@ namespace {
 int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, bool async, bool timed, uint32_t seq,
                  hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks) {
   omr_ar_plan::Set& S = p->set[si];
-  const int N = p->N, me = p->me;
+  const int N = p->N, M = p->M, NA = p->A, me = p->me, sh = p->shard;
   const uint64_t rows = p->rows, B = p->B;
-  const uint32_t NB = N + 1;
-  const uint32_t* counts = p->counts_host + static_cast<size_t>(si) * NB * NB;
+  const uint32_t NS = static_cast<uint32_t>(NA + 1);  // count columns per array (shard bounds)
+  const uint32_t* counts = p->counts_host + static_cast<size_t>(si) * (M + 1) * NS;
   const uint32_t* flag = p->flag_host + si;
-  const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
   hipStream_t xs = st;
   if (async) {
     TRY(hip_check(hipStreamWaitEvent(p->cs, S.ready, 0), "hipStreamWaitEvent"));
     xs = p->cs;
   }
   const omr_stream_t xstream = reinterpret_cast<omr_stream_t>(xs);
-  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER) {
+  auto cnt = [&](int a, int s) -> uint64_t { return counts[a * NS + s]; };
+  auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
+  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER) {  // co-located only (checked by the caller)
     // the dense stand-in: every element of this rank's shard, reduced over all ranks by the transport
+    const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
     const uint64_t row_floats = static_cast<uint64_t>(p->lanes) * B;
     if (timed) TRY(hip_check(hipEventRecord(p->xt0, xs), "hipEventRecord"));
     TRY(p->d->reduce_scatter(x, out + r0 * row_floats, (r1 - r0) * row_floats, xs));
@@ -843,56 +868,76 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     }
     if (sent_blocks != nullptr || union_blocks != nullptr) TRY(wait_flag(flag, seq, st));
     if (sent_blocks) *sent_blocks = (r1 - r0) * p->lanes * static_cast<uint64_t>(N - 1);
-    if (union_blocks) *union_blocks = counts[N * NB + me + 1] - counts[N * NB + me];
+    if (union_blocks) *union_blocks = per(M, me);
     return 0;
   }
   TRY(wait_flag(flag, seq, st));
-  auto cnt = [&](int a, int s) -> uint64_t { return counts[a * NB + s]; };
-  auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
-  const uint64_t own_shard = per(me, me);
-  const uint64_t total_send = cnt(me, N) - own_shard;
-  // 4b. send each slice to its aggregator (common.cc:449); receive this shard's blocks from every peer
-  std::vector<uint64_t> roff(N, 0);
+  const bool wk = p->worker();
+  // a co-located rank keeps its own shard's blocks out of its packed stream (and reads them in place)
+  const uint64_t own_shard = (wk && p->colocated) ? per(me, me) : 0;
+  const uint64_t total_send = wk ? cnt(me, NA) - own_shard : 0;
+  // 4b. workers send each shard's slice to its aggregator (common.cc:449); an aggregator receives its shard's blocks
+  //     from every worker but itself
+  std::vector<uint64_t> roff(M, 0);
+  uint64_t in_blocks = 0;
   if (timed) TRY(hip_check(hipEventRecord(p->xt0, xs), "hipEventRecord"));
   if (N > 1) {
     std::vector<Slices> sends(N), recvs(N);
-    uint64_t acc = 0;
-    for (int s = 0; s < N; ++s) {
-      const uint64_t k0 = cnt(me, s) - (s > me ? own_shard : 0);
-      sends[s] = {Slice{S.packed + k0 * B, s == me ? 0 : per(me, s) * B * sizeof(float)}};
-      roff[s] = acc;
-      recvs[s] = {Slice{p->recv + acc * B, s == me ? 0 : per(s, me) * B * sizeof(float)}};
-      if (s != me) acc += per(s, me);
-    }
+    if (wk)
+      for (int s = 0; s < NA; ++s) {
+        const int ar = p->agg_rank(s);
+        if (ar == me) continue;
+        const uint64_t k0 = cnt(me, s) - (p->colocated && s > me ? own_shard : 0);
+        sends[ar] = {Slice{S.packed + k0 * B, per(me, s) * B * sizeof(float)}};
+      }
+    if (sh >= 0)
+      for (int w = 0; w < M; ++w) {
+        if (w == me) continue;
+        roff[w] = in_blocks;
+        recvs[w] = {Slice{p->recv + in_blocks * B, per(w, sh) * B * sizeof(float)}};
+        in_blocks += per(w, sh);
+      }
     TRY(p->d->exchange(sends, recvs, xs));
   }
   if (timed) {
     TRY(hip_check(hipEventRecord(p->xt1, xs), "hipEventRecord"));
-    uint64_t in_blocks = 0;
-    for (int s = 0; s < N; ++s)
-      if (s != me) in_blocks += per(s, me);
     p->xt_out = total_send * B * sizeof(float);
     p->xt_in = in_blocks * B * sizeof(float);
     p->xt_recorded = true;
   }
-  // 5. aggregator: rank-order shard sums (server.cc:97-98), own contribution read in place
   const bool rs_mode = mode == OMR_ROUND_REDUCE_SCATTER;
-  float* sums = rs_mode ? out : p->results + cnt(N, me) * B;
-  TRY(omr_check(omr_shard_sum_f32(x, static_cast<uint32_t>(me), p->recv, roff.data(), S.masks_all, N, S.prefix,
-                                  S.wset, rows, r0, r1, p->lanes, p->B, rs_mode ? 0 : 1, sums, xstream),
-                "omr_shard_sum_f32"));
+  // 5. aggregator: rank-order shard sums (server.cc:97-98); a co-located rank reads its own blocks in place.
+  //    Co-located reduce-scatter writes them in place (dense); otherwise packed in write-set order
+  float* sums = nullptr;
+  if (sh >= 0) {
+    const uint64_t r0 = p->bounds[sh], r1 = p->bounds[sh + 1];
+    const bool dense_out = rs_mode && p->colocated;
+    // (a dedicated aggregator keeps only its own shard's sums: at the start of `results`)
+    sums = dense_out ? out : p->results + (wk ? cnt(M, sh) * B : 0);
+    TRY(omr_check(omr_shard_sum_f32(p->colocated ? x : nullptr, p->colocated ? static_cast<uint32_t>(me)
+                                                                             : static_cast<uint32_t>(M),
+                                    p->recv, roff.data(), S.masks_all, static_cast<uint32_t>(M), S.prefix, S.wset,
+                                    rows, r0, r1, p->lanes, p->B, dense_out ? 0 : 1, sums, xstream),
+                  "omr_shard_sum_f32"));
+    if (!p->colocated) p->last_sums_blocks = per(M, sh);
+  }
   if (!rs_mode) {
     // 6. sums back to every worker (server.cc:162), scattered in place (client.cc:89)
     if (N > 1) {
       std::vector<Slices> ss(N), sr(N);
-      for (int s = 0; s < N; ++s) {
-        ss[s] = {Slice{sums, s == me ? 0 : per(N, me) * B * sizeof(float)}};
-        sr[s] = {Slice{p->results + cnt(N, s) * B, s == me ? 0 : per(N, s) * B * sizeof(float)}};
-      }
+      if (sh >= 0)
+        for (int w = 0; w < M; ++w)
+          if (w != me) ss[w] = {Slice{sums, per(M, sh) * B * sizeof(float)}};
+      if (wk)
+        for (int s = 0; s < NA; ++s) {
+          const int ar = p->agg_rank(s);
+          if (ar != me) sr[ar] = {Slice{p->results + cnt(M, s) * B, per(M, s) * B * sizeof(float)}};
+        }
       TRY(p->d->exchange(ss, sr, xs));
     }
-    TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, S.wset, S.prefix + static_cast<uint64_t>(N) * (rows + 1),
-                                      rows, p->lanes, p->B, 0, 0, xstream), "omr_move_blocks_f32 unpack"));
+    if (wk && out != nullptr)
+      TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, S.wset, S.prefix + static_cast<uint64_t>(M) * (rows + 1),
+                                        rows, p->lanes, p->B, 0, 0, xstream), "omr_move_blocks_f32 unpack"));
   }
   if (async) {
     TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
@@ -900,7 +945,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     p->last_async = si;
   }
   if (sent_blocks) *sent_blocks = total_send;
-  if (union_blocks) *union_blocks = rs_mode ? per(N, me) : cnt(N, N);
+  if (union_blocks) *union_blocks = (rs_mode || !wk) ? (sh >= 0 ? per(M, sh) : 0) : cnt(M, NA);
   return 0;
 }
 
@@ -925,20 +970,23 @@ extern "C" {
 int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
                          uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
                          omr_stream_t stream) {
-  if (p == nullptr || x == nullptr || out == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL");
+  if (p == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL plan");
+  if (p->worker() && (x == nullptr || out == nullptr)) return derr(OMR_EINVAL, "sparse_round: a worker needs x and out");
   const bool defer = (mode & OMR_ROUND_DEFER) != 0;
   const bool async = defer || (mode & OMR_ROUND_ASYNC) != 0;
   const bool timed = (mode & OMR_ROUND_TIME_EXCHANGE) != 0;
   mode &= ~(OMR_ROUND_ASYNC | OMR_ROUND_DEFER | OMR_ROUND_TIME_EXCHANGE);
   if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
     return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
+  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && !p->colocated)
+    return derr(OMR_EINVAL, "sparse_round: the dense reduce-scatter stand-in needs every rank to be a worker");
   if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && p->rows % p->N != 0)
     return derr(OMR_EINVAL, "sparse_round: dense reduce-scatter needs equal shards (rows %llu, world %d)",
                 static_cast<unsigned long long>(p->rows), p->N);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int N = p->N, me = p->me;
+  const int N = p->N, M = p->M, me = p->me;
   const uint64_t rows = p->rows;
-  const uint32_t NB = N + 1;
+  const uint32_t NS = static_cast<uint32_t>(p->A + 1);
   int32_t* fl = flags ? flags : p->flags_ws;
   uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
   uint32_t* un = union_next ? union_next : p->unext_ws;
@@ -959,9 +1007,11 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   const int si = p->cur;
   omr_ar_plan::Set& S = p->set[si];
   p->cur ^= 1;
-  // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass
-  TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, p->own_masks, nullptr, p->scan_ws,
-                                    p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+  // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass (a dedicated aggregator
+  //    offers its all-zero mask buffer to the all-gather)
+  if (p->worker())
+    TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, p->own_masks, nullptr, p->scan_ws,
+                                      p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
   // the set is refilled from here on: an asynchronous round two calls back must be through with it
   // (skipped when the host already sees the event complete: a stream-wait packet costs the GPU a few
   // microseconds of dispatch even when its event has long fired)
@@ -976,19 +1026,21 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for the next round
   //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
   const uint32_t seq = ++p->seq;
-  TRY(omr_check(omr_round_plan(S.masks_all, N, rows, p->rpp, p->lanes, p->bounds_dev, NB, S.wset, S.umask,
-                               S.prefix, p->counts_map + static_cast<size_t>(si) * NB * NB, p->own_masks, p->arrive,
-                               p->flag_map + si, seq, stream),
+  TRY(omr_check(omr_round_plan(S.masks_all, static_cast<uint32_t>(M), rows, p->rpp, p->lanes, p->bounds_dev, NS,
+                               S.wset, S.umask, S.prefix,
+                               p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, p->own_masks,
+                               p->arrive, p->flag_map + si, seq, stream),
                 "omr_round_plan"));
   // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407), then the
   //     aggregator chain (server.cc:86-96 min_next) over the union: both addressed by device-side data only, so
   //     they are queued before the host learns the counts and run while it waits.  (Every host API call costs
   //     microseconds; a round that spends them on side streams and events is host-bound.)
-  const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
-  if (N > 1 && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
+  if (N > 1 && mode != OMR_ROUND_DENSE_REDUCE_SCATTER && p->worker()) {
+    const uint64_t r0 = p->colocated ? p->bounds[me] : 0, r1 = p->colocated ? p->bounds[me + 1] : 0;
     TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * rows,
                                       S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
                                       r1, stream), "omr_move_blocks_f32 pack"));
+  }
   TRY(omr_check(omr_next_offsets(S.umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
   // the rest goes on the communication stream for an asynchronous round, behind everything queued so far
   if (async) TRY(hip_check(hipEventRecord(S.ready, st), "hipEventRecord"));
@@ -1062,8 +1114,10 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   // reduce-scatter returns only this rank's shard: only those rows travel back
   const uint64_t row_floats = static_cast<uint64_t>(p->lanes) * p->B;
   const bool rs = mode == OMR_ROUND_REDUCE_SCATTER;
-  const uint64_t back0 = rs ? p->bounds[p->me] * row_floats : 0;
-  const uint64_t back_n = rs ? (p->bounds[p->me + 1] - p->bounds[p->me]) * row_floats : p->n;
+  if (!p->worker()) return derr(OMR_EINVAL, "sparse_buckets: a worker's call (this rank aggregates only)");
+  const bool own_rs = rs && p->shard >= 0;  // co-located: the shard's sums land in place
+  const uint64_t back0 = own_rs ? p->bounds[p->shard] * row_floats : 0;
+  const uint64_t back_n = rs ? (own_rs ? (p->bounds[p->shard + 1] - p->bounds[p->shard]) * row_floats : 0) : p->n;
   auto h2d = [&](uint64_t k) -> int {
     const int r = static_cast<int>(k % R);
     if (p->out_used[r]) TRY(hip_check(hipStreamWaitEvent(p->s_in, p->ev_out[r], 0), "hipStreamWaitEvent"));
@@ -1100,6 +1154,17 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   return 0;
 }
 
+int omr_ar_plan_shard(omr_ar_plan* p, int* shard, uint64_t* row_begin, uint64_t* row_end, const float** sums,
+                      uint64_t* num_blocks) {
+  if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_shard: NULL");
+  if (shard) *shard = p->shard;
+  if (row_begin) *row_begin = p->shard >= 0 ? p->bounds[p->shard] : 0;
+  if (row_end) *row_end = p->shard >= 0 ? p->bounds[p->shard + 1] : 0;
+  if (sums) *sums = p->colocated ? nullptr : p->results;
+  if (num_blocks) *num_blocks = p->colocated ? 0 : p->last_sums_blocks;
+  return 0;
+}
+
 int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_join: NULL");
   TRY(flush_pending(p, reinterpret_cast<hipStream_t>(stream), nullptr, nullptr));
@@ -1125,6 +1190,278 @@ int omr_sparse_allreduce_f32(omr_ar_plan* p, const float* x, float* out, int32_t
                              omr_stream_t stream) {
   return omr_sparse_round_f32(p, x, out, flags, next_offsets, union_next, OMR_ROUND_ALLREDUCE, sent_blocks,
                               union_blocks, stream);
+}
+
+}  // extern "C"
+
+// ================================================================ message-level round over a transport
+//
+// The reference's wire messages (common.cc:374-476 -> server.cc:56-199) between worker and aggregator processes:
+// every rank computes the same per-slot schedule from the all-gathered row masks; each worker packs its messages of
+// every slot (omr_msg_pack_f32) and sends aggregator j the slots gs with gs % n == j (common.cc:381-383); aggregator
+// j builds their replies (omr_msg_aggregate_f32) and sends them to every worker, which applies them in place
+// (omr_msg_unpack_f32).  Logs hold one 2*MESSAGE_SIZE-float message per (slot, protocol round); a slot's rounds are
+// contiguous, so one transport piece per (slot, peer) carries all of them.
+struct omr_msgd_plan {
+  omr_dist* d = nullptr;
+  int N = 1, M = 1, A = 1, me = 0, agg = -1;  // world, workers, aggregators, rank, this rank's aggregator index
+  bool colocated = true;
+  uint64_t n = 0, nb = 0, rows = 0;
+  uint32_t B = 0, NB = 0, parts = 0, G = 0, rcap = 0;
+  uint64_t* own_masks = nullptr;  // [rows]
+  uint64_t* masks_all = nullptr;  // [N][rows]
+  uint64_t* umask = nullptr;      // [rows]
+  uint32_t* unext = nullptr;      // [nb]
+  int32_t* flags = nullptr;       // [nb]
+  uint32_t* next = nullptr;       // [nb]
+  void* scan_ws = nullptr;
+  size_t scan_ws_bytes = 0;
+  char* sched = nullptr;          // [G][rcap] schedule records
+  uint32_t* rounds = nullptr;     // [G]
+  uint32_t* maxr = nullptr;       // [1]
+  uint32_t* host_r = nullptr;     // pinned [G + 1]: rounds, then the max
+  float* msgs = nullptr;          // a worker's own log [G][rcap][2*MESSAGE_SIZE]
+  uint32_t* imm = nullptr;        // [G][rcap]
+  std::vector<float*> wmsgs;      // an aggregator's copy of every worker's log (its slots filled)
+  std::vector<uint32_t*> wimm;
+  float* reply = nullptr;         // replies: an aggregator's own slots; a worker: every slot's, received
+  uint32_t* rimm = nullptr;
+  int agg_rank(uint32_t gs) const { return colocated ? static_cast<int>(gs % A) : M + static_cast<int>(gs % A); }
+  bool worker() const { return me < M; }
+};
+
+namespace {
+
+constexpr uint32_t kMsgW = 2 * OMR_MESSAGE_SIZE;
+
+void msgd_free_logs(omr_msgd_plan* p) {
+  (void)hipFree(p->sched);
+  (void)hipFree(p->msgs);
+  (void)hipFree(p->imm);
+  (void)hipFree(p->reply);
+  (void)hipFree(p->rimm);
+  for (float* v : p->wmsgs) (void)hipFree(v);
+  for (uint32_t* v : p->wimm) (void)hipFree(v);
+  p->sched = nullptr;
+  p->msgs = nullptr;
+  p->imm = nullptr;
+  p->reply = nullptr;
+  p->rimm = nullptr;
+  p->wmsgs.assign(p->wmsgs.size(), nullptr);
+  p->wimm.assign(p->wimm.size(), nullptr);
+}
+
+int msgd_alloc_logs(omr_msgd_plan* p, uint32_t rcap) {
+  msgd_free_logs(p);
+  const uint64_t units = static_cast<uint64_t>(p->G) * rcap;
+  TRY(dev_alloc(&p->sched, units * omr_msg_sched_bytes()));
+  if (p->worker()) {
+    TRY(dev_alloc(&p->msgs, units * kMsgW));
+    TRY(dev_alloc(&p->imm, units));
+  }
+  TRY(dev_alloc(&p->reply, units * kMsgW));
+  TRY(dev_alloc(&p->rimm, units));
+  if (p->agg >= 0)
+    for (int w = 0; w < p->M; ++w) {
+      if (w == p->me) continue;  // a co-located aggregator reads its own worker's log in place
+      TRY(dev_alloc(&p->wmsgs[w], units * kMsgW));
+      TRY(dev_alloc(&p->wimm[w], units));
+    }
+  p->rcap = rcap;
+  return 0;
+}
+
+// the schedule, its round counts on the host (one synchronisation: the transport needs the pieces' sizes), and
+// the logs grown until they hold the longest slot; identical on every rank (same masks)
+int msgd_schedule(omr_msgd_plan* p, hipStream_t st) {
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    TRY(omr_check(omr_msg_schedule(p->masks_all, static_cast<uint32_t>(p->M), p->unext, p->n, p->B, p->NB, p->parts,
+                                   p->rcap, p->sched, p->rounds, p->maxr, reinterpret_cast<omr_stream_t>(st)),
+                  "omr_msg_schedule"));
+    TRY(hip_check(hipMemcpyAsync(p->host_r, p->rounds, p->G * sizeof(uint32_t), hipMemcpyDeviceToHost, st),
+                  "hipMemcpyAsync"));
+    TRY(hip_check(hipMemcpyAsync(p->host_r + p->G, p->maxr, sizeof(uint32_t), hipMemcpyDeviceToHost, st),
+                  "hipMemcpyAsync"));
+    TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
+    if (p->host_r[p->G] <= p->rcap) return 0;
+    uint32_t cap = p->rcap;
+    const uint32_t rpp = static_cast<uint32_t>(p->rows / p->parts);
+    while (cap < rpp + 2) cap *= 2;  // a lane carries at most its head plus rows_per_part - 1 blocks
+    TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
+    TRY(msgd_alloc_logs(p, cap));
+  }
+  return derr(OMR_EINVAL, "msgd: %u protocol rounds exceed the logs' %u", p->host_r[p->G], p->rcap);
+}
+
+}  // namespace
+
+extern "C" {
+
+int omr_msgd_plan_destroy(omr_msgd_plan* p) {
+  if (p == nullptr) return 0;
+  (void)hipDeviceSynchronize();
+  msgd_free_logs(p);
+  void* devs[] = {p->own_masks, p->masks_all, p->umask, p->unext, p->flags, p->next, p->scan_ws, p->rounds, p->maxr};
+  for (void* v : devs) (void)hipFree(v);
+  (void)hipHostFree(p->host_r);
+  delete p;
+  return 0;
+}
+
+int omr_msgd_plan_create(omr_dist* d, uint32_t num_workers, uint64_t n, uint32_t block_size, uint32_t num_lanes,
+                         uint32_t num_parts, omr_msgd_plan** out) {
+  if (d == nullptr || out == nullptr) return derr(OMR_EINVAL, "msgd_plan_create: NULL");
+  *out = nullptr;
+  TRY(omr_check(omr_layout_check(n, block_size, num_lanes, num_parts), "omr_layout_check"));
+  if (num_lanes != OMR_NUM_SLOTS * (OMR_MESSAGE_SIZE / block_size))
+    return derr(OMR_EINVAL, "msgd_plan_create: num_lanes must be NUM_SLOTS*MESSAGE_SIZE/BLOCK_SIZE");
+  if (num_workers == 0 || num_workers > static_cast<uint32_t>(d->world) || num_workers > OMR_MAX_WORKERS)
+    return derr(OMR_EINVAL, "msgd_plan_create: %u workers in a world of %d", num_workers, d->world);
+  auto* p = new omr_msgd_plan();
+  p->d = d;
+  p->N = d->world;
+  p->M = static_cast<int>(num_workers);
+  p->colocated = p->M == p->N;
+  p->A = p->colocated ? p->N : p->N - p->M;
+  p->me = d->rank;
+  p->agg = p->colocated ? p->me : (p->me >= p->M ? p->me - p->M : -1);
+  p->n = n;
+  p->B = block_size;
+  p->NB = num_lanes;
+  p->parts = num_parts;
+  p->nb = n / block_size;
+  p->rows = p->nb / num_lanes;
+  p->G = num_parts * OMR_NUM_SLOTS;
+  p->wmsgs.assign(p->M, nullptr);
+  p->wimm.assign(p->M, nullptr);
+  int rc = 0;
+  auto A = [&](int r) {
+    if (rc == 0) rc = r;
+  };
+  A(dev_alloc(&p->own_masks, p->rows));
+  A(dev_alloc(&p->masks_all, static_cast<size_t>(p->N) * p->rows));
+  A(dev_alloc(&p->umask, p->rows));
+  A(dev_alloc(&p->unext, p->nb));
+  A(dev_alloc(&p->flags, p->nb));
+  A(dev_alloc(&p->next, p->nb));
+  p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
+  A(dev_alloc(reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
+  A(dev_alloc(&p->rounds, p->G));
+  A(dev_alloc(&p->maxr, 1));
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->host_r), (p->G + 1) * sizeof(uint32_t)), "hipHostMalloc"));
+  if (rc == 0) A(hip_check(hipMemset(p->own_masks, 0, p->rows * sizeof(uint64_t)), "hipMemset"));
+  if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset"));
+  if (rc == 0) A(msgd_alloc_logs(p, 16));
+  if (rc == 0) A(hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize"));
+  if (rc != 0) {
+    omr_msgd_plan_destroy(p);
+    return rc;
+  }
+  *out = p;
+  return 0;
+}
+
+int omr_msgd_round_f32(omr_msgd_plan* p, const float* x, float* out, uint32_t* max_rounds, omr_stream_t stream) {
+  if (p == nullptr) return derr(OMR_EINVAL, "msgd_round: NULL plan");
+  if (p->worker() && (x == nullptr || out == nullptr)) return derr(OMR_EINVAL, "msgd_round: a worker needs x and out");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint64_t rows = p->rows;
+  // 1. worker scan: flags, next chain (client.cc:19-31), row masks
+  if (p->worker()) {
+    TRY(hip_check(hipMemsetAsync(p->own_masks, 0, rows * sizeof(uint64_t), st), "hipMemsetAsync"));
+    TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->NB, p->parts, p->flags, p->next, p->own_masks, nullptr,
+                                      p->scan_ws, p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+  }
+  // 2. every rank learns every worker's masks; 3. the aggregator chain over their union (server.cc:86-96)
+  TRY(p->d->allgather(p->own_masks, p->masks_all, rows * sizeof(uint64_t), st));
+  TRY(omr_check(omr_mask_union(p->masks_all, static_cast<uint32_t>(p->M), rows, static_cast<uint32_t>(rows / p->parts),
+                               p->NB, 0, p->umask, stream), "omr_mask_union"));
+  TRY(omr_check(omr_next_offsets(p->umask, 1, p->n, p->B, p->NB, p->parts, p->unext, stream), "omr_next_offsets"));
+  // 4. the per-slot schedule (the same on every rank)
+  TRY(msgd_schedule(p, st));
+  const uint32_t G = p->G, cap = p->rcap;
+  const uint32_t* R = p->host_r;
+  const size_t mb = static_cast<size_t>(kMsgW) * sizeof(float);
+  auto msg_piece = [&](float* log, uint32_t gs) { return Slice{log + static_cast<uint64_t>(gs) * cap * kMsgW, R[gs] * mb}; };
+  auto imm_piece = [&](uint32_t* log, uint32_t gs) {
+    return Slice{log + static_cast<uint64_t>(gs) * cap, R[gs] * sizeof(uint32_t)};
+  };
+  // 5. a worker's messages of every slot (client.cc:180-205, :113-127; common.cc:399-408)
+  if (p->worker())
+    TRY(omr_check(omr_msg_pack_f32(x, p->flags, p->next, p->sched, p->rounds, p->parts, cap, p->B, p->msgs, p->imm,
+                                   stream), "omr_msg_pack_f32"));
+  // 6. workers -> the aggregator of each slot (common.cc:381-383, :449)
+  {
+    std::vector<Slices> sends(p->N), recvs(p->N);
+    if (p->worker())
+      for (uint32_t gs = 0; gs < G; ++gs) {
+        const int a = p->agg_rank(gs);
+        if (a == p->me) continue;
+        sends[a].push_back(msg_piece(p->msgs, gs));
+        sends[a].push_back(imm_piece(p->imm, gs));
+      }
+    if (p->agg >= 0)
+      for (int w = 0; w < p->M; ++w) {
+        if (w == p->me) continue;
+        for (uint32_t gs = static_cast<uint32_t>(p->agg); gs < G; gs += static_cast<uint32_t>(p->A)) {
+          recvs[w].push_back(msg_piece(p->wmsgs[w], gs));
+          recvs[w].push_back(imm_piece(p->wimm[w], gs));
+        }
+      }
+    TRY(p->d->exchange(sends, recvs, st));
+  }
+  // 7. the aggregator's replies to its slots (server.cc:68-162)
+  if (p->agg >= 0) {
+    std::vector<const float*> wm(p->M);
+    std::vector<const uint32_t*> wi(p->M);
+    for (int w = 0; w < p->M; ++w) {
+      wm[w] = w == p->me ? p->msgs : p->wmsgs[w];
+      wi[w] = w == p->me ? p->imm : p->wimm[w];
+    }
+    TRY(omr_check(omr_msg_aggregate_f32(wm.data(), wi.data(), static_cast<uint32_t>(p->M), p->sched, p->rounds,
+                                        p->unext, p->parts, cap, p->B, p->NB, static_cast<uint32_t>(p->A),
+                                        static_cast<uint32_t>(p->agg), p->reply, p->rimm, stream),
+                  "omr_msg_aggregate_f32"));
+  }
+  // 8. replies -> every worker (server.cc:162, common.cc:548)
+  {
+    std::vector<Slices> sends(p->N), recvs(p->N);
+    if (p->agg >= 0)
+      for (int w = 0; w < p->M; ++w) {
+        if (w == p->me) continue;
+        for (uint32_t gs = static_cast<uint32_t>(p->agg); gs < G; gs += static_cast<uint32_t>(p->A)) {
+          sends[w].push_back(msg_piece(p->reply, gs));
+          sends[w].push_back(imm_piece(p->rimm, gs));
+        }
+      }
+    if (p->worker())
+      for (uint32_t gs = 0; gs < G; ++gs) {
+        const int a = p->agg_rank(gs);
+        if (a == p->me) continue;
+        recvs[a].push_back(msg_piece(p->reply, gs));
+        recvs[a].push_back(imm_piece(p->rimm, gs));
+      }
+    TRY(p->d->exchange(sends, recvs, st));
+  }
+  // 9. the worker applies every reply in place (client.cc:87-90)
+  if (p->worker())
+    TRY(omr_check(omr_msg_unpack_f32(p->reply, p->rimm, p->sched, p->rounds, p->parts, cap, p->B, p->NB, out, stream),
+                  "omr_msg_unpack_f32"));
+  if (max_rounds) *max_rounds = R[G];
+  return 0;
+}
+
+int omr_msgd_logs(omr_msgd_plan* p, uint32_t worker, float** messages, uint32_t** imm, float** replies,
+                  uint32_t** reply_imm, uint32_t** rounds, uint32_t* round_capacity) {
+  if (p == nullptr || worker >= static_cast<uint32_t>(p->M)) return derr(OMR_EINVAL, "msgd_logs: bad plan or worker");
+  const bool own = static_cast<int>(worker) == p->me;
+  if (messages) *messages = own ? p->msgs : p->wmsgs[worker];
+  if (imm) *imm = own ? p->imm : p->wimm[worker];
+  if (replies) *replies = p->reply;
+  if (reply_imm) *reply_imm = p->rimm;
+  if (rounds) *rounds = p->rounds;
+  if (round_capacity) *round_capacity = p->rcap;
+  return 0;
 }
 
 }  // extern "C"

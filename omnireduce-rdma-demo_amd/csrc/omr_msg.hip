@@ -72,9 +72,9 @@ struct Sched {
 __device__ __forceinline__ uint32_t nib(uint32_t packed, uint32_t p) { return (packed >> (4 * p)) & 0xFu; }
 
 struct SchedArgs {
-  const int32_t* flags;   // [m][nb]
+  const uint64_t* masks;  // [m][rows] the workers' row masks (bit l of row r: block r*NB + l is non-zero)
   const uint32_t* unext;  // [nb] next offsets over the workers' union (the aggregator's min_next chain)
-  uint64_t nb;
+  uint64_t rows;
   uint32_t m, B, NB, rpp, parts, rcap, sentinel;
   Sched* sch;             // [G][rcap]
   uint32_t* rounds;       // [G]
@@ -102,7 +102,8 @@ __global__ __launch_bounds__(64) void k_msg_schedule(SchedArgs a) {
       const uint32_t j = nib(ord, p);
       uint32_t k = a.m - 1;
       if (r > 0)
-        while (k > 0 && a.flags[static_cast<uint64_t>(k) * a.nb + cur[j]] != 1) --k;
+        while (k > 0 && ((a.masks[static_cast<uint64_t>(k) * a.rows + cur[j] / a.NB] >> (cur[j] % a.NB)) & 1u) == 0)
+          --k;
       key[j] = k;
     }
     // reply order: the message order stably sorted by completion rank (server.cc:92-96 appends on completion)
@@ -185,6 +186,7 @@ struct AggArgs {
   float* reply;    // [G][rcap][kSlotW]
   uint32_t* rimm;  // [G][rcap]
   uint32_t m, G, rcap, B, NB;
+  uint32_t naggs, agg;  // this aggregator handles the global slots gs with gs % naggs == agg (common.cc:381-383)
 };
 
 template <int VEC>
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_msg_aggregate(AggArgs a) {
   const uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
   if (u >= static_cast<uint64_t>(a.G) * a.rcap) return;
   const uint32_t gs = static_cast<uint32_t>(u / a.rcap), r = static_cast<uint32_t>(u % a.rcap);
-  if (r >= a.rounds[gs]) return;
+  if (gs % a.naggs != a.agg || r >= a.rounds[gs]) return;
   const Sched rec = a.sch[u];
   const uint32_t lane0 = (gs % kSlots) * BPM;
   v4f acc[BPM][VEC];
@@ -331,26 +333,115 @@ int alloc_logs(omr_msg_plan* p, uint32_t rcap) {
   return 0;
 }
 
-int launch_schedule(omr_msg_plan* p, hipStream_t st) {
-  MTRY(hipc(hipMemsetAsync(p->maxr, 0, sizeof(uint32_t), st), "hipMemsetAsync"));
+int run_schedule(const uint64_t* masks, uint32_t m, uint64_t rows, const uint32_t* unext, uint32_t B, uint32_t NB,
+                 uint32_t rpp, uint32_t parts, uint32_t rcap, Sched* sch, uint32_t* rounds, uint32_t* maxr,
+                 hipStream_t st) {
+  MTRY(hipc(hipMemsetAsync(maxr, 0, sizeof(uint32_t), st), "hipMemsetAsync"));
   SchedArgs a;
-  a.flags = p->flags;
-  a.unext = p->unext;
-  a.nb = p->nb;
-  a.m = p->m;
-  a.B = p->B;
-  a.NB = p->NB;
-  a.rpp = p->rpp;
-  a.parts = p->parts;
-  a.rcap = p->rcap;
-  a.sentinel = omr_sentinel(p->B, p->NB);
-  a.sch = p->sch;
-  a.rounds = p->rounds;
-  a.maxr = p->maxr;
-  k_msg_schedule<<<(p->G + 63) / 64, 64, 0, st>>>(a);
-  MTRY(mlaunch("k_msg_schedule"));
+  a.masks = masks;
+  a.unext = unext;
+  a.rows = rows;
+  a.m = m;
+  a.B = B;
+  a.NB = NB;
+  a.rpp = rpp;
+  a.parts = parts;
+  a.rcap = rcap;
+  a.sentinel = omr_sentinel(B, NB);
+  a.sch = sch;
+  a.rounds = rounds;
+  a.maxr = maxr;
+  const uint32_t G = parts * kSlots;
+  k_msg_schedule<<<(G + 63) / 64, 64, 0, st>>>(a);
+  return mlaunch("k_msg_schedule");
+}
+
+int launch_schedule(omr_msg_plan* p, hipStream_t st) {
+  MTRY(run_schedule(p->masks, p->m, p->rows, p->unext, p->B, p->NB, p->rpp, p->parts, p->rcap, p->sch, p->rounds,
+                    p->maxr, st));
   MTRY(hipc(hipMemcpyAsync(p->maxr_host, p->maxr, sizeof(uint32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync"));
   return hipc(hipStreamSynchronize(st), "hipStreamSynchronize");
+}
+
+int run_pack(const float* x, const int32_t* flags, const uint32_t* next, const Sched* sch, const uint32_t* rounds,
+             uint32_t G, uint32_t rcap, uint32_t B, float* msgs, uint32_t* imm, hipStream_t st) {
+  PackArgs a;
+  a.x = x;
+  a.flags = flags;
+  a.next = next;
+  a.sch = sch;
+  a.rounds = rounds;
+  a.msgs = msgs;
+  a.imm = imm;
+  a.G = G;
+  a.rcap = rcap;
+  a.B = B;
+  const unsigned g = waves_grid(static_cast<uint64_t>(G) * rcap);
+  switch (B / 256) {
+    case 1: k_msg_pack<1><<<g, 64 * kWaves, 0, st>>>(a); break;
+    case 2: k_msg_pack<2><<<g, 64 * kWaves, 0, st>>>(a); break;
+    default: k_msg_pack<4><<<g, 64 * kWaves, 0, st>>>(a); break;
+  }
+  return mlaunch("k_msg_pack");
+}
+
+int run_aggregate(const float* const* msgs, const uint32_t* const* imm, uint32_t m, const Sched* sch,
+                  const uint32_t* rounds, const uint32_t* unext, uint32_t G, uint32_t rcap, uint32_t B, uint32_t NB,
+                  uint32_t naggs, uint32_t agg, float* reply, uint32_t* rimm, hipStream_t st) {
+  AggArgs ag;
+  for (uint32_t w = 0; w < OMR_MAX_WORKERS; ++w) {
+    ag.msgs[w] = w < m ? msgs[w] : nullptr;
+    ag.imm[w] = w < m ? imm[w] : nullptr;
+  }
+  ag.sch = sch;
+  ag.rounds = rounds;
+  ag.unext = unext;
+  ag.reply = reply;
+  ag.rimm = rimm;
+  ag.m = m;
+  ag.G = G;
+  ag.rcap = rcap;
+  ag.B = B;
+  ag.NB = NB;
+  ag.naggs = naggs;
+  ag.agg = agg;
+  const unsigned g = waves_grid(static_cast<uint64_t>(G) * rcap);
+  switch (B / 256) {
+    case 1: k_msg_aggregate<1><<<g, 64 * kWaves, 0, st>>>(ag); break;
+    case 2: k_msg_aggregate<2><<<g, 64 * kWaves, 0, st>>>(ag); break;
+    default: k_msg_aggregate<4><<<g, 64 * kWaves, 0, st>>>(ag); break;
+  }
+  return mlaunch("k_msg_aggregate");
+}
+
+int run_unpack(const float* reply, const uint32_t* rimm, const Sched* sch, const uint32_t* rounds, uint32_t G,
+               uint32_t rcap, uint32_t B, uint32_t NB, float* buf, hipStream_t st) {
+  UnpackArgs u;
+  u.reply = reply;
+  u.rimm = rimm;
+  u.sch = sch;
+  u.rounds = rounds;
+  u.buf = buf;
+  u.G = G;
+  u.rcap = rcap;
+  u.B = B;
+  u.NB = NB;
+  const unsigned g = waves_grid(static_cast<uint64_t>(G) * rcap);
+  switch (B / 256) {
+    case 1: k_msg_unpack<1><<<g, 64 * kWaves, 0, st>>>(u); break;
+    case 2: k_msg_unpack<2><<<g, 64 * kWaves, 0, st>>>(u); break;
+    default: k_msg_unpack<4><<<g, 64 * kWaves, 0, st>>>(u); break;
+  }
+  return mlaunch("k_msg_unpack");
+}
+
+// the message primitives' shared argument check: a layout the wire format supports
+int msg_layout(uint64_t n, uint32_t B, uint32_t NB, uint32_t parts, uint32_t* rpp, uint64_t* rows) {
+  if (int rc = omr_layout_check(n, B, NB, parts)) return rc;
+  if (NB != kSlots * (kMsg / B)) return mfail("message layout: num_lanes must be NUM_SLOTS*MESSAGE_SIZE/BLOCK_SIZE");
+  *rows = n / B / NB;
+  *rpp = static_cast<uint32_t>(*rows / parts);
+  return 0;
 }
 
 }  // namespace
@@ -440,71 +531,75 @@ int omr_msg_round_f32(omr_msg_plan* p, const float* const* bufs, float* const* o
     MTRY(launch_schedule(p, st));
     if (*p->maxr_host > p->rcap) return mfail("msg_round: %u protocol rounds exceed %u", *p->maxr_host, p->rcap);
   }
-  const uint64_t units = static_cast<uint64_t>(p->G) * p->rcap;
-  const unsigned g = waves_grid(units);
   // 4. every worker's messages (client.cc:180-205 first burst, :113-127 later rounds)
-  for (uint32_t w = 0; w < m; ++w) {
-    PackArgs a;
-    a.x = bufs[w];
-    a.flags = p->flags + w * p->nb;
-    a.next = p->next + w * p->nb;
-    a.sch = p->sch;
-    a.rounds = p->rounds;
-    a.msgs = p->msgs[w];
-    a.imm = p->imm[w];
-    a.G = p->G;
-    a.rcap = p->rcap;
-    a.B = p->B;
-    switch (p->vec) {
-      case 1: k_msg_pack<1><<<g, 64 * kWaves, 0, st>>>(a); break;
-      case 2: k_msg_pack<2><<<g, 64 * kWaves, 0, st>>>(a); break;
-      default: k_msg_pack<4><<<g, 64 * kWaves, 0, st>>>(a); break;
-    }
-    MTRY(mlaunch("k_msg_pack"));
-  }
-  // 5. the aggregator's replies (server.cc:68-162)
-  AggArgs ag;
-  for (uint32_t w = 0; w < OMR_MAX_WORKERS; ++w) {
-    ag.msgs[w] = w < m ? p->msgs[w] : nullptr;
-    ag.imm[w] = w < m ? p->imm[w] : nullptr;
-  }
-  ag.sch = p->sch;
-  ag.rounds = p->rounds;
-  ag.unext = p->unext;
-  ag.reply = p->reply;
-  ag.rimm = p->rimm;
-  ag.m = m;
-  ag.G = p->G;
-  ag.rcap = p->rcap;
-  ag.B = p->B;
-  ag.NB = p->NB;
-  switch (p->vec) {
-    case 1: k_msg_aggregate<1><<<g, 64 * kWaves, 0, st>>>(ag); break;
-    case 2: k_msg_aggregate<2><<<g, 64 * kWaves, 0, st>>>(ag); break;
-    default: k_msg_aggregate<4><<<g, 64 * kWaves, 0, st>>>(ag); break;
-  }
-  MTRY(mlaunch("k_msg_aggregate"));
+  for (uint32_t w = 0; w < m; ++w)
+    MTRY(run_pack(bufs[w], p->flags + w * p->nb, p->next + w * p->nb, p->sch, p->rounds, p->G, p->rcap, p->B,
+                  p->msgs[w], p->imm[w], st));
+  // 5. the aggregator's replies (server.cc:68-162): one aggregator owns every slot here
+  std::vector<const float*> mp(p->msgs.begin(), p->msgs.end());
+  std::vector<const uint32_t*> ip(p->imm.begin(), p->imm.end());
+  MTRY(run_aggregate(mp.data(), ip.data(), m, p->sch, p->rounds, p->unext, p->G, p->rcap, p->B, p->NB, 1, 0, p->reply,
+                     p->rimm, st));
   // 6. every worker applies every reply in place (client.cc:87-90)
-  for (uint32_t w = 0; w < m; ++w) {
-    UnpackArgs u;
-    u.reply = p->reply;
-    u.rimm = p->rimm;
-    u.sch = p->sch;
-    u.rounds = p->rounds;
-    u.buf = outs[w];
-    u.G = p->G;
-    u.rcap = p->rcap;
-    u.B = p->B;
-    u.NB = p->NB;
-    switch (p->vec) {
-      case 1: k_msg_unpack<1><<<g, 64 * kWaves, 0, st>>>(u); break;
-      case 2: k_msg_unpack<2><<<g, 64 * kWaves, 0, st>>>(u); break;
-      default: k_msg_unpack<4><<<g, 64 * kWaves, 0, st>>>(u); break;
-    }
-    MTRY(mlaunch("k_msg_unpack"));
-  }
+  for (uint32_t w = 0; w < m; ++w)
+    MTRY(run_unpack(p->reply, p->rimm, p->sch, p->rounds, p->G, p->rcap, p->B, p->NB, outs[w], st));
   if (max_rounds) *max_rounds = *p->maxr_host;
   return 0;
+}
+
+size_t omr_msg_sched_bytes(void) { return sizeof(Sched); }
+
+int omr_msg_schedule(const uint64_t* row_masks, uint32_t m, const uint32_t* union_next, uint64_t n, uint32_t block_size,
+                     uint32_t num_lanes, uint32_t num_parts, uint32_t round_capacity, void* sched, uint32_t* rounds,
+                     uint32_t* max_rounds, omr_stream_t stream) {
+  uint32_t rpp = 0;
+  uint64_t rows = 0;
+  MTRY(msg_layout(n, block_size, num_lanes, num_parts, &rpp, &rows));
+  if (m == 0 || m > OMR_MAX_WORKERS) return mfail("msg_schedule: m=%u out of range", m);
+  if (row_masks == nullptr || union_next == nullptr || sched == nullptr || rounds == nullptr || max_rounds == nullptr)
+    return mfail("msg_schedule: NULL argument");
+  if (round_capacity == 0) return mfail("msg_schedule: round_capacity is 0");
+  return run_schedule(row_masks, m, rows, union_next, block_size, num_lanes, rpp, num_parts, round_capacity,
+                      static_cast<Sched*>(sched), rounds, max_rounds, reinterpret_cast<hipStream_t>(stream));
+}
+
+int omr_msg_pack_f32(const float* x, const int32_t* flags, const uint32_t* next_offsets, const void* sched,
+                     const uint32_t* rounds, uint32_t num_parts, uint32_t round_capacity, uint32_t block_size,
+                     float* messages, uint32_t* imm, omr_stream_t stream) {
+  if (block_size != 256 && block_size != 512 && block_size != 1024) return mfail("msg_pack: block_size %u", block_size);
+  if (x == nullptr || flags == nullptr || next_offsets == nullptr || sched == nullptr || rounds == nullptr ||
+      messages == nullptr || imm == nullptr)
+    return mfail("msg_pack: NULL argument");
+  return run_pack(x, flags, next_offsets, static_cast<const Sched*>(sched), rounds, num_parts * kSlots, round_capacity,
+                  block_size, messages, imm, reinterpret_cast<hipStream_t>(stream));
+}
+
+int omr_msg_aggregate_f32(const float* const* messages, const uint32_t* const* imm, uint32_t m, const void* sched,
+                          const uint32_t* rounds, const uint32_t* union_next, uint32_t num_parts,
+                          uint32_t round_capacity, uint32_t block_size, uint32_t num_lanes, uint32_t num_aggregators,
+                          uint32_t aggregator, float* replies, uint32_t* reply_imm, omr_stream_t stream) {
+  if (block_size != 256 && block_size != 512 && block_size != 1024)
+    return mfail("msg_aggregate: block_size %u", block_size);
+  if (m == 0 || m > OMR_MAX_WORKERS) return mfail("msg_aggregate: m=%u out of range", m);
+  if (num_aggregators == 0 || aggregator >= num_aggregators) return mfail("msg_aggregate: aggregator out of range");
+  if (messages == nullptr || imm == nullptr || sched == nullptr || rounds == nullptr || union_next == nullptr ||
+      replies == nullptr || reply_imm == nullptr)
+    return mfail("msg_aggregate: NULL argument");
+  for (uint32_t w = 0; w < m; ++w)
+    if (messages[w] == nullptr || imm[w] == nullptr) return mfail("msg_aggregate: NULL log for worker %u", w);
+  return run_aggregate(messages, imm, m, static_cast<const Sched*>(sched), rounds, union_next, num_parts * kSlots,
+                       round_capacity, block_size, num_lanes, num_aggregators, aggregator, replies, reply_imm,
+                       reinterpret_cast<hipStream_t>(stream));
+}
+
+int omr_msg_unpack_f32(const float* replies, const uint32_t* reply_imm, const void* sched, const uint32_t* rounds,
+                       uint32_t num_parts, uint32_t round_capacity, uint32_t block_size, uint32_t num_lanes,
+                       float* buf, omr_stream_t stream) {
+  if (block_size != 256 && block_size != 512 && block_size != 1024) return mfail("msg_unpack: block_size %u", block_size);
+  if (replies == nullptr || reply_imm == nullptr || sched == nullptr || rounds == nullptr || buf == nullptr)
+    return mfail("msg_unpack: NULL argument");
+  return run_unpack(replies, reply_imm, static_cast<const Sched*>(sched), rounds, num_parts * kSlots, round_capacity,
+                    block_size, num_lanes, buf, reinterpret_cast<hipStream_t>(stream));
 }
 
 int omr_msg_logs(omr_msg_plan* p, uint32_t worker, float** messages, uint32_t** imm, float** replies,

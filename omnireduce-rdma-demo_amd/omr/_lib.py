@@ -61,6 +61,12 @@ SIGNATURES = {
     "omr_msg_plan_destroy": (c_int, [c_vp]),
     "omr_msg_round_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "omr_msg_logs": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "omr_msg_sched_bytes": (c_size, []),
+    "omr_msg_schedule": (c_int, [c_vp, c_u32, c_vp, c_u64, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp]),
+    "omr_msg_pack_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp]),
+    "omr_msg_aggregate_f32": (c_int, [c_vp, c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_u32, c_u32,
+                                      c_vp, c_vp, c_vp]),
+    "omr_msg_unpack_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_u32, c_u32, c_u32, c_u32, c_vp, c_vp]),
     "omr_sparse_block_sum_f32": (c_int, [c_vp, c_vp, c_vp, c_u32, c_u64, c_vp, c_u64, c_u32, c_vp, c_u32, c_u32,
                                          c_vp, c_vp]),
     "omr_host_last_error": (ctypes.c_char_p, []),

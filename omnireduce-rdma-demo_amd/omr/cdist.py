@@ -46,10 +46,16 @@ def load():
         "omr_dist_destroy": (i, [vp]),
         "omr_ar_plan_create": (i, [vp, u64, u32, u32, u32, vp]),
         "omr_ar_plan_destroy": (i, [vp]),
+        "omr_ar_plan_create_roles": (i, [vp, u32, u64, u32, u32, u32, vp]),
+        "omr_ar_plan_shard": (i, [vp, vp, vp, vp, vp, vp]),
         "omr_sparse_allreduce_f32": (i, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "omr_sparse_round_f32": (i, [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]),
         "omr_ar_plan_join": (i, [vp, vp]),
         "omr_sparse_buckets_f32": (i, [vp, vp, u64, i, vp, vp, vp]),
+        "omr_msgd_plan_create": (i, [vp, u32, u64, u32, u32, u32, vp]),
+        "omr_msgd_plan_destroy": (i, [vp]),
+        "omr_msgd_round_f32": (i, [vp, vp, vp, vp, vp]),
+        "omr_msgd_logs": (i, [vp, u32, vp, vp, vp, vp, vp, vp]),
         "omr_ar_plan_exchange_time": (i, [vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
@@ -78,7 +84,9 @@ class CppSparseAllreduce:
     "local1": a group of one rank (the round with no peers), e.g. for the single-GPU host-resident bench."""
 
     def __init__(self, L: Layout, device, group=None, transport: str = "rccl", uid: Optional[bytes] = None,
-                 rank: Optional[int] = None, world: Optional[int] = None):
+                 rank: Optional[int] = None, world: Optional[int] = None, num_workers: Optional[int] = None):
+        """num_workers < world: ranks >= num_workers are dedicated aggregators (omr_ar_plan_create_roles): they
+        call run() with x = None."""
         D = load()
         self.L = L
         self.device = torch.device(device)
@@ -104,13 +112,14 @@ class CppSparseAllreduce:
             uidt.copy_(t.cpu())
             _check(D.omr_dist_create_rccl(uidt.data_ptr(), rank, world, ctypes.byref(self._d)), "omr_dist_create_rccl")
         self._p = ctypes.c_void_p()
-        _check(D.omr_ar_plan_create(self._d, L.n, L.block_size, L.num_lanes, L.num_threads, ctypes.byref(self._p)),
-               "omr_ar_plan_create")
-        self.rank, self.world = rank, world
+        nw = world if num_workers is None else num_workers
+        _check(D.omr_ar_plan_create_roles(self._d, nw, L.n, L.block_size, L.num_lanes, L.num_threads,
+                                          ctypes.byref(self._p)), "omr_ar_plan_create_roles")
+        self.rank, self.world, self.num_workers = rank, world, nw
 
     ALLREDUCE, REDUCE_SCATTER, DENSE_REDUCE_SCATTER, ASYNC, TIME_EXCHANGE, DEFER = 0, 1, 2, 0x100, 0x200, 0x400
 
-    def run(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, ev=None, flags=None, next_offsets=None,
+    def run(self, x: Optional[torch.Tensor], out: Optional[torch.Tensor] = None, ev=None, flags=None, next_offsets=None,
             union_next=None, mode: int = 0, async_: bool = False, time_exchange: bool = False,
             defer: bool = False):
         """mode 0: all-reduce (every worker gets every shard's sums); 1: reduce-scatter (stop at the
@@ -132,12 +141,21 @@ class CppSparseAllreduce:
         if ev is not None:  # the round starts with the worker scan kernel on this stream
             ev[0].record(st)
         ptr = (lambda t: t.data_ptr() if t is not None else None)
-        _check(load().omr_sparse_round_f32(self._p, x.data_ptr(), out.data_ptr(), ptr(flags), ptr(next_offsets),
+        _check(load().omr_sparse_round_f32(self._p, ptr(x), ptr(out), ptr(flags), ptr(next_offsets),
                                            ptr(union_next), mode, ctypes.byref(sent), ctypes.byref(uni),
                                            st.cuda_stream), "omr_sparse_round_f32")
         if ev is not None:
             ev[1].record(st)
         return sent.value, uni.value
+
+    def shard(self):
+        """(shard, row_begin, row_end, sums, num_blocks) of this rank (omr_ar_plan_shard); `sums` is a device pointer
+        (a dedicated aggregator's last shard sums, write-set order) or None."""
+        sh, r0, r1 = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+        sums, nb = ctypes.c_void_p(), ctypes.c_uint64()
+        _check(load().omr_ar_plan_shard(self._p, ctypes.byref(sh), ctypes.byref(r0), ctypes.byref(r1),
+                                        ctypes.byref(sums), ctypes.byref(nb)), "omr_ar_plan_shard")
+        return sh.value, r0.value, r1.value, sums.value, nb.value
 
     def run_buckets(self, buf: torch.Tensor, mode: int = 0, stream=None):
         """The whole tensor `buf` (numel a multiple of the layout's n) reduced in place, one pipelined round per

@@ -12,7 +12,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import oracle  # noqa: E402  (the generator's inputs only; the round itself runs in libomr_dist.so)
-from omr import Layout, cdist  # noqa: E402
+from omr import Layout, cdist, ops  # noqa: E402
 
 
 def main():
@@ -26,29 +26,48 @@ def main():
     ap.add_argument("--mode", type=int, default=0, help="OMR_ROUND_* (0 all-reduce, 1 reduce-scatter, 2 dense)")
     ap.add_argument("--pipe", choices=("sync", "async", "defer"), default="sync")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--workers", type=int, default=0, help="ranks >= this are dedicated aggregators (0: all workers)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
     L = Layout(n=a.n, block_size=a.block)
-    eng = cdist.CppSparseAllreduce(L, dev, transport="ipc", uid=bytes.fromhex(a.uid), rank=a.rank, world=a.world)
+    nw = a.workers or a.world
+    eng = cdist.CppSparseAllreduce(L, dev, transport="ipc", uid=bytes.fromhex(a.uid), rank=a.rank, world=a.world,
+                                   num_workers=nw)
+    worker = a.rank < nw
     # a different input per round (seed = rank, round): the pipelined rounds must not mix their buffers
     xs, outs = [], []
     for r in range(a.rounds):
-        x = oracle.fill(oracle.gen_bitmap(a.rank + 10 * r, a.density, L.nb), a.block, mode=1, seed=a.rank + 7 + 31 * r)
-        xs.append(torch.from_numpy(x).to(dev))
-        outs.append(xs[-1].clone())
-    flags = torch.empty(L.nb, dtype=torch.int32, device=dev)
-    nxt = torch.empty(L.nb, dtype=torch.int32, device=dev)
+        if worker:
+            x = oracle.fill(oracle.gen_bitmap(a.rank + 10 * r, a.density, L.nb), a.block, mode=1,
+                            seed=a.rank + 7 + 31 * r)
+            xs.append(torch.from_numpy(x).to(dev))
+            outs.append(xs[-1].clone())
+        else:  # a dedicated aggregator holds no tensor
+            xs.append(None)
+            outs.append(None)
+    flags = torch.zeros(L.nb, dtype=torch.int32, device=dev)
+    nxt = torch.zeros(L.nb, dtype=torch.int32, device=dev)
     unx = torch.empty(L.nb, dtype=torch.int32, device=dev)
+    sums = {}
     for r in range(a.rounds):
         eng.run(xs[r], out=outs[r], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
                 async_=a.pipe != "sync", defer=a.pipe == "defer")
+        if not worker and a.pipe == "sync":  # a dedicated aggregator's shard sums of this round
+            torch.cuda.synchronize()
+            sh, r0, r1, ptr, nb = eng.shard()
+            t = (torch.as_tensor(ops._DeviceView(ptr, (nb * a.block,), "<f4"), device=dev).clone() if nb
+                 else torch.empty(0, device=dev))
+            sums[f"sums{r}"] = t.cpu().numpy()
+            sums["shard"] = np.array([sh, r0, r1])
     eng.join()
     torch.cuda.synchronize()
-    np.savez(a.out, **{f"out{r}": outs[r].cpu().numpy() for r in range(a.rounds)},
-             flags=flags.cpu().numpy(), next=nxt.cpu().numpy().view(np.uint32),
-             unext=unx.cpu().numpy().view(np.uint32))
+    arrs = dict(flags=flags.cpu().numpy(), next=nxt.cpu().numpy().view(np.uint32),
+                unext=unx.cpu().numpy().view(np.uint32), **sums)
+    if worker:
+        arrs.update({f"out{r}": outs[r].cpu().numpy() for r in range(a.rounds)})
+    np.savez(a.out, **arrs)
     eng.close()
     print(f"rank {a.rank} ok", flush=True)
 

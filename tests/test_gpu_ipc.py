@@ -19,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "ipc_round_worker.py")
 
 
-def run_ranks(tmp_path, world, n, B, density, mode, pipe, rounds=3):
+def run_ranks(tmp_path, world, n, B, density, mode, pipe, rounds=3, workers=0):
     uid = cdist.ipc_unique_id().hex()
     procs, outs = [], []
     for r in range(world):
@@ -27,7 +27,7 @@ def run_ranks(tmp_path, world, n, B, density, mode, pipe, rounds=3):
         outs.append(out)
         cmd = [sys.executable, WORKER, "--rank", str(r), "--world", str(world), "--uid", uid, "--n", str(n),
                "--block", str(B), "--density", str(density), "--mode", str(mode), "--pipe", pipe,
-               "--rounds", str(rounds), "--out", out]
+               "--rounds", str(rounds), "--workers", str(workers), "--out", out]
         procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     logs = []
     for p in procs:
@@ -85,3 +85,47 @@ def test_cpp_round_processes(gpu, tmp_path, world, pipe, mode, B, density):
                 assert (res[r]["flags"] == flags[r]).all(), f"rank {r} flags"
                 assert (res[r]["next"] == oracle.next_offsets(flags[r], L.n, B, NB, P)).all(), f"rank {r} next"
                 assert (res[r]["unext"] == oracle.next_offsets(uf, L.n, B, NB, P)).all(), f"rank {r} union next"
+
+
+@pytest.mark.parametrize("m,naggs,pipe,mode", [(2, 1, "sync", 0), (3, 2, "defer", 0), (2, 3, "async", 0),
+                                               (3, 2, "sync", 1), (4, 1, "sync", 1)])
+def test_dedicated_aggregators_processes(gpu, tmp_path, m, naggs, pipe, mode):
+    """m worker processes + naggs dedicated aggregator processes (the reference's ./server machines, holding no
+    tensor): all-reduce results on the workers; in reduce-scatter mode each aggregator's packed shard sums (write-set
+    order: union blocks and lane heads of its rows, server.cc:143-147) and the workers' tensors left untouched."""
+    B, density, rounds = 256, 0.2, 3
+    L = Layout(n=2 << 20, block_size=B)
+    world = m + naggs
+    res = run_ranks(tmp_path, world, L.n, B, density, mode, pipe, rounds, workers=m)
+    NB, P = L.num_lanes, L.num_threads
+    bounds = [s * L.rows // naggs for s in range(naggs + 1)]
+    heads = (np.arange(L.nb) // NB) % L.rows_per_part == 0
+    for rd in range(rounds):
+        bufs = [oracle.fill(oracle.gen_bitmap(w + 10 * rd, density, L.nb), B, mode=1, seed=w + 7 + 31 * rd)
+                for w in range(m)]
+        flags = [oracle.flags_from_data(b, B) for b in bufs]
+        uf = oracle.union_flags(flags)
+        full = np.zeros(L.n, dtype=np.float32)
+        oracle.block_sum(bufs, L.n, B, NB, P, uf, full)
+        for r in range(world):
+            if r < m:
+                got = res[r][f"out{rd}"]
+                if mode == 0:
+                    exp = bufs[r].copy()
+                    oracle.block_sum(bufs, L.n, B, NB, P, uf, exp)
+                else:
+                    exp = bufs[r]
+                assert (got.view(np.uint32) == exp.view(np.uint32)).all(), f"round {rd} worker {r}"
+                if rd == rounds - 1:
+                    assert (res[r]["next"] == oracle.next_offsets(flags[r], L.n, B, NB, P)).all()
+            else:
+                if rd == rounds - 1:
+                    assert (res[r]["unext"] == oracle.next_offsets(uf, L.n, B, NB, P)).all(), f"aggregator {r}"
+                if pipe == "sync":
+                    j = r - m
+                    sh, r0, r1 = res[r]["shard"]
+                    assert (sh, r0, r1) == (j, bounds[j], bounds[j + 1])
+                    blocks = np.arange(r0 * NB, r1 * NB)
+                    sel = blocks[(uf.astype(bool) | heads)[r0 * NB:r1 * NB]]
+                    exp = full.reshape(L.nb, B)[sel].reshape(-1)
+                    assert (res[r][f"sums{rd}"].view(np.uint32) == exp.view(np.uint32)).all(), f"agg {j} round {rd}"
