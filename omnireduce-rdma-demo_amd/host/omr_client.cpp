@@ -14,9 +14,13 @@
 //       a {src, dst, imm, len} record of four uint32 (workers 0..k-1, aggregator 100) then its payload, the
 //       (B*len + len)*4 bytes an ibv_post_send would carry (common.cc:424), slot by slot, round by round
 //
-// With an aggregator list, the first entry is the ./omr_server rendezvous: it assigns this worker's ID by IP list
-// position (common.cc:123-133) and relays the RCCL unique id; the round itself is omr_sparse_allreduce_f32 over
-// RCCL (xGMI), every GPU aggregating one shard.  Output lines are the reference's: per round
+// With an aggregator list agg[:port][,agg[:port]...] the worker connects to every ./omr_server in list order, as the
+// reference's sock_connect does (common.cc:71-97): each server gives it its ID (the position of its IP in the
+// server's worker list, common.cc:123-133) and the servers are the round's aggregator ranks, aggregator j owning the
+// j-th shard (-M: the global slots gs with gs % n == j, common.cc:381-383).  -X rccl (default; one process per GPU,
+// RCCL over xGMI) or -X ipc (processes sharing GPUs, HIP IPC: one host, no RCCL)  -C the workers aggregate their own
+// shards instead (the servers only meet them)  -l k orders workers that share an IP and a GPU (default
+// $LOCAL_RANK).  Output lines are the reference's: per round
 // "data size: ... time: ... us; alg bw: ... GB/s" (client.cc:447), the average (client.cc:473), and
 // "test result is N" (client.cc:486).  alg bw keeps the reference formula DATA_SIZE*4/2^30/s (client.cc:445).
 #include <getopt.h>
@@ -45,7 +49,8 @@ struct Opts {
   uint32_t block = 256;
   int warmups = 10, rounds = 101;  // client.cc:368-369
   int gpu = -1, local = 0;
-  bool check = false, inplace = false, messages = false;
+  bool check = false, inplace = false, messages = false, colocated = false;
+  int transport = omrnet::kRccl, local_id = -1;
   const char* trace = nullptr;
 };
 
@@ -60,7 +65,8 @@ void usage(const char* argv0) {  // common.cc:1441-1457 (default port and -r tex
   fprintf(stdout, " -r, --density-ratio <r> fraction of non-zero blocks, as rand()%%100/101 < r (default 1.0)\n");
   fprintf(stdout, " -n <floats> -b <block size> -W <warm-ups> -R <rounds> -G <gpu> -c (check) -I (in place)\n");
   fprintf(stdout, " -L <k> run k workers in this process over the loopback transport\n");
-  fprintf(stdout, " -M (with -L) message mode: the round as the reference's wire messages; -T <file> trace them\n");
+  fprintf(stdout, " -M message mode: the round as the reference's wire messages; -T <file> trace them\n");
+  fprintf(stdout, " -X rccl|ipc transport to the servers (default rccl)  -C co-located aggregation  -l <k> local id\n");
   fprintf(stdout, " -h, --help show this help message\n");
 }
 
@@ -85,9 +91,10 @@ int make_input(uint32_t worker_id, const Opts& o, float* d_x, int32_t* d_bitmap)
   return 0;
 }
 
-int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer) {
+int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer, int num_workers = 0) {
   HIPOK(hipSetDevice(gpu));
-  const int rank = omr_dist_rank(d), world = omr_dist_world(d);
+  const int rank = omr_dist_rank(d);
+  const int world = num_workers > 0 ? num_workers : omr_dist_world(d);  // the workers (the rest aggregate)
   const uint32_t lanes = omr_num_lanes(o.block);
   const uint64_t nb = o.n / o.block;
   if (omr_layout_check(o.n, o.block, lanes, OMR_NUM_THREADS)) {
@@ -102,7 +109,7 @@ int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer) {
   if (make_input(static_cast<uint32_t>(rank), o, d_x, d_bitmap)) return 1;  // srand(res.myId+1)
   HIPOK(hipMemcpy(d_out, d_x, o.n * sizeof(float), hipMemcpyDeviceToDevice));
   omr_ar_plan* plan = nullptr;
-  if (omr_ar_plan_create(d, o.n, o.block, lanes, OMR_NUM_THREADS, &plan)) {
+  if (omr_ar_plan_create_roles(d, static_cast<uint32_t>(world), o.n, o.block, lanes, OMR_NUM_THREADS, &plan)) {
     fprintf(stderr, "omr_ar_plan_create: %s\n", omr_dist_last_error());
     return 1;
   }
@@ -180,7 +187,7 @@ int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer) {
           ok = false;
           break;
         }
-      if (ok && printer) std::cout << "check OK" << std::endl;
+      if (ok) std::cout << "check OK" << std::endl;  // every worker reports its own check (client.cc:460)
       if (!ok) rc = 1;
     } else {
       fprintf(stderr, "check skipped: %s\n", omr_last_error());
@@ -363,6 +370,151 @@ int run_messages(const Opts& o, int gpu) {
   return rc;
 }
 
+// One trace record per message: {src, dst, imm, len} then the (B*len + len)*4 payload
+// bytes an ibv_post_send carries (common.cc:424); workers are 0..m-1, aggregator j is 100 + j.
+struct TraceWriter {
+  FILE* f = nullptr;
+  uint32_t block = 256;
+  uint64_t records = 0;
+  void put(uint32_t src, uint32_t dst, uint32_t word, const float* payload) {
+    const uint32_t len = word >> 16;
+    const uint32_t rec[4] = {src, dst, word, len};
+    fwrite(rec, sizeof(rec), 1, f);
+    fwrite(payload, sizeof(float), static_cast<size_t>(block) * len + len, f);
+    ++records;
+  }
+};
+
+// -M with aggregator processes: this worker's rounds as the reference's messages over the transport (omr_msgd_*);
+// -T writes the messages it sent and the replies it got, slot by slot, round by round
+int run_msg_worker(omr_dist* d, const Opts& o, int gpu, int num_workers, int num_aggs) {
+  HIPOK(hipSetDevice(gpu));
+  const int rank = omr_dist_rank(d);
+  const uint32_t lanes = omr_num_lanes(o.block);
+  const uint64_t nb = o.n / o.block;
+  float *d_x = nullptr, *d_out = nullptr;
+  int32_t* d_bitmap = nullptr;
+  HIPOK(hipMalloc(&d_x, o.n * sizeof(float)));
+  HIPOK(hipMalloc(&d_out, o.n * sizeof(float)));
+  HIPOK(hipMalloc(&d_bitmap, nb * sizeof(int32_t)));
+  if (make_input(static_cast<uint32_t>(rank), o, d_x, d_bitmap)) return 1;
+  omr_msgd_plan* plan = nullptr;
+  if (omr_msgd_plan_create(d, static_cast<uint32_t>(num_workers), o.n, o.block, lanes, OMR_NUM_THREADS, &plan)) {
+    fprintf(stderr, "omr_msgd_plan_create: %s\n", omr_dist_last_error());
+    return 1;
+  }
+  hipStream_t st;
+  HIPOK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  const bool printer = rank == 0;
+  if (printer) std::cout << "density: " << o.density << std::endl;  // client.cc:405
+  const double gib = o.n * sizeof(float) / (1024.0 * 1024.0 * 1024.0);
+  double avg_bw = 0.0;
+  unsigned long avg_time_usec = 0;
+  int print_count = 0;
+  uint32_t maxr = 0;
+  auto start = std::chrono::steady_clock::now();
+  for (int round = 0; round < o.warmups + o.rounds; ++round) {
+    float* out = o.inplace ? d_x : d_out;
+    if (!o.inplace) HIPOK(hipMemcpyAsync(d_out, d_x, o.n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    if (omr_msgd_round_f32(plan, d_x, out, &maxr, st)) {
+      fprintf(stderr, "failed to run the round: %s\n", omr_dist_last_error());
+      return 1;
+    }
+    HIPOK(hipStreamSynchronize(st));
+    if (round >= o.warmups) {
+      if (round - o.warmups > 0) {
+        const auto now = std::chrono::steady_clock::now();
+        const unsigned long us =
+            static_cast<unsigned long>(std::chrono::duration_cast<std::chrono::microseconds>(now - start).count());
+        const double bw = gib / (us / 1e6);
+        ++print_count;
+        avg_time_usec += us;
+        avg_bw += bw;
+        if (printer)
+          fprintf(stdout, "data size: %lu Bytes; time: %lu us; alg bw: %f GB/s\n",
+                  static_cast<unsigned long>(o.n * sizeof(float)), us, bw);
+      }
+      start = std::chrono::steady_clock::now();
+    }
+    if (o.inplace && o.check && round + 1 < o.warmups + o.rounds) {  // res.buf = input (client.cc:463-464)
+      if (make_input(static_cast<uint32_t>(rank), o, d_x, d_bitmap)) return 1;
+      start = std::chrono::steady_clock::now();
+    }
+  }
+  if (printer) std::cout << "protocol rounds (largest slot): " << maxr << std::endl;
+  int rc = 0;
+  if (o.trace) {
+    const uint32_t G = OMR_NUM_THREADS * OMR_NUM_SLOTS, W = 2 * OMR_MESSAGE_SIZE;
+    float *dm = nullptr, *drep = nullptr;
+    uint32_t *dimm = nullptr, *drimm = nullptr, *drounds = nullptr, cap = 0;
+    omr_msgd_logs(plan, static_cast<uint32_t>(rank), &dm, &dimm, &drep, &drimm, &drounds, &cap);
+    std::vector<float> msg(static_cast<size_t>(G) * cap * W), rep(msg.size());
+    std::vector<uint32_t> imm(static_cast<size_t>(G) * cap), rimm(imm.size()), rounds(G);
+    HIPOK(hipMemcpy(msg.data(), dm, msg.size() * sizeof(float), hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(imm.data(), dimm, imm.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(rep.data(), drep, rep.size() * sizeof(float), hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(rimm.data(), drimm, rimm.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(rounds.data(), drounds, G * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    TraceWriter tw;
+    tw.f = fopen(o.trace, "wb");
+    tw.block = o.block;
+    if (!tw.f) {
+      fprintf(stderr, "cannot open %s\n", o.trace);
+      return 1;
+    }
+    const uint32_t A = static_cast<uint32_t>(num_aggs);
+    for (uint32_t gs = 0; gs < G; ++gs)
+      for (uint32_t r = 0; r < rounds[gs]; ++r) {
+        const size_t u = static_cast<size_t>(gs) * cap + r;
+        if (imm[u]) tw.put(static_cast<uint32_t>(rank), 100 + gs % A, imm[u], &msg[u * W]);
+        tw.put(100 + gs % A, static_cast<uint32_t>(rank), rimm[u], &rep[u * W]);
+      }
+    fclose(tw.f);
+    std::cout << "trace: " << tw.records << " messages -> " << o.trace << std::endl;
+  }
+  if (o.check) {  // the CHECK of client.cc:449-465, done right: the rank-order sum of every worker's input
+    std::vector<float*> bufs(num_workers);
+    for (int w = 0; w < num_workers; ++w) {
+      HIPOK(hipMalloc(&bufs[w], o.n * sizeof(float)));
+      if (make_input(static_cast<uint32_t>(w), o, bufs[w], d_bitmap)) return 1;
+    }
+    float* d_exp = nullptr;
+    uint64_t* d_masks = nullptr;
+    HIPOK(hipMalloc(&d_exp, o.n * sizeof(float)));
+    HIPOK(hipMalloc(&d_masks, (num_workers + 1) * (nb / lanes) * sizeof(uint64_t)));
+    HIPOK(hipMemcpy(d_exp, bufs[rank], o.n * sizeof(float), hipMemcpyDeviceToDevice));
+    std::vector<const float*> cb(bufs.begin(), bufs.end());
+    if (omr_scan_sum_f32(cb.data(), num_workers, o.n, o.block, lanes, OMR_NUM_THREADS, nullptr, d_masks, nullptr,
+                         d_exp, nullptr) == 0) {
+      HIPOK(hipDeviceSynchronize());
+      std::vector<float> got(o.n), exp(o.n);
+      HIPOK(hipMemcpy(got.data(), o.inplace ? d_x : d_out, o.n * sizeof(float), hipMemcpyDeviceToHost));
+      HIPOK(hipMemcpy(exp.data(), d_exp, o.n * sizeof(float), hipMemcpyDeviceToHost));
+      for (uint64_t i = 0; i < o.n; ++i)
+        if (memcmp(&got[i], &exp[i], sizeof(float)) != 0) {
+          std::cout << "error: " << exp[i] << "<---->" << got[i] << std::endl;  // client.cc:453-456
+          rc = 1;
+          break;
+        }
+      if (rc == 0) std::cout << "check OK" << std::endl;
+    } else {
+      fprintf(stderr, "check skipped: %s\n", omr_last_error());
+    }
+    for (float* b : bufs) (void)hipFree(b);
+    (void)hipFree(d_exp);
+    (void)hipFree(d_masks);
+  }
+  if (printer && print_count > 0)  // client.cc:473
+    fprintf(stdout, "data size: %lu Bytes; average time: %lu us; average alg bw: %f GB/s\n",
+            static_cast<unsigned long>(o.n * sizeof(float)), avg_time_usec / print_count, avg_bw / print_count);
+  omr_msgd_plan_destroy(plan);
+  (void)hipStreamDestroy(st);
+  (void)hipFree(d_x);
+  (void)hipFree(d_out);
+  (void)hipFree(d_bitmap);
+  return rc;
+}
+
 }  // namespace
 
 int main(int argc, char* argv[]) {
@@ -372,7 +524,7 @@ int main(int argc, char* argv[]) {
                               {"service-level", 1, nullptr, 's'}, {"density-ratio", 1, nullptr, 'r'},
                               {"help", 0, nullptr, 'h'},          {nullptr, 0, nullptr, 0}};
   while (true) {
-    int c = getopt_long(argc, argv, "p:d:i:g:s:r:n:b:W:R:G:L:T:cIMh", longopts, nullptr);
+    int c = getopt_long(argc, argv, "p:d:i:g:s:r:n:b:W:R:G:L:T:X:l:cIMCh", longopts, nullptr);
     if (c == -1) break;
     switch (c) {
       case 'p': o.port = static_cast<int>(strtoul(optarg, nullptr, 0)); break;
@@ -394,6 +546,16 @@ int main(int argc, char* argv[]) {
       case 'I': o.inplace = true; break;
       case 'M': o.messages = true; break;
       case 'T': o.trace = optarg; break;
+      case 'X':
+        if (strcmp(optarg, "ipc") == 0) o.transport = omrnet::kIpc;
+        else if (strcmp(optarg, "rccl") == 0) o.transport = omrnet::kRccl;
+        else {
+          usage(argv[0]);
+          return 1;
+        }
+        break;
+      case 'l': o.local_id = atoi(optarg); break;
+      case 'C': o.colocated = true; break;
       default: usage(argv[0]); return 1;
     }
   }
@@ -406,7 +568,7 @@ int main(int argc, char* argv[]) {
   std::vector<std::string> aggs = omrnet::split_list(optind == argc - 1 ? argv[optind] : nullptr);
   omrnet::print_config(false, aggs, o.port, o.dev, o.ib_port, o.gid, o.sl);
   int rc = 0;
-  if (o.messages) {  // message mode: k workers on one GPU, the round as the reference's wire messages
+  if (o.messages && o.local > 0) {  // message mode, k workers on one GPU: the round as the reference's wire messages
     if (o.local <= 0 || o.local > OMR_MAX_WORKERS) {
       fprintf(stderr, "-M needs -L k with 1 <= k <= %d\n", OMR_MAX_WORKERS);
       return 1;
@@ -451,45 +613,61 @@ int main(int argc, char* argv[]) {
   }
   const char* lr = getenv("LOCAL_RANK");
   const int gpu = o.gpu >= 0 ? o.gpu : (lr ? atoi(lr) : 0) % ndev;
+  const int local_id = o.local_id >= 0 ? o.local_id : (lr ? atoi(lr) : 0);
+  const int naggs = static_cast<int>(aggs.size());
+  auto fail = [&](const char* what) {
+    fprintf(stderr, "%s\n", what);
+    fprintf(stdout, "\ntest result is 1\n");
+    return 1;
+  };
   fprintf(stdout, "start connected\n");  // client.cc:348
-  int fd = omrnet::connect_to(aggs[0].c_str(), o.port);
-  if (fd < 0) {
-    fprintf(stderr, "failed to connect to %s:%d\n", aggs[0].c_str(), o.port);
-    fprintf(stdout, "\ntest result is 1\n");
-    return 1;
-  }
-  omrnet::Hello h{omrnet::kMagic, gpu};
-  omrnet::Assign a{};
-  char uid[omrnet::kIdBytes];
-  if (!omrnet::send_all(fd, &h, sizeof(h)) || !omrnet::recv_all(fd, &a, sizeof(a)) || a.magic != omrnet::kMagic) {
-    fprintf(stderr, "rendezvous failed\n");
-    fprintf(stdout, "\ntest result is 1\n");
-    return 1;
-  }
-  if (hipSetDevice(gpu) != hipSuccess) return 1;
-  if (a.rank == 0) {
-    if (omr_dist_unique_id(uid) || !omrnet::send_all(fd, uid, sizeof(uid))) {
-      fprintf(stderr, "failed to create/send the RCCL id: %s\n", omr_dist_last_error());
-      return 1;
+  // connect to every aggregator in list order (common.cc:71-97) and learn this worker's ID from each
+  std::vector<int> fds(naggs, -1);
+  int rank = -1, num_workers = 0;
+  for (int j = 0; j < naggs; ++j) {
+    fds[j] = omrnet::connect_to(omrnet::host_of(aggs[j]).c_str(), omrnet::port_of(aggs[j], o.port));
+    if (fds[j] < 0) return fail("failed to connect to an aggregator");
+    omrnet::Hello2 h{omrnet::kMagic2, gpu, local_id, j, naggs, o.transport, o.messages ? 1 : 0, o.colocated ? 1 : 0,
+                     o.warmups, o.rounds, o.block, o.n};
+    omrnet::Assign2 a{};
+    if (!omrnet::send_all(fds[j], &h, sizeof(h)) || !omrnet::recv_all(fds[j], &a, sizeof(a)) ||
+        a.magic != omrnet::kMagic2)
+      return fail("rendezvous failed");
+    if (j == 0) {
+      rank = a.rank;
+      num_workers = a.num_workers;
+    } else if (a.rank != rank || a.num_workers != num_workers) {
+      return fail("machine ID or number error");  // common.cc:1225-1230
     }
-  } else if (!omrnet::recv_all(fd, uid, sizeof(uid))) {
-    fprintf(stderr, "failed to receive the RCCL id\n");
-    return 1;
   }
+  if (hipSetDevice(gpu) != hipSuccess) return fail("hipSetDevice failed");
+  // the transport: workers 0..m-1 (+ the n aggregators m..m+n-1 unless -C); worker 0 makes its id, aggregator 0
+  // relays it to the other workers
+  char uid[omrnet::kIdBytes];
+  if (rank == 0) {
+    const int rc0 = o.transport == omrnet::kIpc ? omr_dist_ipc_unique_id(uid) : omr_dist_unique_id(uid);
+    if (rc0) return fail(omr_dist_last_error());
+    for (int j = 0; j < naggs; ++j)
+      if (!omrnet::send_all(fds[j], uid, sizeof(uid))) return fail("failed to send the transport id");
+  } else if (!omrnet::recv_all(fds[0], uid, sizeof(uid))) {
+    return fail("failed to receive the transport id");
+  }
+  const int world = o.colocated ? num_workers : num_workers + naggs;
   omr_dist* d = nullptr;
-  if (omr_dist_create_rccl(uid, a.rank, a.world, &d)) {
-    fprintf(stderr, "failed to connect: %s\n", omr_dist_last_error());
-    fprintf(stdout, "\ntest result is 1\n");
-    return 1;
-  }
-  std::cout << "Number of aggregators: " << a.world << "; Number of workers is " << a.world << "; My ID is "
-            << a.rank << std::endl;  // client.cc:364 (every GPU aggregates one shard)
+  const int crc = o.transport == omrnet::kIpc ? omr_dist_create_ipc(uid, rank, world, &d)
+                                              : omr_dist_create_rccl(uid, rank, world, &d);
+  if (crc) return fail(omr_dist_last_error());
+  std::cout << "Number of aggregators: " << (o.colocated ? num_workers : naggs) << "; Number of workers is "
+            << num_workers << "; My ID is " << rank << std::endl;  // client.cc:364
   printf("Connected.\n");
-  rc = run_worker(d, o, gpu, a.rank == 0);
+  if (o.messages) rc = run_msg_worker(d, o, gpu, num_workers, o.colocated ? num_workers : naggs);
+  else rc = run_worker(d, o, gpu, rank == 0, num_workers);
   omr_dist_destroy(d);
-  omrnet::Done done{omrnet::kMagic, a.rank, rc};
-  omrnet::send_all(fd, &done, sizeof(done));
-  ::close(fd);
+  omrnet::Done done{omrnet::kMagic2, rank, rc};
+  for (int fd : fds) {
+    omrnet::send_all(fd, &done, sizeof(done));
+    ::close(fd);
+  }
   fprintf(stdout, "\ntest result is %d\n", rc);
   return rc;
 }

@@ -17,6 +17,7 @@
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -40,6 +41,39 @@ struct Done {  // client -> server
   int32_t rank;
   int32_t status;
 };
+
+// Protocol 2: the servers are aggregator ranks of the transport (m workers + n aggregators).  Each worker connects to
+// every aggregator of its list in order and tells it its position and the list's length, as the reference's
+// cm_con_data_t does (remoteId = i, num_machines = num_socks: common.cc:1189-1232); the aggregator answers with the
+// worker's ID (its IP's position in the server's list, common.cc:123-133) and the number of workers.  Worker 0 then
+// sends the transport id to every aggregator, and aggregator 0 relays it to the other workers.
+constexpr uint32_t kMagic2 = 0x4f4d5232;  // "OMR2"
+enum Transport : int32_t { kRccl = 0, kIpc = 1 };
+struct Hello2 {  // worker -> aggregator j
+  uint32_t magic;
+  int32_t gpu, local;       // order workers sharing one IP
+  int32_t agg, num_aggs;    // j, n
+  int32_t transport;        // Transport
+  int32_t messages;         // 1: the round as wire messages (-M)
+  int32_t colocated;        // 1: the workers aggregate their own shards; the servers only meet them
+  int32_t warmups, rounds;  // the number of rounds the aggregators must take part in
+  uint32_t block;
+  uint64_t n;
+};
+struct Assign2 {  // aggregator j -> worker
+  uint32_t magic;
+  int32_t rank, num_workers, agg;
+};
+
+// "host" or "host:port" (a port per aggregator lets several run on one host)
+inline std::string host_of(const std::string& s) {
+  const size_t c = s.rfind(':');
+  return c == std::string::npos ? s : s.substr(0, c);
+}
+inline int port_of(const std::string& s, int dflt) {
+  const size_t c = s.rfind(':');
+  return c == std::string::npos ? dflt : atoi(s.c_str() + c + 1);
+}
 
 inline bool send_all(int fd, const void* p, size_t n) {
   const char* c = static_cast<const char*>(p);

@@ -305,7 +305,7 @@ def test_server_client_rccl_one_worker(gpu):
                            stderr=subprocess.STDOUT, text=True)
     try:
         rc, out = _run([os.path.join(BIN, "omr_client"), "-p", port, "-n", str(4 << 20), "-r", "0.095", "-W", "1",
-                        "-R", "3", "-c", "127.0.0.1"])
+                        "-R", "3", "-c", "-C", "127.0.0.1"])
         sout, _ = srv.communicate(timeout=60)
     finally:
         if srv.poll() is None:
@@ -313,6 +313,110 @@ def test_server_client_rccl_one_worker(gpu):
     assert rc == 0, out
     assert "check OK" in out and "My ID is 0" in out
     assert srv.returncode == 0 and "test result is 0" in sout, sout
+
+
+def _free_ports(k):
+    import socket
+    socks, ports = [], []
+    for _ in range(k):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+def _run_servers_clients(m, naggs, client_args, tmp_path, server_timeout=180):
+    """naggs ./omr_server aggregator processes and m ./omr_client worker processes on one host and one GPU (HIP IPC
+    transport); returns (server outputs, client outputs) after every process has exited."""
+    ports = _free_ports(naggs)
+    workers = ",".join(["127.0.0.1"] * m)
+    aggs = ",".join(f"127.0.0.1:{p}" for p in ports)
+    srvs = [subprocess.Popen([os.path.join(BIN, "omr_server"), "-p", str(p), "-G", "0", workers],
+                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for p in ports]
+    clis = [subprocess.Popen([os.path.join(BIN, "omr_client"), "-X", "ipc", "-l", str(w), "-G", "0"] +
+                             [a.replace("{w}", str(w)) for a in client_args] + [aggs],
+                             stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for w in range(m)]
+    outs = []
+    try:
+        for p in clis + srvs:
+            outs.append(p.communicate(timeout=server_timeout)[0])
+    finally:
+        for p in clis + srvs:
+            if p.poll() is None:
+                p.kill()
+    return [(p.returncode, o) for p, o in zip(srvs, outs[m:])], [(p.returncode, o) for p, o in zip(clis, outs[:m])]
+
+
+@pytest.mark.parametrize("m,naggs", [(2, 1), (3, 2)])
+def test_servers_are_aggregators_bulk(gpu, tmp_path, m, naggs):
+    """./omr_server processes as the round's aggregator ranks (m workers + n servers, the reference's topology):
+    every worker passes the working CHECK (client.cc:449-465) and reports the server count; each server reports
+    its ID (server.cc:325)."""
+    srv, cli = _run_servers_clients(m, naggs, ["-n", str(1 << 20), "-r", "0.3", "-W", "1", "-R", "3", "-c"],
+                                    tmp_path)
+    for w, (rc, out) in enumerate(cli):
+        assert rc == 0 and "check OK" in out and "test result is 0" in out, out
+        assert f"Number of aggregators: {naggs}; Number of workers is {m}; My ID is {w}" in out
+    for j, (rc, out) in enumerate(srv):
+        assert rc == 0 and "test result is 0" in out, out
+        assert f"Number of aggregators: {naggs}; Number of workers is {m}; My ID is {j}" in out
+
+
+def _expected_trace(bufs, flags, n, B, L, naggs, worker):
+    """The records worker `worker` sends and receives, in the client's -T order, from the oracle's literal state
+    machines; aggregator of slot gs = 100 + gs % naggs (common.cc:381-383)."""
+    ref = oracle.msg_simulate(bufs, flags, n, B, L.num_lanes, L.num_threads)
+    exp = []
+    for gs in range(L.num_threads * 16):
+        agg = 100 + gs % naggs
+        for rr in range(int(ref["rounds"][gs])):
+            imm = int(ref["wimm"][worker, gs, rr])
+            if imm:
+                ln = imm >> 16
+                exp.append((worker, agg, imm, ln, ref["wmsg"][worker, gs, rr, :ln * B + ln].tobytes()))
+            imm = int(ref["rimm"][gs, rr])
+            ln = imm >> 16
+            exp.append((agg, worker, imm, ln, ref["rmsg"][gs, rr, :ln * B + ln].tobytes()))
+    return exp
+
+
+def _read_trace(path, B):
+    data = open(path, "rb").read()
+    got, pos = [], 0
+    while pos < len(data):
+        src, dst, imm, ln = np.frombuffer(data, dtype=np.uint32, count=4, offset=pos)
+        pos += 16
+        nbytes = (B * int(ln) + int(ln)) * 4
+        got.append((int(src), int(dst), int(imm), int(ln), data[pos:pos + nbytes]))
+        pos += nbytes
+    return got
+
+
+@pytest.mark.parametrize("m,naggs,B", [(3, 2, 256), (2, 1, 1024)])
+def test_servers_are_aggregators_messages_trace(gpu, tmp_path, m, naggs, B):
+    """-M with separate server processes: the workers and the servers exchange the reference's wire messages over
+    the transport; each worker's -T trace (its messages and the replies it received) equals the oracle's per-slot
+    state machines record for record, and every worker passes the CHECK."""
+    n, r = 1 << 20, 0.2
+    trace = str(tmp_path / "wire{w}.bin")
+    srv, cli = _run_servers_clients(m, naggs, ["-M", "-n", str(n), "-b", str(B), "-r", str(r), "-W", "1", "-R", "2",
+                                               "-c", "-T", trace], tmp_path)
+    for rc, out in cli:
+        assert rc == 0 and "check OK" in out, out
+    for rc, out in srv:
+        assert rc == 0 and "protocol rounds" in out, out
+    L = Layout(n=n, block_size=B)
+    bufs = [oracle.fill(oracle.gen_bitmap(w, r, L.nb), B) for w in range(m)]
+    flags = [oracle.flags_from_data(b, B) for b in bufs]
+    for w in range(m):
+        got = _read_trace(trace.replace("{w}", str(w)), B)
+        exp = _expected_trace(bufs, flags, n, B, L, naggs, w)
+        assert len(got) == len(exp), (w, len(got), len(exp))
+        for i, (g, e) in enumerate(zip(got, exp)):
+            assert g == e, f"worker {w} record {i}: {g[:4]} vs {e[:4]}"
 
 
 def test_client_message_mode_trace(gpu, tmp_path):
