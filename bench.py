@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--density", type=float, default=0.095, help="reference -r (0.095 -> 10%% non-zero)")
     p.add_argument("--workers", type=int, default=1, help="m worker tensors per GPU (N=1 only)")
     p.add_argument("--rotate", type=int, default=4, help="buffer sets rotated to defeat the Infinity Cache")
-    p.add_argument("--cpu-rounds", type=int, default=500)
+    p.add_argument("--cpu-rounds", type=int, default=101, help="CPU baseline rounds (client.cc:368-369: 10 + 101)")
     p.add_argument("--cpu-warmups", type=int, default=10)
     p.add_argument("--cpu-threads", type=int, default=8)
     p.add_argument("--no-cpu", action="store_true")
@@ -76,9 +76,6 @@ def parse():
                         "(OMR_ROUND_DEFER, default) = as async, and round k's exchange is issued after round k+1's "
                         "first half is queued, so the host never waits for block counts with the GPU idle")
     p.add_argument("--dist-sync", action="store_true", help="same as --dist-pipe sync")
-    p.add_argument("--dist-impl", choices=("cpp", "torch"), default="cpp",
-                   help="N>1 round driver: C++ (libomr_dist.so, RCCL from C++) or Python (omr.dist over "
-                        "torch.distributed); same protocol and kernels")
     return p.parse_args()
 
 
@@ -276,28 +273,21 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
-    if dist_mode and args.dist_mode == "dense" and args.dist_impl != "cpp":
-        raise SystemExit("--dist-mode dense runs on the C++ round driver only (--dist-impl cpp)")
     if dist_mode:
-        if args.dist_impl == "cpp":
-            from omr import cdist
-            engine = cdist.CppSparseAllreduce(L, device=dev)
-        else:
-            from omr import dist
-            engine = dist.SparseAllreduce(L, device=dev)
+        from omr import cdist
+        engine = cdist.CppSparseAllreduce(L, device=dev)
         for xs, out in sets:  # out-of-place result buffers keep every step's input pristine
             out.copy_(xs[0])
 
-        pipe = "sync" if (args.dist_sync or args.dist_impl != "cpp") else args.dist_pipe
+        pipe = "sync" if args.dist_sync else args.dist_pipe
         pipelined = pipe != "sync"
 
         def step(i, ev=None):
             xs, out = sets[i % len(sets)]
-            if args.dist_impl == "cpp":
-                engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
-                           async_=pipelined, defer=pipe == "defer")
-            else:
-                engine.run(xs[0], out=out, ev=ev, mode=0 if args.dist_mode == "allreduce" else 1)
+            # a timed step (ev given) brackets its worker scan and its exchange with HIP events on the streams they
+            # run on, inside the timed region (omr_ar_plan_timings)
+            engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
+                       async_=pipelined, defer=pipe == "defer", time_exchange=ev is not None)
     else:
         fused = m == 1 and args.kernel == "fused"
         plan = ops.ScanSumPlan(L, m, device=dev, fused=fused)
@@ -315,7 +305,7 @@ def main():
                 plan.resolve_next()
 
     def join():  # asynchronous rounds: the caller's stream waits for the last one (the device sync below covers it too)
-        if dist_mode and args.dist_impl == "cpp":
+        if dist_mode:
             engine.join(stream)
 
     for i in range(args.warmup):
@@ -355,46 +345,27 @@ def main():
     kernel_name = ("k_scan1f (single pass: scan + sum + next)" if (m == 1 and args.kernel == "fused") else
                    ("k_scan1" if m == 1 else "k_scanm"))
     if dist_mode:
-        kernel_name = ("k_scan1f (round worker scan: flags + next + row masks, no out)" if args.dist_impl == "cpp"
-                       else "k_scan1 (worker scan, no out)")
-    if dist_mode and args.dist_impl == "cpp":
-        # the C++ round is one call; time its worker-scan kernel in its own event-bracketed loop, same data
-        # (masks not re-zeroed between launches: same atomics, timing only)
-        plan1 = ops.ScanSumPlan(L, 1, device=dev, fused=True, row_masks=True)
-        for i in range(min(args.steps, 50)):
-            xs, _ = sets[i % len(sets)]
-            kev[i][0].record(stream)
-            plan1.run(xs, None, zero_masks=False)
-            kev[i][1].record(stream)
-        torch.cuda.synchronize()
-        kev = kev[:min(args.steps, 50)]
-        # the worker -> aggregator exchange of a sample of rounds, timed with events on the stream it runs on
-        # (after the timed region: the events cost host time)
-        xs_ms, xs_out, xs_in = [], [], []
-        for i in range(min(args.steps, 20)):
-            xs, out = sets[i % len(sets)]
-            engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
-                       async_=pipelined, defer=pipe == "defer", time_exchange=True)
-            engine.join(stream)  # (issues a deferred round's exchange)
-            ms_x, b_out, b_in = engine.exchange_time()
-            xs_ms.append(ms_x)
-            xs_out.append(b_out)
-            xs_in.append(b_in)
-        join()
-        torch.cuda.synchronize()
-        x_ms = float(np.mean(xs_ms))
-        exchange = {"ms_mean": round(x_ms, 5), "bytes_out_per_rank": int(np.mean(xs_out)),
-                    "bytes_in_per_rank": int(np.mean(xs_in)), "peers": ws - 1,
-                    "GBps_out_per_rank": round(float(np.mean(xs_out)) / (x_ms * 1e-3) / 1e9, 2) if x_ms > 0 else None,
-                    "GBps_out_per_peer": (round(float(np.mean(xs_out)) / (ws - 1) / (x_ms * 1e-3) / 1e9, 2)
+        kernel_name = "k_scan1f (round worker scan: flags + next + row masks, no out)"
+    scan_ms_dist = None
+    if dist_mode:
+        # the timed rounds' own events (every `every`-th timed step): its worker scan kernel on the caller's stream,
+        # its worker -> aggregator exchange on the stream it ran on
+        scan_ms_dist, x_ms, b_out, b_in, n_timed = engine.timings()
+        exchange = {"ms_mean": round(x_ms, 5), "bytes_out_per_rank": int(b_out), "bytes_in_per_rank": int(b_in),
+                    "peers": ws - 1, "timed_rounds": n_timed,
+                    "GBps_out_per_rank": round(b_out / (x_ms * 1e-3) / 1e9, 2) if x_ms > 0 else None,
+                    "GBps_in_per_rank": round(b_in / (x_ms * 1e-3) / 1e9, 2) if x_ms > 0 else None,
+                    "GBps_out_per_peer": (round(b_out / (ws - 1) / (x_ms * 1e-3) / 1e9, 2)
                                           if x_ms > 0 and ws > 1 else None),
                     "xgmi_link_GBps_nominal": XGMI_LINK_GBPS,
-                    "timing": "HIP events around the grouped ncclSend/ncclRecv (dense: ncclReduceScatter) on the "
-                              "round's communication stream, 20 rounds after the timed region, rank 0"}
-    if not (dist_mode and args.dist_impl == "cpp"):
+                    "timing": (f"HIP events around the grouped ncclSend/ncclRecv (dense: ncclReduceScatter) on the "
+                               f"stream it runs on, in every {every}th timed round (inside the timed region), rank 0")}
+    if not dist_mode:
         kev = kev[::every]
     if one_kernel:  # every step is exactly one k_scan1f launch: events around all K steps, divided by K
         kms = span[0].elapsed_time(span[1]) / args.steps
+    elif scan_ms_dist is not None:
+        kms = scan_ms_dist
     else:
         kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
     if True:
@@ -413,7 +384,10 @@ def main():
                     "algorithmic_bytes_per_launch": kbytes,
                     "timing": ("fence-free HIP events (hipEventDisableSystemFence) on the kernel's stream around "
                                "the timed launches" + (" (all K, divided by K)" if one_kernel else
-                                                       f" (every {every}th step)")),
+                                                       f" (every {every}th step)")
+                               if scan_ms_dist is None else
+                               (f"HIP events on the round's stream around its worker scan, in every {every}th timed "
+                                f"round (inside the timed region, omr_ar_plan_timings)")),
                     "traffic_source": ("rocprofv3 PMC 2*FETCH_SIZE+WRITE_SIZE per launch, "
                                        + os.path.relpath(args.pmc, ROOT)) if traffic else None}
         if not dist_mode:
@@ -426,7 +400,7 @@ def main():
             torch.distributed.destroy_process_group()
         return
     pipe_note = ""
-    if dist_mode and args.dist_impl == "cpp" and pipe != "sync":
+    if dist_mode and pipe != "sync":
         pipe_note = (", rounds pipelined: exchange k beside scan k+1" +
                      (", exchange k issued after round k+1's first half (OMR_ROUND_DEFER)" if pipe == "defer" else ""))
     total_bytes = n_gpus * m * L.nbytes
@@ -456,7 +430,7 @@ def main():
                    "workers_per_gpu": m, "rotating_buffer_sets": len(sets),
                    "parallelism": "single GPU" if not dist_mode else
                    f"dp{n_gpus} {dict(allreduce='sparse all-reduce', reduce='sparse reduce-scatter', dense='dense reduce-scatter (stand-in)')[args.dist_mode]} over "
-                   f"RCCL ({args.dist_impl} round driver"
+                   f"RCCL (C++ round driver, libomr_dist.so"
                    f"{pipe_note})"},
         "alg_bw_GiBps_reference_style": round(total_bytes / (ms_per_step * 1e-3) / 2 ** 30, 2),
         "roofline": roofline,

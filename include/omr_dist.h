@@ -141,6 +141,11 @@ int omr_ar_plan_exchange_time(omr_ar_plan* plan, float* ms, uint64_t* bytes_out,
  * the work enqueued on `stream` (joined).  *sent_blocks / *union_blocks: sums over the buckets. */
 int omr_sparse_buckets_f32(omr_ar_plan* plan, float* buf, uint64_t total_n, int mode, uint64_t* sent_blocks,
                            uint64_t* union_blocks, omr_stream_t stream);
+/* Means over the OMR_ROUND_TIME_EXCHANGE rounds issued since the last call (at most the last 64): the worker scan
+ * kernel (events on the round's stream around omr_worker_scan_f32), the worker -> aggregator exchange and its bytes
+ * per rank; *rounds = how many rounds were timed.  Waits for those rounds' events. */
+int omr_ar_plan_timings(omr_ar_plan* plan, float* scan_ms, float* exchange_ms, uint64_t* bytes_out, uint64_t* bytes_in,
+                        uint32_t* rounds);
 /* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
 int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
 

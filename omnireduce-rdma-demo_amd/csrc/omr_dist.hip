@@ -594,9 +594,19 @@ struct omr_ar_plan {
   uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
   // OMR_ROUND_TIME_EXCHANGE: events around the last timed round's worker -> aggregator exchange, and its bytes
-  hipEvent_t xt0 = nullptr, xt1 = nullptr;
+  hipEvent_t xt0 = nullptr, xt1 = nullptr;  // the last timed exchange's events (owned by its ring record)
   bool xt_recorded = false;
   uint64_t xt_out = 0, xt_in = 0;
+  // every OMR_ROUND_TIME_EXCHANGE round also lands in a ring: its worker scan and its exchange, for means over the
+  // timed rounds (omr_ar_plan_timings)
+  struct Timed {
+    hipEvent_t s0 = nullptr, s1 = nullptr, x0 = nullptr, x1 = nullptr;
+    bool scan = false, xchg = false;
+    uint64_t out = 0, in = 0;
+  };
+  static constexpr int kTimed = 64;
+  std::vector<Timed> timed;
+  uint32_t timed_next = 0, timed_first = 0;  // ring [first, next) not yet read
   // OMR_ROUND_DEFER: the round whose exchange and aggregation the next call (or join) issues
   struct Pending {
     bool active = false;
@@ -605,6 +615,7 @@ struct omr_ar_plan {
     const float* x = nullptr;
     float* out = nullptr;
     uint32_t seq = 0;
+    int tslot = -1;            // its timing record (OMR_ROUND_TIME_EXCHANGE)
     hipStream_t st = nullptr;  // the stream its first half went on (the count wait checks it for a failed launch)
   } pend;
   // rounds issued on different streams run in call order: the plan's arrival counter, own-mask buffer and scan
@@ -728,8 +739,9 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p->s_in) (void)hipStreamDestroy(p->s_in);
   if (p->s_out) (void)hipStreamDestroy(p->s_out);
   if (p->st_ev) (void)hipEventDestroy(p->st_ev);
-  if (p->xt0) (void)hipEventDestroy(p->xt0);
-  if (p->xt1) (void)hipEventDestroy(p->xt1);
+  for (auto& t : p->timed)
+    for (hipEvent_t e : {t.s0, t.s1, t.x0, t.x1})
+      if (e) (void)hipEventDestroy(e);
   (void)hipHostFree(p->counts_host);
   (void)hipHostFree(p->flag_host);
   (void)hipFree(p->arrive);
@@ -789,8 +801,6 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   }
   A(hip_check(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking), "hipStreamCreate"));
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, hipEventDisableTiming), "hipEventCreate"));
-  A(hip_check(hipEventCreate(&p->xt0), "hipEventCreate"));
-  A(hip_check(hipEventCreate(&p->xt1), "hipEventCreate"));
   A(dev_alloc(&p->bounds_dev, NA + 1));
   if (N > 1 && p->shard >= 0) A(dev_alloc(&p->recv, static_cast<size_t>(M) * p->shard_nb * block_size));
   A(dev_alloc(&p->results, n));
@@ -833,8 +843,31 @@ namespace {
 
 // The second half of a round (steps 4b-7): wait for the plan's counts, exchange, shard sums [, sums back,
 // unpack].  `async`: on the communication stream, behind the set's `ready` event.
+// a timed round's ring record: the next slot (events created on first use)
+int timed_slot(omr_ar_plan* p, int* slot) {
+  if (p->timed.empty()) p->timed.resize(omr_ar_plan::kTimed);
+  const int k = static_cast<int>(p->timed_next++ % omr_ar_plan::kTimed);
+  if (p->timed_next - p->timed_first > omr_ar_plan::kTimed) p->timed_first = p->timed_next - omr_ar_plan::kTimed;
+  omr_ar_plan::Timed& t = p->timed[k];
+  if (t.s0 == nullptr)
+    for (hipEvent_t* e : {&t.s0, &t.s1, &t.x0, &t.x1}) TRY(hip_check(hipEventCreate(e), "hipEventCreate"));
+  t.scan = t.xchg = false;
+  *slot = k;
+  return 0;
+}
+// the timed round's exchange was bracketed by its record's x0 / x1; note its bytes
+int timed_exchange(omr_ar_plan* p, int slot) {
+  omr_ar_plan::Timed& t = p->timed[slot];
+  t.xchg = true;
+  t.out = p->xt_out;
+  t.in = p->xt_in;
+  p->xt0 = t.x0;  // the last timed exchange (omr_ar_plan_exchange_time)
+  p->xt1 = t.x1;
+  return 0;
+}
+
 int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, bool async, bool timed, uint32_t seq,
-                 hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks) {
+                 hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks, int tslot) {
   omr_ar_plan::Set& S = p->set[si];
   const int N = p->N, M = p->M, NA = p->A, me = p->me, sh = p->shard;
   const uint64_t rows = p->rows, B = p->B;
@@ -853,13 +886,14 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     // the dense stand-in: every element of this rank's shard, reduced over all ranks by the transport
     const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
     const uint64_t row_floats = static_cast<uint64_t>(p->lanes) * B;
-    if (timed) TRY(hip_check(hipEventRecord(p->xt0, xs), "hipEventRecord"));
+    if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].x0, xs), "hipEventRecord"));
     TRY(p->d->reduce_scatter(x, out + r0 * row_floats, (r1 - r0) * row_floats, xs));
     if (timed) {
-      TRY(hip_check(hipEventRecord(p->xt1, xs), "hipEventRecord"));
+      TRY(hip_check(hipEventRecord(p->timed[tslot].x1, xs), "hipEventRecord"));
       // a ring reduce-scatter sends and receives (N-1)/N of the tensor per rank
       p->xt_out = p->xt_in = static_cast<uint64_t>(N - 1) * (r1 - r0) * row_floats * sizeof(float);
       p->xt_recorded = true;
+      TRY(timed_exchange(p, tslot));
     }
     if (async) {
       TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
@@ -880,7 +914,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
   //     from every worker but itself
   std::vector<uint64_t> roff(M, 0);
   uint64_t in_blocks = 0;
-  if (timed) TRY(hip_check(hipEventRecord(p->xt0, xs), "hipEventRecord"));
+  if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].x0, xs), "hipEventRecord"));
   if (N > 1) {
     std::vector<Slices> sends(N), recvs(N);
     if (wk)
@@ -900,10 +934,11 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     TRY(p->d->exchange(sends, recvs, xs));
   }
   if (timed) {
-    TRY(hip_check(hipEventRecord(p->xt1, xs), "hipEventRecord"));
+    TRY(hip_check(hipEventRecord(p->timed[tslot].x1, xs), "hipEventRecord"));
     p->xt_out = total_send * B * sizeof(float);
     p->xt_in = in_blocks * B * sizeof(float);
     p->xt_recorded = true;
+    TRY(timed_exchange(p, tslot));
   }
   const bool rs_mode = mode == OMR_ROUND_REDUCE_SCATTER;
   // 5. aggregator: rank-order shard sums (server.cc:97-98); a co-located rank reads its own blocks in place.
@@ -957,7 +992,7 @@ int flush_pending(omr_ar_plan* p, hipStream_t st, uint64_t* sent_blocks, uint64_
   const omr_ar_plan::Pending q = p->pend;
   p->pend.active = false;
   (void)st;
-  return round_finish(p, q.si, q.x, q.out, q.mode, true, q.timed, q.seq, q.st, sent_blocks, union_blocks);
+  return round_finish(p, q.si, q.x, q.out, q.mode, true, q.timed, q.seq, q.st, sent_blocks, union_blocks, q.tslot);
 }
 
 }  // namespace
@@ -1009,9 +1044,17 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   p->cur ^= 1;
   // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass (a dedicated aggregator
   //    offers its all-zero mask buffer to the all-gather)
-  if (p->worker())
+  int tslot = -1;
+  if (timed) TRY(timed_slot(p, &tslot));
+  if (p->worker()) {
+    if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
     TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, p->own_masks, nullptr, p->scan_ws,
                                       p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+    if (timed) {
+      TRY(hip_check(hipEventRecord(p->timed[tslot].s1, st), "hipEventRecord"));
+      p->timed[tslot].scan = true;
+    }
+  }
   // the set is refilled from here on: an asynchronous round two calls back must be through with it
   // (skipped when the host already sees the event complete: a stream-wait packet costs the GPU a few
   // microseconds of dispatch even when its event has long fired)
@@ -1044,7 +1087,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   TRY(omr_check(omr_next_offsets(S.umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
   // the rest goes on the communication stream for an asynchronous round, behind everything queued so far
   if (async) TRY(hip_check(hipEventRecord(S.ready, st), "hipEventRecord"));
-  if (!defer) return round_finish(p, si, x, out, mode, async, timed, seq, st, sent_blocks, union_blocks);
+  if (!defer) return round_finish(p, si, x, out, mode, async, timed, seq, st, sent_blocks, union_blocks, tslot);
   // deferred: this round's first half is queued; now issue the previous round's exchange, whose counts have long
   // been in host memory, so the host neither waits nor leaves the caller's stream idle
   TRY(flush_pending(p, st, sent_blocks, union_blocks));
@@ -1055,6 +1098,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   p->pend.x = x;
   p->pend.out = out;
   p->pend.seq = seq;
+  p->pend.tslot = tslot;
   p->pend.st = st;
   return 0;
 }
@@ -1182,6 +1226,39 @@ int omr_ar_plan_exchange_time(omr_ar_plan* p, float* ms, uint64_t* bytes_out, ui
   TRY(hip_check(hipEventElapsedTime(ms, p->xt0, p->xt1), "hipEventElapsedTime"));
   if (bytes_out) *bytes_out = p->xt_out;
   if (bytes_in) *bytes_in = p->xt_in;
+  return 0;
+}
+
+int omr_ar_plan_timings(omr_ar_plan* p, float* scan_ms, float* exchange_ms, uint64_t* bytes_out, uint64_t* bytes_in,
+                        uint32_t* rounds) {
+  if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_timings: NULL");
+  double ss = 0, xs = 0;
+  uint64_t bo = 0, bi = 0;
+  uint32_t ns = 0, nx = 0;
+  for (uint32_t i = p->timed_first; i < p->timed_next; ++i) {
+    omr_ar_plan::Timed& t = p->timed[i % omr_ar_plan::kTimed];
+    float ms = 0;
+    if (t.scan) {
+      TRY(hip_check(hipEventSynchronize(t.s1), "hipEventSynchronize"));
+      TRY(hip_check(hipEventElapsedTime(&ms, t.s0, t.s1), "hipEventElapsedTime"));
+      ss += ms;
+      ++ns;
+    }
+    if (t.xchg) {
+      TRY(hip_check(hipEventSynchronize(t.x1), "hipEventSynchronize"));
+      TRY(hip_check(hipEventElapsedTime(&ms, t.x0, t.x1), "hipEventElapsedTime"));
+      xs += ms;
+      bo += t.out;
+      bi += t.in;
+      ++nx;
+    }
+  }
+  p->timed_first = p->timed_next;
+  if (scan_ms) *scan_ms = ns ? static_cast<float>(ss / ns) : 0.f;
+  if (exchange_ms) *exchange_ms = nx ? static_cast<float>(xs / nx) : 0.f;
+  if (bytes_out) *bytes_out = nx ? bo / nx : 0;
+  if (bytes_in) *bytes_in = nx ? bi / nx : 0;
+  if (rounds) *rounds = nx > ns ? nx : ns;
   return 0;
 }
 

@@ -1,6 +1,6 @@
 """ctypes binding of the C++ multi-rank round (include/omr_dist.h, libomr_dist.so).
 
-`CppSparseAllreduce` runs the same OmniReduce round as omr.dist.SparseAllreduce, but the whole round — kernels,
+`CppSparseAllreduce` is one rank of the product's OmniReduce round: the whole round — kernels,
 block-count sync, RCCL all-gather and grouped send/recv — is driven from C++ (omr_dist.hip).  Python only
 bootstraps the RCCL communicator: rank 0's unique id is broadcast over the torch.distributed group the job was
 launched with (torch.distributed.run), standing in for the reference's TCP bootstrap.
@@ -57,6 +57,7 @@ def load():
         "omr_msgd_round_f32": (i, [vp, vp, vp, vp, vp]),
         "omr_msgd_logs": (i, [vp, u32, vp, vp, vp, vp, vp, vp]),
         "omr_ar_plan_exchange_time": (i, [vp, vp, vp, vp]),
+        "omr_ar_plan_timings": (i, [vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -177,6 +178,14 @@ class CppSparseAllreduce:
         _check(load().omr_ar_plan_exchange_time(self._p, ctypes.byref(ms), ctypes.byref(bo), ctypes.byref(bi)),
                "omr_ar_plan_exchange_time")
         return ms.value, bo.value, bi.value
+
+    def timings(self):
+        """Means over the rounds run with time_exchange=True since the last call (omr_ar_plan_timings): (worker scan
+        ms, exchange ms, bytes out per rank, bytes in per rank, timed rounds)."""
+        sm, xm, bo, bi, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint32()
+        _check(load().omr_ar_plan_timings(self._p, ctypes.byref(sm), ctypes.byref(xm), ctypes.byref(bo),
+                                          ctypes.byref(bi), ctypes.byref(n)), "omr_ar_plan_timings")
+        return sm.value, xm.value, bo.value, bi.value, n.value
 
     def join(self, stream=None):
         """Make `stream` (default: the current stream) wait for every asynchronous round issued so far."""

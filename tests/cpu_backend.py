@@ -1,5 +1,5 @@
-"""Test-only stand-ins for omr.dist: a CPU compute backend built on the oracle, and a host-staged comm that lets
-several processes share one GPU over gloo.  Neither is reachable from the product path (omr.dist uses
+"""Test-only stand-ins for the dist twin (tests/dist_twin.py): a CPU compute backend built on the oracle, and a host-staged comm that lets
+several processes share one GPU over gloo.  Neither is reachable from the product path (dist_twin uses
 HipBackend + TorchComm unless a caller injects these)."""
 from __future__ import annotations
 
@@ -15,7 +15,7 @@ def _np(t):
 
 
 class CpuBackend:
-    """Same interface as omr.dist.HipBackend, computed on the host with the oracle (tensors stay on CPU)."""
+    """Same interface as dist_twin.HipBackend, computed on the host with the oracle (tensors stay on CPU)."""
 
     def __init__(self, L, world, device="cpu"):
         self.L = L

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Rehearse the RCCL path of omr.dist on the GPUs this box has: spawn `world` ranks with backend "nccl",
-mapping rank r to device r % device_count, run SparseAllreduce rounds and check each against the oracle.
+"""Rehearse the product's C++ round (libomr_dist.so over RCCL) on the GPUs this box has: spawn `world` ranks with
+backend "nccl", mapping rank r to device r % device_count, run CppSparseAllreduce rounds in the sync, async and
+defer pipelines and check every rank's result against the oracle bit-exactly.
 (Several ranks per device only works if RCCL accepts it; on an 8-GPU node every rank gets its own GPU.)"""
 import argparse
 import os
@@ -19,7 +20,7 @@ import torch.multiprocessing as mp  # noqa: E402
 def worker(rank, world, port, n, B, density, rounds):
     import oracle
     from omr import Layout
-    from omr import dist as odist
+    from omr import cdist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda", rank % torch.cuda.device_count())
     torch.cuda.set_device(dev)
@@ -28,15 +29,21 @@ def worker(rank, world, port, n, B, density, rounds):
     bufs = [oracle.fill(oracle.gen_bitmap(w, density, L.nb), B, mode=1, seed=w + 1) for w in range(world)]
     x = torch.from_numpy(bufs[rank].copy()).to(dev)
     out = x.clone()
-    eng = odist.SparseAllreduce(L, device=dev)
+    eng = cdist.CppSparseAllreduce(L, dev)
     uf = oracle.union_flags([oracle.flags_from_data(b, B) for b in bufs])
     exp = bufs[rank].copy()
     oracle.block_sum(bufs, L.n, B, L.num_lanes, L.num_threads, uf, exp)
-    for _ in range(rounds):
-        eng.run(x, out=out)
-    torch.cuda.synchronize()
-    ok = (out.cpu().numpy().view(np.uint32) == exp.view(np.uint32)).all()
-    print(f"rank {rank}: {'OK' if ok else 'MISMATCH'}", flush=True)
+    ok = True
+    for pipe in ("sync", "async", "defer"):
+        out.copy_(x)
+        for _ in range(rounds):
+            eng.run(x, out=out, async_=pipe != "sync", defer=pipe == "defer")
+        eng.join()
+        torch.cuda.synchronize()
+        good = bool((out.cpu().numpy().view(np.uint32) == exp.view(np.uint32)).all())
+        print(f"rank {rank} {pipe}: {'OK' if good else 'MISMATCH'}", flush=True)
+        ok &= good
+    eng.close()
     dist.barrier()
     dist.destroy_process_group()
     if not ok:
