@@ -353,69 +353,74 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
 
 // ---------------------------------------------------------------- k_scanm: m >= 2 workers on one device
 //
-// One wave per row, rows swept grid-stride.  Per group of SUB blocks of the row, the m workers' blocks are read in
-// rank order (buffer loads, nt; UW workers' SUB*VEC dwordx4 per lane in flight at once) and accumulated from
-// +0.0f (server.cc:148-150, :97-98); each block's ballot gives the worker's flag bit.  Adding a zero-flagged
-// worker's block (all +-0.0) to an accumulator that started at +0.0 never changes it, so summing every worker
-// equals the reference, which only adds the workers that sent the block.  The aggregated blocks go out
-// write-through with a static store schedule (a block outside the write set is pointed past the row's
-// descriptor and dropped).  Lane w keeps worker w's row mask (no runtime-indexed register arrays).
-// tools/tune_scanm.py: SUB*VEC = 16 loads per worker, UW = 1 is fastest (8 x 256 MiB: 391.5 vs 410.8 us for the
-// previous plain-load form, csrc/tune/scanm_variants.hip).
-template <int VEC, int SUB, int UW>
+// Work unit = the blocks of G consecutive lanes of one row, for every worker (G = 32 lanes: 32 KiB per worker at
+// B=256; the whole row when it is narrower).  Units are swept grid-stride, one unit per wave, the workgroup ->
+// unit order XCD-contiguous.  Per group of SUB blocks the m workers' blocks are read in rank order (buffer loads,
+// nt; SUB*VEC = 32 dwordx4 per lane in flight) and accumulated from +0.0f (server.cc:148-150, :97-98); each block's
+// ballot gives the worker's flag bit.  Adding a zero-flagged worker's block (all +-0.0) to an accumulator that
+// started at +0.0 never changes it, so summing every worker equals the reference, which only adds the workers
+// that sent the block.  The aggregated blocks go out write-through with a static store schedule (a block outside
+// the write set is pointed past the row's descriptor and dropped).  Lane w keeps worker w's bits of the unit and
+// stores them as the unit's piece of row mask w (a 32-bit store, or the whole 64-bit mask when the unit is the
+// row); lane m stores the union's piece.
+// The 32-load groups take ~270 VGPRs, i.e. ONE wave per SIMD: tools/tune_scanm_r02.py (profiles/r02/
+// tune_scanm_r02*.log) measured 8 x 256 MiB at 338-353 us against 359-404 us for round 1's kernel (a wave per
+// 64 KiB row, 16 loads in flight, three waves per SIMD) on the same boxes; more waves or more loads in flight
+// per CU (a second register set, or forcing 2-3 waves per SIMD) were slower, and staggering the worker buffers'
+// offsets (the channel-contention hypothesis) changed nothing.
+template <int VEC, int SUB, int G>
 __global__ __launch_bounds__(kWGThreads) void k_scanm(ScanArgs a) {
   constexpr uint32_t B4 = 64 * VEC;  // 16-byte vectors per block
+  static_assert(G % SUB == 0 && G <= 64 && SUB <= 32, "a unit is whole SUB-groups of one row");
   const int lane = threadIdx.x & 63;
-  const uint32_t row_bytes = a.lanes * B4 * 16;
-  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (uint64_t row = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + wave; row < a.rows; row += nwaves) {
+  const uint32_t gl = a.lanes < static_cast<uint32_t>(G) ? a.lanes : static_cast<uint32_t>(G);  // lanes per unit
+  const uint32_t upr = a.lanes / gl;  // units per row (1 or 2)
+  const uint64_t units = a.rows * upr;
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;  // XCD-contiguous units
+  const uint64_t stride = static_cast<uint64_t>(T) * kWavesPerWG;
+  for (uint64_t u = static_cast<uint64_t>(lin) * kWavesPerWG + wave; u < units; u += stride) {
+    const uint64_t row = u / upr;
+    const uint32_t g0 = static_cast<uint32_t>(u % upr) * gl;
     const bool head = (row % a.rows_per_part) == 0;
     const uint64_t rowbase = row * a.lanes * B4 * 4;  // float offset of the row
-    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + rowbase, a.out != nullptr ? row_bytes : 0u);
-    uint64_t lane_wm = 0;  // lane w: worker w's mask
-    uint64_t um = 0;       // union mask (wave-uniform)
-    for (uint32_t l0 = 0; l0 < a.lanes; l0 += SUB) {
+    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + rowbase, a.out != nullptr ? a.lanes * B4 * 16 : 0u);
+    uint64_t lane_wm = 0;  // lane w: worker w's bits of the unit (bit i = lane g0 + i)
+    uint64_t um = 0;       // union bits (wave-uniform)
+    for (uint32_t l0 = g0; l0 < g0 + gl; l0 += SUB) {
       v4f acc[SUB][VEC];
 #pragma unroll
       for (int s = 0; s < SUB; ++s)
 #pragma unroll
         for (int q = 0; q < VEC; ++q) acc[s][q] = v4f{0.f, 0.f, 0.f, 0.f};
       uint32_t sub_any = 0;
-      for (uint32_t w = 0; w < a.m; w += UW) {
-        v4f v[UW][SUB][VEC];
+      const uint64_t goff = rowbase + static_cast<uint64_t>(l0) * B4 * 4;
+      for (uint32_t w = 0; w < a.m; ++w) {
+        const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x.p[w] + goff, SUB * B4 * 16);
+        v4f v[SUB][VEC];
 #pragma unroll
-        for (int j = 0; j < UW; ++j) {
-          // workers past m read through an empty descriptor: zeros, no memory traffic
-          const bool live = w + j < a.m;
-          const __amdgpu_buffer_rsrc_t src =
-              chunk_rsrc(a.x.p[live ? w + j : 0] + rowbase + static_cast<uint64_t>(l0) * B4 * 4, live ? SUB * B4 * 16 : 0u);
+        for (int s = 0; s < SUB; ++s)
 #pragma unroll
-          for (int s = 0; s < SUB; ++s)
+          for (int q = 0; q < VEC; ++q)
+            v[s][q] = __builtin_bit_cast(
+                v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (s * B4 + q * 64 + lane) * 16, 0, kLoadAux));
+        __builtin_amdgcn_sched_barrier(0);  // the whole group in flight before the first use
+        uint32_t wbits = 0;
 #pragma unroll
-            for (int q = 0; q < VEC; ++q)
-              v[j][s][q] = __builtin_bit_cast(
-                  v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (s * B4 + q * 64 + lane) * 16, 0, kLoadAux));
-        }
-        __builtin_amdgcn_sched_barrier(0);  // every load of the group in flight before the first use
+        for (int s = 0; s < SUB; ++s) {
+          uint32_t o = 0;
 #pragma unroll
-        for (int j = 0; j < UW; ++j) {
-          uint32_t wbits = 0;
-#pragma unroll
-          for (int s = 0; s < SUB; ++s) {
-            uint32_t o = 0;
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) {
-              o |= nz_bits(v[j][s][q]);
-              acc[s][q] = add4(acc[s][q], v[j][s][q]);  // rank order: worker w+j after w+j-1 (server.cc:97-98)
-            }
-            wbits |= static_cast<uint32_t>(wave_ballot(o != 0) != 0) << s;
+          for (int q = 0; q < VEC; ++q) {
+            o |= nz_bits(v[s][q]);
+            acc[s][q] = add4(acc[s][q], v[s][q]);  // rank order: worker w after w-1 (server.cc:97-98)
           }
-          if (lane == static_cast<int>(w + j)) lane_wm |= static_cast<uint64_t>(wbits) << l0;
-          sub_any |= wbits;
+          wbits |= static_cast<uint32_t>(wave_ballot(o != 0) != 0) << s;
         }
+        if (lane == static_cast<int>(w)) lane_wm |= static_cast<uint64_t>(wbits) << (l0 - g0);
+        sub_any |= wbits;
       }
-      um |= static_cast<uint64_t>(sub_any) << l0;
+      um |= static_cast<uint64_t>(sub_any) << (l0 - g0);
 #pragma unroll
       for (int s = 0; s < SUB; ++s) {
         const uint32_t drop = (((sub_any >> s) & 1u) || head) ? 0u : kDropStore;
@@ -425,19 +430,28 @@ __global__ __launch_bounds__(kWGThreads) void k_scanm(ScanArgs a) {
                                                  (((l0 + s) * B4 + q * 64 + lane) * 16) | drop, 0, kStoreAux);
       }
     }
-    if (lane < static_cast<int>(a.m)) a.masks[static_cast<uint64_t>(lane) * a.rows + row] = lane_wm;
-    if (lane == 0) a.masks[static_cast<uint64_t>(a.m) * a.rows + row] = um;
+    // the unit's piece of row mask `lane` (workers 0..m-1, union at m); lanes >= NB stay zero
+    if (lane <= static_cast<int>(a.m)) {
+      const uint64_t bits = lane == static_cast<int>(a.m) ? um : lane_wm;
+      uint64_t* mrow = a.masks + static_cast<uint64_t>(lane) * a.rows + row;
+      if (gl == a.lanes)
+        *mrow = bits;
+      else  // two 32-lane units per 64-lane row
+        reinterpret_cast<uint32_t*>(mrow)[g0 / 32] = static_cast<uint32_t>(bits);
+    }
     if (a.flags != nullptr) {
       for (uint32_t w = 0; w < a.m; ++w) {
         const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(lane_wm), w);
         const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(lane_wm >> 32), w);
         const uint64_t wmw = (static_cast<uint64_t>(hi) << 32) | lo;
-        if (lane < static_cast<int>(a.lanes))
-          a.flags[w * a.nb + row * a.lanes + lane] = static_cast<int32_t>((wmw >> lane) & 1u);
+        if (static_cast<uint32_t>(lane) < gl)
+          a.flags[w * a.nb + row * a.lanes + g0 + lane] = static_cast<int32_t>((wmw >> lane) & 1u);
       }
     }
   }
 }
+
+constexpr int kScanmUnitLanes = 32;  // G
 
 // ---------------------------------------------------------------- k_next: next-offset chains
 //
@@ -1278,10 +1292,16 @@ int launch_scan(const Layout& L, const ScanArgs& a, hipStream_t st) {
     }
     return launch_status("k_scan1");
   }
+  // one unit per wave: rows x (lanes / G) units, kWavesPerWG per workgroup, no cap (the workgroups run one
+  // after another at one wave per SIMD)
+  const uint64_t gl = L.lanes < kScanmUnitLanes ? L.lanes : kScanmUnitLanes;
+  const uint64_t units = L.rows * (L.lanes / gl);
+  const unsigned gm = static_cast<unsigned>((units + kWavesPerWG - 1) / kWavesPerWG);
+  (void)g;
   switch (L.vec) {
-    case 1: k_scanm<1, 16, 1><<<g, kWGThreads, 0, st>>>(a); break;
-    case 2: k_scanm<2, 8, 1><<<g, kWGThreads, 0, st>>>(a); break;
-    default: k_scanm<4, 4, 1><<<g, kWGThreads, 0, st>>>(a); break;
+    case 1: k_scanm<1, 32, kScanmUnitLanes><<<gm, kWGThreads, 0, st>>>(a); break;
+    case 2: k_scanm<2, 16, kScanmUnitLanes><<<gm, kWGThreads, 0, st>>>(a); break;
+    default: k_scanm<4, 8, kScanmUnitLanes><<<gm, kWGThreads, 0, st>>>(a); break;
   }
   return launch_status("k_scanm");
 }
