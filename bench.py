@@ -21,6 +21,7 @@ cpu_baseline = the oracle's C restatement of the reference loop (client.cc:19-31
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -52,8 +53,9 @@ def parse():
     p.add_argument("--cpu-warmups", type=int, default=10)
     p.add_argument("--cpu-threads", type=int, default=8)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_r01.json"),
-                   help="rocprofv3 PMC summary giving HBM traffic per launch (optional)")
+    p.add_argument("--pmc", default="",
+                   help="rocprofv3 PMC summary giving HBM traffic per launch (default: the profiles/pmc_*.json "
+                        "measured on this workload)")
     p.add_argument("--print-workload", action="store_true", help="print the workload string and exit")
     p.add_argument("--host-resident", action="store_true",
                    help="BASELINE config 5's end-to-end path: the gradient in pinned host memory, reduced in place by "
@@ -129,15 +131,20 @@ def step_algorithmic_bytes(L: Layout, bitmaps, m: int) -> int:
 
 
 def read_pmc(path: str, workload: str, dist_mode: bool):
-    """HBM bytes per launch from a tools/pmc_traffic.py summary, when it was measured on this workload in this
-    mode (the round's worker scan writes no aggregated blocks, so single-GPU traffic does not describe it)."""
-    try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    same_mode = ("--force-dist" in d.get("bench_args", [])) == dist_mode
-    return d.get("hbm_bytes_per_launch") if d.get("workload") == workload and same_mode else None
+    """(HBM bytes per launch, source file) from a tools/pmc_traffic.py summary measured on this workload in this
+    mode: `path` if given, else the first of profiles/pmc_*.json that matches (the round's worker scan writes no
+    aggregated blocks, so single-GPU traffic does not describe it)."""
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")), reverse=True)
+    for c in cands:
+        try:
+            with open(c) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        same_mode = ("--force-dist" in d.get("bench_args", [])) == dist_mode
+        if d.get("workload") == workload and same_mode:
+            return d.get("hbm_bytes_per_launch"), c
+    return None, None
 
 
 def cpu_baseline(L: Layout, bm: np.ndarray, args):
@@ -376,7 +383,7 @@ def main():
         else:
             kbytes = algorithmic_scan_bytes(L, bitmaps, m)
         achieved = kbytes / (kms * 1e-3) / 1e9
-        traffic = read_pmc(args.pmc, workload, dist_mode)
+        traffic, pmc_src = read_pmc(args.pmc, workload, dist_mode)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                     "kernel": kernel_name,
@@ -389,7 +396,7 @@ def main():
                                (f"HIP events on the round's stream around its worker scan, in every {every}th timed "
                                 f"round (inside the timed region, omr_ar_plan_timings)")),
                     "traffic_source": ("rocprofv3 PMC 2*FETCH_SIZE+WRITE_SIZE per launch, "
-                                       + os.path.relpath(args.pmc, ROOT)) if traffic else None}
+                                       + os.path.relpath(pmc_src, ROOT)) if traffic else None}
         if not dist_mode:
             sbytes = step_algorithmic_bytes(L, bitmaps, m)
             roofline["step_algorithmic_bytes"] = sbytes

@@ -363,11 +363,14 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
 // the write set is pointed past the row's descriptor and dropped).  Lane w keeps worker w's bits of the unit and
 // stores them as the unit's piece of row mask w (a 32-bit store, or the whole 64-bit mask when the unit is the
 // row); lane m stores the union's piece.
-// The 32-load groups take ~270 VGPRs, i.e. ONE wave per SIMD: tools/tune_scanm_r02.py (profiles/r02/
-// tune_scanm_r02*.log) measured 8 x 256 MiB at 338-353 us against 359-404 us for round 1's kernel (a wave per
-// 64 KiB row, 16 loads in flight, three waves per SIMD) on the same boxes; more waves or more loads in flight
-// per CU (a second register set, or forcing 2-3 waves per SIMD) were slower, and staggering the worker buffers'
+// The 32-load groups take ~270 VGPRs, i.e. ONE wave per SIMD.  tools/tune_scanm_r02.py (profiles/r02/scanm/):
+// at 8 x 256 MiB, with one output per input set as bench.py rotates them, this shape with non-temporal stores
+// runs 359 us against 385 us with write-through (sc0 sc1) stores and 439 us for round 1's kernel (a wave per
+// 64 KiB row, 16 loads in flight, three waves per SIMD) on the same box.  More waves or more loads in flight per
+// CU (a second register set, or forcing 2-3 waves per SIMD) were slower, and staggering the worker buffers'
 // offsets (the channel-contention hypothesis) changed nothing.
+constexpr int kScanmStoreAux = 2;  // nt: the sums are a separate output stream, not re-read by this launch
+
 template <int VEC, int SUB, int G>
 __global__ __launch_bounds__(kWGThreads) void k_scanm(ScanArgs a) {
   constexpr uint32_t B4 = 64 * VEC;  // 16-byte vectors per block
@@ -427,7 +430,7 @@ __global__ __launch_bounds__(kWGThreads) void k_scanm(ScanArgs a) {
 #pragma unroll
         for (int q = 0; q < VEC; ++q)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[s][q]), dst,
-                                                 (((l0 + s) * B4 + q * 64 + lane) * 16) | drop, 0, kStoreAux);
+                                                 (((l0 + s) * B4 + q * 64 + lane) * 16) | drop, 0, kScanmStoreAux);
       }
     }
     // the unit's piece of row mask `lane` (workers 0..m-1, union at m); lanes >= NB stay zero

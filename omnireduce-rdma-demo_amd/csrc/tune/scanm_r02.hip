@@ -153,7 +153,7 @@ __device__ __forceinline__ void store_mask_piece(uint64_t* masks, uint64_t row, 
 // 2 = as 1 with scheduling barriers between the phases (no hoisting of the set after next); 3 = three sets.
 // A worker past m reads through an empty descriptor (zeros, no traffic); adding +0.0 to an accumulator that is never
 // -0.0 (it starts at +0.0, and a round-to-nearest sum is -0.0 only if both terms are) leaves it unchanged.
-template <int VEC, int SUB, int G, int WAVES, int PF, bool XCD>
+template <int VEC, int SUB, int G, int WAVES, int PF, bool XCD, int SAUX = kStoreAux>
 __global__ __launch_bounds__(64 * WAVES) void k_scanm_g(ScanArgs a) {
   constexpr uint32_t B4 = 64 * VEC;
   static_assert(G % SUB == 0 && G <= 64, "unit = whole sub-groups of one row");
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_scanm_g(ScanArgs a) {
 #pragma unroll
         for (int q = 0; q < VEC; ++q)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[s][q]), dst,
-                                                 (((l0 + s) * B4 + q * 64 + lane) * 16) | drop, 0, kStoreAux);
+                                                 (((l0 + s) * B4 + q * 64 + lane) * 16) | drop, 0, SAUX);
       }
     }
     if (lane < static_cast<int>(a.m))
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_scanm_g(ScanArgs a) {
 unsigned g_cap = 0;  // grid cap (workgroups); 0 = one unit per wave
 unsigned g_occ = 0;  // workgroups per CU forced through dynamic LDS (0 = registers decide)
 
-template <int VEC, int SUB, int G, int WAVES, int PF, bool XCD>
+template <int VEC, int SUB, int G, int WAVES, int PF, bool XCD, int SAUX = kStoreAux>
 void gog(const ScanArgs& a, hipStream_t st) {
   const uint64_t gl = a.lanes < G ? a.lanes : G;
   const uint64_t units = a.rows * (a.lanes / gl);
@@ -267,10 +267,10 @@ void gog(const ScanArgs& a, hipStream_t st) {
   unsigned lds = 0;
   if (g_occ) {
     lds = (160u * 1024u / g_occ - 512u) & ~255u;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scanm_g<VEC, SUB, G, WAVES, PF, XCD>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scanm_g<VEC, SUB, G, WAVES, PF, XCD, SAUX>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
   }
-  k_scanm_g<VEC, SUB, G, WAVES, PF, XCD><<<static_cast<unsigned>(g), 64 * WAVES, lds, st>>>(a);
+  k_scanm_g<VEC, SUB, G, WAVES, PF, XCD, SAUX><<<static_cast<unsigned>(g), 64 * WAVES, lds, st>>>(a);
 }
 void go_row(const ScanArgs& a, hipStream_t st) { k_scanm_row<1, 16, 1><<<grid_for(a.rows), kWGThreads, 0, st>>>(a); }
 void go_prod(const ScanArgs& a, hipStream_t st) {
@@ -285,9 +285,12 @@ const Variant kVariants[] = {
     {"product k_scanm (G32 SUB32)", go_prod},
     {"round-1 k_scanm (row/wave)", go_row},
     {"G32 SUB32 W4", gog<1, 32, 32, 4, 0, true>},
-    {"G32 SUB32 W1", gog<1, 32, 32, 1, 0, true>},
+    {"G32 SUB32 W4 st-nt", gog<1, 32, 32, 4, 0, true, 2>},
+    {"G32 SUB32 W4 st-plain", gog<1, 32, 32, 4, 0, true, 0>},
+    {"G32 SUB32 W4 st-sc1", gog<1, 32, 32, 4, 0, true, 16>},
+    {"G64 SUB32 W4", gog<1, 32, 64, 4, 0, true>},
+    {"G32 SUB16 W4 PF2", gog<1, 16, 32, 4, 2, true>},
     {"G16 SUB16 W4 PF2", gog<1, 16, 16, 4, 2, true>},
-    {"G16 SUB16 W4", gog<1, 16, 16, 4, 0, true>},
 };
 constexpr int kNum = sizeof(kVariants) / sizeof(kVariants[0]);
 }  // namespace

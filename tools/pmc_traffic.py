@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--workdir", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
     a = ap.parse_args()
+    a.out, a.workdir = os.path.abspath(a.out), os.path.abspath(a.workdir)  # the passes run from /tmp
     bench_args = [x for x in a.bench_args if x != "--"] or ["--steps", "20", "--warmup", "5", "--no-cpu"]
     fetch_csv = run_pass("FETCH_SIZE", os.path.join(a.workdir, "fetch"), bench_args)
     write_csv = run_pass("WRITE_SIZE", os.path.join(a.workdir, "write"), bench_args)

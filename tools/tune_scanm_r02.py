@@ -4,6 +4,8 @@ order, worker-pipelined loads, and the channel-contention test (the m worker buf
 at offsets staggered by --stagger-kib, against separate allocations).  Every variant is first checked against the
 product k_scanm bit for bit (sums, flags, row masks).  Each launch is timed alone (one event pair per launch,
 variants interleaved), so the spread over launches and buffer sets is visible, as in a rocprofv3 kernel trace.
+Each input set has its own output tensor, as in bench.py: one output reused by every launch lets the memory-side
+Infinity Cache absorb part of the 150 MB of sums written per launch, which bench.py does not get.
 usage: python tools/tune_scanm_r02.py [--workers 8] [--stagger-kib sep,0,4,68] [--variants 0,2]"""
 import argparse
 import ctypes
@@ -68,7 +70,8 @@ def main():
     L = Layout.from_bytes(a.size_mib << 20, 256)
     m = a.workers
     bms = [ops.gen_bitmap(w, a.density, L.nb) for w in range(m)]
-    out = torch.zeros(L.n, dtype=torch.float32, device=dev)
+    outs = [torch.zeros(L.n, dtype=torch.float32, device=dev) for _ in range(a.sets)]  # one per set, as bench.py
+    out = outs[0]
     flags = torch.zeros((m, L.nb), dtype=torch.int32, device=dev)
     masks = torch.zeros((m + 1, L.rows), dtype=torch.int64, device=dev)
     st = torch.cuda.current_stream().cuda_stream
@@ -86,8 +89,8 @@ def main():
         cases = [(v, c) for v in vids for c in (caps if v else [(0, 0)])]
 
         def run(v, c, k):
-            return lib.tune_scanm(v, ptrs[k], m, out.data_ptr(), flags.data_ptr(), masks.data_ptr(), L.n, 256, c[0],
-                                  c[1], st)
+            return lib.tune_scanm(v, ptrs[k], m, outs[k].data_ptr(), flags.data_ptr(), masks.data_ptr(), L.n, 256,
+                                  c[0], c[1], st)
 
         ref = None
         for v, c in cases:
