@@ -310,9 +310,20 @@ using Launch = void (*)(const Layout&, const FusedShape&, FusedArgs, hipStream_t
 unsigned grid_of(const Layout& L, const FusedShape& f) {
   return static_cast<unsigned>(static_cast<uint64_t>(L.parts) * L.lanes * f.K);
 }
-template <int VEC, int W, int LD, int ABL>
+unsigned g_occ = 0;  // workgroups per CU forced through dynamic LDS (0 = registers and workgroup size decide)
+
+template <typename K>
+unsigned occ_lds(K kern) {
+  if (!g_occ) return 0;
+  const unsigned lds = (160u * 1024u / g_occ - 4096u) & ~255u;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(lds));
+  return lds;
+}
+template <int VEC, int W, int LD, int ABL, int SAUX = kStoreAux>
 void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
-  k_scan1f<VEC, W, LD, ABL><<<grid_of(L, f), 64 * W, 0, st>>>(a);
+  const unsigned lds = occ_lds(&k_scan1f<VEC, W, LD, ABL, 1, SAUX>);
+  k_scan1f<VEC, W, LD, ABL, 1, SAUX><<<grid_of(L, f), 64 * W, lds, st>>>(a);
 }
 template <int VEC, int W, int LD, int P, int ABL>
 void go_d(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
@@ -335,6 +346,12 @@ struct Variant {
 };
 const Variant kVariants[] = {
     {"f w16 L16 (product)", true, go_f<1, 16, 16, 0>, go_f<4, 16, 16, 0>},
+    {"f w4 L32", true, go_f<1, 4, 32, 0>, go_f<4, 4, 32, 0>},
+    {"f w8 L32", true, go_f<1, 8, 32, 0>, go_f<4, 8, 32, 0>},
+    {"f w4 L16", true, go_f<1, 4, 16, 0>, go_f<4, 4, 16, 0>},
+    {"f w8 L16", true, go_f<1, 8, 16, 0>, go_f<4, 8, 16, 0>},
+    {"f w16 L16 nt-st", true, go_f<1, 16, 16, 0, 2>, go_f<4, 16, 16, 0, 2>},
+    {"f w4 L32 nt-st", true, go_f<1, 4, 32, 0, 2>, go_f<4, 4, 32, 0, 2>},
     {"pure read", false, go_r<1, 16>, go_r<4, 16>},
     {"d w16 L16 P4/P2", true, go_d<1, 16, 16, 4, 0>, go_d<4, 16, 16, 2, 0>},
     {"d w16 L16 P2/P1", true, go_d<1, 16, 16, 2, 0>, go_d<4, 16, 16, 1, 0>},
@@ -361,7 +378,8 @@ int tune_count(void) { return kNumVariants; }
 const char* tune_name(int v) { return (v >= 0 && v < kNumVariants) ? kVariants[v].name : "?"; }
 int tune_checked(int v) { return (v >= 0 && v < kNumVariants) ? kVariants[v].checked : 0; }
 int tune_run(int v, const float* x, float* out, int32_t* flags, uint32_t* next, void* ws, uint64_t n, uint32_t B,
-             uint32_t K, void* stream) {
+             uint32_t K, uint32_t occ, void* stream) {
+  g_occ = occ;
   Layout L;
   if (v < 0 || v >= kNumVariants) return -3;
   if (make_layout(n, B, 16384 / B, 8, &L)) return -1;

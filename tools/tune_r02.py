@@ -28,7 +28,7 @@ def load():
                         "-I" + os.path.join(ROOT, "include"), "-o", LIB, SRC], check=True)
     lib = ctypes.CDLL(LIB)
     vp, u64, u32, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
-    lib.tune_run.argtypes = [i, vp, vp, vp, vp, vp, u64, u32, u32, vp]
+    lib.tune_run.argtypes = [i, vp, vp, vp, vp, vp, u64, u32, u32, u32, vp]
     lib.tune_name.restype = ctypes.c_char_p
     return lib
 
@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20, help="launches between one pair of events")
     ap.add_argument("--variants", default="", help="comma list of variant indices (default: all)")
     ap.add_argument("--ks", default="1")
+    ap.add_argument("--occs", default="0", help="workgroups per CU forced with dynamic LDS (0 = natural)")
     a = ap.parse_args()
     torch.cuda.init()
     lib = load()
@@ -58,16 +59,18 @@ def main():
     vids = [int(x) for x in a.variants.split(",")] if a.variants else list(range(lib.tune_count()))
     ks = [int(x) for x in a.ks.split(",")]
     cases = []
+    occs = [int(x) for x in a.occs.split(",")]
     for v in vids:
         for K in ks:
-            cases.append((f"{lib.tune_name(v).decode()} K{K}", v, K))
+            for o in (occs if v else [0]):
+                cases.append((f"{lib.tune_name(v).decode()} K{K}" + (f" occ{o}" if o else ""), v, (K, o)))
 
-    def run(v, K, x, out):
+    def run(v, Ko, x, out):
         return lib.tune_run(v, x.data_ptr(), out.data_ptr() if out is not None else None, flags.data_ptr(),
-                            nxt.data_ptr(), ws.data_ptr(), L.n, L.block_size, K, st)
+                            nxt.data_ptr(), ws.data_ptr(), L.n, L.block_size, Ko[0], Ko[1], st)
 
     ref_out = torch.zeros(L.n, device=dev)
-    assert run(0, ks[0], xs[0], ref_out) == 0
+    assert run(0, (ks[0], 0), xs[0], ref_out) == 0
     torch.cuda.synchronize()
     ref_flags, ref_next = flags.clone(), nxt.clone()
     for name, v, K in cases:
