@@ -1,8 +1,8 @@
 // omr_dist.hip — C++ host side of the multi-rank sparse all-reduce (include/omr_dist.h).
 //
-// The round is the one omr/dist.py drives from Python (same shard bounds, same packed-stream layout, same
-// kernels from libomr.so); this is the C++ host path the ./omr_client and ./omr_server drivers run, with either
-// RCCL over xGMI (one process per GPU) or an in-process loopback transport (threads, device-to-device copies).
+// The product's round driver (same shard bounds and packed-stream layout as the test-only Python twin
+// tests/dist_twin.py; kernels from libomr.so), run by ./omr_client, ./omr_server, bench.py and omr/cdist.py over
+// RCCL (one process per GPU), HIP IPC (processes sharing GPUs) or an in-process loopback transport (threads).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
