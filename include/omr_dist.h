@@ -104,25 +104,26 @@ int omr_sparse_allreduce_f32(omr_ar_plan* plan, const float* x, float* out, int3
  *                             is its own (results within fp32 reassociation error of the rank-order sum).  Shards
  *                             must be equal: rows % world == 0.  Moves 7/8*S per rank at N=8 whatever the density. */
 #define OMR_ROUND_DENSE_REDUCE_SCATTER 2
-/* OR-ed into `mode`: the round's exchange and aggregation (send/recv, shard sums [, sums back, unpack]) go on the
- * plan's own communication stream instead of `stream`, so the next call's worker scan overlaps this round's
- * transfer over xGMI (the bucket pipeline of a training step).  flags / next_offsets / union_next are ready in
- * `stream` order as usual; `out` is ready once omr_ar_plan_join() has made a stream wait for the round (or after
- * a device-wide synchronise).  Two consecutive rounds use alternating plan buffers; a round waits for the one two
- * calls back before reusing its buffers.  x and out must stay untouched (and must not be a later round's input)
+/* OR-ed into `mode`: only the worker scan runs on `stream`.  The round's bookkeeping (mask all-gather, plan, pack,
+ * aggregator chain) goes on the plan's own plan stream, and its exchange and aggregation (send/recv, shard sums
+ * [, sums back, unpack]) on its communication stream, so the next call's worker scan overlaps this round's
+ * bookkeeping and its transfer over xGMI (the bucket pipeline of a training step).  flags / next_offsets are ready
+ * in `stream` order as usual; union_next and `out` are ready once omr_ar_plan_join() has made a stream wait for the
+ * round (or after a device-wide synchronise).  Rounds use three plan buffer sets in turn; a round waits for the one
+ * three calls back before reusing its set.  x and out must stay untouched (and must not be a later round's input)
  * until the round is joined. */
 #define OMR_ROUND_ASYNC 0x100
 /* OR-ed into `mode`: bracket this round's worker -> aggregator exchange (the grouped send/recv; the dense
  * stand-in's reduce-scatter) with timing events on the stream it runs on; read them with
  * omr_ar_plan_exchange_time().  Measurement only: the events cost host time, so time a sample of rounds. */
 #define OMR_ROUND_TIME_EXCHANGE 0x200
-/* OR-ed into `mode` (implies OMR_ROUND_ASYNC): a deeper pipeline.  The call queues this round's first half
- * (worker scan, mask all-gather, plan, pack, aggregator chain) on `stream` and only then issues the PREVIOUS
- * deferred round's exchange and aggregation on the communication stream; this round's follow at the next call,
- * at a call without this flag, or at omr_ar_plan_join().  The host therefore never waits for block counts with the
- * caller's stream idle: the previous round's counts are in host memory while this round's scan runs.
- * *sent_blocks / *union_blocks receive the values of the previous round (the one whose exchange this call
- * issued; 0 if none).  Every rank must use the same sequence of modes; join (or a non-deferred call) before
+/* OR-ed into `mode` (implies OMR_ROUND_ASYNC): a deeper pipeline.  The call queues this round's first half (worker
+ * scan on `stream`; mask all-gather, plan, pack, aggregator chain on the plan stream) and only then issues the
+ * exchange and aggregation of the deferred round TWO calls back on the communication stream; this round's follow two
+ * deferred calls later, at a call without this flag, or at omr_ar_plan_join().  The host therefore never waits for
+ * block counts: that round's counts have been in host memory since the middle of the previous round's scan, and
+ * the caller's stream always has the next scan queued.  *sent_blocks / *union_blocks receive the values of the
+ * round whose exchange this call issued (0 if none).  Every rank must use the same sequence of modes; join (or a non-deferred call) before
  * reading `out` or destroying the plan (destroy issues a pending exchange and synchronises the device). */
 #define OMR_ROUND_DEFER 0x400
 int omr_sparse_round_f32(omr_ar_plan* plan, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,

@@ -540,6 +540,43 @@ int wait_flag(const uint32_t* flag, uint32_t seq, hipStream_t st) {
   }
 }
 
+// OMR_HOST_TRACE=1 (diagnostic): host time of a round's steps, summed per step and printed to stderr when the plan
+// is destroyed.  The round is host-bound when a call takes longer than the worker scan it queues.
+// OMR_HOST_TRACE=2 also logs every lap's end (CLOCK_MONOTONIC ns, the clock of rocprofv3's kernel trace) to
+// $OMR_HOST_TRACE_FILE (default /tmp/omr_host_trace.<rank>.txt), to lay the host calls beside the kernels.
+struct HostTrace {
+  bool on = false, log = false;
+  std::chrono::steady_clock::time_point t;
+  std::map<std::string, std::pair<double, uint64_t>> acc;  // label -> (microseconds, laps)
+  std::vector<std::pair<const char*, int64_t>> events;
+  void start() {
+    if (!on) return;
+    t = std::chrono::steady_clock::now();
+    if (log) events.emplace_back("start", std::chrono::duration_cast<std::chrono::nanoseconds>(t.time_since_epoch()).count());
+  }
+  void lap(const char* label) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    auto& a = acc[label];
+    a.first += std::chrono::duration<double, std::micro>(n - t).count();
+    a.second += 1;
+    t = n;
+    if (log) events.emplace_back(label, std::chrono::duration_cast<std::chrono::nanoseconds>(n.time_since_epoch()).count());
+  }
+  void print(int rank) const {
+    for (const auto& kv : acc)
+      fprintf(stderr, "[omr host trace rank %d] %-14s %9.2f us mean over %llu\n", rank, kv.first.c_str(),
+              kv.second.first / static_cast<double>(kv.second.second), static_cast<unsigned long long>(kv.second.second));
+    if (!log) return;
+    const char* f = getenv("OMR_HOST_TRACE_FILE");
+    const std::string path = f ? std::string(f) : "/tmp/omr_host_trace." + std::to_string(rank) + ".txt";
+    if (FILE* fp = fopen(path.c_str(), "w")) {
+      for (const auto& e : events) fprintf(fp, "%lld %s\n", static_cast<long long>(e.second), e.first);
+      fclose(fp);
+    }
+  }
+};
+
 template <typename T>
 int dev_alloc(T** p, size_t count) {
   return hip_check(hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(count, 1) * sizeof(T)), "hipMalloc");
@@ -562,24 +599,29 @@ struct omr_ar_plan {
   bool worker() const { return me < M; }
   std::vector<uint64_t> bounds;   // shard s = rows [bounds[s], bounds[s+1])
   uint64_t shard_nb = 0;          // blocks of the largest shard
-  uint64_t* own_masks = nullptr;  // [rows] this rank's masks (the scan ORs into it; the plan kernel re-zeroes it)
-  // per-round state, two sets used alternately (an asynchronous round's exchange still reads its set while the
-  // next round fills the other)
+  // per-round state, kSets sets used in turn: an asynchronous round's bookkeeping and exchange still read their
+  // set while the next rounds' scans fill the others
+  static constexpr int kSets = 3;
   struct Set {
+    uint64_t* own = nullptr;        // [rows] this rank's masks (the scan ORs into them; the plan kernel re-zeroes them)
     uint64_t* masks_all = nullptr;  // [N][rows] every worker's masks (all-gather)
     uint64_t* wset = nullptr;       // [rows] write set: union + lane heads
     uint64_t* umask = nullptr;      // [rows] union of the workers' masks
     uint32_t* prefix = nullptr;     // [N+1][rows+1] popcount prefixes: workers, then the write set
     float* packed = nullptr;        // own non-zero blocks of the other shards, block order
-    hipEvent_t ready = nullptr;     // recorded on the caller's stream once the set is filled (async rounds)
+    hipEvent_t scanned = nullptr;   // async: recorded on the caller's stream after the worker scan
+    hipEvent_t planned = nullptr;   // async: recorded on the plan stream once `own` is consumed and re-zeroed
+    hipEvent_t ready = nullptr;     // recorded once the set is filled (the plan stream for async rounds)
     hipEvent_t done = nullptr;      // recorded on the communication stream once the round is through with it
     bool pending = false;           // `done` recorded and not yet waited for by a refill
-  } set[2];
+    bool plan_pending = false;      // `planned` recorded and not yet waited for by a scan
+  } set[kSets];
   int cur = 0;                      // the set the next round fills
   int last_async = -1;              // set of the last asynchronous round (for join)
-  hipStream_t cs = nullptr;         // communication stream of asynchronous rounds
+  hipStream_t ps = nullptr;         // plan stream of asynchronous rounds: mask all-gather, plan, pack, union chain
+  hipStream_t cs = nullptr;         // communication stream of asynchronous rounds: exchange, shard sums [, sums back]
   uint64_t* bounds_dev = nullptr;
-  uint32_t* counts_host = nullptr;  // [2][N+1][N+1] per set: prefix[a][bounds[s]], pinned memory the plan kernel writes
+  uint32_t* counts_host = nullptr;  // [kSets][M+1][A+1] per set: prefix[a][bounds[s]], pinned memory the plan kernel writes
   uint32_t* counts_map = nullptr;   // its device-side address
   float* recv = nullptr;     // this shard's blocks from each peer, peer-major
   float* results = nullptr;  // all-reduce: every shard's sums, write-set order (a dedicated aggregator: its own)
@@ -590,7 +632,7 @@ struct omr_ar_plan {
   void* scan_ws = nullptr;   // omr_worker_scan_f32 segment workspace (zeroed once, self-resetting)
   size_t scan_ws_bytes = 0;
   uint32_t* arrive = nullptr;     // device arrival counter of the plan kernel's completion notice
-  uint32_t* flag_host = nullptr;  // [2] pinned, per set: the plan kernel stores the round's sequence number here
+  uint32_t* flag_host = nullptr;  // [kSets] pinned, per set: the plan kernel stores the round's sequence number here
   uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
   // OMR_ROUND_TIME_EXCHANGE: events around the last timed round's worker -> aggregator exchange, and its bytes
@@ -607,7 +649,11 @@ struct omr_ar_plan {
   static constexpr int kTimed = 64;
   std::vector<Timed> timed;
   uint32_t timed_next = 0, timed_first = 0;  // ring [first, next) not yet read
-  // OMR_ROUND_DEFER: the round whose exchange and aggregation the next call (or join) issues
+  // OMR_ROUND_DEFER: the rounds whose exchange and aggregation later calls (or join) issue, oldest first.  Call k
+  // issues round k - kDeferDepth's: its block counts have been in host memory since about the middle of round k-1's
+  // scan, so the host never waits for them, and the caller's stream always has the next scan queued.
+  static constexpr int kDeferDepth = 2;  // <= kSets - 1 (a set is refilled kSets calls later)
+  int defer_depth = kDeferDepth;         // OMR_DEFER_DEPTH=1 (diagnostic): issue the previous round's instead
   struct Pending {
     bool active = false;
     int si = 0, mode = 0;
@@ -616,12 +662,14 @@ struct omr_ar_plan {
     float* out = nullptr;
     uint32_t seq = 0;
     int tslot = -1;            // its timing record (OMR_ROUND_TIME_EXCHANGE)
-    hipStream_t st = nullptr;  // the stream its first half went on (the count wait checks it for a failed launch)
-  } pend;
+    hipStream_t st = nullptr;  // the stream its plan went on (the count wait checks it for a failed launch)
+  } pend[kDeferDepth + 1];
+  int npend = 0;
   // rounds issued on different streams run in call order: the plan's arrival counter, own-mask buffer and scan
   // workspace are shared by every round
   hipStream_t last_st = nullptr;
   hipEvent_t st_ev = nullptr;
+  HostTrace ht;
   // omr_sparse_buckets_f32 on a pinned-host gradient: a ring of device staging buckets and two copy streams
   static constexpr int kStage = 3;
   float* stage[kStage] = {nullptr, nullptr, nullptr};
@@ -717,19 +765,20 @@ int omr_dist_destroy(omr_dist* d) {
 
 int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p == nullptr) return 0;
-  if (p->pend.active) {  // a deferred round still owes its exchange to the peers: issue it and let it drain
+  if (p->ht.on) p->ht.print(p->me);
+  if (p->npend > 0) {  // deferred rounds still owe their exchanges to the peers: issue them and let them drain
     (void)flush_pending(p, p->cs, nullptr, nullptr);
     (void)hipDeviceSynchronize();
   }
-  void* devs[] = {p->own_masks, p->bounds_dev, p->recv,    p->results,
-                  p->flags_ws,  p->next_ws,    p->unext_ws, p->scan_ws};
+  void* devs[] = {p->bounds_dev, p->recv, p->results, p->flags_ws, p->next_ws, p->unext_ws, p->scan_ws};
   for (void* v : devs) (void)hipFree(v);
   for (auto& st : p->set) {
-    void* sv[] = {st.masks_all, st.wset, st.umask, st.prefix, st.packed};
+    void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed};
     for (void* v : sv) (void)hipFree(v);
-    if (st.ready) (void)hipEventDestroy(st.ready);
-    if (st.done) (void)hipEventDestroy(st.done);
+    for (hipEvent_t e : {st.scanned, st.planned, st.ready, st.done})
+      if (e) (void)hipEventDestroy(e);
   }
+  if (p->ps) (void)hipStreamDestroy(p->ps);
   if (p->cs) (void)hipStreamDestroy(p->cs);
   for (int r = 0; r < omr_ar_plan::kStage; ++r) {
     (void)hipFree(p->stage[r]);
@@ -766,6 +815,10 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   const int naggs = num_workers == static_cast<uint32_t>(d->world) ? d->world : d->world - static_cast<int>(num_workers);
   if (naggs > OMR_MAX_WORKERS) return derr(OMR_EINVAL, "ar_plan_create: %d aggregators > %d", naggs, OMR_MAX_WORKERS);
   auto* p = new omr_ar_plan();
+  const char* trace = getenv("OMR_HOST_TRACE");
+  p->ht.on = trace != nullptr && (trace[0] == '1' || trace[0] == '2');
+  p->ht.log = trace != nullptr && trace[0] == '2';
+  if (const char* dd = getenv("OMR_DEFER_DEPTH")) p->defer_depth = std::min(std::max(atoi(dd), 1), omr_ar_plan::kDeferDepth);
   p->M = static_cast<int>(num_workers);
   p->A = naggs;
   p->colocated = num_workers == static_cast<uint32_t>(d->world);
@@ -789,16 +842,17 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   auto A = [&](int r) {
     if (rc == 0) rc = r;
   };
-  A(dev_alloc(&p->own_masks, p->rows));
   for (auto& st : p->set) {
+    A(dev_alloc(&st.own, p->rows));
     A(dev_alloc(&st.masks_all, static_cast<size_t>(N) * p->rows));
     A(dev_alloc(&st.wset, p->rows));
     A(dev_alloc(&st.umask, p->rows));
     A(dev_alloc(&st.prefix, static_cast<size_t>(M + 1) * (p->rows + 1)));
     if (N > 1 && p->worker()) A(dev_alloc(&st.packed, n));
-    A(hip_check(hipEventCreateWithFlags(&st.ready, hipEventDisableTiming), "hipEventCreate"));
-    A(hip_check(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "hipEventCreate"));
+    for (hipEvent_t* e : {&st.scanned, &st.planned, &st.ready, &st.done})
+      A(hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate"));
   }
+  A(hip_check(hipStreamCreateWithFlags(&p->ps, hipStreamNonBlocking), "hipStreamCreate"));
   A(hip_check(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking), "hipStreamCreate"));
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, hipEventDisableTiming), "hipEventCreate"));
   A(dev_alloc(&p->bounds_dev, NA + 1));
@@ -809,21 +863,23 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   A(dev_alloc(&p->unext_ws, p->nb));
   p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
   A(dev_alloc(reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
-  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), 2 * (M + 1) * (NA + 1) * sizeof(uint32_t),
+  constexpr int NSETS = omr_ar_plan::kSets;
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), NSETS * (M + 1) * (NA + 1) * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0)
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->counts_map), p->counts_host, 0),
                 "hipHostGetDevicePointer"));
   A(dev_alloc(&p->arrive, 1));
-  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), 2 * sizeof(uint32_t),
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), NSETS * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0) {
-    p->flag_host[0] = p->flag_host[1] = 0;
+    for (int i = 0; i < NSETS; ++i) p->flag_host[i] = 0;
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->flag_map), p->flag_host, 0),
                 "hipHostGetDevicePointer"));
   }
   if (rc == 0) A(hip_check(hipMemset(p->arrive, 0, sizeof(uint32_t)), "hipMemset arrive"));
-  if (rc == 0) A(hip_check(hipMemset(p->own_masks, 0, p->rows * sizeof(uint64_t)), "hipMemset own masks"));
+  for (auto& st : p->set)
+    if (rc == 0) A(hip_check(hipMemset(st.own, 0, p->rows * sizeof(uint64_t)), "hipMemset own masks"));
   if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset scan ws"));
   if (rc == 0)
     A(hip_check(hipMemcpy(p->bounds_dev, p->bounds.data(), (NA + 1) * sizeof(uint64_t), hipMemcpyHostToDevice),
@@ -875,10 +931,12 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
   const uint32_t* counts = p->counts_host + static_cast<size_t>(si) * (M + 1) * NS;
   const uint32_t* flag = p->flag_host + si;
   hipStream_t xs = st;
+  p->ht.start();
   if (async) {
     TRY(hip_check(hipStreamWaitEvent(p->cs, S.ready, 0), "hipStreamWaitEvent"));
     xs = p->cs;
   }
+  p->ht.lap("2:cs wait ready");
   const omr_stream_t xstream = reinterpret_cast<omr_stream_t>(xs);
   auto cnt = [&](int a, int s) -> uint64_t { return counts[a * NS + s]; };
   auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
@@ -906,6 +964,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     return 0;
   }
   TRY(wait_flag(flag, seq, st));
+  p->ht.lap("2:wait counts");
   const bool wk = p->worker();
   // a co-located rank keeps its own shard's blocks out of its packed stream (and reads them in place)
   const uint64_t own_shard = (wk && p->colocated) ? per(me, me) : 0;
@@ -933,6 +992,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       }
     TRY(p->d->exchange(sends, recvs, xs));
   }
+  p->ht.lap("2:exchange");
   if (timed) {
     TRY(hip_check(hipEventRecord(p->timed[tslot].x1, xs), "hipEventRecord"));
     p->xt_out = total_send * B * sizeof(float);
@@ -956,6 +1016,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
                   "omr_shard_sum_f32"));
     if (!p->colocated) p->last_sums_blocks = per(M, sh);
   }
+  p->ht.lap("2:shard sum");
   if (!rs_mode) {
     // 6. sums back to every worker (server.cc:162), scattered in place (client.cc:89)
     if (N > 1) {
@@ -979,20 +1040,27 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     S.pending = true;
     p->last_async = si;
   }
+  p->ht.lap("2:rest");
   if (sent_blocks) *sent_blocks = total_send;
   if (union_blocks) *union_blocks = (rs_mode || !wk) ? (sh >= 0 ? per(M, sh) : 0) : cnt(M, NA);
   return 0;
 }
 
-// Issue the deferred round's second half, if there is one.
+// Issue the oldest deferred round's second half.
+int issue_oldest(omr_ar_plan* p, uint64_t* sent_blocks, uint64_t* union_blocks) {
+  const omr_ar_plan::Pending q = p->pend[0];
+  for (int i = 1; i < p->npend; ++i) p->pend[i - 1] = p->pend[i];
+  --p->npend;
+  return round_finish(p, q.si, q.x, q.out, q.mode, true, q.timed, q.seq, q.st, sent_blocks, union_blocks, q.tslot);
+}
+
+// Issue every deferred round's second half, oldest first (outputs: the last one's counts; 0 if none).
 int flush_pending(omr_ar_plan* p, hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks) {
+  (void)st;
   if (sent_blocks) *sent_blocks = 0;
   if (union_blocks) *union_blocks = 0;
-  if (!p->pend.active) return 0;
-  const omr_ar_plan::Pending q = p->pend;
-  p->pend.active = false;
-  (void)st;
-  return round_finish(p, q.si, q.x, q.out, q.mode, true, q.timed, q.seq, q.st, sent_blocks, union_blocks, q.tslot);
+  while (p->npend > 0) TRY(issue_oldest(p, sent_blocks, union_blocks));
+  return 0;
 }
 
 }  // namespace
@@ -1022,6 +1090,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   const int N = p->N, M = p->M, me = p->me;
   const uint64_t rows = p->rows;
   const uint32_t NS = static_cast<uint32_t>(p->A + 1);
+  p->ht.start();
   int32_t* fl = flags ? flags : p->flags_ws;
   uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
   uint32_t* un = union_next ? union_next : p->unext_ws;
@@ -1033,47 +1102,77 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   p->last_st = st;
   // a round that is not deferred finishes a deferred one first (rounds complete in call order)
   if (!defer) TRY(flush_pending(p, st, nullptr, nullptr));
-  // a synchronous round after asynchronous ones: its exchange goes on `stream`, so the communication stream
-  // must be idle first (one communicator is never driven from two streams at once)
+  // a synchronous round after asynchronous ones: its all-gather and exchange go on `stream`, so the plan and
+  // communication streams must be idle first (one communicator is never driven from two streams at once; the
+  // last asynchronous round's `done` follows all of its plan-stream work)
   if (!async && p->last_async >= 0) {
     TRY(hip_check(hipStreamWaitEvent(st, p->set[p->last_async].done, 0), "hipStreamWaitEvent"));
     p->last_async = -1;
   }
   const int si = p->cur;
   omr_ar_plan::Set& S = p->set[si];
-  p->cur ^= 1;
+  p->cur = (p->cur + 1) % omr_ar_plan::kSets;
+  // the round's bookkeeping stream: an asynchronous round runs it on the plan stream, so the caller's stream is
+  // left with the worker scans alone (round k+1's scan overlaps round k's all-gather, plan and pack, and round
+  // k-1's exchange)
+  hipStream_t qs = async ? p->ps : st;
+  const omr_stream_t qstream = reinterpret_cast<omr_stream_t>(qs);
+  // (event waits are skipped when the host already sees the event complete: a stream-wait packet costs the GPU a
+  // few microseconds of dispatch even when its event has long fired)
+  auto wait_ev = [](hipStream_t on, hipEvent_t ev) -> int {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipErrorNotReady) return hip_check(hipStreamWaitEvent(on, ev, 0), "hipStreamWaitEvent");
+    return hip_check(q, "hipEventQuery");
+  };
   // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass (a dedicated aggregator
-  //    offers its all-zero mask buffer to the all-gather)
+  //    offers its all-zero mask buffer to the all-gather).  The set's own masks must have been consumed and
+  //    re-zeroed by the plan of the round kSets calls back.
   int tslot = -1;
   if (timed) TRY(timed_slot(p, &tslot));
+  if (S.plan_pending) {
+    TRY(wait_ev(st, S.planned));
+    S.plan_pending = false;
+  }
   if (p->worker()) {
     if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
-    TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, p->own_masks, nullptr, p->scan_ws,
+    TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, nullptr, p->scan_ws,
                                       p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
     if (timed) {
       TRY(hip_check(hipEventRecord(p->timed[tslot].s1, st), "hipEventRecord"));
       p->timed[tslot].scan = true;
     }
+    p->ht.lap("1:scan");
+    if (async) {
+      TRY(hip_check(hipEventRecord(S.scanned, st), "hipEventRecord"));
+      TRY(hip_check(hipStreamWaitEvent(qs, S.scanned, 0), "hipStreamWaitEvent"));
+    }
+    p->ht.lap("1:scan events");
+  } else if (async) {  // nothing to scan: the plan stream starts behind whatever the caller queued before this call
+    TRY(hip_check(hipEventRecord(S.scanned, st), "hipEventRecord"));
+    TRY(hip_check(hipStreamWaitEvent(qs, S.scanned, 0), "hipStreamWaitEvent"));
   }
-  // the set is refilled from here on: an asynchronous round two calls back must be through with it
-  // (skipped when the host already sees the event complete: a stream-wait packet costs the GPU a few
-  // microseconds of dispatch even when its event has long fired)
+  // the rest of the set is refilled from here on: the asynchronous round kSets calls back must be through with it
   if (S.pending) {
-    const hipError_t q = hipEventQuery(S.done);
-    if (q == hipErrorNotReady) TRY(hip_check(hipStreamWaitEvent(st, S.done, 0), "hipStreamWaitEvent"));
-    else TRY(hip_check(q, "hipEventQuery"));
+    TRY(wait_ev(qs, S.done));
     S.pending = false;
   }
   // 2. every worker's row masks
-  TRY(p->d->allgather(p->own_masks, S.masks_all, rows * sizeof(uint64_t), st));
-  // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for the next round
+  p->ht.lap("1:refill wait");
+  TRY(p->d->allgather(S.own, S.masks_all, rows * sizeof(uint64_t), qs));
+  p->ht.lap("1:allgather");
+  // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for its next round
   //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
   const uint32_t seq = ++p->seq;
   TRY(omr_check(omr_round_plan(S.masks_all, static_cast<uint32_t>(M), rows, p->rpp, p->lanes, p->bounds_dev, NS,
                                S.wset, S.umask, S.prefix,
-                               p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, p->own_masks,
-                               p->arrive, p->flag_map + si, seq, stream),
+                               p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own,
+                               p->arrive, p->flag_map + si, seq, qstream),
                 "omr_round_plan"));
+  if (async) {
+    TRY(hip_check(hipEventRecord(S.planned, qs), "hipEventRecord"));
+    S.plan_pending = true;
+  }
+  p->ht.lap("1:plan");
   // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407), then the
   //     aggregator chain (server.cc:86-96 min_next) over the union: both addressed by device-side data only, so
   //     they are queued before the host learns the counts and run while it waits.  (Every host API call costs
@@ -1082,24 +1181,29 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
     const uint64_t r0 = p->colocated ? p->bounds[me] : 0, r1 = p->colocated ? p->bounds[me + 1] : 0;
     TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * rows,
                                       S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
-                                      r1, stream), "omr_move_blocks_f32 pack"));
+                                      r1, qstream), "omr_move_blocks_f32 pack"));
   }
-  TRY(omr_check(omr_next_offsets(S.umask, 1, p->n, p->B, p->lanes, p->parts, un, stream), "omr_next_offsets"));
+  p->ht.lap("1:pack");
+  TRY(omr_check(omr_next_offsets(S.umask, 1, p->n, p->B, p->lanes, p->parts, un, qstream), "omr_next_offsets"));
   // the rest goes on the communication stream for an asynchronous round, behind everything queued so far
-  if (async) TRY(hip_check(hipEventRecord(S.ready, st), "hipEventRecord"));
-  if (!defer) return round_finish(p, si, x, out, mode, async, timed, seq, st, sent_blocks, union_blocks, tslot);
-  // deferred: this round's first half is queued; now issue the previous round's exchange, whose counts have long
-  // been in host memory, so the host neither waits nor leaves the caller's stream idle
-  TRY(flush_pending(p, st, sent_blocks, union_blocks));
-  p->pend.active = true;
-  p->pend.si = si;
-  p->pend.mode = mode;
-  p->pend.timed = timed;
-  p->pend.x = x;
-  p->pend.out = out;
-  p->pend.seq = seq;
-  p->pend.tslot = tslot;
-  p->pend.st = st;
+  if (async) TRY(hip_check(hipEventRecord(S.ready, qs), "hipEventRecord"));
+  p->ht.lap("1:next+ready");
+  if (!defer) return round_finish(p, si, x, out, mode, async, timed, seq, qs, sent_blocks, union_blocks, tslot);
+  // deferred: this round's first half is queued; now issue the exchange of the round kDeferDepth calls back, whose
+  // counts have long been in host memory, so the host neither waits nor leaves the caller's stream idle
+  omr_ar_plan::Pending& q = p->pend[p->npend++];
+  q.active = true;
+  q.si = si;
+  q.mode = mode;
+  q.timed = timed;
+  q.x = x;
+  q.out = out;
+  q.seq = seq;
+  q.tslot = tslot;
+  q.st = qs;
+  if (sent_blocks) *sent_blocks = 0;
+  if (union_blocks) *union_blocks = 0;
+  if (p->npend > p->defer_depth) TRY(issue_oldest(p, sent_blocks, union_blocks));
   return 0;
 }
 
@@ -1135,8 +1239,10 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
       TRY(omr_sparse_round_f32(p, b, b, nullptr, nullptr, nullptr, rmode, &s1, &u1, stream));
       acc();
     }
-    TRY(flush_pending(p, st, &s1, &u1));
-    acc();
+    while (p->npend > 0) {
+      TRY(issue_oldest(p, &s1, &u1));
+      acc();
+    }
     TRY(omr_ar_plan_join(p, stream));
     if (sent_blocks) *sent_blocks = sent;
     if (union_blocks) *union_blocks = uni;
@@ -1179,18 +1285,25 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
     p->out_used[r] = true;
     return hip_check(hipEventRecord(p->ev_out[r], p->s_out), "hipEventRecord");
   };
+  // after call k, the second halves of buckets <= k - kDeferDepth are queued: the D2H of bucket k - kDeferDepth
+  // goes behind it, and frees its staging buffer for the H2D of bucket k + 1 (R = kDeferDepth + 1 buffers)
+  static_assert(omr_ar_plan::kStage == omr_ar_plan::kDeferDepth + 1, "staging ring = deferral depth + 1");
+  const uint64_t DD = static_cast<uint64_t>(p->defer_depth);  // <= kStage - 1
   TRY(h2d(0));
   for (uint64_t k = 0; k < K; ++k) {
     const int r = static_cast<int>(k % R);
     TRY(hip_check(hipStreamWaitEvent(st, p->ev_in[r], 0), "hipStreamWaitEvent"));
     TRY(omr_sparse_round_f32(p, p->stage[r], p->stage[r], nullptr, nullptr, nullptr, rmode, &s1, &u1, stream));
-    acc();  // (the previous bucket's counts: its second half was issued by this call)
-    if (k >= 1) TRY(d2h(k - 1));
+    acc();  // (the counts of bucket k - kDeferDepth, whose second half this call issued)
+    if (k >= DD) TRY(d2h(k - DD));
     if (k + 1 < K) TRY(h2d(k + 1));
   }
-  TRY(flush_pending(p, st, &s1, &u1));
-  acc();
-  TRY(d2h(K - 1));
+  while (p->npend > 0) {  // the last buckets' second halves, oldest first, each followed by its D2H
+    const uint64_t k = K - static_cast<uint64_t>(p->npend);
+    TRY(issue_oldest(p, &s1, &u1));
+    acc();
+    TRY(d2h(k));
+  }
   TRY(hip_check(hipStreamSynchronize(p->s_out), "hipStreamSynchronize"));  // the host buffer holds the result
   TRY(omr_ar_plan_join(p, stream));
   if (sent_blocks) *sent_blocks = sent;

@@ -125,11 +125,12 @@ class CppSparseAllreduce:
             defer: bool = False):
         """mode 0: all-reduce (every worker gets every shard's sums); 1: reduce-scatter (stop at the
         aggregators: `out` gets this rank's shard sums only); 2: the dense stand-in (the whole tensor reduce-scattered
-        by RCCL, every block).  async_: the exchange and the sums run on the plan's
-        communication stream, overlapping the next call's worker scan; `out` is ready after join().
-        time_exchange: bracket the worker -> aggregator exchange with timing events (read with exchange_time()).
-        defer: OMR_ROUND_DEFER, this round's exchange is issued by the next call (or join()), after the next
-        round's worker scan is queued; the returned counts are the previous round's."""
+        by RCCL, every block).  async_: only the worker scan runs on the caller's stream; the bookkeeping runs on the
+        plan stream and the exchange and sums on the communication stream, overlapping the next calls' scans;
+        `out` (and union_next) are ready after join().  time_exchange: bracket the worker scan and the worker ->
+        aggregator exchange with timing events (read with timings() / exchange_time()).  defer: OMR_ROUND_DEFER,
+        this round's exchange is issued two calls later (or by a call without the flag, or join()); the returned
+        counts are those of the round whose exchange this call issued."""
         if defer:
             mode |= self.DEFER
         if async_:

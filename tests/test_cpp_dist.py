@@ -146,17 +146,17 @@ A, D_ = 0x100, 0x400  # OMR_ROUND_ASYNC, OMR_ROUND_DEFER
 
 
 @pytest.mark.parametrize("world,mode,round_flags", [
-    (3, 1, (A,) * 5), (8, 1, (A,) * 5), (4, 0, (A,) * 5), (3, 1, (A, A, 0, A, 0)),
-    (3, 1, (D_,) * 5), (8, 1, (D_,) * 5), (4, 0, (D_,) * 5), (4, 2, (D_,) * 5),
-    (3, 1, (D_, D_, 0, D_, A)), (4, 0, (A, D_, D_, A, D_))])
+    (3, 1, (A,) * 7), (8, 1, (A,) * 7), (4, 0, (A,) * 7), (3, 1, (A, A, 0, A, 0)),
+    (3, 1, (D_,) * 7), (8, 1, (D_,) * 7), (4, 0, (D_,) * 7), (4, 2, (D_,) * 7),
+    (3, 1, (D_, D_, 0, D_, A)), (4, 0, (A, D_, D_, A, D_, D_, D_)), (3, 0, (D_, D_, D_, 0, D_, D_, A, D_))])
 def test_cpp_async_rounds_loopback(gpu, world, mode, round_flags):
-    """OMR_ROUND_ASYNC: the exchange and sums of round k run on the plan's communication stream while round k+1
-    scans; rounds take different inputs and outputs (the bench's rotation), use the two plan buffer sets in
-    turn (five rounds: each set refilled twice), and are joined once at the end.  OMR_ROUND_DEFER: round k's
-    exchange is issued by call k+1 (or the join), after round k+1's first half.  Rounds issued without a flag in
-    between must first finish a deferred round and wait for the asynchronous ones before using the stream."""
-    sync_rounds = ()
-    B, rounds = 256, 5
+    """OMR_ROUND_ASYNC: the bookkeeping of round k runs on the plan stream and its exchange and sums on the
+    communication stream while round k+1 scans; rounds take different inputs and outputs (the bench's rotation),
+    use the three plan buffer sets in turn (seven rounds: every set refilled), and are joined once at the end.
+    OMR_ROUND_DEFER: round k's exchange is issued by call k+2 (or a call without the flag, or the join).  Rounds
+    issued without a flag in between must first finish the deferred rounds and wait for the asynchronous ones
+    before using the stream."""
+    B, rounds = 256, len(round_flags)
     L = Layout(n=2 << 20, block_size=B)
     D = dist_lib()
     bufs = [[oracle.fill(oracle.gen_bitmap(w + 10 * k, 0.15, L.nb), B, mode=1, seed=w + 10 * k + 1)
