@@ -203,7 +203,8 @@ __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
 // branching around the stores; write-through sc0 sc1 beat plain, sc1-only and nt stores).
 // ABL (timing-only builds, csrc/tune/): bit 0 drops the data stores, bit 1 the flag/next stores.  MINW: the
 // amdgpu_waves_per_eu floor (occupancy study; 1 = the compiler's choice).  SAUX: the block stores' cache policy
-// (store-policy study; the product's is kStoreAux).
+// (store-policy study; the product's is kStoreAux).  SKIP: a batch with no block to write skips its (dropped) data
+// stores through a wave-uniform branch (the product's choice at B = 1024).
 struct FusedArgs {
   const float* x;
   float* out;
@@ -218,7 +219,7 @@ struct FusedArgs {
 
 constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
 
-template <int VEC, int WAVES, int LOADS = 16, int ABL = 0, int MINW = 1, int SAUX = kStoreAux>
+template <int VEC, int WAVES, int LOADS = 16, int ABL = 0, int MINW = 1, int SAUX = kStoreAux, int SKIP = 0>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW))) void k_scan1f(FusedArgs a) {
   constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
   static_assert(RB >= 1 && RB <= 32, "batch bits are 32-bit");
@@ -265,13 +266,29 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
       for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
       const bool nz = wave_ballot(o != 0) != 0 && static_cast<uint32_t>(s) < nrow;
       bits |= static_cast<uint32_t>(nz) << s;
-      const bool head = (r0 + rr + s) == 0;  // lane head: row 0 of the partition, always sent (client.cc:201-205)
-      // aggregated block 0.0f + x (server.cc:148-150 zero, :97-98 add), written in place (client.cc:89)
-      const uint32_t drop = (nz || head) ? 0u : kDropStore;
+      if constexpr (!SKIP) {
+        const bool head = (r0 + rr + s) == 0;  // lane head: row 0 of the partition, always sent (client.cc:201-205)
+        // aggregated block 0.0f + x (server.cc:148-150 zero, :97-98 add), written in place (client.cc:89)
+        const uint32_t drop = (nz || head) ? 0u : kDropStore;
 #pragma unroll
-      for (int q = 0; q < VEC; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])), dst,
-                                               (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, SAUX);
+        for (int q = 0; q < VEC; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
+                                                 dst, (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, SAUX);
+      }
+    }
+    if constexpr (SKIP) {
+      // the batch's stores only when it has a block to write (a wave-uniform branch; inside it, the static schedule)
+      if (bits != 0 || rr + r0 == 0) {
+#pragma unroll
+        for (int s = 0; s < RB; ++s) {
+          const bool head = (r0 + rr + s) == 0;
+          const uint32_t drop = (((bits >> s) & 1u) || head) ? 0u : kDropStore;
+#pragma unroll
+          for (int q = 0; q < VEC; ++q)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
+                                                   dst, (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, SAUX);
+        }
+      }
     }
     if (!(ABL & 2) && static_cast<uint32_t>(lane) < nrow) {
       const uint64_t blk = blk0 + static_cast<uint64_t>(lane) * a.lanes;
@@ -1272,7 +1289,10 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
   switch (L.vec) {
     case 1: k_scan1f<1, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
     case 2: k_scan1f<2, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
-    default: k_scan1f<4, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
+    // B = 1024 (1 % non-zero at config 3): a batch of 4 rows rarely has a block to write, and skipping its
+    // dropped-store issue altogether measured 1-2 % faster (profiles/r02/fused/tune_c3_skip*.log); at B = 256 the
+    // static schedule is faster (most 16-row batches write something)
+    default: k_scan1f<4, kFusedWaves, kFusedLoads, 0, 1, kStoreAux, 1><<<grid, T, 0, st>>>(a); break;
   }
   return launch_status("k_scan1f");
 }

@@ -256,6 +256,137 @@ __global__ __launch_bounds__(64 * W) void k_read_geom2(FusedArgs a) {
   if (acc == 0x12345678u) a.next[0] = acc;  // never true for the generator's data; keeps the loads
 }
 
+// k_scan1g — the single-pass worker step for NB = 16 lanes (B = 1024), with a workgroup per (partition, row
+// segment) owning ALL 16 lane columns of its rows: wave w streams column w of the segment backwards (as k_scan1f's
+// waves do), and each batch's flags / next offsets (RB rows x 16 lanes) are staged in LDS and stored by the workgroup
+// as contiguous 64-byte row runs, instead of 4-byte stores 64 bytes apart from 16 different workgroups.  The row
+// masks (multi-rank round) become one plain 8-byte store per row.  A row whose successor lies in a later segment is
+// left to that column's fix-up, as in k_scan1f (no double writes).
+constexpr uint32_t kUnset = 0xFFFFFFFFu;  // "successor in a later segment": stored by the fix-up, not here
+template <int VEC, int LOADS = 16>
+__global__ __launch_bounds__(1024) void k_scan1g(FusedArgs a) {
+  constexpr int W = 16;            // waves = lane columns
+  constexpr int RB = LOADS / VEC;  // rows per batch
+  static_assert(RB >= 1 && RB <= 32 && 2 * RB * W + RB <= 1024, "batch");
+  __shared__ uint32_t s_next[2][RB][W];
+  __shared__ int32_t s_flag[2][RB][W];
+  __shared__ uint32_t s_first[W][64], s_last[W][64];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t k = lin % a.K, p = lin / a.K + a.part0;
+  const uint32_t l = wave, col = p * a.lanes + l;
+  const uint32_t r0 = k * a.S;
+  const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  const uint32_t lane_b = l * a.block;
+  const uint32_t row_stride = a.lanes * a.block;
+  const bool last_seg = (k + 1 == a.K);
+  uint32_t carry = kNone, wlast = kNone;
+  int buf = 0;
+  for (uint32_t nb_ = (a.S + RB - 1) / RB; nb_ > 0; --nb_, buf ^= 1) {
+    const uint32_t rr = (nb_ - 1) * RB;
+    const uint32_t nrow = (a.S - rr < static_cast<uint32_t>(RB)) ? a.S - rr : RB;
+    const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+    const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, nrow * row_bytes);
+    v4f v[RB][VEC];
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                              src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
+    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + blk0 * a.block, a.out != nullptr ? nrow * row_bytes : 0u);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
+      const bool nz = wave_ballot(o != 0) != 0 && static_cast<uint32_t>(s) < nrow;
+      bits |= static_cast<uint32_t>(nz) << s;
+      const bool head = (r0 + rr + s) == 0;
+      const uint32_t drop = (nz || head) ? 0u : kDropStore;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])), dst,
+                                               (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, kStoreAux);
+    }
+    if (static_cast<uint32_t>(lane) < nrow) {
+      const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
+      const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : carry;
+      s_flag[buf][lane][l] = static_cast<int32_t>((bits >> lane) & 1u);
+      s_next[buf][lane][l] = nr != kNone ? static_cast<uint32_t>(row0 + nr) * row_stride + lane_b
+                                         : (last_seg ? a.sentinel + lane_b : kUnset);
+    }
+    if (bits != 0) {
+      if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
+      carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
+    }
+    __syncthreads();  // the batch's RB x 16 flags / next offsets are in LDS (double-buffered: one barrier per batch)
+    const uint32_t t = threadIdx.x;
+    if (t < nrow * W) {
+      const uint64_t g = (row0 + rr + t / W) * a.lanes + t % W;
+      if (a.flags != nullptr) a.flags[g] = s_flag[buf][t / W][t % W];
+    } else if (t >= 256 && t < 256 + nrow * W) {
+      const uint32_t u = t - 256;
+      const uint32_t nv = s_next[buf][u / W][u % W];
+      if (nv != kUnset) a.next[(row0 + rr + u / W) * a.lanes + u % W] = nv;
+    } else if (a.masks != nullptr && t >= 512 && t < 512 + nrow) {
+      const uint32_t r = t - 512;
+      uint64_t m = 0;
+#pragma unroll
+      for (int c = 0; c < W; ++c) m |= static_cast<uint64_t>(s_flag[buf][r][c] & 1) << c;
+      a.masks[row0 + rr + r] = m;
+    }
+  }
+  if (a.K == 1) return;
+  // multi-segment columns: every store of this workgroup done, then each wave publishes its column's {first, last}
+  // and counts arrivals; the wave whose arrival completes its column fixes the rows whose successor lies in a later
+  // segment (k_scan1f's fix-up, one wave per column)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint32_t fix = 0;
+  if (lane == 0) {
+    const uint64_t sm = (static_cast<uint64_t>(carry) << 32) | (carry == kNone ? kNone : wlast);
+    (void)__hip_atomic_exchange(&a.summary[static_cast<uint64_t>(col) * a.K + k], sm, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&a.cnt[col], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fix = (old == a.K - 1) ? 1u : 0u;
+  }
+  fix = __builtin_amdgcn_readfirstlane(fix);
+  if (!fix) return;
+  if (static_cast<uint32_t>(lane) < a.K) {
+    const uint64_t sm = __hip_atomic_fetch_or(&a.summary[static_cast<uint64_t>(col) * a.K + lane], 0ull,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_first[l][lane] = static_cast<uint32_t>(sm >> 32);
+    s_last[l][lane] = static_cast<uint32_t>(sm);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {  // s_first[l][kk] := first non-zero row (partition-relative) in segments after kk
+    uint32_t c = kNone;
+    for (int kk = static_cast<int>(a.K) - 1; kk >= 0; --kk) {
+      const uint32_t first = s_first[l][kk];
+      s_first[l][kk] = c;
+      if (first != kNone) c = static_cast<uint32_t>(kk) * a.S + first;
+    }
+    __hip_atomic_store(&a.cnt[col], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t part_row0 = static_cast<uint64_t>(p) * a.rpp;
+  const uint32_t tail_total = (a.K - 1) * a.S;
+  for (uint32_t t = lane; t < tail_total; t += 64) {
+    const uint32_t kk = t / a.S, i = t % a.S;
+    const uint32_t last = s_last[l][kk];
+    if (last != kNone && i < last) continue;
+    const uint32_t c = s_first[l][kk];
+    a.next[(part_row0 + static_cast<uint64_t>(kk) * a.S + i) * a.lanes + l] =
+        (c != kNone) ? static_cast<uint32_t>(part_row0 + c) * row_stride + lane_b : a.sentinel + lane_b;
+  }
+}
+
 // Mixed read/write ceiling probes (timing only): what the HBM gives for the kernel's byte mix without any of its
 // logic.  Every probe is one grid-stride kernel of 256-thread workgroups, 16 one-KiB pieces in flight per wave.
 //   MODE 0  write only: the blocks whose flag is set (the kernel's scattered 1 KiB writes), nothing read but flags
@@ -320,10 +451,10 @@ unsigned occ_lds(K kern) {
                             static_cast<int>(lds));
   return lds;
 }
-template <int VEC, int W, int LD, int ABL, int SAUX = kStoreAux>
+template <int VEC, int W, int LD, int ABL, int SAUX = kStoreAux, int SKIP = 0>
 void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
-  const unsigned lds = occ_lds(&k_scan1f<VEC, W, LD, ABL, 1, SAUX>);
-  k_scan1f<VEC, W, LD, ABL, 1, SAUX><<<grid_of(L, f), 64 * W, lds, st>>>(a);
+  const unsigned lds = occ_lds(&k_scan1f<VEC, W, LD, ABL, 1, SAUX, SKIP>);
+  k_scan1f<VEC, W, LD, ABL, 1, SAUX, SKIP><<<grid_of(L, f), 64 * W, lds, st>>>(a);
 }
 template <int VEC, int W, int LD, int P, int ABL>
 void go_d(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
@@ -332,6 +463,11 @@ void go_d(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
 template <int VEC, int W>
 void go_r(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   k_read_geom2<VEC, W><<<grid_of(L, f), 64 * W, 0, st>>>(a);
+}
+template <int VEC, int LD>
+void go_g(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  if (L.lanes != 16) return;  // B = 1024 only
+  k_scan1g<VEC, LD><<<static_cast<unsigned>(static_cast<uint64_t>(L.parts) * f.K), 1024, 0, st>>>(a);
 }
 template <int MODE, int SAUX = kStoreAux>
 void go_m(const Layout& L, const FusedShape&, FusedArgs a, hipStream_t st) {
@@ -346,6 +482,8 @@ struct Variant {
 };
 const Variant kVariants[] = {
     {"f w16 L16 (product)", true, go_f<1, 16, 16, 0>, go_f<4, 16, 16, 0>},
+    {"f w16 L16 skip-empty-batch stores", true, go_f<1, 16, 16, 0, kStoreAux, 1>, go_f<4, 16, 16, 0, kStoreAux, 1>},
+    {"g rowgroup L16 (B=1024)", true, go_f<1, 16, 16, 0>, go_g<4, 16>},
     {"f w4 L32", true, go_f<1, 4, 32, 0>, go_f<4, 4, 32, 0>},
     {"f w8 L32", true, go_f<1, 8, 32, 0>, go_f<4, 8, 32, 0>},
     {"f w4 L16", true, go_f<1, 4, 16, 0>, go_f<4, 4, 16, 0>},
