@@ -91,6 +91,41 @@ int make_input(uint32_t worker_id, const Opts& o, float* d_x, int32_t* d_bitmap)
   return 0;
 }
 
+// The CHECK of client.cc:449-465, done right and without the GPU: the expected result is the rank-order sum of every
+// worker's input (the reference's MPI_Allreduce SUM).  Every input is the generator's (client.cc:396-421): a non-zero
+// block holds 0.01f in every element, so block b of the sum is the k-fold sequential fp32 sum of 0.01f from +0.0f,
+// k = the number of workers whose bitmap flags b (+0.0 when none does).  The bitmaps are regenerated on the host
+// (omr_gen_bitmap: glibc's rand() restated); no kernel of this library computes the expectation.
+// Returns 0 (check OK), 1 (mismatch, the reference's "error: " line printed) or -1 (could not check).
+int host_check(const Opts& o, int workers, const float* d_result) {
+  const uint64_t nb = o.n / o.block;
+  std::vector<uint8_t> cnt(nb, 0);
+  std::vector<int32_t> bm(nb);
+  for (int w = 0; w < workers; ++w) {
+    uint64_t nz = 0;
+    if (omr_gen_bitmap(static_cast<uint32_t>(w), o.density, nb, bm.data(), &nz)) return -1;
+    for (uint64_t b = 0; b < nb; ++b) cnt[b] = static_cast<uint8_t>(cnt[b] + (bm[b] != 0 ? 1 : 0));
+  }
+  std::vector<float> ka(static_cast<size_t>(workers) + 1);
+  volatile float acc = 0.0f;  // one fp32 rounding per add, as server.cc:97-98 accumulates
+  ka[0] = acc;
+  for (int k = 1; k <= workers; ++k) {
+    acc = acc + 0.01f;
+    ka[k] = acc;
+  }
+  std::vector<float> got(o.n);
+  if (hipMemcpy(got.data(), d_result, o.n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  for (uint64_t b = 0; b < nb; ++b) {
+    const float e = ka[cnt[b]];
+    for (uint64_t i = b * o.block; i < (b + 1) * o.block; ++i)
+      if (memcmp(&got[i], &e, sizeof(float)) != 0) {
+        std::cout << "error: " << e << "<---->" << got[i] << std::endl;  // client.cc:453-456
+        return 1;
+      }
+  }
+  return 0;
+}
+
 int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer, int num_workers = 0) {
   HIPOK(hipSetDevice(gpu));
   const int rank = omr_dist_rank(d);
@@ -162,39 +197,11 @@ int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer, int num_worker
   (void)hipFree(d_in);
   int rc = 0;
   if (o.check) {  // the CHECK of client.cc:449-465, done right: expected = rank-order sum of every input
-    std::vector<float*> bufs(world);
-    for (int w = 0; w < world; ++w) {
-      HIPOK(hipMalloc(&bufs[w], o.n * sizeof(float)));
-      if (make_input(static_cast<uint32_t>(w), o, bufs[w], d_bitmap)) return 1;
-    }
-    float* d_exp = nullptr;
-    uint64_t* d_masks = nullptr;
-    HIPOK(hipMalloc(&d_exp, o.n * sizeof(float)));
-    HIPOK(hipMalloc(&d_masks, (world + 1) * (nb / lanes) * sizeof(uint64_t)));
-    HIPOK(hipMemcpy(d_exp, bufs[rank], o.n * sizeof(float), hipMemcpyDeviceToDevice));
-    std::vector<const float*> cb(bufs.begin(), bufs.end());
-    if (world <= OMR_MAX_WORKERS &&
-        omr_scan_sum_f32(cb.data(), world, o.n, o.block, lanes, OMR_NUM_THREADS, nullptr, d_masks, nullptr, d_exp,
-                         nullptr) == 0) {
-      HIPOK(hipDeviceSynchronize());
-      std::vector<float> got(o.n), exp(o.n);
-      HIPOK(hipMemcpy(got.data(), o.inplace ? d_x : d_out, o.n * sizeof(float), hipMemcpyDeviceToHost));
-      HIPOK(hipMemcpy(exp.data(), d_exp, o.n * sizeof(float), hipMemcpyDeviceToHost));
-      bool ok = true;
-      for (uint64_t i = 0; i < o.n; ++i)
-        if (memcmp(&got[i], &exp[i], sizeof(float)) != 0) {
-          std::cout << "error: " << exp[i] << "<---->" << got[i] << std::endl;  // client.cc:453-456
-          ok = false;
-          break;
-        }
-      if (ok) std::cout << "check OK" << std::endl;  // every worker reports its own check (client.cc:460)
-      if (!ok) rc = 1;
-    } else {
-      fprintf(stderr, "check skipped: %s\n", omr_last_error());
-    }
-    for (float* b : bufs) (void)hipFree(b);
-    (void)hipFree(d_exp);
-    (void)hipFree(d_masks);
+    HIPOK(hipDeviceSynchronize());
+    const int c = host_check(o, world, o.inplace ? d_x : d_out);
+    if (c == 0) std::cout << "check OK" << std::endl;  // every worker reports its own check (client.cc:460)
+    if (c < 0) fprintf(stderr, "check skipped: %s\n", omr_last_error());
+    if (c == 1) rc = 1;
   }
   if (printer && print_count > 0)  // client.cc:473
     fprintf(stdout, "data size: %lu Bytes; average time: %lu us; average alg bw: %f GB/s\n",
@@ -324,38 +331,16 @@ int run_messages(const Opts& o, int gpu) {
     std::cout << "trace: " << records << " messages -> " << o.trace << std::endl;
   }
   if (o.check) {  // every worker must hold the rank-order sum of every input (client.cc:449-465, done right)
-    float* d_exp = nullptr;
-    uint64_t* d_masks = nullptr;
-    HIPOK(hipMalloc(&d_exp, o.n * sizeof(float)));
-    HIPOK(hipMalloc(&d_masks, (k + 1) * (nb / lanes) * sizeof(uint64_t)));
-    std::vector<float*> orig(k);
-    for (int w = 0; w < k; ++w) {
-      HIPOK(hipMalloc(&orig[w], o.n * sizeof(float)));
-      if (make_input(static_cast<uint32_t>(w), o, orig[w], d_bitmap)) return 1;
-    }
-    std::vector<const float*> cb(orig.begin(), orig.end());
-    std::vector<float> got(o.n), exp(o.n);
+    HIPOK(hipDeviceSynchronize());
     for (int w = 0; w < k && rc == 0; ++w) {
-      HIPOK(hipMemcpy(d_exp, orig[w], o.n * sizeof(float), hipMemcpyDeviceToDevice));
-      if (omr_scan_sum_f32(cb.data(), k, o.n, o.block, lanes, OMR_NUM_THREADS, nullptr, d_masks, nullptr, d_exp,
-                           nullptr)) {
+      const int c = host_check(o, k, o.inplace ? x[w] : out[w]);
+      if (c < 0) {
         fprintf(stderr, "check skipped: %s\n", omr_last_error());
         break;
       }
-      HIPOK(hipDeviceSynchronize());
-      HIPOK(hipMemcpy(got.data(), o.inplace ? x[w] : out[w], o.n * sizeof(float), hipMemcpyDeviceToHost));
-      HIPOK(hipMemcpy(exp.data(), d_exp, o.n * sizeof(float), hipMemcpyDeviceToHost));
-      for (uint64_t i = 0; i < o.n; ++i)
-        if (memcmp(&got[i], &exp[i], sizeof(float)) != 0) {
-          std::cout << "error: " << exp[i] << "<---->" << got[i] << std::endl;  // client.cc:453-456
-          rc = 1;
-          break;
-        }
+      rc = c;
     }
     if (rc == 0) std::cout << "check OK" << std::endl;
-    for (float* b : orig) (void)hipFree(b);
-    (void)hipFree(d_exp);
-    (void)hipFree(d_masks);
   }
   if (print_count > 0)  // client.cc:473
     fprintf(stdout, "data size: %lu Bytes; average time: %lu us; average alg bw: %f GB/s\n",
@@ -473,36 +458,11 @@ int run_msg_worker(omr_dist* d, const Opts& o, int gpu, int num_workers, int num
     std::cout << "trace: " << tw.records << " messages -> " << o.trace << std::endl;
   }
   if (o.check) {  // the CHECK of client.cc:449-465, done right: the rank-order sum of every worker's input
-    std::vector<float*> bufs(num_workers);
-    for (int w = 0; w < num_workers; ++w) {
-      HIPOK(hipMalloc(&bufs[w], o.n * sizeof(float)));
-      if (make_input(static_cast<uint32_t>(w), o, bufs[w], d_bitmap)) return 1;
-    }
-    float* d_exp = nullptr;
-    uint64_t* d_masks = nullptr;
-    HIPOK(hipMalloc(&d_exp, o.n * sizeof(float)));
-    HIPOK(hipMalloc(&d_masks, (num_workers + 1) * (nb / lanes) * sizeof(uint64_t)));
-    HIPOK(hipMemcpy(d_exp, bufs[rank], o.n * sizeof(float), hipMemcpyDeviceToDevice));
-    std::vector<const float*> cb(bufs.begin(), bufs.end());
-    if (omr_scan_sum_f32(cb.data(), num_workers, o.n, o.block, lanes, OMR_NUM_THREADS, nullptr, d_masks, nullptr,
-                         d_exp, nullptr) == 0) {
-      HIPOK(hipDeviceSynchronize());
-      std::vector<float> got(o.n), exp(o.n);
-      HIPOK(hipMemcpy(got.data(), o.inplace ? d_x : d_out, o.n * sizeof(float), hipMemcpyDeviceToHost));
-      HIPOK(hipMemcpy(exp.data(), d_exp, o.n * sizeof(float), hipMemcpyDeviceToHost));
-      for (uint64_t i = 0; i < o.n; ++i)
-        if (memcmp(&got[i], &exp[i], sizeof(float)) != 0) {
-          std::cout << "error: " << exp[i] << "<---->" << got[i] << std::endl;  // client.cc:453-456
-          rc = 1;
-          break;
-        }
-      if (rc == 0) std::cout << "check OK" << std::endl;
-    } else {
-      fprintf(stderr, "check skipped: %s\n", omr_last_error());
-    }
-    for (float* b : bufs) (void)hipFree(b);
-    (void)hipFree(d_exp);
-    (void)hipFree(d_masks);
+    HIPOK(hipDeviceSynchronize());
+    const int c = host_check(o, num_workers, o.inplace ? d_x : d_out);
+    if (c == 0) std::cout << "check OK" << std::endl;
+    if (c < 0) fprintf(stderr, "check skipped: %s\n", omr_last_error());
+    if (c == 1) rc = 1;
   }
   if (printer && print_count > 0)  // client.cc:473
     fprintf(stdout, "data size: %lu Bytes; average time: %lu us; average alg bw: %f GB/s\n",
