@@ -1214,11 +1214,14 @@ unsigned grid_for(uint64_t work_items_per_wave_units) {
   return static_cast<unsigned>(g);
 }
 
-// Lanes per work unit of the mask-addressed movers: whole rows when there are enough of them to give every SIMD
-// a few units, otherwise rows split into groups (>= 4 lanes).
-uint32_t unit_lanes(uint64_t rows, uint32_t lanes) {
+// Lanes per work unit of the mask-addressed movers: whole rows when there are enough of them, otherwise rows split
+// into groups (>= 4 lanes), for at least `min_units` units.  tools/tune_round_r02.py
+// (profiles/r02/round/tune_round_r02*.log): 4096 units pack an 8-worker round's blocks 20 % faster than 8192 (whole
+// rows: 10.8 vs 13.5 us) and sum an 8-worker shard 20 % faster (8-lane units: 16.9 vs 21.1 us); a one-contributor
+// sum (world 1) is a plain move of few blocks per lane group and keeps 8192 (16.9 vs 18.9 us).
+uint32_t unit_lanes(uint64_t rows, uint32_t lanes, uint64_t min_units = 4096) {
   uint32_t lg = lanes;
-  while (lg > 4 && rows * (lanes / lg) < 8192) lg /= 2;
+  while (lg > 4 && rows * (lanes / lg) < min_units) lg /= 2;
   return lg;
 }
 
@@ -1822,7 +1825,7 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
   a.lanes = num_lanes;
   a.block = block_size;
   a.packed_out = packed_out ? 1u : 0u;
-  a.lg = unit_lanes(row_end - row_begin, num_lanes);
+  a.lg = unit_lanes(row_end - row_begin, num_lanes, count > 1 ? 4096 : 8192);
   const unsigned g = grid_for((row_end - row_begin) * (num_lanes / a.lg));
   hipStream_t st = S(stream);
   switch (vec) {

@@ -90,6 +90,78 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum_all(ShardArgs a) {
   }
 }
 
+// k_move with SL slots per batch and prefetched index loads: a wave sweeps several units (grid-stride) and issues
+// the next unit's mask + prefix loads before the current unit's data loads are consumed.
+template <int VEC, int SL, bool PF>
+__global__ __launch_bounds__(kWGThreads) void k_move_v(MoveArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t groups = a.lanes / a.lg;
+  const uint32_t bbytes = a.block * 4;
+  const uint64_t units = a.rows * groups;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
+  const uint32_t skip_cnt = a.prefix[a.skip_e] - a.prefix[a.skip_b];
+  uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint64_t m_n = 0;
+  uint32_t pr_n = 0;
+  if (PF && u < units) {
+    m_n = a.masks[u / groups];
+    pr_n = a.prefix[u / groups];
+  }
+  for (; u < units; u += nw) {
+    const uint64_t r = u / groups;
+    const uint32_t g0 = static_cast<uint32_t>(u % groups) * a.lg;
+    uint64_t m;
+    uint32_t pr;
+    if constexpr (PF) {
+      m = m_n;
+      pr = pr_n;
+      const uint64_t un = u + nw;
+      if (un < units) {  // the next unit's index loads, in flight under this unit's data
+        m_n = a.masks[un / groups];
+        pr_n = a.prefix[un / groups];
+      }
+    } else {
+      m = a.masks[r];
+      pr = a.prefix[r];
+    }
+    if (r >= a.skip_b && r < a.skip_e) continue;
+    uint64_t rem = m & (below(g0 + a.lg) & ~below(g0));
+    if (rem == 0) continue;
+    uint64_t k = pr + static_cast<uint64_t>(__builtin_popcountll(m & below(g0))) - (r >= a.skip_e ? skip_cnt : 0u);
+    float* dense = const_cast<float*>(a.dir == 0 ? a.src : a.dst) + r * a.lanes * a.block;
+    const __amdgpu_buffer_rsrc_t rd = chunk_rsrc(dense, a.lanes * bbytes);
+    while (rem != 0) {
+      uint32_t lj[SL];
+      uint64_t bm;
+      const uint32_t nv = take_bits<SL>(rem, lj, bm);
+      float* packed = const_cast<float*>(a.dir == 0 ? a.dst : a.src) + k * a.block;
+      const __amdgpu_buffer_rsrc_t rp = chunk_rsrc(packed, nv * bbytes);
+      const __amdgpu_buffer_rsrc_t rs = a.dir == 0 ? rd : rp;
+      const __amdgpu_buffer_rsrc_t rt = a.dir == 0 ? rp : rd;
+      v4f v[SL][VEC];
+#pragma unroll
+      for (int j = 0; j < SL; ++j) {
+        const uint32_t off = (a.dir == 0 ? lj[j] : static_cast<uint32_t>(j)) * bbytes;
+        const uint32_t drop = static_cast<uint32_t>(j) < nv ? 0u : kDropStore;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q)
+          v[j][q] = __builtin_bit_cast(
+              v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, (off + (q * 64 + lane) * 16) | drop, 0, kLoadAux));
+      }
+#pragma unroll
+      for (int j = 0; j < SL; ++j) {
+        const uint32_t off = (a.dir == 0 ? static_cast<uint32_t>(j) : lj[j]) * bbytes;
+        const uint32_t drop = static_cast<uint32_t>(j) < nv ? 0u : kDropStore;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v[j][q]), rt,
+                                                 (off + (q * 64 + lane) * 16) | drop, 0, 0);
+      }
+      k += nv;
+    }
+  }
+}
+
 struct Shape {
   uint32_t lg;
   unsigned grid;
@@ -127,9 +199,45 @@ const Variant kVariants[] = {
     {"all-contributors MC4 SL8", go_all<4, 8>, 4},
 };
 constexpr int kNum = sizeof(kVariants) / sizeof(kVariants[0]);
+
+struct MoveVariant {
+  const char* name;
+  void (*fn)(const MoveArgs&, unsigned, hipStream_t);
+};
+template <int SL, bool PF>
+void gm(const MoveArgs& a, unsigned g, hipStream_t st) {
+  k_move_v<1, SL, PF><<<g, kWGThreads, 0, st>>>(a);
+}
+const MoveVariant kMoves[] = {
+    {"move SL16 (product shape)", gm<16, false>}, {"move SL8", gm<8, false>}, {"move SL4", gm<4, false>},
+    {"move SL16 prefetch", gm<16, true>},          {"move SL8 prefetch", gm<8, true>},
+};
+constexpr int kNumMoves = sizeof(kMoves) / sizeof(kMoves[0]);
 }  // namespace
 
 extern "C" {
+int tune_move_count(void) { return kNumMoves; }
+const char* tune_move_name(int v) { return (v >= 0 && v < kNumMoves) ? kMoves[v].name : "?"; }
+// the pack (dir 0) of rows outside [skip_b, skip_e), B = 256; lg lanes per unit (0: the product's choice); grid cap
+int tune_move(int v, const float* src, float* dst, const uint64_t* masks, const uint32_t* prefix, uint64_t rows,
+              uint32_t lanes, uint64_t skip_b, uint64_t skip_e, uint32_t lg, uint32_t grid, void* stream) {
+  if (v < 0 || v >= kNumMoves) return -3;
+  MoveArgs a;
+  a.src = src;
+  a.dst = dst;
+  a.masks = masks;
+  a.prefix = prefix;
+  a.rows = rows;
+  a.skip_b = skip_b;
+  a.skip_e = skip_e;
+  a.lanes = lanes;
+  a.block = 256;
+  a.dir = 0;
+  a.lg = lg ? lg : unit_lanes(rows, lanes);
+  const unsigned g = grid ? grid : grid_for(rows * (lanes / a.lg));
+  kMoves[v].fn(a, g, reinterpret_cast<hipStream_t>(stream));
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 uint32_t omr_sentinel(uint32_t block_size, uint32_t num_lanes) {  // the product's, compiled out by OMR_NO_CAPI
   return (UINT32_MAX / block_size / num_lanes - 1u) * num_lanes * block_size;
 }

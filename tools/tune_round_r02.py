@@ -32,6 +32,8 @@ def load():
     lib.tune_shard_sum.argtypes = [i, vp, u32, vp, vp, vp, u32, vp, vp, u64, u64, u64, u32, i, vp, u32, vp]
     lib.tune_name.restype = ctypes.c_char_p
     lib.tune_max_count.restype = u32
+    lib.tune_move.argtypes = [i, vp, vp, vp, vp, u64, u32, u64, u64, u32, u32, vp]
+    lib.tune_move_name.restype = ctypes.c_char_p
     return lib
 
 
@@ -115,6 +117,19 @@ def main():
         work = [S["xs"][0].clone() for _ in range(2)]
         times = {c: [] for c in cases}
         times["pack"] = []
+        mcases = [(v, lg, g) for v in range(tl.tune_move_count()) for lg in (0, 16, 64) for g in (0, 1024, 4096)]
+        for mc in mcases:
+            times[mc] = []
+        ref_pack = torch.zeros(L.n, dtype=torch.float32, device=dev)
+        lib.omr_move_blocks_f32(S["xs"][0].data_ptr(), ref_pack.data_ptr(), 0, S["masks"][0].data_ptr(),
+                                S["prefix"][0].data_ptr(), L.rows, L.num_lanes, 256, r0, r1, st)
+        for v, lg, g in mcases:
+            chk = torch.zeros(L.n, dtype=torch.float32, device=dev)
+            assert tl.tune_move(v, S["xs"][0].data_ptr(), chk.data_ptr(), S["masks"][0].data_ptr(),
+                                S["prefix"][0].data_ptr(), L.rows, L.num_lanes, r0, r1, lg, g, st) == 0
+            torch.cuda.synchronize()
+            assert torch.equal(chk.view(torch.int32), ref_pack.view(torch.int32)), tl.tune_move_name(v)
+        del chk, ref_pack
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for r in range(a.rounds):
             for c in cases:
@@ -133,6 +148,15 @@ def main():
             torch.cuda.synchronize()
             if r:
                 times["pack"].append(e0.elapsed_time(e1) / a.reps)
+            for mc in mcases:
+                e0.record()
+                for i in range(a.reps):
+                    tl.tune_move(mc[0], S["xs"][0].data_ptr(), packed.data_ptr(), S["masks"][0].data_ptr(),
+                                 S["prefix"][0].data_ptr(), L.rows, L.num_lanes, r0, r1, mc[1], mc[2], st)
+                e1.record()
+                torch.cuda.synchronize()
+                if r:
+                    times[mc].append(e0.elapsed_time(e1) / a.reps)
         ub, nc = S["union_blocks"], S["contributions"]
         own_blocks = int(sum(bin(int(x) & 0xFFFFFFFFFFFFFFFF).count("1") for x in S["masks"][0][r0:r1].cpu().numpy()))
         sbytes = (nc + own_blocks + ub) * 1024
@@ -147,6 +171,10 @@ def main():
         t = np.median(times["pack"]) * 1e-3
         print(f"{'product pack (k_move)':28s}           median {t * 1e6:8.2f} us  {2 * tot * 1024 / t / 1e9:7.1f} GB/s "
               f"({tot} blocks read + written)", flush=True)
+        for mc in sorted(mcases, key=lambda mc: np.median(times[mc]))[:8]:
+            t = np.median(times[mc]) * 1e-3
+            print(f"  {tl.tune_move_name(mc[0]).decode():26s} lg {mc[1] or 'auto':>4} grid {mc[2] or 'auto':>5}  "
+                  f"median {t * 1e6:8.2f} us  {2 * tot * 1024 / t / 1e9:7.1f} GB/s", flush=True)
         del S, work, packed
         torch.cuda.empty_cache()
 
