@@ -78,6 +78,10 @@ def parse():
                         "(OMR_ROUND_DEFER, default) = as async, and round k's exchange is issued after round k+1's "
                         "first half is queued, so the host never waits for block counts with the GPU idle")
     p.add_argument("--dist-sync", action="store_true", help="same as --dist-pipe sync")
+    p.add_argument("--dist-transport", choices=("rccl", "ipc"), default="rccl",
+                   help="N>1 round transport: RCCL over xGMI, one process per GPU (the product path), or HIP IPC "
+                        "between processes that may share a GPU (a rehearsal of the N>1 path on one GPU; the "
+                        "torch.distributed group is then gloo and only carries the id, barriers and timings)")
     return p.parse_args()
 
 
@@ -262,10 +266,16 @@ def main():
         print(workload_string(args, args.workers if ws == 1 else 1))
         return
     n_gpus = ws if ws > 1 else args.gpus
-    if dist_mode:
+    ipc = dist_mode and args.dist_transport == "ipc"
+    if ipc:  # ranks may share GPUs: rank r on GPU r mod count; gloo for the id broadcast, barriers and timings
+        local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("gloo")
+    elif dist_mode:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local if dist_mode else 0)
+    tdev = torch.device("cpu") if ipc else dev  # where the torch.distributed timing reduction runs
     L = Layout.from_bytes(args.size_mib << 20, args.block_size)
     m = args.workers if not dist_mode else 1
     workload = workload_string(args, m)
@@ -282,7 +292,12 @@ def main():
     stream = torch.cuda.current_stream(dev)
     if dist_mode:
         from omr import cdist
-        engine = cdist.CppSparseAllreduce(L, device=dev)
+        if ipc:
+            uid = [cdist.ipc_unique_id() if rank == 0 else None]
+            torch.distributed.broadcast_object_list(uid, src=0)
+            engine = cdist.CppSparseAllreduce(L, dev, transport="ipc", uid=uid[0], rank=rank, world=ws)
+        else:
+            engine = cdist.CppSparseAllreduce(L, device=dev)
         for xs, out in sets:  # out-of-place result buffers keep every step's input pristine
             out.copy_(xs[0])
 
@@ -342,7 +357,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist_mode:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
@@ -365,7 +380,7 @@ def main():
                     "GBps_out_per_peer": (round(b_out / (ws - 1) / (x_ms * 1e-3) / 1e9, 2)
                                           if x_ms > 0 and ws > 1 else None),
                     "xgmi_link_GBps_nominal": XGMI_LINK_GBPS,
-                    "timing": (f"HIP events around the grouped ncclSend/ncclRecv (dense: ncclReduceScatter) on the "
+                    "timing": (f"HIP events around the worker -> aggregator exchange ({'grouped ncclSend/ncclRecv, dense: ncclReduceScatter' if not ipc else 'the IPC transport copies'}) on the "
                                f"stream it runs on, in every {every}th timed round (inside the timed region), rank 0")}
     if not dist_mode:
         kev = kev[::every]
@@ -402,6 +417,8 @@ def main():
             roofline["step_algorithmic_bytes"] = sbytes
             roofline["step_frac"] = round(sbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
 
+    if dist_mode:
+        engine.close()  # every rank (the IPC transport's board is released when the last rank leaves)
     if rank != 0:
         if dist_mode:
             torch.distributed.destroy_process_group()
@@ -410,6 +427,9 @@ def main():
     if dist_mode and pipe != "sync":
         pipe_note = (", rounds pipelined: exchange k beside scan k+1" +
                      (", exchange k issued after round k+1's first half (OMR_ROUND_DEFER)" if pipe == "defer" else ""))
+    transport_note = ("RCCL" if not ipc else
+                      f"HIP IPC, {ws} ranks on {torch.cuda.device_count()} GPU(s): a rehearsal of the N>1 path, not a "
+                      f"scaling figure")
     total_bytes = n_gpus * m * L.nbytes
     value = total_bytes / (ms_per_step * 1e-3) / 1e9
     metric = "GB/s device-resident block scan+sum, 256 MiB fp32 @ 90% block-sparse"   # BASELINE.json
@@ -437,8 +457,7 @@ def main():
                    "workers_per_gpu": m, "rotating_buffer_sets": len(sets),
                    "parallelism": "single GPU" if not dist_mode else
                    f"dp{n_gpus} {dict(allreduce='sparse all-reduce', reduce='sparse reduce-scatter', dense='dense reduce-scatter (stand-in)')[args.dist_mode]} over "
-                   f"RCCL (C++ round driver, libomr_dist.so"
-                   f"{pipe_note})"},
+                   f"{transport_note} (C++ round driver, libomr_dist.so{pipe_note})"},
         "alg_bw_GiBps_reference_style": round(total_bytes / (ms_per_step * 1e-3) / 2 ** 30, 2),
         "roofline": roofline,
         "cpu_baseline": None,

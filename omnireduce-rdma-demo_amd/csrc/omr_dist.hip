@@ -291,7 +291,7 @@ struct IpcDist final : omr_dist {
     if (b != nullptr) {
       const bool last = b->attached.fetch_sub(1) == 1;
       munmap(b, sizeof(IpcBoard));
-      if (last) shm_unlink(name.c_str());
+      if (last) shm_unlink(name.c_str());  // (normally gone already: rank 0 removes the name once all have joined)
     }
   }
 
@@ -336,11 +336,18 @@ struct IpcDist final : omr_dist {
         TRY(hip_check(hipIpcGetEventHandle(&me.rdone[c][k], rdone[c][k]), "hipIpcGetEventHandle"));
       }
     me.joined.store(1, std::memory_order_release);
+    if (rank == 0) {  // the name is only needed until every rank has mapped the board
+      for (int p = 0; p < world; ++p)
+        TRY(ipc_spin([&] { return b->rank[p].joined.load(std::memory_order_acquire) != 0; }, "peers to join", rank));
+      shm_unlink(name.c_str());
+    }
     pready.assign(world, {});
     prdone.assign(world, {});
     for (int p = 0; p < world; ++p) {
       TRY(ipc_spin([&] { return b->rank[p].joined.load(std::memory_order_acquire) != 0; }, "peers to join", rank));
       if (p == rank) continue;
+      // (once every rank has joined, every rank has the board mapped: rank 0 removes its name below, so a job that
+      // dies leaves nothing in /dev/shm)
       for (int c = 0; c < kIpcChans; ++c)
         for (int k = 0; k < kIpcRing; ++k) {
           TRY(hip_check(hipIpcOpenEventHandle(&pready[p][c * kIpcRing + k], b->rank[p].ready[c][k]),

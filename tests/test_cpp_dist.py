@@ -481,6 +481,33 @@ def test_bench_distributed_path_world1(gpu, extra):
     assert line["exchange"]["peers"] == 0 and line["exchange"]["ms_mean"] >= 0
 
 
+@pytest.mark.parametrize("world,extra", [(2, []), (3, ["--dist-mode", "allreduce"]), (2, ["--dist-sync"]),
+                                         (4, ["--dist-mode", "dense"])])
+def test_bench_distributed_path_ipc(gpu, world, extra):
+    """bench.py's N>1 path with real exchanges on one GPU: torch.distributed.run with `world` ranks sharing the GPU
+    over the HIP-IPC transport (gloo carries the id, barriers and the max-over-ranks time).  Rank 0's line reports
+    the timed rounds' exchange with peers and non-zero bytes each way."""
+    import json
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(PKG)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--force-dist",
+           "--dist-transport", "ipc", "--no-cpu", "--steps", "12", "--warmup", "2", "--size-mib", "64",
+           "--event-every", "3"] + extra
+    rc, out = _run(cmd, timeout=240)
+    assert rc == 0, out[-3000:]
+    line = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0
+    assert "HIP IPC" in line["config"]["parallelism"]
+    x = line["exchange"]
+    assert x["peers"] == world - 1 and x["timed_rounds"] >= 3 and x["ms_mean"] > 0
+    assert x["bytes_out_per_rank"] > 0 and x["bytes_in_per_rank"] > 0
+
+
 @pytest.mark.parametrize("world,mode", [(4, 1 | 0x100), (3, 0), (4, 2), (4, 1 | 0x400), (3, 0x400)])
 def test_cpp_exchange_timing_loopback(gpu, world, mode):
     """OMR_ROUND_TIME_EXCHANGE: the timed round's result is unchanged, omr_ar_plan_exchange_time reports a
