@@ -100,7 +100,7 @@ __global__ __launch_bounds__(kWGThreads) void k_scanm_row(ScanArgs a) {
   }
 }
 
-template <int VEC, int SUB>
+template <int VEC, int SUB, int LAUX = kLoadAux>
 __device__ __forceinline__ void load_group(v4f (&v)[SUB][VEC], const float* base, bool live, int lane) {
   constexpr uint32_t B4 = 64 * VEC;
   const __amdgpu_buffer_rsrc_t src = chunk_rsrc(base, live ? SUB * B4 * 16 : 0u);
@@ -109,7 +109,7 @@ __device__ __forceinline__ void load_group(v4f (&v)[SUB][VEC], const float* base
 #pragma unroll
     for (int q = 0; q < VEC; ++q)
       v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (s * B4 + q * 64 + lane) * 16, 0,
-                                                                              kLoadAux));
+                                                                              LAUX));
 }
 
 // acc += v in rank order; returns the group's non-zero bits of this worker (bit s = block l0 + s)
@@ -153,7 +153,7 @@ __device__ __forceinline__ void store_mask_piece(uint64_t* masks, uint64_t row, 
 // 2 = as 1 with scheduling barriers between the phases (no hoisting of the set after next); 3 = three sets.
 // A worker past m reads through an empty descriptor (zeros, no traffic); adding +0.0 to an accumulator that is never
 // -0.0 (it starts at +0.0, and a round-to-nearest sum is -0.0 only if both terms are) leaves it unchanged.
-template <int VEC, int SUB, int G, int WAVES, int PF, bool XCD, int SAUX = kStoreAux>
+template <int VEC, int SUB, int G, int WAVES, int PF, bool XCD, int SAUX = kStoreAux, int LAUX = kLoadAux>
 __global__ __launch_bounds__(64 * WAVES) void k_scanm_g(ScanArgs a) {
   constexpr uint32_t B4 = 64 * VEC;
   static_assert(G % SUB == 0 && G <= 64, "unit = whole sub-groups of one row");
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_scanm_g(ScanArgs a) {
       };
       auto ld = [&](v4f (&v)[SUB][VEC], uint32_t w) {
         const bool live = w < a.m;
-        load_group<VEC, SUB>(v, a.x.p[live ? w : 0] + goff, live, lane);
+        load_group<VEC, SUB, LAUX>(v, a.x.p[live ? w : 0] + goff, live, lane);
       };
       if constexpr (PF == 1 || PF == 2) {
         v4f va[SUB][VEC], vb[SUB][VEC];
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_scanm_g(ScanArgs a) {
 unsigned g_cap = 0;  // grid cap (workgroups); 0 = one unit per wave
 unsigned g_occ = 0;  // workgroups per CU forced through dynamic LDS (0 = registers decide)
 
-template <int VEC, int SUB, int G, int WAVES, int PF, bool XCD, int SAUX = kStoreAux>
+template <int VEC, int SUB, int G, int WAVES, int PF, bool XCD, int SAUX = kStoreAux, int LAUX = kLoadAux>
 void gog(const ScanArgs& a, hipStream_t st) {
   const uint64_t gl = a.lanes < G ? a.lanes : G;
   const uint64_t units = a.rows * (a.lanes / gl);
@@ -267,10 +267,10 @@ void gog(const ScanArgs& a, hipStream_t st) {
   unsigned lds = 0;
   if (g_occ) {
     lds = (160u * 1024u / g_occ - 512u) & ~255u;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scanm_g<VEC, SUB, G, WAVES, PF, XCD, SAUX>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scanm_g<VEC, SUB, G, WAVES, PF, XCD, SAUX, LAUX>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
   }
-  k_scanm_g<VEC, SUB, G, WAVES, PF, XCD, SAUX><<<static_cast<unsigned>(g), 64 * WAVES, lds, st>>>(a);
+  k_scanm_g<VEC, SUB, G, WAVES, PF, XCD, SAUX, LAUX><<<static_cast<unsigned>(g), 64 * WAVES, lds, st>>>(a);
 }
 void go_row(const ScanArgs& a, hipStream_t st) { k_scanm_row<1, 16, 1><<<grid_for(a.rows), kWGThreads, 0, st>>>(a); }
 void go_prod(const ScanArgs& a, hipStream_t st) {
@@ -282,15 +282,13 @@ struct Variant {
   void (*fn)(const ScanArgs&, hipStream_t);
 };
 const Variant kVariants[] = {
-    {"product k_scanm (G32 SUB32)", go_prod},
-    {"round-1 k_scanm (row/wave)", go_row},
-    {"G32 SUB32 W4", gog<1, 32, 32, 4, 0, true>},
-    {"G32 SUB32 W4 st-nt", gog<1, 32, 32, 4, 0, true, 2>},
-    {"G32 SUB32 W4 st-plain", gog<1, 32, 32, 4, 0, true, 0>},
-    {"G32 SUB32 W4 st-sc1", gog<1, 32, 32, 4, 0, true, 16>},
-    {"G64 SUB32 W4", gog<1, 32, 64, 4, 0, true>},
-    {"G32 SUB16 W4 PF2", gog<1, 16, 32, 4, 2, true>},
-    {"G16 SUB16 W4 PF2", gog<1, 16, 16, 4, 2, true>},
+    {"product k_scanm (G32 SUB32 nt-st)", go_prod},
+    {"G32 SUB32 W4 nt-st ld-nt", gog<1, 32, 32, 4, 0, true, 2, 2>},
+    {"G32 SUB32 W4 nt-st ld-plain", gog<1, 32, 32, 4, 0, true, 2, 0>},
+    {"G32 SUB32 W4 nt-st ld-sc1", gog<1, 32, 32, 4, 0, true, 2, 16>},
+    {"G32 SUB32 W4 plain-st ld-nt", gog<1, 32, 32, 4, 0, true, 0, 2>},
+    {"G32 SUB32 W4 nt-st noxcd", gog<1, 32, 32, 4, 0, false, 2, 2>},
+    {"G64 SUB32 W4 nt-st", gog<1, 32, 64, 4, 0, true, 2, 2>},
 };
 constexpr int kNum = sizeof(kVariants) / sizeof(kVariants[0]);
 }  // namespace
