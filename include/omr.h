@@ -225,6 +225,15 @@ int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uin
                    uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
                    uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
                    uint32_t* arrive, uint32_t* done_flag, uint32_t seq, omr_stream_t stream);
+/* omr_round_plan plus, in the same launch, the aggregator chain (server.cc:86-96: min_next over the workers =
+ * next offsets over the union) into union_next (device uint32[rows * num_lanes], the omr_next_offsets layout of
+ * the union masks), computed by extra workgroups from the workers' masks directly.  union_next NULL: exactly
+ * omr_round_plan. */
+int omr_round_plan_chain(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
+                         uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
+                         uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
+                         uint32_t* arrive, uint32_t* done_flag, uint32_t seq, uint32_t* union_next,
+                         uint32_t block_size, omr_stream_t stream);
 
 /* Block movement addressed by a row mask and its prefix (no block list): the k-th set bit of `row_masks` over
  * rows [0, rows) minus [skip_begin, skip_end) is block k of the packed stream.

@@ -1170,20 +1170,20 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for its next round
   //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
   const uint32_t seq = ++p->seq;
-  TRY(omr_check(omr_round_plan(S.masks_all, static_cast<uint32_t>(M), rows, p->rpp, p->lanes, p->bounds_dev, NS,
-                               S.wset, S.umask, S.prefix,
-                               p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own,
-                               p->arrive, p->flag_map + si, seq, qstream),
-                "omr_round_plan"));
+  //    ... and, by extra workgroups of the same launch, the aggregator chain (server.cc:86-96 min_next) over the union
+  TRY(omr_check(omr_round_plan_chain(S.masks_all, static_cast<uint32_t>(M), rows, p->rpp, p->lanes, p->bounds_dev,
+                                     NS, S.wset, S.umask, S.prefix,
+                                     p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, p->arrive,
+                                     p->flag_map + si, seq, un, p->B, qstream),
+                "omr_round_plan_chain"));
   if (async) {
     TRY(hip_check(hipEventRecord(S.planned, qs), "hipEventRecord"));
     S.plan_pending = true;
   }
   p->ht.lap("1:plan");
-  // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407), then the
-  //     aggregator chain (server.cc:86-96 min_next) over the union: both addressed by device-side data only, so
-  //     they are queued before the host learns the counts and run while it waits.  (Every host API call costs
-  //     microseconds; a round that spends them on side streams and events is host-bound.)
+  // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407): addressed by
+  //     device-side data only, so it is queued before the host learns the counts and runs while it waits.  (Every
+  //     host API call costs microseconds; a round that spends them on side streams and events is host-bound.)
   if (N > 1 && mode != OMR_ROUND_DENSE_REDUCE_SCATTER && p->worker()) {
     const uint64_t r0 = p->colocated ? p->bounds[me] : 0, r1 = p->colocated ? p->bounds[me + 1] : 0;
     TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * rows,
@@ -1191,7 +1191,6 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
                                       r1, qstream), "omr_move_blocks_f32 pack"));
   }
   p->ht.lap("1:pack");
-  TRY(omr_check(omr_next_offsets(S.umask, 1, p->n, p->B, p->lanes, p->parts, un, qstream), "omr_next_offsets"));
   // the rest goes on the communication stream for an asynchronous round, behind everything queued so far
   if (async) TRY(hip_check(hipEventRecord(S.ready, qs), "hipEventRecord"));
   p->ht.lap("1:next+ready");

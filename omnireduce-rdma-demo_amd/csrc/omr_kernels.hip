@@ -515,16 +515,16 @@ __device__ __forceinline__ uint64_t wave_transpose64(uint64_t a, int lane) {
   return a;
 }
 
-__global__ __launch_bounds__(kWGThreads) void k_next(NextArgs a) {
+// One k_next segment with W waves; mask_of(r) gives row r's mask (one array, or the union of several).
+template <int W, typename MaskOf>
+__device__ __forceinline__ void next_segment(const NextArgs& a, uint32_t seg_id, const MaskOf& mask_of, uint32_t* next) {
   __shared__ uint64_t s_col[64];
-  __shared__ uint32_t s_first[kWavesPerWG][64];
+  __shared__ uint32_t s_first[W][64];
   __shared__ uint32_t s_carry_row[64];
   __shared__ int s_done;
   if (threadIdx.x == 0) s_done = 0;
-  const uint64_t* masks = a.masks + static_cast<uint64_t>(blockIdx.y) * a.rows;
-  uint32_t* next = a.next + static_cast<uint64_t>(blockIdx.y) * a.nb;
-  const uint32_t part = blockIdx.x / a.segs_per_part;
-  const uint32_t seg = blockIdx.x % a.segs_per_part;
+  const uint32_t part = seg_id / a.segs_per_part;
+  const uint32_t seg = seg_id % a.segs_per_part;
   const uint64_t part_row0 = static_cast<uint64_t>(part) * a.rows_per_part;
   const uint64_t part_end = part_row0 + a.rows_per_part;
   const uint64_t row0 = part_row0 + static_cast<uint64_t>(seg) * 64;
@@ -535,10 +535,10 @@ __global__ __launch_bounds__(kWGThreads) void k_next(NextArgs a) {
 
   // the segment's own masks and the first look-ahead rows are loaded together (independent round trips)
   const uint64_t r = row0 + lane;
-  const uint64_t seg_mask = (wave == 0 && r < seg_end) ? masks[r] : 0ull;
+  const uint64_t seg_mask = (wave == 0 && r < seg_end) ? mask_of(r) : 0ull;
   uint64_t look = seg_end;
   uint64_t rr = look + static_cast<uint64_t>(wave) * 64 + lane;
-  uint64_t look_mask = (rr < part_end) ? masks[rr] : 0ull;
+  uint64_t look_mask = (rr < part_end) ? mask_of(rr) : 0ull;
   if (wave == 0) {
     s_col[lane] = wave_transpose64(seg_mask, lane);
     s_carry_row[lane] = kNone;
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(kWGThreads) void k_next(NextArgs a) {
     if (wave == 0) {
       uint32_t cr = s_carry_row[lane];
 #pragma unroll
-      for (int w = 0; w < kWavesPerWG; ++w)
+      for (int w = 0; w < W; ++w)
         if (cr == kNone) cr = s_first[w][lane];
       s_carry_row[lane] = cr;
       const uint64_t open = __ballot(lane < static_cast<int>(a.lanes) && cr == kNone);
@@ -558,15 +558,15 @@ __global__ __launch_bounds__(kWGThreads) void k_next(NextArgs a) {
     }
     __syncthreads();
     if (s_done) break;
-    look += 64 * kWavesPerWG;
+    look += 64 * W;
     rr = look + static_cast<uint64_t>(wave) * 64 + lane;
-    look_mask = (rr < part_end) ? masks[rr] : 0ull;
+    look_mask = (rr < part_end) ? mask_of(rr) : 0ull;
   }
   __syncthreads();
   const uint32_t nrows = static_cast<uint32_t>(seg_end - row0);
   const uint32_t lshift = static_cast<uint32_t>(__builtin_ctz(a.lanes));  // lanes is a power of two
   const uint32_t total = nrows << lshift;
-  for (uint32_t idx = threadIdx.x; idx < total; idx += kWGThreads) {
+  for (uint32_t idx = threadIdx.x; idx < total; idx += 64 * W) {
     const uint32_t i = idx >> lshift;
     const uint32_t l = idx & (a.lanes - 1);
     const uint64_t c = (i >= 63) ? 0 : (s_col[l] >> (i + 1));
@@ -579,6 +579,12 @@ __global__ __launch_bounds__(kWGThreads) void k_next(NextArgs a) {
     }
     next[(row0 << lshift) + idx] = v;
   }
+}
+
+__global__ __launch_bounds__(kWGThreads) void k_next(NextArgs a) {
+  const uint64_t* masks = a.masks + static_cast<uint64_t>(blockIdx.y) * a.rows;
+  next_segment<kWavesPerWG>(a, blockIdx.x, [&](uint64_t r) { return masks[r]; },
+                            a.next + static_cast<uint64_t>(blockIdx.y) * a.nb);
 }
 
 // ---------------------------------------------------------------- compaction (mask -> block list)
@@ -891,9 +897,21 @@ struct PlanArgs {
   uint32_t* arrive;     // device arrival counter (zero between launches) or null
   uint32_t* done_flag;  // receives `seq` once every workgroup's counts are visible system-wide, or null
   uint32_t seq;
+  NextArgs chain;       // union_next: the aggregator chain over the union, by workgroups count+1.. (chain.next null: none)
 };
 
 __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
+  if (blockIdx.x > a.count) {  // the aggregator chain (server.cc:86-96 min_next) over the union, one segment each
+    const uint64_t* m = a.masks;
+    const uint32_t cnt = a.count;
+    const uint64_t rows = a.rows;
+    next_segment<kPlanThreads / 64>(a.chain, blockIdx.x - a.count - 1, [&](uint64_t r) {
+      uint64_t u = 0;
+      for (uint32_t c = 0; c < cnt; ++c) u |= m[static_cast<uint64_t>(c) * rows + r];
+      return u;
+    }, a.chain.next);
+    return;
+  }
   extern __shared__ uint64_t s_val[];  // [rows] when rows <= kPlanLdsRows
   __shared__ uint32_t s_wave[kPlanThreads / 64];
   __shared__ uint64_t s_bounds[OMR_MAX_WORKERS + 2];
@@ -1720,10 +1738,11 @@ int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint3
   return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks);
 }
 
-int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
-                   uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
-                   uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                   uint32_t* arrive, uint32_t* done_flag, uint32_t seq, omr_stream_t stream) {
+int omr_round_plan_chain(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
+                         uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
+                         uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
+                         uint32_t* arrive, uint32_t* done_flag, uint32_t seq, uint32_t* union_next,
+                         uint32_t block_size, omr_stream_t stream) {
   if (count == 0 || count > OMR_MAX_WORKERS) return fail("round_plan: count %u out of range", count);
   if (rows == 0 || rows_per_part == 0 || rows % rows_per_part != 0) return fail("round_plan: bad rows");
   if (num_lanes == 0 || num_lanes > 64) return fail("round_plan: num_lanes %u out of range", num_lanes);
@@ -1749,9 +1768,34 @@ int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uin
   a.arrive = arrive;
   a.done_flag = done_flag;
   a.seq = seq;
+  memset(&a.chain, 0, sizeof(a.chain));
+  uint32_t chain_wgs = 0;
+  if (union_next != nullptr) {
+    if (block_size != 256 && block_size != 512 && block_size != 1024)
+      return fail("round_plan: block_size %u unsupported", block_size);
+    if ((num_lanes & (num_lanes - 1)) != 0) return fail("round_plan: num_lanes %u", num_lanes);
+    const uint64_t parts = rows / rows_per_part;
+    a.chain.next = union_next;
+    a.chain.rows = rows;
+    a.chain.nb = rows * num_lanes;
+    a.chain.rows_per_part = rows_per_part;
+    a.chain.segs_per_part = (rows_per_part + 63) / 64;
+    a.chain.lanes = num_lanes;
+    a.chain.block = block_size;
+    a.chain.sentinel = omr_sentinel(block_size, num_lanes);
+    chain_wgs = static_cast<uint32_t>(parts * a.chain.segs_per_part);
+  }
   const size_t lds = rows <= kPlanLdsRows ? rows * sizeof(uint64_t) : 0;
-  k_round_plan<<<count + 1, kPlanThreads, lds, S(stream)>>>(a);
+  k_round_plan<<<count + 1 + chain_wgs, kPlanThreads, lds, S(stream)>>>(a);
   return launch_status("k_round_plan");
+}
+
+int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
+                   uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
+                   uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
+                   uint32_t* arrive, uint32_t* done_flag, uint32_t seq, omr_stream_t stream) {
+  return omr_round_plan_chain(row_masks, count, rows, rows_per_part, num_lanes, bounds, num_bounds, write_set,
+                              union_masks, prefix, counts, zero_masks, arrive, done_flag, seq, nullptr, 0, stream);
 }
 
 int omr_move_blocks_f32(const float* src, float* dst, int dir, const uint64_t* row_masks, const uint32_t* prefix,

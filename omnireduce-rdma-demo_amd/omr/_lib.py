@@ -54,6 +54,8 @@ SIGNATURES = {
     "omr_worker_scan_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "omr_round_plan": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_vp, c_u32, c_vp]),
+    "omr_round_plan_chain": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp, c_vp, c_u32, c_vp, c_u32, c_vp]),
     "omr_move_blocks_f32": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_u64, c_u32, c_u32, c_u64, c_u64, c_vp]),
     "omr_shard_sum_f32": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, c_vp, c_vp, c_u64, c_u64, c_u64, c_u32,
                                   c_u32, c_int, c_vp, c_vp]),

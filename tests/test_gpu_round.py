@@ -1,6 +1,6 @@
 """GPU parity of the mask-addressed multi-rank round kernels, called through the C ABI (include/omr.h):
-omr_worker_scan_f32 (scan + row masks), omr_round_plan (union / write set / prefixes / shard counts, the
-aggregator bookkeeping of server.cc:83-96), omr_move_blocks_f32 (pack common.cc:405-407 / unpack client.cc:89)
+omr_worker_scan_f32 (scan + row masks), omr_round_plan / omr_round_plan_chain (union / write set / prefixes / shard
+counts, the aggregator bookkeeping of server.cc:83-96, and the aggregator chain in the same launch), omr_move_blocks_f32 (pack common.cc:405-407 / unpack client.cc:89)
 and omr_shard_sum_f32 (server.cc:97-98 in rank order).  Checked against the oracle (flags, masks, next chains,
 block sums) and plain numpy restatements of the index arithmetic.  Bar: bit-exact (integer work and rank-order
 fp32 sums, 0 ulp)."""
@@ -118,6 +118,44 @@ def test_round_plan(gpu, count, rows, rpp, lanes):
         assert (pre[a] == exp).all(), a
         assert (cn[a] == exp[bounds.astype(np.int64)]).all(), a
     assert int(zero.count_nonzero()) == 0
+
+
+@pytest.mark.parametrize("count,rows,rpp,lanes", [(1, 64, 8, 64), (3, 512, 64, 64), (8, 4096, 512, 64),
+                                                   (5, 1280, 256, 16), (16, 100, 25, 32), (3, 20480, 2560, 16)])
+def test_round_plan_chain(gpu, count, rows, rpp, lanes):
+    """omr_round_plan_chain: the plan's outputs exactly as omr_round_plan, plus the aggregator chain (server.cc:86-96,
+    min_next over the workers) computed by the same launch from the workers' masks = the oracle's next offsets over
+    the union of the workers' flags."""
+    rng = np.random.default_rng(count * 7 + rows)
+    B = 16384 // lanes
+    masks = np.zeros((count, rows), dtype=np.uint64)
+    for c in range(count):
+        bits = rng.random((rows, lanes)) < rng.random() * 0.3
+        masks[c] = (bits.astype(np.uint64) << np.arange(lanes, dtype=np.uint64)).sum(axis=1).astype(np.uint64)
+    N = max(1, min(count, 8))
+    bounds = np.array([s * rows // N for s in range(N + 1)], dtype=np.uint64)
+    lib = _lib.load()
+    md = torch.from_numpy(masks.view(np.int64)).to(gpu)
+    bd = torch.from_numpy(bounds.view(np.int64)).to(gpu)
+    outs = []
+    for chain in (False, True):
+        wset = torch.zeros(rows, dtype=torch.int64, device=gpu)
+        umask = torch.zeros(rows, dtype=torch.int64, device=gpu)
+        prefix = torch.zeros((count + 1) * (rows + 1), dtype=torch.int32, device=gpu)
+        counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int32, device=gpu)
+        unext = torch.full((rows * lanes,), -1, dtype=torch.int32, device=gpu)
+        assert lib.omr_round_plan_chain(P(md), count, rows, rpp, lanes, P(bd), N + 1, P(wset), P(umask), P(prefix),
+                                        P(counts), None, None, None, 0, P(unext) if chain else None, B,
+                                        stream()) == 0, lib.omr_last_error()
+        torch.cuda.synchronize()
+        outs.append((wset.cpu(), umask.cpu(), prefix.cpu(), counts.cpu(), unext.cpu()))
+    for a, b in zip(outs[0][:4], outs[1][:4]):
+        assert torch.equal(a, b)
+    assert (outs[0][4] == -1).all()  # no chain requested: union_next untouched
+    u = np.bitwise_or.reduce(masks, axis=0)
+    flags = ((u[:, None] >> np.arange(lanes, dtype=np.uint64)) & np.uint64(1)).astype(np.int32).ravel()
+    exp = oracle.next_offsets(flags, rows * lanes * B, B, lanes, rows // rpp)
+    assert (outs[1][4].numpy().view(np.uint32) == exp).all()
 
 
 @pytest.mark.parametrize("B,rows,skip", [(256, 512, (0, 0)), (256, 512, (128, 256)), (512, 256, (200, 256)),
