@@ -210,9 +210,17 @@ struct LocalDist final : omr_dist {
 // is still reading).  The hosts only exchange sequence numbers (no stream synchronisation).  Two channels, as
 // RcclDist's two communicators: 0 carries the all-gather, 1 the exchange and the dense reduce-scatter; every rank
 // issues each channel's operations in the same order.
+//
+// An IPC event fails ("hipStreamWaitEvent: invalid argument") once it has been recorded about 32 times (ROCm 7.2,
+// measured: the CLI at -W 10 -R 101 died at round ~32), so the events come in generations: a channel's operations
+// [g K, (g+1) K) use generation g's events (each recorded K / kIpcRing times).  A rank creates and posts generation
+// g+1 when it enters g and opens its peers' generation g then; generations are retired two back and destroyed in
+// batches behind a device sync (a peer's or this rank's stream may still hold a wait on them).
 constexpr uint32_t kIpcMagic = 0x4f4d5249;  // "OMRI"
 constexpr int kIpcChans = 2, kIpcRing = 2, kIpcMaxRanks = 2 * OMR_MAX_WORKERS, kIpcMaxHandles = 32;
 constexpr int kIpcMaxEntries = 4096;
+constexpr uint64_t kIpcGenOps = 16;  // operations per event generation
+constexpr size_t kIpcReap = 256;     // retired events destroyed (behind a device sync) in batches of this size
 constexpr uint32_t kIpcAll = 0xFFFFFFFFu;  // an entry every peer reads (all-gather / reduce-scatter input)
 
 struct IpcEntry {
@@ -227,7 +235,8 @@ struct IpcPost {
 struct IpcRank {
   std::atomic<uint64_t> posted[kIpcChans], done[kIpcChans];
   std::atomic<uint32_t> joined, left;
-  hipIpcEventHandle_t ready[kIpcChans][kIpcRing], rdone[kIpcChans][kIpcRing];
+  std::atomic<uint64_t> evgen[kIpcChans][2];  // 1 + the generation whose handles slot [c][g % 2] holds (0: none)
+  hipIpcEventHandle_t ready[kIpcChans][2][kIpcRing], rdone[kIpcChans][2][kIpcRing];
 };
 struct IpcBoard {
   std::atomic<uint32_t> magic;
@@ -258,14 +267,27 @@ int ipc_spin(F ready, const char* what, int rank) {
   }
 }
 
+struct IpcEvents {
+  hipEvent_t ready[kIpcRing] = {}, rdone[kIpcRing] = {};
+};
+
 struct IpcDist final : omr_dist {
   IpcBoard* b = nullptr;
   std::string name;
-  hipEvent_t ready[kIpcChans][kIpcRing] = {}, rdone[kIpcChans][kIpcRing] = {};
-  std::vector<std::array<hipEvent_t, kIpcChans * kIpcRing>> pready, prdone;  // peers' events, opened
+  IpcEvents mine[kIpcChans][2];                          // this rank's events, generation g in [c][g % 2]
+  std::vector<std::array<IpcEvents, kIpcChans * 2>> peer;  // peers' events, opened, [p][c * 2 + g % 2]
+  std::vector<hipEvent_t> retired;                         // events of old generations, destroyed in batches
   uint64_t seq[kIpcChans] = {0, 0};
   std::map<std::pair<uintptr_t, size_t>, hipIpcMemHandle_t> own;  // allocation (base, size) -> its handle
   std::map<std::string, char*> opened;                               // peer handle bytes -> mapped base
+
+  static void release(IpcEvents& e, std::vector<hipEvent_t>& to) {
+    for (int k = 0; k < kIpcRing; ++k) {
+      if (e.ready[k]) to.push_back(e.ready[k]);
+      if (e.rdone[k]) to.push_back(e.rdone[k]);
+      e.ready[k] = e.rdone[k] = nullptr;
+    }
+  }
 
   ~IpcDist() override {
     if (b != nullptr) {
@@ -276,18 +298,12 @@ struct IpcDist final : omr_dist {
       for (int p = 0; p < world; ++p)
         (void)ipc_spin([&] { return b->rank[p].left.load(std::memory_order_acquire) != 0; }, "peers to leave", rank);
       for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
-      for (auto& v : pready)
-        for (hipEvent_t e : v)
-          if (e) (void)hipEventDestroy(e);
-      for (auto& v : prdone)
-        for (hipEvent_t e : v)
-          if (e) (void)hipEventDestroy(e);
     }
-    for (int c = 0; c < kIpcChans; ++c)
-      for (int k = 0; k < kIpcRing; ++k) {
-        if (ready[c][k]) (void)hipEventDestroy(ready[c][k]);
-        if (rdone[c][k]) (void)hipEventDestroy(rdone[c][k]);
-      }
+    for (auto& v : peer)
+      for (IpcEvents& e : v) release(e, retired);
+    for (auto& row : mine)
+      for (IpcEvents& e : row) release(e, retired);
+    for (hipEvent_t e : retired) (void)hipEventDestroy(e);
     if (b != nullptr) {
       const bool last = b->attached.fetch_sub(1) == 1;
       munmap(b, sizeof(IpcBoard));
@@ -326,38 +342,66 @@ struct IpcDist final : omr_dist {
       return derr(OMR_EINVAL, "ipc transport: board world %u, this rank says %d", b->world, world);
     b->attached.fetch_add(1);
     IpcRank& me = b->rank[rank];
-    for (int c = 0; c < kIpcChans; ++c)
-      for (int k = 0; k < kIpcRing; ++k) {
-        TRY(hip_check(hipEventCreateWithFlags(&ready[c][k], hipEventDisableTiming | hipEventInterprocess),
-                      "hipEventCreate"));
-        TRY(hip_check(hipEventCreateWithFlags(&rdone[c][k], hipEventDisableTiming | hipEventInterprocess),
-                      "hipEventCreate"));
-        TRY(hip_check(hipIpcGetEventHandle(&me.ready[c][k], ready[c][k]), "hipIpcGetEventHandle"));
-        TRY(hip_check(hipIpcGetEventHandle(&me.rdone[c][k], rdone[c][k]), "hipIpcGetEventHandle"));
-      }
+    for (int c = 0; c < kIpcChans; ++c) {
+      TRY(publish(c, 0));
+      TRY(publish(c, 1));
+    }
     me.joined.store(1, std::memory_order_release);
     if (rank == 0) {  // the name is only needed until every rank has mapped the board
       for (int p = 0; p < world; ++p)
         TRY(ipc_spin([&] { return b->rank[p].joined.load(std::memory_order_acquire) != 0; }, "peers to join", rank));
       shm_unlink(name.c_str());
     }
-    pready.assign(world, {});
-    prdone.assign(world, {});
-    for (int p = 0; p < world; ++p) {
+    peer.assign(world, {});
+    for (int p = 0; p < world; ++p)
       TRY(ipc_spin([&] { return b->rank[p].joined.load(std::memory_order_acquire) != 0; }, "peers to join", rank));
+    for (int c = 0; c < kIpcChans; ++c) TRY(open_gen(c, 0));
+    return 0;
+  }
+
+  // create this rank's events of generation g of channel c and post their handles (slot g % 2; the events it
+  // replaces, generation g - 2, are retired)
+  int publish(int c, uint64_t g) {
+    IpcEvents& e = mine[c][g % 2];
+    release(e, retired);
+    IpcRank& me = b->rank[rank];
+    for (int k = 0; k < kIpcRing; ++k) {
+      TRY(hip_check(hipEventCreateWithFlags(&e.ready[k], hipEventDisableTiming | hipEventInterprocess),
+                    "hipEventCreate"));
+      TRY(hip_check(hipEventCreateWithFlags(&e.rdone[k], hipEventDisableTiming | hipEventInterprocess),
+                    "hipEventCreate"));
+      TRY(hip_check(hipIpcGetEventHandle(&me.ready[c][g % 2][k], e.ready[k]), "hipIpcGetEventHandle"));
+      TRY(hip_check(hipIpcGetEventHandle(&me.rdone[c][g % 2][k], e.rdone[k]), "hipIpcGetEventHandle"));
+    }
+    me.evgen[c][g % 2].store(g + 1, std::memory_order_release);
+    return 0;
+  }
+  // open every peer's events of generation g of channel c, on entering g.  A peer posts them when it enters g - 1
+  // (this rank cannot be in g before every peer has passed g - 1's first operation), and overwrites them when it
+  // enters g + 1 (it cannot before this rank has posted g's last operation, i.e. after this call)
+  int open_gen(int c, uint64_t g) {
+    for (int p = 0; p < world; ++p) {
       if (p == rank) continue;
-      // (once every rank has joined, every rank has the board mapped: rank 0 removes its name below, so a job that
-      // dies leaves nothing in /dev/shm)
-      for (int c = 0; c < kIpcChans; ++c)
-        for (int k = 0; k < kIpcRing; ++k) {
-          TRY(hip_check(hipIpcOpenEventHandle(&pready[p][c * kIpcRing + k], b->rank[p].ready[c][k]),
-                        "hipIpcOpenEventHandle"));
-          TRY(hip_check(hipIpcOpenEventHandle(&prdone[p][c * kIpcRing + k], b->rank[p].rdone[c][k]),
-                        "hipIpcOpenEventHandle"));
-        }
+      const IpcRank& pr = b->rank[p];
+      TRY(ipc_spin([&] { return pr.evgen[c][g % 2].load(std::memory_order_acquire) == g + 1; },
+                   "a peer's events", rank));
+      IpcEvents& e = peer[p][c * 2 + g % 2];
+      release(e, retired);
+      for (int k = 0; k < kIpcRing; ++k) {
+        TRY(hip_check(hipIpcOpenEventHandle(&e.ready[k], pr.ready[c][g % 2][k]), "hipIpcOpenEventHandle"));
+        TRY(hip_check(hipIpcOpenEventHandle(&e.rdone[k], pr.rdone[c][g % 2][k]), "hipIpcOpenEventHandle"));
+      }
+    }
+    if (retired.size() >= kIpcReap) {  // this rank's streams may still hold records of, or waits on, them
+      TRY(hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize"));
+      for (hipEvent_t e : retired) TRY(hip_check(hipEventDestroy(e), "hipEventDestroy"));
+      retired.clear();
     }
     return 0;
   }
+  static uint64_t gen_of(uint64_t s) { return (s - 1) / kIpcGenOps; }
+  const IpcEvents& mine_of(int c, uint64_t s) const { return mine[c][gen_of(s) % 2]; }
+  const IpcEvents& peer_of(int c, uint64_t s, int p) const { return peer[p][c * 2 + gen_of(s) % 2]; }
 
   // the IPC handle of the allocation holding `ptr`, and ptr's offset in it
   int handle_of(const void* ptr, hipIpcMemHandle_t* h, uint64_t* off) {
@@ -395,6 +439,10 @@ struct IpcDist final : omr_dist {
   int begin(int c, hipStream_t st, const std::vector<std::pair<uint32_t, Slice>>& items, uint64_t* s_out) {
     const uint64_t s = ++seq[c];
     const int k = static_cast<int>(s % kIpcRing);
+    if (s > 1 && (s - 1) % kIpcGenOps == 0) {  // entering generation g: post g + 1, open the peers' g
+      TRY(publish(c, gen_of(s) + 1));
+      TRY(open_gen(c, gen_of(s)));
+    }
     IpcPost& P = b->post[c][k][rank];
     P.nent = P.nh = 0;
     for (const auto& it : items) {
@@ -411,7 +459,7 @@ struct IpcDist final : omr_dist {
       }
       P.e[P.nent++] = IpcEntry{it.first, hi, off, it.second.bytes};
     }
-    TRY(hip_check(hipEventRecord(ready[c][k], st), "hipEventRecord"));
+    TRY(hip_check(hipEventRecord(mine_of(c, s).ready[k], st), "hipEventRecord"));
     b->rank[rank].posted[c].store(s, std::memory_order_release);
     for (int p = 0; p < world; ++p)
       TRY(ipc_spin([&] { return b->rank[p].posted[c].load(std::memory_order_acquire) >= s; }, "a peer's post",
@@ -421,18 +469,18 @@ struct IpcDist final : omr_dist {
   }
   // st waits until peer p's offered pieces are ready on the device
   int wait_ready(int c, uint64_t s, int p, hipStream_t st) {
-    return hip_check(hipStreamWaitEvent(st, pready[p][c * kIpcRing + s % kIpcRing], 0), "hipStreamWaitEvent");
+    return hip_check(hipStreamWaitEvent(st, peer_of(c, s, p).ready[s % kIpcRing], 0), "hipStreamWaitEvent");
   }
   // this rank is through reading its peers; st then waits until every peer is through reading this rank
   int end(int c, uint64_t s, hipStream_t st) {
     const int k = static_cast<int>(s % kIpcRing);
-    TRY(hip_check(hipEventRecord(rdone[c][k], st), "hipEventRecord"));
+    TRY(hip_check(hipEventRecord(mine_of(c, s).rdone[k], st), "hipEventRecord"));
     b->rank[rank].done[c].store(s, std::memory_order_release);
     for (int p = 0; p < world; ++p) {
       if (p == rank) continue;
       TRY(ipc_spin([&] { return b->rank[p].done[c].load(std::memory_order_acquire) >= s; }, "a peer's copies",
                    rank));
-      TRY(hip_check(hipStreamWaitEvent(st, prdone[p][c * kIpcRing + k], 0), "hipStreamWaitEvent"));
+      TRY(hip_check(hipStreamWaitEvent(st, peer_of(c, s, p).rdone[k], 0), "hipStreamWaitEvent"));
     }
     return 0;
   }

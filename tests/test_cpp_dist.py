@@ -365,6 +365,18 @@ def test_servers_are_aggregators_bulk(gpu, tmp_path, m, naggs):
         assert f"Number of aggregators: {naggs}; Number of workers is {m}; My ID is {j}" in out
 
 
+def test_servers_clients_reference_round_count(gpu, tmp_path):
+    """The reference's own warm-up / round counts (client.cc: 10 + 101 rounds) over the IPC transport, the CHECK on:
+    every event of the transport is recorded far more often than the ~32 records one ROCm IPC event survives, so
+    this pins the transport's event generations (csrc/omr_dist.hip, IpcDist)."""
+    srv, cli = _run_servers_clients(2, 1, ["-n", str(1 << 20), "-r", "0.095", "-W", "10", "-R", "101", "-c"],
+                                    tmp_path)
+    for rc, out in cli + srv:
+        assert rc == 0 and "test result is 0" in out, out
+    for rc, out in cli:
+        assert "check OK" in out, out
+
+
 def _expected_trace(bufs, flags, n, B, L, naggs, worker):
     """The records worker `worker` sends and receives, in the client's -T order, from the oracle's literal state
     machines; aggregator of slot gs = 100 + gs % naggs (common.cc:381-383)."""
