@@ -907,8 +907,16 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     for (hipEvent_t* e : {&st.scanned, &st.planned, &st.ready, &st.done})
       A(hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate"));
   }
-  A(hip_check(hipStreamCreateWithFlags(&p->ps, hipStreamNonBlocking), "hipStreamCreate"));
-  A(hip_check(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking), "hipStreamCreate"));
+  {
+    // OMR_SIDE_PRIORITY (study knob): 1 = the plan and communication streams at the device's greatest priority, so
+    // their short kernels are dispatched ahead of the caller's scan workgroups; 0 = normal priority
+    const char* pe = getenv("OMR_SIDE_PRIORITY");
+    int least = 0, greatest = 0;
+    A(hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange"));
+    const int prio = (pe != nullptr && atoi(pe) != 0) ? greatest : least;
+    A(hip_check(hipStreamCreateWithPriority(&p->ps, hipStreamNonBlocking, prio), "hipStreamCreate"));
+    A(hip_check(hipStreamCreateWithPriority(&p->cs, hipStreamNonBlocking, prio), "hipStreamCreate"));
+  }
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, hipEventDisableTiming), "hipEventCreate"));
   A(dev_alloc(&p->bounds_dev, NA + 1));
   if (N > 1 && p->shard >= 0) A(dev_alloc(&p->recv, static_cast<size_t>(M) * p->shard_nb * block_size));
