@@ -897,6 +897,10 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   auto A = [&](int r) {
     if (rc == 0) rc = r;
   };
+  // the round's events order work between streams of this device only: no system-scope fence (a record costs
+  // its stream 1.2 us instead of 2.8, tools/event_cost.hip); what the host reads goes out as system-scope stores
+  const char* sf = getenv("OMR_EVENT_SYSFENCE");
+  const unsigned evflags = hipEventDisableTiming | ((sf != nullptr && atoi(sf) != 0) ? 0u : hipEventDisableSystemFence);
   for (auto& st : p->set) {
     A(dev_alloc(&st.own, p->rows));
     A(dev_alloc(&st.masks_all, static_cast<size_t>(N) * p->rows));
@@ -905,7 +909,7 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     A(dev_alloc(&st.prefix, static_cast<size_t>(M + 1) * (p->rows + 1)));
     if (N > 1 && p->worker()) A(dev_alloc(&st.packed, n));
     for (hipEvent_t* e : {&st.scanned, &st.planned, &st.ready, &st.done})
-      A(hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate"));
+      A(hip_check(hipEventCreateWithFlags(e, evflags), "hipEventCreate"));
   }
   {
     // OMR_SIDE_PRIORITY (study knob): 1 = the plan and communication streams at the device's greatest priority, so
@@ -917,7 +921,7 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     A(hip_check(hipStreamCreateWithPriority(&p->ps, hipStreamNonBlocking, prio), "hipStreamCreate"));
     A(hip_check(hipStreamCreateWithPriority(&p->cs, hipStreamNonBlocking, prio), "hipStreamCreate"));
   }
-  A(hip_check(hipEventCreateWithFlags(&p->st_ev, hipEventDisableTiming), "hipEventCreate"));
+  A(hip_check(hipEventCreateWithFlags(&p->st_ev, evflags), "hipEventCreate"));
   A(dev_alloc(&p->bounds_dev, NA + 1));
   if (N > 1 && p->shard >= 0) A(dev_alloc(&p->recv, static_cast<size_t>(M) * p->shard_nb * block_size));
   A(dev_alloc(&p->results, n));

@@ -3,6 +3,8 @@
 // launch: nothing; an event record; an event record that stream B waits on before a small kernel; a device flag
 // the kernel itself sets that stream B's small kernel spins on; hipStreamWriteValue32 / hipStreamWaitValue32.
 // Prints the period of stream A per variant.
+// Then the same record / wait with events created hipEventDisableSystemFence, and stream A waiting each iteration on
+// an event of stream B that has long completed (the scan's wait for the plan three rounds back).
 //   hipcc --offload-arch=gfx950 -O3 -o build/event_cost tools/event_cost.hip && build/event_cost
 #include <hip/hip_runtime.h>
 
@@ -65,13 +67,16 @@ int main() {
   hipStream_t a, b;
   CK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&b, hipStreamNonBlocking));
-  hipEvent_t ev[4];
+  hipEvent_t ev[4], evf[4];
   for (auto& e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : evf) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
   const int iters = 200;
   const char* names[] = {"kernel only", "+ event record", "+ record, stream B waits + small kernel",
-                         "+ kernel-set flag, stream B spin kernel", "+ hipStreamWriteValue32 / WaitValue32"};
+                         "+ kernel-set flag, stream B spin kernel", "+ hipStreamWriteValue32 / WaitValue32",
+                         "+ event record (no system fence)", "+ record, stream B waits + small kernel (no sys fence)",
+                         "+ stream A waits a completed event of B", "+ stream A waits a completed event of B (no sys fence)"};
   unsigned seq = 0;
-  for (int v = 0; v < 5; ++v) {
+  for (int v = 0; v < 9; ++v) {
     for (int rep = 0; rep < 2; ++rep) {
       CK(hipDeviceSynchronize());
       const auto t0 = std::chrono::steady_clock::now();
@@ -82,6 +87,17 @@ int main() {
         if (v == 2) {
           CK(hipStreamWaitEvent(b, ev[i % 4], 0));
           k_small<<<1, 64, 0, b>>>(y);
+        }
+        if (v == 5 || v == 6) CK(hipEventRecord(evf[i % 4], a));
+        if (v == 6) {
+          CK(hipStreamWaitEvent(b, evf[i % 4], 0));
+          k_small<<<1, 64, 0, b>>>(y);
+        }
+        if (v == 7 || v == 8) {  // B recorded its event long ago (three iterations back); A waits on it
+          hipEvent_t* E = v == 7 ? ev : evf;
+          if (i >= 3) CK(hipStreamWaitEvent(a, E[(i - 3) % 4], 0));
+          k_small<<<1, 64, 0, b>>>(y);
+          CK(hipEventRecord(E[i % 4], b));
         }
         if (v == 3) k_spin<<<1, 64, 0, b>>>(flag, seq, y);
         if (v == 4) {
