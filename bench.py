@@ -304,17 +304,24 @@ def main():
         pipe = "sync" if args.dist_sync else args.dist_pipe
         pipelined = pipe != "sync"
 
-        def step(i, ev=None):
+        host_s = [0.0, 0]  # host time inside engine.run over the timed steps, and their count
+
+        def step(i, ev=None, timed_region=False):
             xs, out = sets[i % len(sets)]
-            # a timed step (ev given) brackets its worker scan and its exchange with HIP events on the streams they
-            # run on, inside the timed region (omr_ar_plan_timings)
+            # a timed step (ev given) brackets each stage of its round (worker scan, bookkeeping, exchange,
+            # aggregation) with HIP events on the streams they run on, inside the timed region
+            # (omr_ar_plan_stage_timings)
+            h0 = time.perf_counter()
             engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
                        async_=pipelined, defer=pipe == "defer", time_exchange=ev is not None)
+            if timed_region:
+                host_s[0] += time.perf_counter() - h0
+                host_s[1] += 1
     else:
         fused = m == 1 and args.kernel == "fused"
         plan = ops.ScanSumPlan(L, m, device=dev, fused=fused)
 
-        def step(i, ev=None):
+        def step(i, ev=None, timed_region=False):
             xs, out = sets[i % len(sets)]
             if m == 1:
                 out = xs[0]  # in place, as the reference returns results into res->buf (client.cc:89)
@@ -347,7 +354,7 @@ def main():
     if one_kernel:
         span[0].record(stream)
     for i in range(args.steps):
-        step(args.warmup + i, None if one_kernel else (kev[i] if i % every == 0 else None))
+        step(args.warmup + i, None if one_kernel else (kev[i] if i % every == 0 else None), timed_region=True)
     if one_kernel:
         span[1].record(stream)
     join()
@@ -372,7 +379,8 @@ def main():
     if dist_mode:
         # the timed rounds' own events (every `every`-th timed step): its worker scan kernel on the caller's stream,
         # its worker -> aggregator exchange on the stream it ran on
-        scan_ms_dist, x_ms, b_out, b_in, n_timed = engine.timings()
+        stages, b_out, b_in, n_timed = engine.stage_timings()
+        scan_ms_dist, x_ms = stages["scan"], stages["exchange"]
         exchange = {"ms_mean": round(x_ms, 5), "bytes_out_per_rank": int(b_out), "bytes_in_per_rank": int(b_in),
                     "peers": ws - 1, "timed_rounds": n_timed,
                     "GBps_out_per_rank": round(b_out / (x_ms * 1e-3) / 1e9, 2) if x_ms > 0 else None,
@@ -381,7 +389,11 @@ def main():
                                           if x_ms > 0 and ws > 1 else None),
                     "xgmi_link_GBps_nominal": XGMI_LINK_GBPS,
                     "timing": (f"HIP events around the worker -> aggregator exchange ({'grouped ncclSend/ncclRecv, dense: ncclReduceScatter' if not ipc else 'the IPC transport copies'}) on the "
-                               f"stream it runs on, in every {every}th timed round (inside the timed region), rank 0")}
+                               f"stream it runs on, in every {every}th timed round (inside the timed region), rank 0"),
+                    # where a round's time goes (rank 0): each stage's mean from events on its own stream, and the
+                    # host time of one engine.run call (a round is host-bound when that exceeds ms_per_step)
+                    "stages_ms": {k: round(v, 5) for k, v in stages.items()},
+                    "host_ms_per_call": round(host_s[0] / max(1, host_s[1]) * 1e3, 5)}
     if not dist_mode:
         kev = kev[::every]
     if one_kernel:  # every step is exactly one k_scan1f launch: events around all K steps, divided by K

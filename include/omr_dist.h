@@ -147,6 +147,16 @@ int omr_sparse_buckets_f32(omr_ar_plan* plan, float* buf, uint64_t total_n, int 
  * per rank; *rounds = how many rounds were timed.  Waits for those rounds' events. */
 int omr_ar_plan_timings(omr_ar_plan* plan, float* scan_ms, float* exchange_ms, uint64_t* bytes_out, uint64_t* bytes_in,
                         uint32_t* rounds);
+/* As omr_ar_plan_timings, per stage of the timed rounds: stage_ms[OMR_ROUND_STAGES] = the means of
+ *   [0] the worker scan (the caller's stream),
+ *   [1] the bookkeeping: mask all-gather, plan (+ aggregator chain), pack (the plan stream when asynchronous),
+ *   [2] the worker -> aggregator exchange,
+ *   [3] the aggregation after it: shard sums [, sums back to the workers, unpack] (the communication stream),
+ * each from HIP events on the stream it runs on (a stage's time includes what that stream does meanwhile, e.g. a
+ * transport's waits). */
+#define OMR_ROUND_STAGES 4
+int omr_ar_plan_stage_timings(omr_ar_plan* plan, float* stage_ms, uint64_t* bytes_out, uint64_t* bytes_in,
+                              uint32_t* rounds);
 /* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
 int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
 

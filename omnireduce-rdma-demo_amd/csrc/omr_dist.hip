@@ -697,8 +697,10 @@ struct omr_ar_plan {
   // every OMR_ROUND_TIME_EXCHANGE round also lands in a ring: its worker scan and its exchange, for means over the
   // timed rounds (omr_ar_plan_timings)
   struct Timed {
-    hipEvent_t s0 = nullptr, s1 = nullptr, x0 = nullptr, x1 = nullptr;
-    bool scan = false, xchg = false;
+    // s: worker scan (caller's stream); q: all-gather .. pack (bookkeeping stream); x: exchange, x1 .. a1: shard
+    // sums [, sums back, unpack] (communication stream)
+    hipEvent_t s0 = nullptr, s1 = nullptr, x0 = nullptr, x1 = nullptr, q0 = nullptr, q1 = nullptr, a1 = nullptr;
+    bool scan = false, xchg = false, prep = false, agg = false;
     uint64_t out = 0, in = 0;
   };
   static constexpr int kTimed = 64;
@@ -973,8 +975,9 @@ int timed_slot(omr_ar_plan* p, int* slot) {
   if (p->timed_next - p->timed_first > omr_ar_plan::kTimed) p->timed_first = p->timed_next - omr_ar_plan::kTimed;
   omr_ar_plan::Timed& t = p->timed[k];
   if (t.s0 == nullptr)
-    for (hipEvent_t* e : {&t.s0, &t.s1, &t.x0, &t.x1}) TRY(hip_check(hipEventCreate(e), "hipEventCreate"));
-  t.scan = t.xchg = false;
+    for (hipEvent_t* e : {&t.s0, &t.s1, &t.x0, &t.x1, &t.q0, &t.q1, &t.a1})
+      TRY(hip_check(hipEventCreate(e), "hipEventCreate"));
+  t.scan = t.xchg = t.prep = t.agg = false;
   *slot = k;
   return 0;
 }
@@ -1102,6 +1105,10 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, S.wset, S.prefix + static_cast<uint64_t>(M) * (rows + 1),
                                         rows, p->lanes, p->B, 0, 0, xstream), "omr_move_blocks_f32 unpack"));
   }
+  if (timed && p->timed[tslot].xchg) {
+    TRY(hip_check(hipEventRecord(p->timed[tslot].a1, xs), "hipEventRecord"));
+    p->timed[tslot].agg = true;
+  }
   if (async) {
     TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
     S.pending = true;
@@ -1225,6 +1232,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   }
   // 2. every worker's row masks
   p->ht.lap("1:refill wait");
+  if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].q0, qs), "hipEventRecord"));
   TRY(p->d->allgather(S.own, S.masks_all, rows * sizeof(uint64_t), qs));
   p->ht.lap("1:allgather");
   // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for its next round
@@ -1249,6 +1257,10 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
     TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * rows,
                                       S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
                                       r1, qstream), "omr_move_blocks_f32 pack"));
+  }
+  if (timed) {
+    TRY(hip_check(hipEventRecord(p->timed[tslot].q1, qs), "hipEventRecord"));
+    p->timed[tslot].prep = true;
   }
   p->ht.lap("1:pack");
   // the rest goes on the communication stream for an asynchronous round, behind everything queued so far
@@ -1408,36 +1420,46 @@ int omr_ar_plan_exchange_time(omr_ar_plan* p, float* ms, uint64_t* bytes_out, ui
   return 0;
 }
 
-int omr_ar_plan_timings(omr_ar_plan* p, float* scan_ms, float* exchange_ms, uint64_t* bytes_out, uint64_t* bytes_in,
-                        uint32_t* rounds) {
-  if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_timings: NULL");
-  double ss = 0, xs = 0;
+int omr_ar_plan_stage_timings(omr_ar_plan* p, float* stage_ms, uint64_t* bytes_out, uint64_t* bytes_in,
+                              uint32_t* rounds) {
+  if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_stage_timings: NULL");
+  double sum[OMR_ROUND_STAGES] = {0, 0, 0, 0};
+  uint32_t cnt[OMR_ROUND_STAGES] = {0, 0, 0, 0};
   uint64_t bo = 0, bi = 0;
-  uint32_t ns = 0, nx = 0;
+  auto add = [&](int k, hipEvent_t a, hipEvent_t b) -> int {
+    float ms = 0;
+    TRY(hip_check(hipEventSynchronize(b), "hipEventSynchronize"));
+    TRY(hip_check(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime"));
+    sum[k] += ms;
+    ++cnt[k];
+    return 0;
+  };
   for (uint32_t i = p->timed_first; i < p->timed_next; ++i) {
     omr_ar_plan::Timed& t = p->timed[i % omr_ar_plan::kTimed];
-    float ms = 0;
-    if (t.scan) {
-      TRY(hip_check(hipEventSynchronize(t.s1), "hipEventSynchronize"));
-      TRY(hip_check(hipEventElapsedTime(&ms, t.s0, t.s1), "hipEventElapsedTime"));
-      ss += ms;
-      ++ns;
-    }
+    if (t.scan) TRY(add(0, t.s0, t.s1));
+    if (t.prep) TRY(add(1, t.q0, t.q1));
     if (t.xchg) {
-      TRY(hip_check(hipEventSynchronize(t.x1), "hipEventSynchronize"));
-      TRY(hip_check(hipEventElapsedTime(&ms, t.x0, t.x1), "hipEventElapsedTime"));
-      xs += ms;
+      TRY(add(2, t.x0, t.x1));
       bo += t.out;
       bi += t.in;
-      ++nx;
     }
+    if (t.agg) TRY(add(3, t.x1, t.a1));
   }
   p->timed_first = p->timed_next;
-  if (scan_ms) *scan_ms = ns ? static_cast<float>(ss / ns) : 0.f;
-  if (exchange_ms) *exchange_ms = nx ? static_cast<float>(xs / nx) : 0.f;
-  if (bytes_out) *bytes_out = nx ? bo / nx : 0;
-  if (bytes_in) *bytes_in = nx ? bi / nx : 0;
-  if (rounds) *rounds = nx > ns ? nx : ns;
+  if (stage_ms)
+    for (int k = 0; k < OMR_ROUND_STAGES; ++k) stage_ms[k] = cnt[k] ? static_cast<float>(sum[k] / cnt[k]) : 0.f;
+  if (bytes_out) *bytes_out = cnt[2] ? bo / cnt[2] : 0;
+  if (bytes_in) *bytes_in = cnt[2] ? bi / cnt[2] : 0;
+  if (rounds) *rounds = std::max(cnt[0], cnt[2]);
+  return 0;
+}
+
+int omr_ar_plan_timings(omr_ar_plan* p, float* scan_ms, float* exchange_ms, uint64_t* bytes_out, uint64_t* bytes_in,
+                        uint32_t* rounds) {
+  float ms[OMR_ROUND_STAGES];
+  TRY(omr_ar_plan_stage_timings(p, ms, bytes_out, bytes_in, rounds));
+  if (scan_ms) *scan_ms = ms[0];
+  if (exchange_ms) *exchange_ms = ms[2];
   return 0;
 }
 

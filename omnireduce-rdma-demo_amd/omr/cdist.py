@@ -58,6 +58,7 @@ def load():
         "omr_msgd_logs": (i, [vp, u32, vp, vp, vp, vp, vp, vp]),
         "omr_ar_plan_exchange_time": (i, [vp, vp, vp, vp]),
         "omr_ar_plan_timings": (i, [vp, vp, vp, vp, vp, vp]),
+        "omr_ar_plan_stage_timings": (i, [vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -187,6 +188,17 @@ class CppSparseAllreduce:
         _check(load().omr_ar_plan_timings(self._p, ctypes.byref(sm), ctypes.byref(xm), ctypes.byref(bo),
                                           ctypes.byref(bi), ctypes.byref(n)), "omr_ar_plan_timings")
         return sm.value, xm.value, bo.value, bi.value, n.value
+
+    STAGES = ("scan", "bookkeeping", "exchange", "aggregate")
+
+    def stage_timings(self):
+        """As timings(), per stage (omr_ar_plan_stage_timings): ({stage: mean ms} over STAGES, bytes out per rank,
+        bytes in per rank, timed rounds)."""
+        ms = (ctypes.c_float * len(self.STAGES))()
+        bo, bi, n = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint32()
+        _check(load().omr_ar_plan_stage_timings(self._p, ms, ctypes.byref(bo), ctypes.byref(bi), ctypes.byref(n)),
+               "omr_ar_plan_stage_timings")
+        return dict(zip(self.STAGES, list(ms))), bo.value, bi.value, n.value
 
     def join(self, stream=None):
         """Make `stream` (default: the current stream) wait for every asynchronous round issued so far."""

@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--mode", type=int, default=0, help="OMR_ROUND_* (0 all-reduce, 1 reduce-scatter, 2 dense)")
     ap.add_argument("--pipe", choices=("sync", "async", "defer"), default="sync")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--cycle", type=int, default=0,
+                    help="round r runs input (and output buffer) r mod cycle (0: one of each per round); a long run "
+                         "thus reuses its buffers as a training loop does")
     ap.add_argument("--workers", type=int, default=0, help="ranks >= this are dedicated aggregators (0: all workers)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
@@ -37,8 +40,9 @@ def main():
                                    num_workers=nw)
     worker = a.rank < nw
     # a different input per round (seed = rank, round): the pipelined rounds must not mix their buffers
+    K = a.cycle or a.rounds
     xs, outs = [], []
-    for r in range(a.rounds):
+    for r in range(K):
         if worker:
             x = oracle.fill(oracle.gen_bitmap(a.rank + 10 * r, a.density, L.nb), a.block, mode=1,
                             seed=a.rank + 7 + 31 * r)
@@ -52,7 +56,7 @@ def main():
     unx = torch.empty(L.nb, dtype=torch.int32, device=dev)
     sums = {}
     for r in range(a.rounds):
-        eng.run(xs[r], out=outs[r], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
+        eng.run(xs[r % K], out=outs[r % K], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
                 async_=a.pipe != "sync", defer=a.pipe == "defer")
         if not worker and a.pipe == "sync":  # a dedicated aggregator's shard sums of this round
             torch.cuda.synchronize()
@@ -66,7 +70,7 @@ def main():
     arrs = dict(flags=flags.cpu().numpy(), next=nxt.cpu().numpy().view(np.uint32),
                 unext=unx.cpu().numpy().view(np.uint32), **sums)
     if worker:
-        arrs.update({f"out{r}": outs[r].cpu().numpy() for r in range(a.rounds)})
+        arrs.update({f"out{r}": outs[r].cpu().numpy() for r in range(K)})
     np.savez(a.out, **arrs)
     eng.close()
     print(f"rank {a.rank} ok", flush=True)
