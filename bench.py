@@ -72,11 +72,13 @@ def parse():
                    help="N>1 step: workers -> aggregators reduce-scatter (BASELINE config 4, default), the full "
                         "all-reduce (sums back to every worker), or the dense stand-in (ncclReduceScatter of the "
                         "whole tensor, C++ driver only)")
-    p.add_argument("--dist-pipe", choices=("sync", "async", "defer"), default="defer",
+    p.add_argument("--dist-pipe", choices=("sync", "async", "defer", "thread"), default="defer",
                    help="N>1, C++ driver: sync = each round's exchange on the caller's stream; async "
                         "(OMR_ROUND_ASYNC) = round k's exchange over xGMI overlaps round k+1's worker scan; defer "
                         "(OMR_ROUND_DEFER, default) = as async, and round k's exchange is issued after round k+1's "
-                        "first half is queued, so the host never waits for block counts with the GPU idle")
+                        "first half is queued, so the host never waits for block counts with the GPU idle; thread "
+                        "(OMR_ROUND_THREAD | OMR_ROUND_DEFER) = as defer, with everything after the worker scan "
+                        "issued by the plan's progress thread")
     p.add_argument("--dist-sync", action="store_true", help="same as --dist-pipe sync")
     p.add_argument("--dist-transport", choices=("rccl", "ipc"), default="rccl",
                    help="N>1 round transport: RCCL over xGMI, one process per GPU (the product path), or HIP IPC "
@@ -313,7 +315,8 @@ def main():
             # (omr_ar_plan_stage_timings)
             h0 = time.perf_counter()
             engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
-                       async_=pipelined, defer=pipe == "defer", time_exchange=ev is not None)
+                       async_=pipelined, defer=pipe in ("defer", "thread"), thread=pipe == "thread",
+                       time_exchange=ev is not None)
             if timed_region:
                 host_s[0] += time.perf_counter() - h0
                 host_s[1] += 1
@@ -438,7 +441,10 @@ def main():
     pipe_note = ""
     if dist_mode and pipe != "sync":
         pipe_note = (", rounds pipelined: exchange k beside scan k+1" +
-                     (", exchange k issued after round k+1's first half (OMR_ROUND_DEFER)" if pipe == "defer" else ""))
+                     (", exchange k issued after round k+1's first half (OMR_ROUND_DEFER)"
+                      if pipe in ("defer", "thread") else "") +
+                     (", steps after the scan issued by a progress thread (OMR_ROUND_THREAD)" if pipe == "thread"
+                      else ""))
     transport_note = ("RCCL" if not ipc else
                       f"HIP IPC, {ws} ranks on {torch.cuda.device_count()} GPU(s): a rehearsal of the N>1 path, not a "
                       f"scaling figure")

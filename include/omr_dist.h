@@ -126,6 +126,16 @@ int omr_sparse_allreduce_f32(omr_ar_plan* plan, const float* x, float* out, int3
  * round whose exchange this call issued (0 if none).  Every rank must use the same sequence of modes; join (or a non-deferred call) before
  * reading `out` or destroying the plan (destroy issues a pending exchange and synchronises the device). */
 #define OMR_ROUND_DEFER 0x400
+/* OR-ed into `mode` (implies OMR_ROUND_ASYNC; combines with OMR_ROUND_DEFER): the call only queues the worker scan
+ * on `stream`.  A progress thread of the plan then issues everything else (steps 2-7 above, every host API call and
+ * transport call of the round) in call order, so the host cost of a round is split over two cores.  The round's
+ * stream order, results and buffer rules are those of OMR_ROUND_ASYNC / OMR_ROUND_DEFER.  *sent_blocks /
+ * *union_blocks receive 0: the counts are not known when the call returns.  A call runs at most two rounds
+ * ahead of the thread.  An error in the thread is returned by the next call on the plan (and by omr_ar_plan_join).
+ * Calls without this flag, omr_ar_plan_join, the timing reads and omr_ar_plan_shard first wait until the thread
+ * has issued every queued round.  Transports are driven from the thread: RCCL, the IPC and the loopback
+ * transports all allow it. */
+#define OMR_ROUND_THREAD 0x800
 int omr_sparse_round_f32(omr_ar_plan* plan, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
                          uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
                          omr_stream_t stream);

@@ -21,9 +21,11 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -727,6 +729,27 @@ struct omr_ar_plan {
   hipStream_t last_st = nullptr;
   hipEvent_t st_ev = nullptr;
   HostTrace ht;
+  // OMR_ROUND_THREAD: a progress thread issues each round's steps after the worker scan, in call order.  The
+  // calling thread queues the scan, then a job; it runs at most kSets - 1 rounds ahead of the thread's first halves
+  // (a set's `planned` / `scanned` events must have been recorded / waited for before the set is reused).
+  struct Job {
+    int si = 0, mode = 0, tslot = -1;
+    bool async = false, defer = false, timed = false, flush_first = false;
+    const float* x = nullptr;
+    float* out = nullptr;
+    uint32_t* un = nullptr;
+    hipStream_t st = nullptr;
+  };
+  int device = 0;
+  std::thread progress;
+  std::mutex mu;
+  std::condition_variable cv_job, cv_done;
+  std::deque<Job> jobs;
+  uint64_t rounds_begun = 0, first_halves = 0;  // rounds whose scan is queued / whose bookkeeping is issued
+  bool busy = false, stop = false;
+  int thread_rc = 0;
+  std::string thread_err;
+  HostTrace ht_thread;
   // omr_sparse_buckets_f32 on a pinned-host gradient: a ring of device staging buckets and two copy streams
   static constexpr int kStage = 3;
   float* stage[kStage] = {nullptr, nullptr, nullptr};
@@ -737,6 +760,10 @@ struct omr_ar_plan {
 
 namespace {
 int flush_pending(omr_ar_plan* p, hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks);
+int thread_drain(omr_ar_plan* p);
+void thread_stop(omr_ar_plan* p);
+thread_local bool t_progress = false;  // this thread is a plan's progress thread (OMR_ROUND_THREAD)
+HostTrace& ht_of(omr_ar_plan* p) { return t_progress ? p->ht_thread : p->ht; }
 }  // namespace
 
 extern "C" {
@@ -822,7 +849,13 @@ int omr_dist_destroy(omr_dist* d) {
 
 int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p == nullptr) return 0;
+  (void)thread_drain(p);
+  thread_stop(p);
   if (p->ht.on) p->ht.print(p->me);
+  if (p->ht_thread.on && !p->ht_thread.acc.empty()) {
+    fprintf(stderr, "[omr host trace rank %d] progress thread:\n", p->me);
+    p->ht_thread.print(p->me);
+  }
   if (p->npend > 0) {  // deferred rounds still owe their exchanges to the peers: issue them and let them drain
     (void)flush_pending(p, p->cs, nullptr, nullptr);
     (void)hipDeviceSynchronize();
@@ -846,7 +879,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p->s_out) (void)hipStreamDestroy(p->s_out);
   if (p->st_ev) (void)hipEventDestroy(p->st_ev);
   for (auto& t : p->timed)
-    for (hipEvent_t e : {t.s0, t.s1, t.x0, t.x1})
+    for (hipEvent_t e : {t.s0, t.s1, t.x0, t.x1, t.q0, t.q1, t.a1})
       if (e) (void)hipEventDestroy(e);
   (void)hipHostFree(p->counts_host);
   (void)hipHostFree(p->flag_host);
@@ -1001,12 +1034,12 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
   const uint32_t* counts = p->counts_host + static_cast<size_t>(si) * (M + 1) * NS;
   const uint32_t* flag = p->flag_host + si;
   hipStream_t xs = st;
-  p->ht.start();
+  ht_of(p).start();
   if (async) {
     TRY(hip_check(hipStreamWaitEvent(p->cs, S.ready, 0), "hipStreamWaitEvent"));
     xs = p->cs;
   }
-  p->ht.lap("2:cs wait ready");
+  ht_of(p).lap("2:cs wait ready");
   const omr_stream_t xstream = reinterpret_cast<omr_stream_t>(xs);
   auto cnt = [&](int a, int s) -> uint64_t { return counts[a * NS + s]; };
   auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
@@ -1034,7 +1067,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     return 0;
   }
   TRY(wait_flag(flag, seq, st));
-  p->ht.lap("2:wait counts");
+  ht_of(p).lap("2:wait counts");
   const bool wk = p->worker();
   // a co-located rank keeps its own shard's blocks out of its packed stream (and reads them in place)
   const uint64_t own_shard = (wk && p->colocated) ? per(me, me) : 0;
@@ -1062,7 +1095,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       }
     TRY(p->d->exchange(sends, recvs, xs));
   }
-  p->ht.lap("2:exchange");
+  ht_of(p).lap("2:exchange");
   if (timed) {
     TRY(hip_check(hipEventRecord(p->timed[tslot].x1, xs), "hipEventRecord"));
     p->xt_out = total_send * B * sizeof(float);
@@ -1086,7 +1119,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
                   "omr_shard_sum_f32"));
     if (!p->colocated) p->last_sums_blocks = per(M, sh);
   }
-  p->ht.lap("2:shard sum");
+  ht_of(p).lap("2:shard sum");
   if (!rs_mode) {
     // 6. sums back to every worker (server.cc:162), scattered in place (client.cc:89)
     if (N > 1) {
@@ -1114,7 +1147,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     S.pending = true;
     p->last_async = si;
   }
-  p->ht.lap("2:rest");
+  ht_of(p).lap("2:rest");
   if (sent_blocks) *sent_blocks = total_send;
   if (union_blocks) *union_blocks = (rs_mode || !wk) ? (sh >= 0 ? per(M, sh) : 0) : cnt(M, NA);
   return 0;
@@ -1137,104 +1170,43 @@ int flush_pending(omr_ar_plan* p, hipStream_t st, uint64_t* sent_blocks, uint64_
   return 0;
 }
 
-}  // namespace
+// (event waits are skipped when the host already sees the event complete: a stream-wait packet costs the GPU a
+// few microseconds of dispatch even when its event has long fired)
+int wait_ev(hipStream_t on, hipEvent_t ev) {
+  const hipError_t q = hipEventQuery(ev);
+  if (q == hipErrorNotReady) return hip_check(hipStreamWaitEvent(on, ev, 0), "hipStreamWaitEvent");
+  return hip_check(q, "hipEventQuery");
+}
 
-extern "C" {
-
-// One round (DESIGN.md §5): scan -> mask all-gather -> one bookkeeping launch -> block counts to the host (the
-// round's single mid-round sync: the transport needs host-side sizes) -> pack -> send/recv -> shard sums
-// [-> sums back -> unpack].  Every block movement is addressed by masks and prefixes.
-int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
-                         uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
-                         omr_stream_t stream) {
-  if (p == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL plan");
-  if (p->worker() && (x == nullptr || out == nullptr)) return derr(OMR_EINVAL, "sparse_round: a worker needs x and out");
-  const bool defer = (mode & OMR_ROUND_DEFER) != 0;
-  const bool async = defer || (mode & OMR_ROUND_ASYNC) != 0;
-  const bool timed = (mode & OMR_ROUND_TIME_EXCHANGE) != 0;
-  mode &= ~(OMR_ROUND_ASYNC | OMR_ROUND_DEFER | OMR_ROUND_TIME_EXCHANGE);
-  if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
-    return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
-  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && !p->colocated)
-    return derr(OMR_EINVAL, "sparse_round: the dense reduce-scatter stand-in needs every rank to be a worker");
-  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && p->rows % p->N != 0)
-    return derr(OMR_EINVAL, "sparse_round: dense reduce-scatter needs equal shards (rows %llu, world %d)",
-                static_cast<unsigned long long>(p->rows), p->N);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int N = p->N, M = p->M, me = p->me;
+// Steps 2-7 of a round whose worker scan (and, when asynchronous, its `scanned` record) is queued: on the calling
+// thread, or on the progress thread (OMR_ROUND_THREAD) in call order.
+int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks, uint64_t* union_blocks) {
+  HostTrace& ht = ht_of(p);
+  if (t_progress) ht.start();
+  const int si = j.si, mode = j.mode, tslot = j.tslot, M = p->M, me = p->me, N = p->N;
+  const bool async = j.async, timed = j.timed;
   const uint64_t rows = p->rows;
   const uint32_t NS = static_cast<uint32_t>(p->A + 1);
-  p->ht.start();
-  int32_t* fl = flags ? flags : p->flags_ws;
-  uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
-  uint32_t* un = union_next ? union_next : p->unext_ws;
-  // a stream other than the previous round's starts behind it (plan-wide state is shared by every round)
-  if (p->last_st != nullptr && p->last_st != st) {
-    TRY(hip_check(hipEventRecord(p->st_ev, p->last_st), "hipEventRecord"));
-    TRY(hip_check(hipStreamWaitEvent(st, p->st_ev, 0), "hipStreamWaitEvent"));
-  }
-  p->last_st = st;
-  // a round that is not deferred finishes a deferred one first (rounds complete in call order)
-  if (!defer) TRY(flush_pending(p, st, nullptr, nullptr));
-  // a synchronous round after asynchronous ones: its all-gather and exchange go on `stream`, so the plan and
-  // communication streams must be idle first (one communicator is never driven from two streams at once; the
-  // last asynchronous round's `done` follows all of its plan-stream work)
-  if (!async && p->last_async >= 0) {
-    TRY(hip_check(hipStreamWaitEvent(st, p->set[p->last_async].done, 0), "hipStreamWaitEvent"));
-    p->last_async = -1;
-  }
-  const int si = p->cur;
+  const float* x = j.x;
   omr_ar_plan::Set& S = p->set[si];
-  p->cur = (p->cur + 1) % omr_ar_plan::kSets;
+  // a threaded round that is not deferred finishes the deferred ones first (rounds complete in call order)
+  if (j.flush_first) TRY(flush_pending(p, j.st, nullptr, nullptr));
   // the round's bookkeeping stream: an asynchronous round runs it on the plan stream, so the caller's stream is
   // left with the worker scans alone (round k+1's scan overlaps round k's all-gather, plan and pack, and round
   // k-1's exchange)
-  hipStream_t qs = async ? p->ps : st;
+  hipStream_t qs = async ? p->ps : j.st;
   const omr_stream_t qstream = reinterpret_cast<omr_stream_t>(qs);
-  // (event waits are skipped when the host already sees the event complete: a stream-wait packet costs the GPU a
-  // few microseconds of dispatch even when its event has long fired)
-  auto wait_ev = [](hipStream_t on, hipEvent_t ev) -> int {
-    const hipError_t q = hipEventQuery(ev);
-    if (q == hipErrorNotReady) return hip_check(hipStreamWaitEvent(on, ev, 0), "hipStreamWaitEvent");
-    return hip_check(q, "hipEventQuery");
-  };
-  // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass (a dedicated aggregator
-  //    offers its all-zero mask buffer to the all-gather).  The set's own masks must have been consumed and
-  //    re-zeroed by the plan of the round kSets calls back.
-  int tslot = -1;
-  if (timed) TRY(timed_slot(p, &tslot));
-  if (S.plan_pending) {
-    TRY(wait_ev(st, S.planned));
-    S.plan_pending = false;
-  }
-  if (p->worker()) {
-    if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
-    TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, nullptr, p->scan_ws,
-                                      p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
-    if (timed) {
-      TRY(hip_check(hipEventRecord(p->timed[tslot].s1, st), "hipEventRecord"));
-      p->timed[tslot].scan = true;
-    }
-    p->ht.lap("1:scan");
-    if (async) {
-      TRY(hip_check(hipEventRecord(S.scanned, st), "hipEventRecord"));
-      TRY(hip_check(hipStreamWaitEvent(qs, S.scanned, 0), "hipStreamWaitEvent"));
-    }
-    p->ht.lap("1:scan events");
-  } else if (async) {  // nothing to scan: the plan stream starts behind whatever the caller queued before this call
-    TRY(hip_check(hipEventRecord(S.scanned, st), "hipEventRecord"));
-    TRY(hip_check(hipStreamWaitEvent(qs, S.scanned, 0), "hipStreamWaitEvent"));
-  }
+  if (async) TRY(hip_check(hipStreamWaitEvent(qs, S.scanned, 0), "hipStreamWaitEvent"));
   // the rest of the set is refilled from here on: the asynchronous round kSets calls back must be through with it
   if (S.pending) {
     TRY(wait_ev(qs, S.done));
     S.pending = false;
   }
   // 2. every worker's row masks
-  p->ht.lap("1:refill wait");
+  ht.lap("1:refill wait");
   if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].q0, qs), "hipEventRecord"));
   TRY(p->d->allgather(S.own, S.masks_all, rows * sizeof(uint64_t), qs));
-  p->ht.lap("1:allgather");
+  ht.lap("1:allgather");
   // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for its next round
   //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
   const uint32_t seq = ++p->seq;
@@ -1242,13 +1214,13 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   TRY(omr_check(omr_round_plan_chain(S.masks_all, static_cast<uint32_t>(M), rows, p->rpp, p->lanes, p->bounds_dev,
                                      NS, S.wset, S.umask, S.prefix,
                                      p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, p->arrive,
-                                     p->flag_map + si, seq, un, p->B, qstream),
+                                     p->flag_map + si, seq, j.un, p->B, qstream),
                 "omr_round_plan_chain"));
   if (async) {
     TRY(hip_check(hipEventRecord(S.planned, qs), "hipEventRecord"));
     S.plan_pending = true;
   }
-  p->ht.lap("1:plan");
+  ht.lap("1:plan");
   // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407): addressed by
   //     device-side data only, so it is queued before the host learns the counts and runs while it waits.  (Every
   //     host API call costs microseconds; a round that spends them on side streams and events is host-bound.)
@@ -1262,11 +1234,16 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
     TRY(hip_check(hipEventRecord(p->timed[tslot].q1, qs), "hipEventRecord"));
     p->timed[tslot].prep = true;
   }
-  p->ht.lap("1:pack");
+  ht.lap("1:pack");
   // the rest goes on the communication stream for an asynchronous round, behind everything queued so far
   if (async) TRY(hip_check(hipEventRecord(S.ready, qs), "hipEventRecord"));
-  p->ht.lap("1:next+ready");
-  if (!defer) return round_finish(p, si, x, out, mode, async, timed, seq, qs, sent_blocks, union_blocks, tslot);
+  {  // the set's `planned` is recorded and its `scanned` waited for: the caller may reuse it
+    std::lock_guard<std::mutex> g(p->mu);
+    ++p->first_halves;
+  }
+  p->cv_done.notify_all();
+  ht.lap("1:next+ready");
+  if (!j.defer) return round_finish(p, si, x, j.out, mode, async, timed, seq, qs, sent_blocks, union_blocks, tslot);
   // deferred: this round's first half is queued; now issue the exchange of the round kDeferDepth calls back, whose
   // counts have long been in host memory, so the host neither waits nor leaves the caller's stream idle
   omr_ar_plan::Pending& q = p->pend[p->npend++];
@@ -1275,7 +1252,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   q.mode = mode;
   q.timed = timed;
   q.x = x;
-  q.out = out;
+  q.out = j.out;
   q.seq = seq;
   q.tslot = tslot;
   q.st = qs;
@@ -1285,9 +1262,181 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   return 0;
 }
 
+// The progress thread: runs queued rounds' steps 2-7 in call order.  After a failure it records the error and
+// skips the remaining jobs (counting them as issued, so no caller waits on them); calls then return the error.
+void progress_main(omr_ar_plan* p) {
+  t_progress = true;
+  (void)hipSetDevice(p->device);
+  std::unique_lock<std::mutex> lk(p->mu);
+  for (;;) {
+    p->cv_job.wait(lk, [&] { return p->stop || !p->jobs.empty(); });
+    if (p->jobs.empty()) return;  // stop requested, nothing left
+    const omr_ar_plan::Job j = p->jobs.front();
+    p->jobs.pop_front();
+    p->busy = true;
+    const bool failed = p->thread_rc != 0;
+    lk.unlock();
+    const int rc = failed ? 0 : round_rest(p, j, nullptr, nullptr);
+    lk.lock();
+    if (rc != 0) {
+      p->thread_rc = rc;
+      p->thread_err = g_derr;
+    }
+    if (p->thread_rc != 0) p->first_halves = p->rounds_begun;
+    p->busy = false;
+    p->cv_done.notify_all();
+  }
+}
+
+int thread_start(omr_ar_plan* p) {
+  if (p->progress.joinable()) return 0;
+  TRY(hip_check(hipGetDevice(&p->device), "hipGetDevice"));
+  p->ht_thread.on = p->ht.on;
+  try {
+    p->progress = std::thread(progress_main, p);
+  } catch (const std::exception& e) {
+    return derr(OMR_EINVAL, "sparse_round: cannot start the progress thread: %s", e.what());
+  }
+  return 0;
+}
+
+// every queued round issued; returns (and keeps) the progress thread's error, if any
+int thread_drain(omr_ar_plan* p) {
+  if (!p->progress.joinable()) return 0;
+  std::unique_lock<std::mutex> lk(p->mu);
+  p->cv_done.wait(lk, [&] { return p->jobs.empty() && !p->busy; });
+  if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
+  return 0;
+}
+
+void thread_stop(omr_ar_plan* p) {
+  if (!p->progress.joinable()) return;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    p->stop = true;
+  }
+  p->cv_job.notify_one();
+  p->progress.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+// One round (DESIGN.md §5): scan -> mask all-gather -> one bookkeeping launch -> block counts to the host (the
+// round's single mid-round sync: the transport needs host-side sizes) -> pack -> send/recv -> shard sums
+// [-> sums back -> unpack].  Every block movement is addressed by masks and prefixes.
+int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
+                         uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
+                         omr_stream_t stream) {
+  if (p == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL plan");
+  if (p->worker() && (x == nullptr || out == nullptr)) return derr(OMR_EINVAL, "sparse_round: a worker needs x and out");
+  const bool threaded = (mode & OMR_ROUND_THREAD) != 0;
+  const bool defer = (mode & OMR_ROUND_DEFER) != 0;
+  const bool async = threaded || defer || (mode & OMR_ROUND_ASYNC) != 0;
+  const bool timed = (mode & OMR_ROUND_TIME_EXCHANGE) != 0;
+  mode &= ~(OMR_ROUND_ASYNC | OMR_ROUND_DEFER | OMR_ROUND_TIME_EXCHANGE | OMR_ROUND_THREAD);
+  if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
+    return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
+  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && !p->colocated)
+    return derr(OMR_EINVAL, "sparse_round: the dense reduce-scatter stand-in needs every rank to be a worker");
+  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && p->rows % p->N != 0)
+    return derr(OMR_EINVAL, "sparse_round: dense reduce-scatter needs equal shards (rows %llu, world %d)",
+                static_cast<unsigned long long>(p->rows), p->N);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // a threaded round hands its steps after the scan to the progress thread; any other call first lets the thread
+  // issue everything queued (the plan's state is then this thread's alone)
+  TRY(threaded ? thread_start(p) : thread_drain(p));
+  p->ht.start();
+  int32_t* fl = flags ? flags : p->flags_ws;
+  uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
+  uint32_t* un = union_next ? union_next : p->unext_ws;
+  // a stream other than the previous round's starts behind it (plan-wide state is shared by every round)
+  if (p->last_st != nullptr && p->last_st != st) {
+    TRY(hip_check(hipEventRecord(p->st_ev, p->last_st), "hipEventRecord"));
+    TRY(hip_check(hipStreamWaitEvent(st, p->st_ev, 0), "hipStreamWaitEvent"));
+  }
+  p->last_st = st;
+  // a round that is not deferred finishes a deferred one first (rounds complete in call order; a threaded round's
+  // progress thread does this, it owns the deferred rounds)
+  if (!defer && !threaded) TRY(flush_pending(p, st, nullptr, nullptr));
+  // a synchronous round after asynchronous ones: its all-gather and exchange go on `stream`, so the plan and
+  // communication streams must be idle first (one communicator is never driven from two streams at once; the
+  // last asynchronous round's `done` follows all of its plan-stream work)
+  if (!async && p->last_async >= 0) {
+    TRY(hip_check(hipStreamWaitEvent(st, p->set[p->last_async].done, 0), "hipStreamWaitEvent"));
+    p->last_async = -1;
+  }
+  const int si = p->cur;
+  omr_ar_plan::Set& S = p->set[si];
+  p->cur = (p->cur + 1) % omr_ar_plan::kSets;
+  // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass (a dedicated aggregator
+  //    offers its all-zero mask buffer to the all-gather).  The set's own masks must have been consumed and
+  //    re-zeroed by the plan of the round kSets calls back.
+  int tslot = -1;
+  if (timed) TRY(timed_slot(p, &tslot));
+  if (threaded) {  // that plan has been issued (and this set's `scanned` waited for) by the progress thread
+    std::unique_lock<std::mutex> lk(p->mu);
+    const uint64_t need = p->rounds_begun >= omr_ar_plan::kSets - 1 ? p->rounds_begun - (omr_ar_plan::kSets - 1) : 0;
+    p->cv_done.wait(lk, [&] { return p->first_halves >= need || p->thread_rc != 0; });
+    if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
+  }
+  if (S.plan_pending) {
+    TRY(wait_ev(st, S.planned));
+    S.plan_pending = false;
+  }
+  if (p->worker()) {
+    if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
+    TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, nullptr, p->scan_ws,
+                                      p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+    if (timed) {
+      TRY(hip_check(hipEventRecord(p->timed[tslot].s1, st), "hipEventRecord"));
+      p->timed[tslot].scan = true;
+    }
+    p->ht.lap("1:scan");
+  }
+  // (a dedicated aggregator has nothing to scan: the plan stream starts behind whatever the caller queued)
+  if (async) TRY(hip_check(hipEventRecord(S.scanned, st), "hipEventRecord"));
+  p->ht.lap("1:scan events");
+  omr_ar_plan::Job j;
+  j.si = si;
+  j.mode = mode;
+  j.tslot = tslot;
+  j.async = async;
+  j.defer = defer;
+  j.timed = timed;
+  j.flush_first = threaded && !defer;
+  j.x = x;
+  j.out = out;
+  j.un = un;
+  j.st = st;
+  if (!threaded) {
+    {
+      std::lock_guard<std::mutex> g(p->mu);
+      ++p->rounds_begun;
+    }
+    const int rc = round_rest(p, j, sent_blocks, union_blocks);
+    if (rc != 0) {  // (a failed first half still counts as issued: no later threaded call waits on it)
+      std::lock_guard<std::mutex> g(p->mu);
+      p->first_halves = p->rounds_begun;
+    }
+    return rc;
+  }
+  if (sent_blocks) *sent_blocks = 0;
+  if (union_blocks) *union_blocks = 0;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    ++p->rounds_begun;
+    p->jobs.push_back(j);
+  }
+  p->cv_job.notify_one();
+  return 0;
+}
+
 int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mode, uint64_t* sent_blocks,
                            uint64_t* union_blocks, omr_stream_t stream) {
   if (p == nullptr || buf == nullptr) return derr(OMR_EINVAL, "sparse_buckets: NULL");
+  TRY(thread_drain(p));
   if (total_n == 0 || total_n % p->n != 0)
     return derr(OMR_EINVAL, "sparse_buckets: total_n %llu is not a multiple of the plan's bucket of %llu floats",
                 static_cast<unsigned long long>(total_n), static_cast<unsigned long long>(p->n));
@@ -1392,6 +1541,7 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
 int omr_ar_plan_shard(omr_ar_plan* p, int* shard, uint64_t* row_begin, uint64_t* row_end, const float** sums,
                       uint64_t* num_blocks) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_shard: NULL");
+  TRY(thread_drain(p));
   if (shard) *shard = p->shard;
   if (row_begin) *row_begin = p->shard >= 0 ? p->bounds[p->shard] : 0;
   if (row_end) *row_end = p->shard >= 0 ? p->bounds[p->shard + 1] : 0;
@@ -1402,6 +1552,7 @@ int omr_ar_plan_shard(omr_ar_plan* p, int* shard, uint64_t* row_begin, uint64_t*
 
 int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_join: NULL");
+  TRY(thread_drain(p));
   TRY(flush_pending(p, reinterpret_cast<hipStream_t>(stream), nullptr, nullptr));
   if (p->last_async < 0) return 0;
   // the communication stream runs rounds in issue order: waiting for the last one covers every earlier one
@@ -1412,6 +1563,7 @@ int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
 
 int omr_ar_plan_exchange_time(omr_ar_plan* p, float* ms, uint64_t* bytes_out, uint64_t* bytes_in) {
   if (p == nullptr || ms == nullptr) return derr(OMR_EINVAL, "ar_plan_exchange_time: NULL");
+  TRY(thread_drain(p));
   if (!p->xt_recorded) return derr(OMR_EINVAL, "ar_plan_exchange_time: no OMR_ROUND_TIME_EXCHANGE round issued");
   TRY(hip_check(hipEventSynchronize(p->xt1), "hipEventSynchronize"));
   TRY(hip_check(hipEventElapsedTime(ms, p->xt0, p->xt1), "hipEventElapsedTime"));
@@ -1423,6 +1575,7 @@ int omr_ar_plan_exchange_time(omr_ar_plan* p, float* ms, uint64_t* bytes_out, ui
 int omr_ar_plan_stage_timings(omr_ar_plan* p, float* stage_ms, uint64_t* bytes_out, uint64_t* bytes_in,
                               uint32_t* rounds) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_stage_timings: NULL");
+  TRY(thread_drain(p));
   double sum[OMR_ROUND_STAGES] = {0, 0, 0, 0};
   uint32_t cnt[OMR_ROUND_STAGES] = {0, 0, 0, 0};
   uint64_t bo = 0, bi = 0;

@@ -120,10 +120,11 @@ class CppSparseAllreduce:
         self.rank, self.world, self.num_workers = rank, world, nw
 
     ALLREDUCE, REDUCE_SCATTER, DENSE_REDUCE_SCATTER, ASYNC, TIME_EXCHANGE, DEFER = 0, 1, 2, 0x100, 0x200, 0x400
+    THREAD = 0x800
 
     def run(self, x: Optional[torch.Tensor], out: Optional[torch.Tensor] = None, ev=None, flags=None, next_offsets=None,
             union_next=None, mode: int = 0, async_: bool = False, time_exchange: bool = False,
-            defer: bool = False):
+            defer: bool = False, thread: bool = False):
         """mode 0: all-reduce (every worker gets every shard's sums); 1: reduce-scatter (stop at the
         aggregators: `out` gets this rank's shard sums only); 2: the dense stand-in (the whole tensor reduce-scattered
         by RCCL, every block).  async_: only the worker scan runs on the caller's stream; the bookkeeping runs on the
@@ -131,7 +132,10 @@ class CppSparseAllreduce:
         `out` (and union_next) are ready after join().  time_exchange: bracket the worker scan and the worker ->
         aggregator exchange with timing events (read with timings() / exchange_time()).  defer: OMR_ROUND_DEFER,
         this round's exchange is issued two calls later (or by a call without the flag, or join()); the returned
-        counts are those of the round whose exchange this call issued."""
+        counts are those of the round whose exchange this call issued.  thread: OMR_ROUND_THREAD (implies async_),
+        the plan's progress thread issues everything after the worker scan; the returned counts are 0."""
+        if thread:
+            mode |= self.THREAD
         if defer:
             mode |= self.DEFER
         if async_:

@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--block", type=int, default=256)
     ap.add_argument("--density", type=float, default=0.1)
     ap.add_argument("--mode", type=int, default=0, help="OMR_ROUND_* (0 all-reduce, 1 reduce-scatter, 2 dense)")
-    ap.add_argument("--pipe", choices=("sync", "async", "defer"), default="sync")
+    ap.add_argument("--pipe", choices=("sync", "async", "defer", "thread", "thread-async"), default="sync",
+                    help="thread: deferred rounds issued by the plan's progress thread; thread-async: not deferred")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--cycle", type=int, default=0,
                     help="round r runs input (and output buffer) r mod cycle (0: one of each per round); a long run "
@@ -57,7 +58,7 @@ def main():
     sums = {}
     for r in range(a.rounds):
         eng.run(xs[r % K], out=outs[r % K], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
-                async_=a.pipe != "sync", defer=a.pipe == "defer")
+                async_=a.pipe != "sync", defer=a.pipe in ("defer", "thread"), thread=a.pipe.startswith("thread"))
         if not worker and a.pipe == "sync":  # a dedicated aggregator's shard sums of this round
             torch.cuda.synchronize()
             sh, r0, r1, ptr, nb = eng.shard()

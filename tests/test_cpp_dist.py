@@ -142,20 +142,24 @@ def test_cpp_reduce_scatter_loopback(gpu, world, rounds):
         assert (outs[r].view(np.uint32) == exp.view(np.uint32)).all(), f"rank {r}"
 
 
-A, D_ = 0x100, 0x400  # OMR_ROUND_ASYNC, OMR_ROUND_DEFER
+A, D_, T = 0x100, 0x400, 0x800  # OMR_ROUND_ASYNC, OMR_ROUND_DEFER, OMR_ROUND_THREAD
 
 
 @pytest.mark.parametrize("world,mode,round_flags", [
     (3, 1, (A,) * 7), (8, 1, (A,) * 7), (4, 0, (A,) * 7), (3, 1, (A, A, 0, A, 0)),
     (3, 1, (D_,) * 7), (8, 1, (D_,) * 7), (4, 0, (D_,) * 7), (4, 2, (D_,) * 7),
-    (3, 1, (D_, D_, 0, D_, A)), (4, 0, (A, D_, D_, A, D_, D_, D_)), (3, 0, (D_, D_, D_, 0, D_, D_, A, D_))])
+    (3, 1, (D_, D_, 0, D_, A)), (4, 0, (A, D_, D_, A, D_, D_, D_)), (3, 0, (D_, D_, D_, 0, D_, D_, A, D_)),
+    # the progress thread (OMR_ROUND_THREAD), alone and mixed with calls that must first drain it
+    (3, 1, (T,) * 7), (8, 1, (T | D_,) * 7), (4, 2, (T | D_,) * 7),
+    (4, 0, (T | D_, T | D_, 0, T, D_, T | D_, A, T | D_)), (3, 1, (T | D_, A, T, T | D_, T | D_, 0, T))])
 def test_cpp_async_rounds_loopback(gpu, world, mode, round_flags):
     """OMR_ROUND_ASYNC: the bookkeeping of round k runs on the plan stream and its exchange and sums on the
     communication stream while round k+1 scans; rounds take different inputs and outputs (the bench's rotation),
     use the three plan buffer sets in turn (seven rounds: every set refilled), and are joined once at the end.
     OMR_ROUND_DEFER: round k's exchange is issued by call k+2 (or a call without the flag, or the join).  Rounds
     issued without a flag in between must first finish the deferred rounds and wait for the asynchronous ones
-    before using the stream."""
+    before using the stream.  OMR_ROUND_THREAD: the plan's progress thread issues everything after each scan; a
+    call without it first waits until the thread has issued every queued round."""
     B, rounds = 256, len(round_flags)
     L = Layout(n=2 << 20, block_size=B)
     D = dist_lib()
@@ -471,7 +475,7 @@ def test_client_message_mode_trace(gpu, tmp_path):
 
 
 @pytest.mark.parametrize("extra", [[], ["--dist-sync"], ["--dist-pipe", "async"], ["--dist-mode", "allreduce"],
-                                   ["--dist-mode", "dense"]])
+                                   ["--dist-mode", "dense"], ["--dist-pipe", "thread"]])
 def test_bench_distributed_path_world1(gpu, extra):
     """bench.py's N>1 path as the driver launches it (torch.distributed.run, RCCL, the C++ round with two
     communicators, pipelined rounds joined before the closing sync), rehearsed at world 1."""
@@ -494,7 +498,7 @@ def test_bench_distributed_path_world1(gpu, extra):
 
 
 @pytest.mark.parametrize("world,extra", [(2, []), (3, ["--dist-mode", "allreduce"]), (2, ["--dist-sync"]),
-                                         (4, ["--dist-mode", "dense"])])
+                                         (4, ["--dist-mode", "dense"]), (3, ["--dist-pipe", "thread"])])
 def test_bench_distributed_path_ipc(gpu, world, extra):
     """bench.py's N>1 path with real exchanges on one GPU: torch.distributed.run with `world` ranks sharing the GPU
     over the HIP-IPC transport (gloo carries the id, barriers and the max-over-ranks time).  Rank 0's line reports

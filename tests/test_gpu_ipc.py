@@ -54,6 +54,10 @@ def run_ranks(tmp_path, world, n, B, density, mode, pipe, rounds=3, workers=0, c
     # generations, under the deferred pipeline, with the inputs and outputs reused every third round
     (3, "defer", 0, 256, 0.095, 60),
     (2, "async", 1, 256, 0.2, 45),
+    # the progress thread (OMR_ROUND_THREAD) drives the transport
+    (3, "thread", 0, 256, 0.095, 40),
+    (4, "thread-async", 1, 512, 0.3, 9),
+    (2, "thread", 2, 256, 0.2, 9),
 ])
 def test_cpp_round_processes(gpu, tmp_path, world, pipe, mode, B, density, rounds):
     L = Layout(n=2 << 20, block_size=B)
