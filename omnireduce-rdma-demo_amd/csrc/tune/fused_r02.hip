@@ -436,6 +436,232 @@ __global__ __launch_bounds__(256) void k_mix_probe(FusedArgs a, uint64_t nb) {
   }
 }
 
+// k_scan1w — k_scan1f with a WRITER WAVE (study).  Waves 0..WAVES-2 only read: loads, ballots, and LDS.  The last
+// wave of the workgroup issues every global store of the workgroup.  On gfx9 a wave's vmcnt counts its loads and
+// stores together, in issue order, so in k_scan1f (and in k_scan1d, one batch later) a wave that stores a block
+// waits for that store's acknowledgement before it can use its next batch's first load.  At config 3 that costs
+// 8.7 us for 11 MB of block writes (DESIGN.md §3.1 ablations): far more than their bandwidth.  Here a reader copies
+// its batch's blocks to write (non-zero + lane head) into an LDS ring, and one record per batch {rows, flag bits,
+// carry, blocks} into a record ring (one 64-bit LDS atomic hands out both tickets, so records and ring slots are
+// consumed in the same order).  The writer takes the records in ticket order and stores the blocks (META = 0) or the
+// blocks and the batch's flags / next offsets / row-mask bits (META = 1).  Readers wait only when a ring is full.
+template <int VEC, int WAVES, int LOADS = 16, int META = 1, int RING_KB = 32>
+__global__ __launch_bounds__(64 * WAVES) void k_scan1w(FusedArgs a) {
+  constexpr int RB = LOADS / VEC;
+  constexpr uint32_t R = WAVES - 1;  // reader waves; wave R is the writer
+  constexpr int BLK4 = 64 * VEC;     // 16-byte vectors per block
+  constexpr uint32_t NSLOT = RING_KB * 1024 / (BLK4 * 16);
+  constexpr uint32_t NREC = 64;
+  static_assert(NSLOT >= static_cast<uint32_t>(RB) && (NSLOT & (NSLOT - 1)) == 0, "ring holds a batch");
+  __shared__ v4f s_ring[NSLOT * BLK4];
+  __shared__ uint32_t s_rec[NREC][5];  // rr, nrow, bits, carry, wmask
+  __shared__ uint32_t s_rready[NREC];
+  __shared__ uint64_t s_head;          // records << 32 | ring slots handed out
+  __shared__ uint32_t s_rtail, s_btail, s_done;
+  __shared__ uint32_t s_wfirst[WAVES], s_wlast[WAVES];
+  __shared__ int s_fix;
+  __shared__ uint32_t s_carry[64];
+  __shared__ uint32_t s_seg_last[64];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t k = lin % a.K, col = lin / a.K + a.part0 * a.lanes;
+  const uint32_t l = col % a.lanes, p = col / a.lanes;
+  const uint32_t r0 = k * a.S;
+  const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  const uint32_t lane_b = l * a.block;
+  const uint32_t row_stride = a.lanes * a.block;
+  const bool last_seg = (k + 1 == a.K);
+  const bool data_out = a.out != nullptr;
+  if (threadIdx.x == 0) {
+    s_head = 0;
+    s_rtail = s_btail = s_done = 0;
+  }
+  if (threadIdx.x < NREC) s_rready[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t rw = ((a.S + R * RB - 1) / (R * RB)) * RB;
+  const uint32_t lo = wave < R ? (wave * rw < a.S ? wave * rw : a.S) : a.S;
+  const uint32_t hi = wave < R ? (lo + rw < a.S ? lo + rw : a.S) : a.S;
+  uint32_t carry = kNone, wlast = kNone;
+  // the batch's flag / next / mask stores (k_scan1f's, by whichever wave issues them)
+  auto meta_stores = [&](uint32_t rr, uint32_t nrow, uint32_t bits, uint32_t c) {
+    if (static_cast<uint32_t>(lane) < nrow) {
+      const uint64_t blk = (row0 + rr) * a.lanes + l + static_cast<uint64_t>(lane) * a.lanes;
+      if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>((bits >> lane) & 1u);
+      const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
+      const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : c;
+      if (nr != kNone) a.next[blk] = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+      if (a.masks != nullptr && ((bits >> lane) & 1u))
+        (void)__hip_atomic_fetch_or(&a.masks[row0 + rr + lane], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  if (wave < R) {
+    for (uint32_t nb_ = (hi - lo + RB - 1) / RB; nb_ > 0; --nb_) {
+      const uint32_t rr = lo + (nb_ - 1) * RB;
+      const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
+      const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+      const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, nrow * row_bytes);
+      v4f v[RB][VEC];
+#pragma unroll
+      for (int s = 0; s < RB; ++s)
+#pragma unroll
+        for (int q = 0; q < VEC; ++q)
+          v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                                src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
+      uint32_t bits = 0;
+#pragma unroll
+      for (int s = 0; s < RB; ++s) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
+        const bool nz = wave_ballot(o != 0) != 0 && static_cast<uint32_t>(s) < nrow;
+        bits |= static_cast<uint32_t>(nz) << s;
+      }
+      const uint32_t wmask = data_out ? (bits | ((r0 + rr) == 0 ? 1u : 0u)) : 0u;
+      if (META || wmask != 0) {
+        const uint32_t n = static_cast<uint32_t>(__builtin_popcount(wmask));
+        uint64_t tk = 0;
+        if (lane == 0)
+          tk = __hip_atomic_fetch_add(&s_head, (1ull << 32) | n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t rt = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tk >> 32));
+        const uint32_t bt = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(tk));
+        while (rt - __hip_atomic_load(&s_rtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= NREC ||
+               bt + n - __hip_atomic_load(&s_btail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > NSLOT)
+          __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");  // the ring writes stay behind the space check
+        uint32_t t = bt;
+#pragma unroll
+        for (int s = 0; s < RB; ++s)
+          if ((wmask >> s) & 1u) {
+            const uint32_t slot = t % NSLOT;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) s_ring[slot * BLK4 + q * 64 + lane] = add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q]);
+            ++t;
+          }
+        if (lane == 0) {
+          uint32_t* rec = s_rec[rt % NREC];
+          rec[0] = rr; rec[1] = nrow; rec[2] = bits; rec[3] = carry; rec[4] = wmask;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the record and its blocks are in LDS
+        if (lane == 0) __hip_atomic_store(&s_rready[rt % NREC], rt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (!META) meta_stores(rr, nrow, bits, carry);
+      if (bits != 0) {
+        if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
+        carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) (void)__hip_atomic_fetch_add(&s_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+    // the writer: records in ticket order until every reader is done and the record ring is drained
+    uint32_t rt = 0, bt = 0;
+    for (;;) {
+      const uint32_t slot = rt % NREC;
+      bool have = false;
+      for (;;) {
+        if (__hip_atomic_load(&s_rready[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == rt + 1) {
+          have = true;
+          break;
+        }
+        if (__hip_atomic_load(&s_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == R) {
+          have = __hip_atomic_load(&s_rready[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == rt + 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!have) break;
+      asm volatile("" ::: "memory");  // the record and ring reads stay behind the ready flag (LDS is in order)
+      const uint32_t* rec = s_rec[slot];
+      const uint32_t rr = __builtin_amdgcn_readfirstlane(rec[0]);
+      const uint32_t nrow = __builtin_amdgcn_readfirstlane(rec[1]);
+      const uint32_t bits = __builtin_amdgcn_readfirstlane(rec[2]);
+      const uint32_t c = __builtin_amdgcn_readfirstlane(rec[3]);
+      uint32_t wm = __builtin_amdgcn_readfirstlane(rec[4]);
+      const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+      const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + blk0 * a.block, data_out ? nrow * row_bytes : 0u);
+      while (wm != 0) {
+        const uint32_t s = static_cast<uint32_t>(__builtin_ctz(wm));
+        wm &= wm - 1;
+        const uint32_t bslot = bt % NSLOT;
+        v4f d[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) d[q] = s_ring[bslot * BLK4 + q * 64 + lane];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        ++bt;
+        if (lane == 0) __hip_atomic_store(&s_btail, bt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, d[q]), dst,
+                                                 s * row_bytes + (q * 64 + lane) * 16, 0, kStoreAux);
+      }
+      if (META) meta_stores(rr, nrow, bits, c);
+      ++rt;
+      if (lane == 0) __hip_atomic_store(&s_rtail, rt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  if (lane == 0) {
+    s_wfirst[wave] = carry;
+    s_wlast[wave] = wlast;
+  }
+  __syncthreads();
+  uint32_t succ = kNone;
+  for (uint32_t w2 = wave + 1; w2 < WAVES; ++w2)
+    if (s_wfirst[w2] != kNone) {
+      succ = s_wfirst[w2];
+      break;
+    }
+  if (wave < R && (succ != kNone || last_seg)) {
+    const uint32_t val = succ != kNone ? static_cast<uint32_t>(row0 + succ) * row_stride + lane_b : a.sentinel + lane_b;
+    for (uint32_t i = (wlast == kNone ? lo : wlast) + lane; i < hi; i += 64) a.next[(row0 + i) * a.lanes + l] = val;
+  }
+  if (a.K == 1) return;
+  if (threadIdx.x == 0) {
+    uint32_t first = kNone, last = 0;
+    for (uint32_t w2 = 0; w2 < WAVES; ++w2) {
+      if (first == kNone) first = s_wfirst[w2];
+      if (s_wlast[w2] != kNone) last = s_wlast[w2];
+    }
+    const uint64_t sm = (static_cast<uint64_t>(first) << 32) | (first == kNone ? kNone : last);
+    (void)__hip_atomic_exchange(&a.summary[static_cast<uint64_t>(col) * a.K + k], sm, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&a.cnt[col], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_fix = (old == a.K - 1);
+  }
+  __syncthreads();
+  if (!s_fix) return;
+  if (threadIdx.x < a.K) {
+    const uint64_t sm = __hip_atomic_fetch_or(&a.summary[static_cast<uint64_t>(col) * a.K + threadIdx.x], 0ull,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_carry[threadIdx.x] = static_cast<uint32_t>(sm >> 32);
+    s_seg_last[threadIdx.x] = static_cast<uint32_t>(sm);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = kNone;
+    for (int kk = static_cast<int>(a.K) - 1; kk >= 0; --kk) {
+      const uint32_t first = s_carry[kk];
+      s_carry[kk] = c;
+      if (first != kNone) c = static_cast<uint32_t>(kk) * a.S + first;
+    }
+    __hip_atomic_store(&a.cnt[col], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint64_t part_row0 = static_cast<uint64_t>(p) * a.rpp;
+  const uint32_t tail_total = (a.K - 1) * a.S;
+  for (uint32_t t = threadIdx.x; t < tail_total; t += blockDim.x) {
+    const uint32_t kk = t / a.S, i = t % a.S;
+    const uint32_t last = s_seg_last[kk];
+    if (last != kNone && i < last) continue;
+    const uint32_t c = s_carry[kk];
+    a.next[(part_row0 + static_cast<uint64_t>(kk) * a.S + i) * a.lanes + l] =
+        (c != kNone) ? static_cast<uint32_t>(part_row0 + c) * row_stride + lane_b : a.sentinel + lane_b;
+  }
+}
+
 using Launch = void (*)(const Layout&, const FusedShape&, FusedArgs, hipStream_t);
 
 unsigned grid_of(const Layout& L, const FusedShape& f) {
@@ -459,6 +685,10 @@ void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
 template <int VEC, int W, int LD, int P, int ABL>
 void go_d(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   k_scan1d<VEC, W, LD, P, false, ABL><<<grid_of(L, f), 64 * W, 0, st>>>(a);
+}
+template <int VEC, int W, int LD, int META>
+void go_w(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  k_scan1w<VEC, W, LD, META><<<grid_of(L, f), 64 * W, 0, st>>>(a);
 }
 template <int VEC, int W>
 void go_r(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
@@ -504,6 +734,9 @@ const Variant kVariants[] = {
     {"probe flat read + write flagged, plain st", false, go_m<2, 0>, go_m<2, 0>},
     {"probe flat read + write flagged, nt st", false, go_m<2, 2>, go_m<2, 2>},
     {"probe flat read + write flagged, sc1 st", false, go_m<2, 16>, go_m<2, 16>},
+    {"w16 writer wave: blocks", true, go_w<1, 16, 16, 0>, go_w<4, 16, 16, 0>},
+    {"w16 writer wave: blocks + meta", true, go_w<1, 16, 16, 1>, go_w<4, 16, 16, 1>},
+    {"w8 writer wave: blocks + meta", true, go_w<1, 8, 16, 1>, go_w<4, 8, 16, 1>},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 }  // namespace
