@@ -219,7 +219,8 @@ struct FusedArgs {
 
 constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
 
-template <int VEC, int WAVES, int LOADS = 16, int ABL = 0, int MINW = 1, int SAUX = kStoreAux, int SKIP = 0>
+template <int VEC, int WAVES, int LOADS = 16, int ABL = 0, int MINW = 1, int SAUX = kStoreAux, int SKIP = 0,
+          int MAUX = -1>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW))) void k_scan1f(FusedArgs a) {
   constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
   static_assert(RB >= 1 && RB <= 32, "batch bits are 32-bit");
@@ -292,11 +293,20 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
     }
     if (!(ABL & 2) && static_cast<uint32_t>(lane) < nrow) {
       const uint64_t blk = blk0 + static_cast<uint64_t>(lane) * a.lanes;
-      if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>((bits >> lane) & 1u);
       // successor of row rr+lane: next set bit above it in this batch, else the carry (client.cc:19-31)
       const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
       const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : carry;
-      if (nr != kNone) a.next[blk] = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+      if constexpr (MAUX < 0) {
+        if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>((bits >> lane) & 1u);
+        if (nr != kNone) a.next[blk] = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+      } else {  // study: the flag / next stores with cache policy MAUX (byte offsets < 2^31 in the study's sizes)
+        const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(a.flags, 0, a.flags ? 0x7FFFFFFF : 0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(a.next, 0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32((bits >> lane) & 1u, rf, static_cast<uint32_t>(blk * 4), 0, MAUX);
+        if (nr != kNone)
+          __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(row0 + nr) * row_stride + lane_b, rn,
+                                                static_cast<uint32_t>(blk * 4), 0, MAUX);
+      }
       if (a.masks != nullptr && ((bits >> lane) & 1u))
         (void)__hip_atomic_fetch_or(&a.masks[row0 + rr + lane], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

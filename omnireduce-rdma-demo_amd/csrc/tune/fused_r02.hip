@@ -662,6 +662,204 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1w(FusedArgs a) {
   }
 }
 
+// k_scan1e — k_scan1f with the workgroup's stores STASHED in LDS and written at its end (study).  The writer-wave
+// variant above takes the stores out of the readers' vmcnt queue and still pays ~9 us for config 3's 11 MB of block
+// writes: the cost is on the memory side (writes interleaved one block at a time into a saturating read stream),
+// not in the waves.  Here every wave keeps reading; the blocks to write (STASH bit 0) and the flag / next values
+// (bit 1, segments of <= kStashRows rows) go to LDS, and the workgroup writes them out after its last read — so
+// at config 3 (one workgroup per CU, all ending together) the chip's writes form one phase after the reads.  A
+// batch whose blocks no longer fit stores them directly, as k_scan1f does.
+constexpr uint32_t kStashRows = 2048;
+constexpr uint32_t kUnsetNext = 0xFFFFFFFEu;  // successor in a later segment: the column's fix-up stores it
+template <int VEC, int WAVES, int LOADS = 16, int STASH = 1, int CAP_KB = 96>
+__global__ __launch_bounds__(64 * WAVES) void k_scan1e(FusedArgs a) {
+  constexpr int RB = LOADS / VEC;
+  constexpr uint32_t BLK4 = 64 * VEC;
+  constexpr uint32_t NSLOT = CAP_KB * 1024 / (BLK4 * 16);
+  constexpr uint32_t MR = (STASH & 2) ? kStashRows : 1;
+  __shared__ v4f s_blk[NSLOT * BLK4];
+  __shared__ uint32_t s_bdst[NSLOT];
+  __shared__ uint32_t s_mflag[MR], s_mnext[MR];
+  __shared__ uint32_t s_bcnt;
+  __shared__ uint32_t s_wfirst[WAVES], s_wlast[WAVES];
+  __shared__ int s_fix;
+  __shared__ uint32_t s_carry[64];
+  __shared__ uint32_t s_seg_last[64];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t k = lin % a.K, col = lin / a.K + a.part0 * a.lanes;
+  const uint32_t l = col % a.lanes, p = col / a.lanes;
+  const uint32_t r0 = k * a.S;
+  const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  const uint32_t lane_b = l * a.block;
+  const uint32_t row_stride = a.lanes * a.block;
+  const bool last_seg = (k + 1 == a.K);
+  const bool data_out = a.out != nullptr && (STASH & 1);
+  const bool mstash = (STASH & 2) && a.S <= MR;
+  if (threadIdx.x == 0) s_bcnt = 0;
+  __syncthreads();
+  const uint32_t rw = ((a.S + WAVES * RB - 1) / (WAVES * RB)) * RB;
+  const uint32_t lo = wave * rw < a.S ? wave * rw : a.S;
+  const uint32_t hi = lo + rw < a.S ? lo + rw : a.S;
+  uint32_t carry = kNone, wlast = kNone;
+  for (uint32_t nb_ = (hi - lo + RB - 1) / RB; nb_ > 0; --nb_) {
+    const uint32_t rr = lo + (nb_ - 1) * RB;
+    const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
+    const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+    const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, nrow * row_bytes);
+    v4f v[RB][VEC];
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                              src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
+      bits |= static_cast<uint32_t>(wave_ballot(o != 0) != 0 && static_cast<uint32_t>(s) < nrow) << s;
+    }
+    const uint32_t wmask = (a.out != nullptr) ? (bits | ((r0 + rr) == 0 ? 1u : 0u)) : 0u;
+    if (wmask != 0) {
+      const uint32_t n = static_cast<uint32_t>(__builtin_popcount(wmask));
+      uint32_t t0 = NSLOT;
+      if (data_out) {
+        uint32_t tk = 0;
+        if (lane == 0) tk = __hip_atomic_fetch_add(&s_bcnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        t0 = __builtin_amdgcn_readfirstlane(tk);
+      }
+      if (t0 + n <= NSLOT) {
+        uint32_t t = t0;
+#pragma unroll
+        for (int s = 0; s < RB; ++s)
+          if ((wmask >> s) & 1u) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) s_blk[t * BLK4 + q * 64 + lane] = add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q]);
+            if (lane == 0) s_bdst[t] = static_cast<uint32_t>(blk0 + static_cast<uint64_t>(s) * a.lanes);
+            ++t;
+          }
+      } else {
+        if (t0 < NSLOT && static_cast<uint32_t>(lane) < NSLOT - t0) s_bdst[t0 + lane] = kNone;
+        const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + blk0 * a.block, nrow * row_bytes);
+#pragma unroll
+        for (int s = 0; s < RB; ++s)
+          if ((wmask >> s) & 1u) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
+                                                     dst, s * row_bytes + (q * 64 + lane) * 16, 0, kStoreAux);
+          }
+      }
+    }
+    if (static_cast<uint32_t>(lane) < nrow) {
+      const uint64_t blk = blk0 + static_cast<uint64_t>(lane) * a.lanes;
+      const uint32_t fl = (bits >> lane) & 1u;
+      const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
+      const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : carry;
+      const uint32_t nv = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+      if (mstash) {
+        s_mflag[rr + lane] = fl;
+        s_mnext[rr + lane] = nr != kNone ? nv : kUnsetNext;
+      } else {
+        if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>(fl);
+        if (nr != kNone) a.next[blk] = nv;
+      }
+      if (a.masks != nullptr && fl)
+        (void)__hip_atomic_fetch_or(&a.masks[row0 + rr + lane], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (bits != 0) {
+      if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
+      carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
+    }
+  }
+  if (lane == 0) {
+    s_wfirst[wave] = carry;
+    s_wlast[wave] = wlast;
+  }
+  __syncthreads();
+  uint32_t succ = kNone;
+  for (uint32_t w2 = wave + 1; w2 < WAVES; ++w2)
+    if (s_wfirst[w2] != kNone) {
+      succ = s_wfirst[w2];
+      break;
+    }
+  if (succ != kNone || last_seg) {
+    const uint32_t val = succ != kNone ? static_cast<uint32_t>(row0 + succ) * row_stride + lane_b : a.sentinel + lane_b;
+    for (uint32_t i = (wlast == kNone ? lo : wlast) + lane; i < hi; i += 64) {
+      if (mstash) s_mnext[i] = val;
+      else a.next[(row0 + i) * a.lanes + l] = val;
+    }
+  }
+  __syncthreads();
+  // the workgroup's stash, written after its last read
+  const uint32_t cnt = s_bcnt < NSLOT ? s_bcnt : NSLOT;
+  for (uint32_t j = wave; j < cnt; j += WAVES) {
+    const uint32_t d = __builtin_amdgcn_readfirstlane(s_bdst[j]);
+    if (d == kNone) continue;
+    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + static_cast<uint64_t>(d) * a.block, a.block * 4);
+#pragma unroll
+    for (int q = 0; q < VEC; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, s_blk[j * BLK4 + q * 64 + lane]), dst,
+                                             (q * 64 + lane) * 16, 0, kStoreAux);
+  }
+  if (mstash) {
+    for (uint32_t i = threadIdx.x; i < a.S; i += blockDim.x) {
+      const uint64_t blk = (row0 + i) * a.lanes + l;
+      if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>(s_mflag[i]);
+      if (s_mnext[i] != kUnsetNext) a.next[blk] = s_mnext[i];
+    }
+  }
+  if (a.K == 1) return;
+  if (threadIdx.x == 0) {
+    uint32_t first = kNone, last = 0;
+    for (uint32_t w2 = 0; w2 < WAVES; ++w2) {
+      if (first == kNone) first = s_wfirst[w2];
+      if (s_wlast[w2] != kNone) last = s_wlast[w2];
+    }
+    const uint64_t sm = (static_cast<uint64_t>(first) << 32) | (first == kNone ? kNone : last);
+    (void)__hip_atomic_exchange(&a.summary[static_cast<uint64_t>(col) * a.K + k], sm, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&a.cnt[col], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_fix = (old == a.K - 1);
+  }
+  __syncthreads();
+  if (!s_fix) return;
+  if (threadIdx.x < a.K) {
+    const uint64_t sm = __hip_atomic_fetch_or(&a.summary[static_cast<uint64_t>(col) * a.K + threadIdx.x], 0ull,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_carry[threadIdx.x] = static_cast<uint32_t>(sm >> 32);
+    s_seg_last[threadIdx.x] = static_cast<uint32_t>(sm);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = kNone;
+    for (int kk = static_cast<int>(a.K) - 1; kk >= 0; --kk) {
+      const uint32_t first = s_carry[kk];
+      s_carry[kk] = c;
+      if (first != kNone) c = static_cast<uint32_t>(kk) * a.S + first;
+    }
+    __hip_atomic_store(&a.cnt[col], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint64_t part_row0 = static_cast<uint64_t>(p) * a.rpp;
+  const uint32_t tail_total = (a.K - 1) * a.S;
+  for (uint32_t t = threadIdx.x; t < tail_total; t += blockDim.x) {
+    const uint32_t kk = t / a.S, i = t % a.S;
+    const uint32_t last = s_seg_last[kk];
+    if (last != kNone && i < last) continue;
+    const uint32_t c = s_carry[kk];
+    a.next[(part_row0 + static_cast<uint64_t>(kk) * a.S + i) * a.lanes + l] =
+        (c != kNone) ? static_cast<uint32_t>(part_row0 + c) * row_stride + lane_b : a.sentinel + lane_b;
+  }
+}
+
 using Launch = void (*)(const Layout&, const FusedShape&, FusedArgs, hipStream_t);
 
 unsigned grid_of(const Layout& L, const FusedShape& f) {
@@ -682,6 +880,10 @@ void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   const unsigned lds = occ_lds(&k_scan1f<VEC, W, LD, ABL, 1, SAUX, SKIP>);
   k_scan1f<VEC, W, LD, ABL, 1, SAUX, SKIP><<<grid_of(L, f), 64 * W, lds, st>>>(a);
 }
+template <int VEC, int W, int SKIP, int MAUX>
+void go_fm(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  k_scan1f<VEC, W, 16, 0, 1, kStoreAux, SKIP, MAUX><<<grid_of(L, f), 64 * W, 0, st>>>(a);
+}
 template <int VEC, int W, int LD, int P, int ABL>
 void go_d(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   k_scan1d<VEC, W, LD, P, false, ABL><<<grid_of(L, f), 64 * W, 0, st>>>(a);
@@ -689,6 +891,10 @@ void go_d(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
 template <int VEC, int W, int LD, int META>
 void go_w(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   k_scan1w<VEC, W, LD, META><<<grid_of(L, f), 64 * W, 0, st>>>(a);
+}
+template <int VEC, int W, int ST, int CAP>
+void go_e(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  k_scan1e<VEC, W, 16, ST, CAP><<<grid_of(L, f), 64 * W, 0, st>>>(a);
 }
 template <int VEC, int W>
 void go_r(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
@@ -737,6 +943,16 @@ const Variant kVariants[] = {
     {"w16 writer wave: blocks", true, go_w<1, 16, 16, 0>, go_w<4, 16, 16, 0>},
     {"w16 writer wave: blocks + meta", true, go_w<1, 16, 16, 1>, go_w<4, 16, 16, 1>},
     {"w8 writer wave: blocks + meta", true, go_w<1, 8, 16, 1>, go_w<4, 8, 16, 1>},
+    {"e stash blocks 96K", true, go_e<1, 16, 1, 96>, go_e<4, 16, 1, 96>},
+    {"e stash blocks + meta 96K", true, go_e<1, 16, 3, 96>, go_e<4, 16, 3, 96>},
+    {"e stash meta only", true, go_e<1, 16, 2, 4>, go_e<4, 16, 2, 4>},
+    {"e stash blocks + meta 128K", true, go_e<1, 16, 3, 128>, go_e<4, 16, 3, 128>},
+    {"f meta st plain (buffer)", true, go_fm<1, 16, 0, 0>, go_fm<4, 16, 1, 0>},
+    {"f meta st sc0 sc1", true, go_fm<1, 16, 0, 17>, go_fm<4, 16, 1, 17>},
+    {"f meta st nt", true, go_fm<1, 16, 0, 2>, go_fm<4, 16, 1, 2>},
+    {"f meta st sc1", true, go_fm<1, 16, 0, 16>, go_fm<4, 16, 1, 16>},
+    {"f meta st sc0", true, go_fm<1, 16, 0, 1>, go_fm<4, 16, 1, 1>},
+    {"f meta st nt sc1", true, go_fm<1, 16, 0, 18>, go_fm<4, 16, 1, 18>},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 }  // namespace

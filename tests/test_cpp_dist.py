@@ -498,7 +498,8 @@ def test_bench_distributed_path_world1(gpu, extra):
 
 
 @pytest.mark.parametrize("world,extra", [(2, []), (3, ["--dist-mode", "allreduce"]), (2, ["--dist-sync"]),
-                                         (4, ["--dist-mode", "dense"]), (3, ["--dist-pipe", "thread"])])
+                                         (4, ["--dist-mode", "dense"]), (3, ["--dist-pipe", "thread"]),
+                                         (8, []), (8, ["--dist-mode", "allreduce", "--dist-pipe", "thread"])])
 def test_bench_distributed_path_ipc(gpu, world, extra):
     """bench.py's N>1 path with real exchanges on one GPU: torch.distributed.run with `world` ranks sharing the GPU
     over the HIP-IPC transport (gloo carries the id, barriers and the max-over-ranks time).  Rank 0's line reports
