@@ -72,13 +72,16 @@ def parse():
                    help="N>1 step: workers -> aggregators reduce-scatter (BASELINE config 4, default), the full "
                         "all-reduce (sums back to every worker), or the dense stand-in (ncclReduceScatter of the "
                         "whole tensor, C++ driver only)")
-    p.add_argument("--dist-pipe", choices=("sync", "async", "defer", "thread"), default="defer",
+    p.add_argument("--dist-pipe", choices=("sync", "async", "defer", "thread", "auto"), default="auto",
                    help="N>1, C++ driver: sync = each round's exchange on the caller's stream; async "
                         "(OMR_ROUND_ASYNC) = round k's exchange over xGMI overlaps round k+1's worker scan; defer "
-                        "(OMR_ROUND_DEFER, default) = as async, and round k's exchange is issued after round k+1's "
+                        "(OMR_ROUND_DEFER) = as async, and round k's exchange is issued after round k+1's "
                         "first half is queued, so the host never waits for block counts with the GPU idle; thread "
                         "(OMR_ROUND_THREAD | OMR_ROUND_DEFER) = as defer, with everything after the worker scan "
-                        "issued by the plan's progress thread")
+                        "issued by the plan's progress thread; auto (default) = defer or thread, whichever ran the "
+                        "untimed probe rounds faster (max over ranks; a round whose host issue time reaches its GPU "
+                        "time gains from the thread)")
+    p.add_argument("--pipe-probe", type=int, default=12, help="--dist-pipe auto: untimed rounds per probe trial")
     p.add_argument("--dist-sync", action="store_true", help="same as --dist-pipe sync")
     p.add_argument("--dist-transport", choices=("rccl", "ipc"), default="rccl",
                    help="N>1 round transport: RCCL over xGMI, one process per GPU (the product path), or HIP IPC "
@@ -304,7 +307,7 @@ def main():
             out.copy_(xs[0])
 
         pipe = "sync" if args.dist_sync else args.dist_pipe
-        pipelined = pipe != "sync"
+        pipe_probe = None  # --dist-pipe auto: the probe's per-round times (ms, max over ranks) per candidate
 
         host_s = [0.0, 0]  # host time inside engine.run over the timed steps, and their count
 
@@ -315,7 +318,7 @@ def main():
             # (omr_ar_plan_stage_timings)
             h0 = time.perf_counter()
             engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
-                       async_=pipelined, defer=pipe in ("defer", "thread"), thread=pipe == "thread",
+                       async_=pipe != "sync", defer=pipe in ("defer", "thread"), thread=pipe == "thread",
                        time_exchange=ev is not None)
             if timed_region:
                 host_s[0] += time.perf_counter() - h0
@@ -347,6 +350,28 @@ def main():
     if dist_mode:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    if dist_mode and pipe == "auto":
+        # untimed probe: the same rounds under defer and thread, alternated twice; every rank takes the candidate
+        # with the smaller max-over-ranks round time (so all ranks run one mode)
+        best = {"defer": float("inf"), "thread": float("inf")}
+        k = args.warmup
+        for _ in range(2):
+            for cand in ("defer", "thread"):
+                pipe = cand
+                torch.distributed.barrier()
+                t0 = time.perf_counter()
+                for _ in range(args.pipe_probe):
+                    step(k)
+                    k += 1
+                join()
+                torch.cuda.synchronize()
+                dt = torch.tensor([(time.perf_counter() - t0) / args.pipe_probe], dtype=torch.float64, device=tdev)
+                torch.distributed.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
+                best[cand] = min(best[cand], float(dt.item()))
+        pipe = min(best, key=best.get)
+        pipe_probe = {c: round(v * 1e3, 5) for c, v in best.items()}
+        torch.distributed.barrier()
+        torch.cuda.synchronize()
 
     from omr import timing
     kev = [(timing.Event(), timing.Event()) for _ in range(args.steps)]
@@ -482,6 +507,9 @@ def main():
     }
     if exchange is not None:
         line["exchange"] = exchange
+        line["exchange"]["pipe"] = pipe
+        if pipe_probe is not None:
+            line["exchange"]["pipe_probe_ms_per_round"] = pipe_probe
     if not dist_mode and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(L, bitmaps[0], args)
     print(json.dumps(line), flush=True)
