@@ -350,6 +350,8 @@ def main():
     if dist_mode:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    if dist_mode and pipe == "auto" and args.pipe_probe < 1:
+        pipe = "defer"
     if dist_mode and pipe == "auto":
         # untimed probe: the same rounds under defer and thread, alternated twice; every rank takes the candidate
         # with the smaller max-over-ranks round time (so all ranks run one mode)
