@@ -277,6 +277,20 @@ void go_prod(const ScanArgs& a, hipStream_t st) {
   k_scanm<1, 32, kScanmUnitLanes><<<static_cast<unsigned>(a.rows * 2 / kWavesPerWG), kWGThreads, 0, st>>>(a);
 }
 
+// ablations (timing only, not checked): the product's loads and masks without the sums' stores, and without the
+// sums' and the flags' stores
+void go_prod_nosum(const ScanArgs& a0, hipStream_t st) {
+  ScanArgs a = a0;
+  a.out = nullptr;  // every sum store dropped by the empty descriptor
+  go_prod(a, st);
+}
+void go_prod_read(const ScanArgs& a0, hipStream_t st) {
+  ScanArgs a = a0;
+  a.out = nullptr;
+  a.flags = nullptr;
+  go_prod(a, st);
+}
+
 struct Variant {
   const char* name;
   void (*fn)(const ScanArgs&, hipStream_t);
@@ -289,6 +303,8 @@ const Variant kVariants[] = {
     {"G32 SUB32 W4 plain-st ld-nt", gog<1, 32, 32, 4, 0, true, 0, 2>},
     {"G32 SUB32 W4 nt-st noxcd", gog<1, 32, 32, 4, 0, false, 2, 2>},
     {"G64 SUB32 W4 nt-st", gog<1, 32, 64, 4, 0, true, 2, 2>},
+    {"ablation: product without sum stores", go_prod_nosum},
+    {"ablation: product, reads + masks only", go_prod_read},
 };
 constexpr int kNum = sizeof(kVariants) / sizeof(kVariants[0]);
 }  // namespace

@@ -98,6 +98,8 @@ def main():
             assert run(v, c, 0) == 0, lib.tune_scanm_name(v)
             torch.cuda.synchronize()
             got = (out.clone(), flags.clone(), masks.clone())
+            if b"ablation" in lib.tune_scanm_name(v):  # timing-only variants write a subset of the outputs
+                continue
             if ref is None:
                 ref = got
             else:
