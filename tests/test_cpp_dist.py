@@ -42,7 +42,10 @@ def dist_lib():
 
 
 @pytest.mark.parametrize("world,B,density", [(2, 256, 0.095), (3, 1024, 0.0099), (4, 512, 0.49),
-                                                   (8, 256, 0.095)])
+                                                   (8, 256, 0.095),
+                                                   # world sizes that do not divide the 128 rows (ragged shards), and
+                                                   # the largest group the shard sum takes (OMR_MAX_WORKERS)
+                                                   (5, 256, 0.3), (6, 512, 0.095), (7, 256, 0.2), (16, 256, 0.095)])
 def test_cpp_round_loopback(gpu, world, B, density):
     L = Layout(n=2 << 20, block_size=B)
     D = dist_lib()
