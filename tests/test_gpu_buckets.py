@@ -59,7 +59,10 @@ def check(outs, bms, L, world, mode, dev):
 @pytest.mark.parametrize("world,mode,host,bucket_mib,total_mib", [
     (2, AR, True, 16, 64),
     (4, RS, True, 16, 64),
+    (2, RS, True, 64, 256),
+    (4, AR, True, 64, 256),
     (8, AR, True, 64, 256),   # config-5 shape per rank at 256 MiB: 8 ranks, pinned host, 4 buckets
+    (2, AR, True, 256, 4096),  # config 5 per rank (4 GiB pinned host, -r 0.49) in bench's 256 MiB buckets
     (8, RS, True, 64, 256),
     (3, AR, False, 8, 24),    # device memory: deferred rounds only
 ])
