@@ -201,7 +201,10 @@ __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
 // the buffer range check.  The number of memory operations per batch is then static, so the compiler's vmcnt
 // wait for a load never includes a younger, data-dependent store (tools/tune_fused.py: 2-4 % faster than
 // branching around the stores; write-through sc0 sc1 beat plain, sc1-only and nt stores).
-// ABL (timing-only builds, csrc/tune/): bit 0 drops the data stores, bit 1 the flag/next stores.  MINW: the
+// ABL (timing-only builds, csrc/tune/): bit 0 drops the data stores, bit 1 the flag/next stores, bit 2 sends every
+// data store of a batch to the same block at the start of `out` (the same store count, no scattered HBM writes), bit 3
+// records per-workgroup timestamps {start, loop end, end with stores acknowledged, XCC} in place of the row masks
+// (tools/wg_timeline.py), bit 4 rotates the workgroup -> column map by one XCD.  MINW: the
 // amdgpu_waves_per_eu floor (occupancy study; 1 = the compiler's choice).  SAUX: the block stores' cache policy
 // (store-policy study; the product's is kStoreAux).  SKIP: a batch with no block to write skips its (dropped) data
 // stores through a wave-uniform branch (the product's choice at B = 1024).
@@ -231,11 +234,15 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t T = gridDim.x, bid = blockIdx.x;
-  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t lin0 = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const uint32_t lin = (ABL & 16) ? (lin0 + T / 8) % T : lin0;  // ABL bit 4: every XCD takes the next XCD's columns
   const uint32_t k = lin % a.K, col = lin / a.K + a.part0 * a.lanes;  // col: global (partition, lane) index
   const uint32_t l = col % a.lanes, p = col / a.lanes;
   const uint32_t r0 = k * a.S;                                  // segment's first row within the partition
   const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;  // its global row
+  uint64_t* const tl = (ABL & 8) ? a.masks : nullptr;           // timing-only: per-workgroup timestamps
+  uint64_t* const masks = (ABL & 8) ? nullptr : a.masks;
+  if ((ABL & 8) && threadIdx.x == 0) tl[bid * 4] = __builtin_amdgcn_s_memrealtime();
   const uint32_t row_bytes = a.lanes * a.block * 4;
   const uint32_t lane_b = l * a.block;
   const uint32_t row_stride = a.lanes * a.block;
@@ -258,7 +265,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
         v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
                                               src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
     const __amdgpu_buffer_rsrc_t dst =
-        chunk_rsrc(a.out + blk0 * a.block, (a.out != nullptr && !(ABL & 1)) ? nrow * row_bytes : 0u);
+        chunk_rsrc((ABL & 4) ? a.out : a.out + blk0 * a.block, (a.out != nullptr && !(ABL & 1)) ? nrow * row_bytes : 0u);
+    const uint32_t row_step = (ABL & 4) ? 0u : row_bytes;  // ABL bit 2: every row's store to the same block
     uint32_t bits = 0;
 #pragma unroll
     for (int s = 0; s < RB; ++s) {
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
 #pragma unroll
         for (int q = 0; q < VEC; ++q)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
-                                                 dst, (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, SAUX);
+                                                 dst, (s * row_step + (q * 64 + lane) * 16) | drop, 0, SAUX);
       }
     }
     if constexpr (SKIP) {
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
 #pragma unroll
           for (int q = 0; q < VEC; ++q)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
-                                                   dst, (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, SAUX);
+                                                   dst, (s * row_step + (q * 64 + lane) * 16) | drop, 0, SAUX);
         }
       }
     }
@@ -307,8 +315,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
           __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(row0 + nr) * row_stride + lane_b, rn,
                                                 static_cast<uint32_t>(blk * 4), 0, MAUX);
       }
-      if (a.masks != nullptr && ((bits >> lane) & 1u))
-        (void)__hip_atomic_fetch_or(&a.masks[row0 + rr + lane], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (masks != nullptr && ((bits >> lane) & 1u))
+        (void)__hip_atomic_fetch_or(&masks[row0 + rr + lane], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (bits != 0) {
       if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
@@ -320,6 +328,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
     s_wlast[wave] = wlast;   // last one
   }
   __syncthreads();
+  if ((ABL & 8) && threadIdx.x == 0) tl[bid * 4 + 1] = __builtin_amdgcn_s_memrealtime();
   // tail rows [wlast or lo, hi): successor = first non-zero row of a later wave, else of a later segment
   uint32_t succ = kNone;
   for (uint32_t w2 = wave + 1; w2 < WAVES; ++w2)
@@ -330,6 +339,14 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
   if (!(ABL & 2) && (succ != kNone || last_seg)) {
     const uint32_t val = succ != kNone ? static_cast<uint32_t>(row0 + succ) * row_stride + lane_b : a.sentinel + lane_b;
     for (uint32_t i = (wlast == kNone ? lo : wlast) + lane; i < hi; i += 64) a.next[(row0 + i) * a.lanes + l] = val;
+  }
+  if constexpr ((ABL & 8) != 0) {  // every store of the workgroup acknowledged
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      tl[bid * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+      tl[bid * 4 + 3] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg((15 << 11) | 20));  // HW_REG_XCC_ID
+    }
   }
   if (a.K == 1) return;
   // multi-segment column: publish {first, last}, count arrivals; the last arriver fixes every tail row

@@ -860,6 +860,265 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1e(FusedArgs a) {
   }
 }
 
+// k_scan1q — k_scan1f with the work balanced across XCDs at run time (study).  Workgroups go to XCDs round-robin
+// by ID, so a static column split gives every XCD the same bytes; tools/wg_timeline.py shows the XCDs then finish up
+// to 20 % apart (config 3: the last workgroup of the fastest XCD ends 135.7 us after the start, of the slowest
+// 170.4 us), and the launch lasts as long as the slowest.  Here persistent waves take items (CR rows of one column)
+// from eight queues, one per XCD and starting with their own (a partition per queue, its items chunk by chunk so
+// that the waves of one XCD stream the same rows of all lanes), and move to the next queue when theirs runs dry.
+// A wave streams its item as k_scan1f's waves stream their ranges (backwards, next offsets in-stream with a carry),
+// publishes the item's {first, last} non-zero row with a device-scope atomic, and counts the column's arrivals; the
+// wave that completes a column writes every next offset whose successor lies in a later item (a suffix minimum
+// over the column's items, one lane per item).  The last wave out re-arms the queues for the next launch.
+// FusedArgs reuse: K = partitions; cnt = [cols] arrival counters, then 8 queue counters and the exit counter;
+// summary = [cols][rpp / CR].
+template <int VEC, int WAVES, int LOADS = 16, int NBATCH = 2, int SKIP = 0>
+__global__ __launch_bounds__(64 * WAVES) void k_scan1q(FusedArgs a) {
+  constexpr int RB = LOADS / VEC;
+  constexpr uint32_t CR = RB * NBATCH;  // rows per item
+  const int lane = threadIdx.x & 63;
+  const uint32_t parts = a.K;
+  const uint32_t ncol = parts * a.lanes;
+  const uint32_t nch = a.rpp / CR;  // items per column (<= 64)
+  const uint32_t per_p = a.lanes * nch;
+  const uint32_t total = ncol * nch;
+  const uint32_t per_q = (total + 7) / 8;
+  uint32_t* qc = a.cnt + ncol;
+  uint32_t* exits = qc + 8;
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  const uint32_t row_stride = a.lanes * a.block;
+  uint32_t q = static_cast<uint32_t>(__builtin_amdgcn_s_getreg((15 << 11) | 20)) & 7u;  // HW_REG_XCC_ID
+  uint32_t tried = 0;
+  for (;;) {
+    uint32_t i = kNone;
+    while (tried < 8) {
+      uint32_t j = 0;
+      if (lane == 0) j = __hip_atomic_fetch_add(&qc[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      j = __builtin_amdgcn_readfirstlane(j);
+      if (j < per_q && q * per_q + j < total) {
+        i = q * per_q + j;
+        break;
+      }
+      q = (q + 1) & 7u;
+      ++tried;
+    }
+    if (i == kNone) break;
+    const uint32_t p = i / per_p, rem = i % per_p;
+    const uint32_t chunk = rem / a.lanes, l = rem % a.lanes;
+    const uint32_t col = p * a.lanes + l;
+    const uint32_t r0 = chunk * CR;                               // partition-relative first row of the item
+    const uint64_t prow0 = static_cast<uint64_t>(p) * a.rpp;      // the partition's first global row
+    const uint64_t row0 = prow0 + r0;
+    const uint32_t lane_b = l * a.block;
+    uint32_t carry = kNone, wlast = kNone;  // item-relative rows
+#pragma unroll 1
+    for (uint32_t nb_ = NBATCH; nb_ > 0; --nb_) {
+      const uint32_t rr = (nb_ - 1) * RB;
+      const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+      const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, RB * row_bytes);
+      v4f v[RB][VEC];
+#pragma unroll
+      for (int s = 0; s < RB; ++s)
+#pragma unroll
+        for (int qq = 0; qq < VEC; ++qq)
+          v[s][qq] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 src, s * row_bytes + (qq * 64 + lane) * 16, 0, kLoadAux));
+      const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + blk0 * a.block, a.out != nullptr ? RB * row_bytes : 0u);
+      uint32_t bits = 0;
+#pragma unroll
+      for (int s = 0; s < RB; ++s) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int qq = 0; qq < VEC; ++qq) o |= nz_bits(v[s][qq]);
+        bits |= static_cast<uint32_t>(wave_ballot(o != 0) != 0) << s;
+      }
+      const uint32_t need = bits | ((r0 + rr) == 0 ? 1u : 0u);  // + the lane head (client.cc:201-205)
+      if (!SKIP || need != 0) {
+#pragma unroll
+        for (int s = 0; s < RB; ++s) {
+          const uint32_t drop = ((need >> s) & 1u) ? 0u : kDropStore;
+#pragma unroll
+          for (int qq = 0; qq < VEC; ++qq)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][qq])),
+                                                   dst, (s * row_bytes + (qq * 64 + lane) * 16) | drop, 0, kStoreAux);
+        }
+      }
+      if (static_cast<uint32_t>(lane) < static_cast<uint32_t>(RB)) {
+        const uint64_t blk = blk0 + static_cast<uint64_t>(lane) * a.lanes;
+        if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>((bits >> lane) & 1u);
+        const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
+        const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : carry;
+        if (nr != kNone) a.next[blk] = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+        if (a.masks != nullptr && ((bits >> lane) & 1u))
+          (void)__hip_atomic_fetch_or(&a.masks[row0 + rr + lane], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (bits != 0) {
+        if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
+        carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
+      }
+    }
+    // the item's {first, last} non-zero row (partition-relative), then its arrival; the arrival waits for the
+    // summary's return, so the column's last arriver reads every item's summary
+    const uint32_t f_abs = carry == kNone ? kNone : r0 + carry;
+    const uint32_t l_abs = wlast == kNone ? kNone : r0 + wlast;
+    uint32_t old = 0;
+    if (lane == 0) {
+      const uint64_t prev = __hip_atomic_exchange(&a.summary[static_cast<uint64_t>(col) * nch + chunk],
+                                                  (static_cast<uint64_t>(f_abs) << 32) | l_abs, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      old = __hip_atomic_fetch_add(&a.cnt[col], 1u + static_cast<uint32_t>(prev == 0x5a5a5a5a5a5a5a5aull),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != nch - 1) continue;
+    // the column's last item: next offsets of every row whose successor lies in a later item
+    uint64_t sm = ~0ull;
+    if (static_cast<uint32_t>(lane) < nch)
+      sm = __hip_atomic_fetch_or(&a.summary[static_cast<uint64_t>(col) * nch + lane], 0ull, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t first = static_cast<uint32_t>(sm >> 32), last = static_cast<uint32_t>(sm);
+    uint32_t suf = first;  // inclusive suffix minimum over items >= lane
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = __shfl_down(suf, off, 64);
+      if (lane + off < 64) suf = o < suf ? o : suf;
+    }
+    uint32_t cy = __shfl_down(suf, 1, 64);  // first non-zero row in a later item
+    if (lane == 63) cy = kNone;
+    const uint32_t start = last == kNone ? static_cast<uint32_t>(lane) * CR : last;
+    for (uint32_t j = 0; j < nch; ++j) {
+      const uint32_t cj = __builtin_amdgcn_readlane(cy, j), sj = __builtin_amdgcn_readlane(start, j);
+      const uint32_t val = cj != kNone ? static_cast<uint32_t>(prow0 + cj) * row_stride + lane_b : a.sentinel + lane_b;
+      for (uint32_t r = sj + lane; r < (j + 1) * CR; r += 64) a.next[(prow0 + r) * a.lanes + l] = val;
+    }
+    if (lane == 0) __hip_atomic_store(&a.cnt[col], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (lane == 0) {
+    const uint32_t o = __hip_atomic_fetch_add(exits, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (o == gridDim.x * WAVES - 1) {  // every wave is out of the queues: re-arm them for the next launch
+      for (int k2 = 0; k2 < 8; ++k2) __hip_atomic_store(&qc[k2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// k_scan1s — k_scan1f at K = 2 with the two segments of a column on an XCD pair (study).  tools/wg_timeline.py shows
+// the odd XCDs stream 10-15 % slower than the even ones at config 3 whatever partition they read (the rotated map
+// moves the partitions, not the slowness).  Here XCD 2i takes segment 0 (rows [0, S0)) and XCD 2i+1 segment 1
+// (rows [S0, rpp)) of the same columns, with S0 = rpp * PM / 1000, so the slower XCD of each pair streams fewer rows.
+// K = 2 only; the column's second arriver writes the rows of segment 0 whose successor lies in segment 1.
+template <int VEC, int WAVES, int PM, int SKIP>
+__global__ __launch_bounds__(64 * WAVES) void k_scan1s(FusedArgs a) {
+  constexpr int RB = 16 / VEC;
+  __shared__ uint32_t s_wfirst[WAVES], s_wlast[WAVES];
+  __shared__ int s_fix;
+  __shared__ uint64_t s_sm[2];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = gridDim.x, bid = blockIdx.x;
+  const uint32_t x = bid % 8, jw = bid / 8;
+  const uint32_t k = x & 1u, col = (x >> 1) * (T / 8) + jw;
+  const uint32_t l = col % a.lanes, p = col / a.lanes;
+  const uint32_t S0 = ((a.rpp * PM / 1000) / RB) * RB;
+  const uint32_t r0 = k ? S0 : 0u, S = k ? a.rpp - S0 : S0;
+  const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;
+  const uint32_t row_bytes = a.lanes * a.block * 4;
+  const uint32_t lane_b = l * a.block;
+  const uint32_t row_stride = a.lanes * a.block;
+  const uint32_t rw = ((S + WAVES * RB - 1) / (WAVES * RB)) * RB;
+  const uint32_t lo = wave * rw < S ? wave * rw : S;
+  const uint32_t hi = lo + rw < S ? lo + rw : S;
+  uint32_t carry = kNone, wlast = kNone;
+  for (uint32_t nb_ = (hi - lo + RB - 1) / RB; nb_ > 0; --nb_) {
+    const uint32_t rr = lo + (nb_ - 1) * RB;
+    const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
+    const uint64_t blk0 = (row0 + rr) * a.lanes + l;
+    const __amdgpu_buffer_rsrc_t src = chunk_rsrc(a.x + blk0 * a.block, nrow * row_bytes);
+    v4f v[RB][VEC];
+#pragma unroll
+    for (int s = 0; s < RB; ++s)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                              src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
+    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + blk0 * a.block, a.out != nullptr ? nrow * row_bytes : 0u);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+      uint32_t o = 0;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) o |= nz_bits(v[s][q]);
+      bits |= static_cast<uint32_t>(wave_ballot(o != 0) != 0 && static_cast<uint32_t>(s) < nrow) << s;
+    }
+    const uint32_t need = bits | ((r0 + rr) == 0 ? 1u : 0u);
+    if (!SKIP || need != 0) {
+#pragma unroll
+      for (int s = 0; s < RB; ++s) {
+        const uint32_t drop = ((need >> s) & 1u) ? 0u : kDropStore;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
+                                                 dst, (s * row_bytes + (q * 64 + lane) * 16) | drop, 0, kStoreAux);
+      }
+    }
+    if (static_cast<uint32_t>(lane) < nrow) {
+      const uint64_t blk = blk0 + static_cast<uint64_t>(lane) * a.lanes;
+      if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>((bits >> lane) & 1u);
+      const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
+      const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : carry;
+      if (nr != kNone) a.next[blk] = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
+    }
+    if (bits != 0) {
+      if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
+      carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
+    }
+  }
+  if (lane == 0) {
+    s_wfirst[wave] = carry;
+    s_wlast[wave] = wlast;
+  }
+  __syncthreads();
+  uint32_t succ = kNone;
+  for (uint32_t w2 = wave + 1; w2 < WAVES; ++w2)
+    if (s_wfirst[w2] != kNone) {
+      succ = s_wfirst[w2];
+      break;
+    }
+  if (succ != kNone || k == 1) {
+    const uint32_t val = succ != kNone ? static_cast<uint32_t>(row0 + succ) * row_stride + lane_b : a.sentinel + lane_b;
+    for (uint32_t i = (wlast == kNone ? lo : wlast) + lane; i < hi; i += 64) a.next[(row0 + i) * a.lanes + l] = val;
+  }
+  if (threadIdx.x == 0) {
+    uint32_t first = kNone, last = 0;
+    for (uint32_t w2 = 0; w2 < WAVES; ++w2) {
+      if (first == kNone) first = s_wfirst[w2];
+      if (s_wlast[w2] != kNone) last = s_wlast[w2];
+    }
+    const uint64_t sm = (static_cast<uint64_t>(first) << 32) | (first == kNone ? kNone : last);
+    (void)__hip_atomic_exchange(&a.summary[static_cast<uint64_t>(col) * 2 + k], sm, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(&a.cnt[col], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_fix = (old == 1);
+    if (old == 1) {
+      s_sm[0] = __hip_atomic_fetch_or(&a.summary[static_cast<uint64_t>(col) * 2], 0ull, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+      s_sm[1] = __hip_atomic_fetch_or(&a.summary[static_cast<uint64_t>(col) * 2 + 1], 0ull, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.cnt[col], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!s_fix) return;
+  // rows of segment 0 at or after its last non-zero row: successor = segment 1's first non-zero row, else sentinel
+  const uint32_t last0 = static_cast<uint32_t>(s_sm[0]), first1 = static_cast<uint32_t>(s_sm[1] >> 32);
+  const uint64_t prow0 = static_cast<uint64_t>(p) * a.rpp;
+  const uint32_t val = first1 != kNone ? static_cast<uint32_t>(prow0 + S0 + first1) * row_stride + lane_b
+                                       : a.sentinel + lane_b;
+  for (uint32_t i = (last0 == kNone ? 0u : last0) + threadIdx.x; i < S0; i += blockDim.x)
+    a.next[(prow0 + i) * a.lanes + l] = val;
+}
+
 using Launch = void (*)(const Layout&, const FusedShape&, FusedArgs, hipStream_t);
 
 unsigned grid_of(const Layout& L, const FusedShape& f) {
@@ -895,6 +1154,30 @@ void go_w(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
 template <int VEC, int W, int ST, int CAP>
 void go_e(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   k_scan1e<VEC, W, 16, ST, CAP><<<grid_of(L, f), 64 * W, 0, st>>>(a);
+}
+template <int VEC, int W, int NBATCH, int SKIP>
+void go_q(const Layout& L, const FusedShape&, FusedArgs a, hipStream_t st) {
+  constexpr int RB = 16 / VEC;
+  if (L.rows_per_part % (RB * NBATCH) != 0 || L.rows_per_part / (RB * NBATCH) > 64) return;
+  int per_cu = 0, dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_scan1q<VEC, W, 16, NBATCH, SKIP>),
+                                                     64 * W, 0);
+  // K = partitions; arrival + queue counters at 128 KiB into the workspace (clear of the product's K > 1 state),
+  // summaries at 256 KiB
+  a.K = L.parts;
+  a.summary = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(a.cnt) + (256u << 10));
+  a.cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.cnt) + (128u << 10));
+  k_scan1q<VEC, W, 16, NBATCH, SKIP><<<static_cast<unsigned>(cus * (per_cu > 0 ? per_cu : 1)), 64 * W, 0, st>>>(a);
+}
+template <int VEC, int W, int PM, int SKIP>
+void go_s(const Layout& L, const FusedShape&, FusedArgs a, hipStream_t st) {
+  const uint64_t cols = static_cast<uint64_t>(L.parts) * L.lanes;
+  if (cols % 32 != 0) return;  // every XCD pair takes cols / 4 columns
+  a.cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.cnt) + (384u << 10));
+  a.summary = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(a.cnt) + (64u << 10));
+  k_scan1s<VEC, W, PM, SKIP><<<static_cast<unsigned>(cols * 2), 64 * W, 0, st>>>(a);
 }
 template <int VEC, int W>
 void go_r(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
@@ -953,6 +1236,22 @@ const Variant kVariants[] = {
     {"f meta st sc1", true, go_fm<1, 16, 0, 16>, go_fm<4, 16, 1, 16>},
     {"f meta st sc0", true, go_fm<1, 16, 0, 1>, go_fm<4, 16, 1, 1>},
     {"f meta st nt sc1", true, go_fm<1, 16, 0, 18>, go_fm<4, 16, 1, 18>},
+    {"f skip data st to one block (ablation)", false, go_f<1, 16, 16, 4, kStoreAux, 0>, go_f<4, 16, 16, 4, kStoreAux, 1>},
+    {"f skip -meta", false, go_f<1, 16, 16, 2, kStoreAux, 0>, go_f<4, 16, 16, 2, kStoreAux, 1>},
+    {"f skip -data", false, go_f<1, 16, 16, 1, kStoreAux, 0>, go_f<4, 16, 16, 1, kStoreAux, 1>},
+    {"f skip plain st", true, go_f<1, 16, 16, 0, 0, 0>, go_f<4, 16, 16, 0, 0, 1>},
+    {"f skip data to one block, plain st (ablation)", false, go_f<1, 16, 16, 4, 0, 0>, go_f<4, 16, 16, 4, 0, 1>},
+    {"timeline product", false, go_f<1, 16, 16, 8, kStoreAux, 0>, go_f<4, 16, 16, 8, kStoreAux, 1>},
+    {"timeline -data", false, go_f<1, 16, 16, 9, kStoreAux, 0>, go_f<4, 16, 16, 9, kStoreAux, 1>},
+    {"timeline -data-meta", false, go_f<1, 16, 16, 11, kStoreAux, 0>, go_f<4, 16, 16, 11, kStoreAux, 1>},
+    {"timeline -data-meta rotated", false, go_f<1, 16, 16, 27, kStoreAux, 0>, go_f<4, 16, 16, 27, kStoreAux, 1>},
+    {"s xcd pair 500", true, go_s<1, 16, 500, 0>, go_s<4, 16, 500, 1>},
+    {"s xcd pair 530", true, go_s<1, 16, 530, 0>, go_s<4, 16, 530, 1>},
+    {"s xcd pair 545", true, go_s<1, 16, 545, 0>, go_s<4, 16, 545, 1>},
+    {"s xcd pair 560", true, go_s<1, 16, 560, 0>, go_s<4, 16, 560, 1>},
+    {"q queues w4 CR32", true, go_q<1, 4, 2, 0>, go_q<4, 4, 8, 1>},
+    {"q queues w16 CR32", true, go_q<1, 16, 2, 0>, go_q<4, 16, 8, 1>},
+    {"q queues w4 CR64/32", true, go_q<1, 4, 4, 0>, go_q<4, 4, 8, 1>},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 }  // namespace
@@ -980,6 +1279,8 @@ int tune_run(int v, const float* x, float* out, int32_t* flags, uint32_t* next, 
   a.summary = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + ((cols * 4 + 15) / 16) * 16);
   a.lanes = L.lanes; a.rpp = L.rows_per_part; a.K = f.K; a.S = f.S; a.block = L.block;
   a.sentinel = omr_sentinel(L.block, L.lanes);
+  // timeline variants: per-workgroup timestamps in the second half of the workspace (in place of the row masks)
+  if (strncmp(kVariants[v].name, "timeline", 8) == 0) a.masks = reinterpret_cast<uint64_t*>(static_cast<char*>(ws) + (512u << 10));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (L.vec == 4) kVariants[v].v4(L, f, a, st);
   else if (L.vec == 1) kVariants[v].v1(L, f, a, st);
