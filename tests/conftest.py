@@ -21,6 +21,8 @@ def _ensure_built():
         subprocess.run(["make", "-C", PKG, "-s"], check=True)
     if have_hipcc and not os.path.exists(os.path.join(PKG, "bin", "omr_client")):
         subprocess.run(["make", "-C", PKG, "-s", "host"], check=True)  # ./omr_client, ./omr_server
+    if have_hipcc and not os.path.exists(os.path.join(ROOT, "tests", "integration", "worker_partition")):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "integration"), "-s"], check=True)
 
 
 def pytest_configure(config):
