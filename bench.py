@@ -254,7 +254,11 @@ def host_resident(args, ws, rank, local):
             "roofline": None,
             "pcie": {"per_rank_GBps": round(total.nbytes / (ms * 1e-3) / 1e9, 2),
                      "plain_h2d_GBps": round(h2d, 2), "plain_d2h_GBps": round(d2h, 2),
-                     "spec_GBps": 63.0, "note": "per rank: S in + S out over its own PCIe Gen5 x16 link"},
+                     "spec_GBps": 63.0,
+                     "write_back": ("staged: the whole bucket copied back" if os.environ.get("OMR_BUCKETS_STAGED_D2H")
+                                    else "zero-copy: the rounds store the write set (union + lane heads) into the "
+                                         "pinned buffer"),
+                     "note": "per rank, over its own PCIe Gen5 x16 link: S in, the write set out"},
             "cpu_baseline": None}), flush=True)
     if dist_mode:
         torch.distributed.destroy_process_group()

@@ -17,6 +17,7 @@
 #include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -1492,6 +1493,18 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   const uint64_t row_floats = static_cast<uint64_t>(p->lanes) * p->B;
   const bool rs = mode == OMR_ROUND_REDUCE_SCATTER;
   if (!p->worker()) return derr(OMR_EINVAL, "sparse_buckets: a worker's call (this rank aggregates only)");
+  // Write-back.  When the pinned buffer has a device mapping, each round writes its results straight into it: the
+  // unpack (all-reduce) or the shard sum (reduce-scatter) stores only the write-set blocks over PCIe, as the
+  // reference's worker copies only the blocks it gets back (client.cc:89), and every other block already holds its
+  // (all-zero) input.  Otherwise (or with OMR_BUCKETS_STAGED_D2H set) the bucket, or the rank's shard, is copied
+  // back whole from its staging buffer.
+  float* hdev = nullptr;
+  {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, hbuf, 0) == hipSuccess && d != nullptr) hdev = static_cast<float*>(d);
+    else (void)hipGetLastError();
+  }
+  const bool zc = hdev != nullptr && getenv("OMR_BUCKETS_STAGED_D2H") == nullptr;
   const bool own_rs = rs && p->shard >= 0;  // co-located: the shard's sums land in place
   const uint64_t back0 = own_rs ? p->bounds[p->shard] * row_floats : 0;
   const uint64_t back_n = rs ? (own_rs ? (p->bounds[p->shard + 1] - p->bounds[p->shard]) * row_floats : 0) : p->n;
@@ -1504,6 +1517,10 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   };
   auto d2h = [&](uint64_t k) -> int {  // after round k's second half, which is queued on the plan's stream
     const int r = static_cast<int>(k % R);
+    if (zc) {  // the results are already in host memory: the staging buffer is free once the second half is through
+      p->out_used[r] = true;
+      return hip_check(hipEventRecord(p->ev_out[r], p->cs), "hipEventRecord");
+    }
     TRY(hip_check(hipEventRecord(p->ev_round[r], p->cs), "hipEventRecord"));
     TRY(hip_check(hipStreamWaitEvent(p->s_out, p->ev_round[r], 0), "hipStreamWaitEvent"));
     if (back_n)
@@ -1520,7 +1537,8 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   for (uint64_t k = 0; k < K; ++k) {
     const int r = static_cast<int>(k % R);
     TRY(hip_check(hipStreamWaitEvent(st, p->ev_in[r], 0), "hipStreamWaitEvent"));
-    TRY(omr_sparse_round_f32(p, p->stage[r], p->stage[r], nullptr, nullptr, nullptr, rmode, &s1, &u1, stream));
+    TRY(omr_sparse_round_f32(p, p->stage[r], zc ? hdev + k * p->n : p->stage[r], nullptr, nullptr, nullptr, rmode,
+                             &s1, &u1, stream));
     acc();  // (the counts of bucket k - kDeferDepth, whose second half this call issued)
     if (k >= DD) TRY(d2h(k - DD));
     if (k + 1 < K) TRY(h2d(k + 1));
@@ -1533,6 +1551,7 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   }
   TRY(hip_check(hipStreamSynchronize(p->s_out), "hipStreamSynchronize"));  // the host buffer holds the result
   TRY(omr_ar_plan_join(p, stream));
+  if (zc) TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));  // (written by the rounds themselves)
   if (sent_blocks) *sent_blocks = sent;
   if (union_blocks) *union_blocks = uni;
   return 0;
