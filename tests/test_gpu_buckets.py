@@ -108,6 +108,14 @@ def test_buckets_loopback(gpu, world, mode, host, bucket_mib, total_mib):
     check(bufs, bms, L, world, mode, gpu)
 
 
+@pytest.mark.parametrize("world,mode", [(2, AR), (4, RS)])
+def test_buckets_loopback_staged_writeback(gpu, world, mode, monkeypatch):
+    """The previous write-back (each bucket, or the rank's shard, copied back whole from its staging buffer), kept
+    behind OMR_BUCKETS_STAGED_D2H for buffers without a device mapping."""
+    monkeypatch.setenv("OMR_BUCKETS_STAGED_D2H", "1")
+    test_buckets_loopback(gpu, world, mode, True, 16, 64)
+
+
 def test_buckets_reject_pageable(gpu):
     L = Layout.from_bytes(4 << 20, 256)
     D = cdist.load()
