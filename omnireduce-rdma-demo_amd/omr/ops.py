@@ -116,6 +116,25 @@ class ScanSumPlan:
         ws = lib.omr_scan_workspace_bytes(layout.n, layout.block_size, layout.num_lanes, layout.num_threads)
         self.workspace = torch.zeros(max(ws, 16), dtype=torch.uint8, device=device) if fused else None
 
+    def bind(self, buf: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None):
+        """The fused m = 1 launch with its arguments checked and converted once: returns a zero-argument callable
+        that issues omr_scan_sum_fused_f32 (one C call per step, for a host-light loop; raises on error)."""
+        if not self.fused or self.row_masks or self.m != 1:
+            raise ValueError("bind(): the fused m = 1 scan + sum only")
+        L = self.layout
+        _check_f32(buf, L.n, "buf")
+        if out is not None:
+            _check_f32(out, L.n, "out")
+        fn = _lib.load().omr_scan_sum_fused_f32
+        args = (_ptr(buf), L.n, L.block_size, L.num_lanes, L.num_threads, _ptr(self.flags), _ptr(self.next_offsets),
+                _ptr(out), _ptr(self.workspace), self.workspace.numel(), _stream(stream))
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                _lib.check(rc, "omr_scan_sum_fused_f32")
+        return launch
+
     def run(self, bufs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None, stream=None,
             with_next: bool = True, zero_masks: bool = True) -> ScanResult:
         """Fused scan (+ sum into `out`) and, unless with_next=False, the next-offset chains."""

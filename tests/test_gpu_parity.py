@@ -354,3 +354,26 @@ def test_fused_full_size(gpu, nbytes, B, r):
     assert (res.flags[0].cpu().numpy() == bm).all()
     assert (u32(res.next_offsets[0]) == oracle.next_offsets(bm, L.n, B, L.num_lanes, 8)).all()
     assert torch.equal(x, ref)  # 0.0f + x == x for these values: the in-place result is the input
+
+
+@pytest.mark.parametrize("B,density", [(256, 0.095), (1024, 0.0099)])
+def test_fused_bound_launch(gpu, B, density):
+    """ScanSumPlan.bind (bench.py's per-step launch, arguments converted once): the same flags, next offsets and
+    in-place sums as the oracle, over repeated launches on a side stream."""
+    L = Layout(n=4 << 20, block_size=B)
+    x_np = oracle.fill(oracle.gen_bitmap(2, density, L.nb), B, mode=1, seed=9)
+    x = torch.from_numpy(x_np.copy()).to(gpu)
+    plan = ops.ScanSumPlan(L, 1, device=gpu, fused=True)
+    st = torch.cuda.Stream()
+    launch = plan.bind(x, x, st)
+    for _ in range(3):
+        launch()
+    st.synchronize()
+    f = oracle.flags_from_data(x_np, B)
+    assert (plan.flags[0].cpu().numpy() == f).all()
+    assert (u32(plan.next_offsets[0]) == oracle.next_offsets(f, L.n, B, L.num_lanes, 8)).all()
+    exp = x_np.copy()
+    oracle.block_sum([x_np], L.n, B, L.num_lanes, 8, f, exp)
+    assert (x.cpu().numpy().view(np.uint32) == exp.view(np.uint32)).all()
+    with pytest.raises(ValueError):
+        ops.ScanSumPlan(L, 2, device=gpu).bind(x, x)
