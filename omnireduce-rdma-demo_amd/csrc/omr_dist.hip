@@ -757,6 +757,10 @@ struct omr_ar_plan {
   hipStream_t s_in = nullptr, s_out = nullptr;
   hipEvent_t ev_in[kStage] = {}, ev_round[kStage] = {}, ev_out[kStage] = {};
   bool out_used[kStage] = {false, false, false};
+  // set by omr_sparse_buckets_f32 for one round: the worker scan reads the gradient from here (the pinned host
+  // buffer, over PCIe) and writes its non-zero blocks and lane heads (0.0f + x) into the round's x, the staging
+  // buffer the rest of the round reads (a sum of 0.0f + x_w equals a sum of x_w bit for bit)
+  const float* scan_from = nullptr;
 };
 
 namespace {
@@ -1388,8 +1392,9 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   }
   if (p->worker()) {
     if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
-    TRY(omr_check(omr_worker_scan_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, nullptr, p->scan_ws,
-                                      p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+    TRY(omr_check(omr_worker_scan_f32(p->scan_from ? p->scan_from : x, p->n, p->B, p->lanes, p->parts, fl, nx, S.own,
+                                      p->scan_from ? const_cast<float*>(x) : nullptr, p->scan_ws, p->scan_ws_bytes,
+                                      stream), "omr_worker_scan_f32"));
     if (timed) {
       TRY(hip_check(hipEventRecord(p->timed[tslot].s1, st), "hipEventRecord"));
       p->timed[tslot].scan = true;
@@ -1505,6 +1510,11 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
     else (void)hipGetLastError();
   }
   const bool zc = hdev != nullptr && getenv("OMR_BUCKETS_STAGED_D2H") == nullptr;
+  // Read-in: each bucket is copied into a staging buffer (H2D on s_in).  With OMR_BUCKETS_SCAN_HOST=1 (and the
+  // mapping) the worker scan instead reads the bucket straight from the pinned buffer and leaves its non-zero blocks
+  // and lane heads in the staging buffer for the pack and the shard sum, so no copy engine runs.  That measured the
+  // same (config 5, N = 1: 35.9 against 36.3 GB/s), so the copy stays the default.
+  const bool zr = zc && getenv("OMR_BUCKETS_SCAN_HOST") != nullptr;
   const bool own_rs = rs && p->shard >= 0;  // co-located: the shard's sums land in place
   const uint64_t back0 = own_rs ? p->bounds[p->shard] * row_floats : 0;
   const uint64_t back_n = rs ? (own_rs ? (p->bounds[p->shard + 1] - p->bounds[p->shard]) * row_floats : 0) : p->n;
@@ -1533,15 +1543,22 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   // goes behind it, and frees its staging buffer for the H2D of bucket k + 1 (R = kDeferDepth + 1 buffers)
   static_assert(omr_ar_plan::kStage == omr_ar_plan::kDeferDepth + 1, "staging ring = deferral depth + 1");
   const uint64_t DD = static_cast<uint64_t>(p->defer_depth);  // <= kStage - 1
-  TRY(h2d(0));
+  if (!zr) TRY(h2d(0));
   for (uint64_t k = 0; k < K; ++k) {
     const int r = static_cast<int>(k % R);
-    TRY(hip_check(hipStreamWaitEvent(st, p->ev_in[r], 0), "hipStreamWaitEvent"));
-    TRY(omr_sparse_round_f32(p, p->stage[r], zc ? hdev + k * p->n : p->stage[r], nullptr, nullptr, nullptr, rmode,
-                             &s1, &u1, stream));
+    if (zr) {  // the scan refills stage[r]: the second half that last read it must be through
+      if (p->out_used[r]) TRY(hip_check(hipStreamWaitEvent(st, p->ev_out[r], 0), "hipStreamWaitEvent"));
+      p->scan_from = hdev + k * p->n;
+    } else {
+      TRY(hip_check(hipStreamWaitEvent(st, p->ev_in[r], 0), "hipStreamWaitEvent"));
+    }
+    const int rc = omr_sparse_round_f32(p, p->stage[r], zc ? hdev + k * p->n : p->stage[r], nullptr, nullptr,
+                                        nullptr, rmode, &s1, &u1, stream);
+    p->scan_from = nullptr;
+    TRY(rc);
     acc();  // (the counts of bucket k - kDeferDepth, whose second half this call issued)
     if (k >= DD) TRY(d2h(k - DD));
-    if (k + 1 < K) TRY(h2d(k + 1));
+    if (!zr && k + 1 < K) TRY(h2d(k + 1));
   }
   while (p->npend > 0) {  // the last buckets' second halves, oldest first, each followed by its D2H
     const uint64_t k = K - static_cast<uint64_t>(p->npend);

@@ -116,6 +116,14 @@ def test_buckets_loopback_staged_writeback(gpu, world, mode, monkeypatch):
     test_buckets_loopback(gpu, world, mode, True, 16, 64)
 
 
+@pytest.mark.parametrize("world,mode", [(2, AR), (3, RS)])
+def test_buckets_loopback_scan_from_host(gpu, world, mode, monkeypatch):
+    """OMR_BUCKETS_SCAN_HOST: the worker scan reads each bucket from the pinned buffer over PCIe and writes its
+    non-zero blocks into the staging buffer the rest of the round reads (no H2D copy)."""
+    monkeypatch.setenv("OMR_BUCKETS_SCAN_HOST", "1")
+    test_buckets_loopback(gpu, world, mode, True, 16, 64)
+
+
 def test_buckets_reject_pageable(gpu):
     L = Layout.from_bytes(4 << 20, 256)
     D = cdist.load()
