@@ -752,11 +752,15 @@ struct omr_ar_plan {
   std::string thread_err;
   HostTrace ht_thread;
   // omr_sparse_buckets_f32 on a pinned-host gradient: a ring of device staging buckets and two copy streams
-  static constexpr int kStage = 3;
-  float* stage[kStage] = {nullptr, nullptr, nullptr};
+  // kStage = kDeferDepth + 2: bucket k+1's H2D goes into the buffer of bucket k-3, whose second half (and
+  // write-back) was issued a call earlier than bucket k-2's, so the copy in overlaps the write-back out.  With
+  // kDeferDepth + 1 buffers the H2D waited for the second half issued just before it, and the two PCIe directions
+  // took turns (tools trace).
+  static constexpr int kStage = 4;
+  float* stage[kStage] = {};
   hipStream_t s_in = nullptr, s_out = nullptr;
   hipEvent_t ev_in[kStage] = {}, ev_round[kStage] = {}, ev_out[kStage] = {};
-  bool out_used[kStage] = {false, false, false};
+  bool out_used[kStage] = {};
   // set by omr_sparse_buckets_f32 for one round: the worker scan reads the gradient from here (the pinned host
   // buffer, over PCIe) and writes its non-zero blocks and lane heads (0.0f + x) into the round's x, the staging
   // buffer the rest of the round reads (a sum of 0.0f + x_w equals a sum of x_w bit for bit)
@@ -1539,9 +1543,9 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
     p->out_used[r] = true;
     return hip_check(hipEventRecord(p->ev_out[r], p->s_out), "hipEventRecord");
   };
-  // after call k, the second halves of buckets <= k - kDeferDepth are queued: the D2H of bucket k - kDeferDepth
-  // goes behind it, and frees its staging buffer for the H2D of bucket k + 1 (R = kDeferDepth + 1 buffers)
-  static_assert(omr_ar_plan::kStage == omr_ar_plan::kDeferDepth + 1, "staging ring = deferral depth + 1");
+  // after call k, the second halves of buckets <= k - kDeferDepth are queued: the write-back of bucket
+  // k - kDeferDepth goes behind it, and frees its staging buffer for the H2D of bucket k - kDeferDepth + R
+  static_assert(omr_ar_plan::kStage >= omr_ar_plan::kDeferDepth + 1, "staging ring >= deferral depth + 1");
   const uint64_t DD = static_cast<uint64_t>(p->defer_depth);  // <= kStage - 1
   if (!zr) TRY(h2d(0));
   for (uint64_t k = 0; k < K; ++k) {
