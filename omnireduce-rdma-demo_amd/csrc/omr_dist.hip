@@ -1516,8 +1516,8 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   const bool zc = hdev != nullptr && getenv("OMR_BUCKETS_STAGED_D2H") == nullptr;
   // Read-in: each bucket is copied into a staging buffer (H2D on s_in).  With OMR_BUCKETS_SCAN_HOST=1 (and the
   // mapping) the worker scan instead reads the bucket straight from the pinned buffer and leaves its non-zero blocks
-  // and lane heads in the staging buffer for the pack and the shard sum, so no copy engine runs.  That measured the
-  // same (config 5, N = 1: 35.9 against 36.3 GB/s), so the copy stays the default.
+  // and lane heads in the staging buffer for the pack and the shard sum, so no copy engine runs.  That measured
+  // slower (config 5, N = 1: 38.9 against 49.1 GB/s with the copy), so the copy stays the default.
   const bool zr = zc && getenv("OMR_BUCKETS_SCAN_HOST") != nullptr;
   const bool own_rs = rs && p->shard >= 0;  // co-located: the shard's sums land in place
   const uint64_t back0 = own_rs ? p->bounds[p->shard] * row_floats : 0;
