@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -135,6 +136,18 @@ int omr_host_scan_sum_f32(omr_host_plan* p, float* host_buf, int32_t* host_flags
   }
   const auto t0 = std::chrono::steady_clock::now();
   const uint64_t row_floats = static_cast<uint64_t>(p->lanes) * p->block;
+  // Write-back: with a device mapping of the pinned buffer, the scan stores its aggregated blocks (non-zero blocks
+  // and lane heads, the ones the reference's worker gets back: client.cc:89) straight into it, beside the copy
+  // engine's H2D of the next chunk; every other block is zero and unchanged.  Without one (or with
+  // OMR_HOST_STAGED_D2H set) each chunk is copied back whole.
+  float* hdev = nullptr;
+  {
+    void* d = nullptr;
+    if (getenv("OMR_HOST_STAGED_D2H") == nullptr && hipHostGetDevicePointer(&d, host_buf, 0) == hipSuccess && d)
+      hdev = static_cast<float*>(d);
+    else
+      (void)hipGetLastError();
+  }
   for (uint64_t k = 0; k < p->nchunks; ++k) {
     const uint64_t r0 = k * p->chunk_rows;
     const uint64_t r1 = (r0 + p->chunk_rows < p->rows) ? r0 + p->chunk_rows : p->rows;
@@ -144,8 +157,9 @@ int omr_host_scan_sum_f32(omr_host_plan* p, float* host_buf, int32_t* host_flags
     OMR_HIP(hipEventRecord(p->ev_in[k], p->s_in));
     OMR_HIP(hipStreamWaitEvent(p->s_cmp, p->ev_in[k], 0));
     if (int rc = omr_scan_sum_rows_f32(p->d_buf, p->n, p->block, p->lanes, p->parts, r0, r1, p->d_flags,
-                                       p->d_masks, p->d_buf, p->s_cmp))
+                                       p->d_masks, hdev ? hdev : p->d_buf, p->s_cmp))
       return fail_drain(p, rc, "omr_scan_sum_rows_f32");
+    if (hdev) continue;
     OMR_HIP(hipEventRecord(p->ev_cmp[k], p->s_cmp));
     OMR_HIP(hipStreamWaitEvent(p->s_out, p->ev_cmp[k], 0));
     OMR_HIP(hipMemcpyAsync(host_buf + off, p->d_buf + off, bytes, hipMemcpyDeviceToHost, p->s_out));
