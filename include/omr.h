@@ -308,8 +308,10 @@ int omr_msg_unpack_f32(const float* replies, const uint32_t* reply_imm, const vo
 /* ---------------------------------------------------------------- host-resident end-to-end path */
 
 /* The gradient lives in host memory (the reference's registered region, common.cc:873-914): H2D in row chunks,
- * in-place scan + aggregate of each landed chunk, D2H back into the same host buffer, overlapped on three HIP
- * streams; then the next-offset chains.  host_buf should be pinned (omr_host_register or hipHostMalloc).
+ * scan + aggregate of each landed chunk, whose aggregated blocks (non-zero blocks + lane heads, client.cc:89) the
+ * kernel stores straight into the pinned buffer through its device mapping while the next chunk comes in (without
+ * a mapping, or with OMR_HOST_STAGED_D2H set, each chunk is copied back whole); then the next-offset chains.
+ * host_buf should be pinned (omr_host_register or hipHostMalloc).
  * host_flags / host_next (may be NULL) receive the int32 flags / uint32 next offsets.  *seconds = wall time. */
 typedef struct omr_host_plan omr_host_plan;
 const char* omr_host_last_error(void);

@@ -146,10 +146,13 @@ int omr_ar_plan_exchange_time(omr_ar_plan* plan, float* ms, uint64_t* bytes_out,
  * one round per bucket with the next bucket's worker scan queued before the previous bucket's exchange
  * (OMR_ROUND_DEFER).  mode: OMR_ROUND_ALLREDUCE or OMR_ROUND_REDUCE_SCATTER (the rank's shard of every bucket).
  * buf is device memory, or PINNED HOST memory (the reference's registered region res->buf, common.cc:873-914, that
- * the worker fills and gets the results back in: client.cc:89, :401-421): then buckets are staged through a ring of
- * three device buffers, H2D of bucket k+1 and D2H of bucket k-2 on two copy streams beside bucket k's scan and
- * bucket k-1's exchange, and the call returns once the host buffer holds the result.  Device memory: returns with
- * the work enqueued on `stream` (joined).  *sent_blocks / *union_blocks: sums over the buckets. */
+ * the worker fills and gets the results back in: client.cc:89, :401-421): then buckets come in through a ring of
+ * four device buffers (H2D of bucket k+1 beside bucket k's scan and the earlier buckets' exchanges), each round
+ * stores its write set (union + lane heads; the shard's, for reduce-scatter) straight into the pinned buffer
+ * through its device mapping, and the call returns once the host buffer holds the result (a buffer without a
+ * mapping, or OMR_BUCKETS_STAGED_D2H set: each bucket, or the rank's shard, is copied back whole instead).  Device
+ * memory: returns with the work enqueued on `stream` (joined).  *sent_blocks / *union_blocks: sums over the
+ * buckets. */
 int omr_sparse_buckets_f32(omr_ar_plan* plan, float* buf, uint64_t total_n, int mode, uint64_t* sent_blocks,
                            uint64_t* union_blocks, omr_stream_t stream);
 /* Means over the OMR_ROUND_TIME_EXCHANGE rounds issued since the last call (at most the last 64): the worker scan
