@@ -1,7 +1,15 @@
-// fused_r02.hip — tuning harness (not the product), round 2: the decoupled-store single-pass kernel k_scan1d
-// (stores issued after the next batch's loads) against the product k_scan1f, with timing-only ablations (ABL bit 0:
-// no data stores, bit 1: no flag/next stores) and the pure read of the same geometry.  Timed side by side, in
-// place, by tools/tune_r02.py.
+// fused_r02.hip — tuning harness (not the product), round 2: variants of the single-pass worker step, each checked
+// bit for bit against the product k_scan1f (or marked timing-only) and timed side by side, in place, by
+// tools/tune_r02.py; per-workgroup timelines by tools/wg_timeline.py.  All measured slower or equal:
+//   k_scan1d  stores issued after the next batch's loads
+//   k_scan1g  a workgroup per row range owning all 16 lanes (B = 1024), contiguous flag/next runs
+//   k_scan1w  a writer wave: 15 waves only read, the 16th issues every store (LDS rings)
+//   k_scan1e  the workgroup's stores stashed in LDS and written after its last read
+//   k_scan1q  persistent waves and per-XCD work queues with stealing (XCD balancing)
+//   k_scan1s  K = 2 segments split unequally over an XCD pair (XCD balancing)
+// plus the product's ablations (ABL bits: no data stores, no flag/next stores, data stores to one block,
+// per-workgroup timestamps, rotated XCD map), flag/next store policies (MAUX), the pure read of the geometry and
+// flat mixed read/write probes.
 #define OMR_NO_CAPI
 #include "../omr_kernels.hip"
 
