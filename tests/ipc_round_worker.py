@@ -1,5 +1,6 @@
-"""One rank of the product's C++ round (libomr_dist.so) in its own process, over the HIP-IPC transport: launched
-by tests/test_gpu_ipc.py, several of these share the one GPU.  Writes this rank's outputs to an .npz file."""
+"""One rank of the product's C++ round (libomr_dist.so) in its own process: over the HIP-IPC transport, launched by
+tests/test_gpu_ipc.py (several of these share the one GPU), or over RCCL under torch.distributed.run, one rank per
+GPU (tests/test_gpu_rccl_multi.py, on nodes with enough GPUs).  Writes this rank's outputs to an .npz file."""
 import argparse
 import os
 import sys
@@ -17,10 +18,12 @@ from omr import Layout, cdist, ops  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--rank", type=int, required=True)
-    ap.add_argument("--world", type=int, required=True)
-    ap.add_argument("--uid", required=True, help="hex of the board id")
-    ap.add_argument("--n", type=int, required=True)
+    ap.add_argument("--transport", choices=("ipc", "rccl"), default="ipc",
+                    help="rccl: rank, world and the GPU from torch.distributed.run's environment")
+    ap.add_argument("--rank", type=int, default=-1)
+    ap.add_argument("--world", type=int, default=-1)
+    ap.add_argument("--uid", default="", help="hex of the board id (ipc)")
+    ap.add_argument("--n", "--floats", dest="n", type=int, required=True)  # --floats under torch.distributed.run
     ap.add_argument("--block", type=int, default=256)
     ap.add_argument("--density", type=float, default=0.1)
     ap.add_argument("--mode", type=int, default=0, help="OMR_ROUND_* (0 all-reduce, 1 reduce-scatter, 2 dense)")
@@ -33,12 +36,22 @@ def main():
     ap.add_argument("--workers", type=int, default=0, help="ranks >= this are dedicated aggregators (0: all workers)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda:0")
     L = Layout(n=a.n, block_size=a.block)
-    nw = a.workers or a.world
-    eng = cdist.CppSparseAllreduce(L, dev, transport="ipc", uid=bytes.fromhex(a.uid), rank=a.rank, world=a.world,
-                                   num_workers=nw)
+    if a.transport == "rccl":
+        a.rank, a.world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        torch.distributed.init_process_group("nccl", device_id=dev)
+        nw = a.workers or a.world
+        eng = cdist.CppSparseAllreduce(L, dev, num_workers=nw)
+        a.out = a.out.replace("RANK", str(a.rank))
+    else:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        nw = a.workers or a.world
+        eng = cdist.CppSparseAllreduce(L, dev, transport="ipc", uid=bytes.fromhex(a.uid), rank=a.rank, world=a.world,
+                                       num_workers=nw)
     worker = a.rank < nw
     # a different input per round (seed = rank, round): the pipelined rounds must not mix their buffers
     K = a.cycle or a.rounds
@@ -74,6 +87,8 @@ def main():
         arrs.update({f"out{r}": outs[r].cpu().numpy() for r in range(K)})
     np.savez(a.out, **arrs)
     eng.close()
+    if a.transport == "rccl":
+        torch.distributed.destroy_process_group()
     print(f"rank {a.rank} ok", flush=True)
 
 

@@ -63,6 +63,12 @@ def test_cpp_round_processes(gpu, tmp_path, world, pipe, mode, B, density, round
     L = Layout(n=2 << 20, block_size=B)
     K = min(rounds, 3)
     res = run_ranks(tmp_path, world, L.n, B, density, mode, pipe, rounds, cycle=K)
+    check_rounds(res, L, world, B, density, mode, rounds, K)
+
+
+def check_rounds(res, L, world, B, density, mode, rounds, K):
+    """Every rank's outputs of rounds 0..K-1 (inputs seeded rank + 10 round, as the worker makes them) against the
+    oracle: rank-order block sums, flags, next chains and the union chain of the last round."""
     NB, P = L.num_lanes, L.num_threads
     bounds = [s * L.rows // world for s in range(world + 1)]
     for rd in range(K):

@@ -1,0 +1,48 @@
+"""The product's C++ round over RCCL with one process per GPU (torch.distributed.run), as the N>1 bench runs it:
+two communicators (ncclCommSplit), the mask all-gather beside the grouped send/recv exchange, zero-byte pieces
+skipped on both sides, in the synchronous, asynchronous, deferred and progress-thread pipelines; every rank's outputs
+checked bit for bit against the oracle (test_gpu_ipc.check_rounds).  RCCL refuses two ranks on one GPU, so these
+run only where the node has the GPUs (skipped on a one-GPU box)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from omr import Layout
+from test_gpu_ipc import check_rounds
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "ipc_round_worker.py")
+
+
+@pytest.mark.parametrize("world,pipe,mode,B,density,rounds", [
+    (2, "sync", 0, 256, 0.095, 3),
+    (2, "defer", 1, 256, 0.2, 9),
+    (4, "async", 0, 1024, 0.05, 5),
+    (4, "defer", 0, 256, 0.3, 9),
+    (8, "defer", 1, 256, 0.095, 9),
+    (8, "thread", 0, 512, 0.095, 9),
+])
+def test_cpp_round_rccl_processes(gpu, tmp_path, world, pipe, mode, B, density, rounds):
+    if torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs (RCCL refuses two ranks on one GPU)")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    L = Layout(n=2 << 20, block_size=B)
+    K = min(rounds, 3)
+    out = str(tmp_path / "rankRANK.npz")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), WORKER, "--transport", "rccl",
+           "--floats", str(L.n), "--block", str(B), "--density", str(density), "--mode", str(mode), "--pipe", pipe,
+           "--rounds", str(rounds), "--cycle", str(K), "--out", out]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
+    res = [np.load(out.replace("RANK", str(r))) for r in range(world)]
+    check_rounds(res, L, world, B, density, mode, rounds, K)
