@@ -483,14 +483,11 @@ def test_bench_distributed_path_world1(gpu, extra):
     """bench.py's N>1 path as the driver launches it (torch.distributed.run, RCCL, the C++ round with two
     communicators, pipelined rounds joined before the closing sync), rehearsed at world 1."""
     import json
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     root = os.path.dirname(PKG)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--force-dist", "--no-cpu",
+    # --standalone: the rendezvous store binds a free port itself (a port probed here can be taken before torchrun
+    # binds it: EADDRINUSE)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes=1",
+           "--nproc-per-node", "1", os.path.join(root, "bench.py"), "--force-dist", "--no-cpu",
            "--steps", "5", "--warmup", "2", "--size-mib", "64"] + extra
     rc, out = _run(cmd, timeout=240)
     assert rc == 0, out[-3000:]
@@ -508,14 +505,9 @@ def test_bench_distributed_path_ipc(gpu, world, extra):
     over the HIP-IPC transport (gloo carries the id, barriers and the max-over-ranks time).  Rank 0's line reports
     the timed rounds' exchange with peers and non-zero bytes each way."""
     import json
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     root = os.path.dirname(PKG)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--force-dist",
+           "--standalone", "--local-addr", "127.0.0.1", os.path.join(root, "bench.py"), "--force-dist",
            "--dist-transport", "ipc", "--no-cpu", "--steps", "12", "--warmup", "2", "--size-mib", "64",
            "--event-every", "3"] + extra
     rc, out = _run(cmd, timeout=240)

@@ -4,7 +4,6 @@ skipped on both sides, in the synchronous, asynchronous, deferred and progress-t
 checked bit for bit against the oracle (test_gpu_ipc.check_rounds).  RCCL refuses two ranks on one GPU, so these
 run only where the node has the GPUs (skipped on a one-GPU box)."""
 import os
-import socket
 import subprocess
 import sys
 
@@ -31,15 +30,11 @@ WORKER = os.path.join(HERE, "ipc_round_worker.py")
 def test_cpp_round_rccl_processes(gpu, tmp_path, world, pipe, mode, B, density, rounds):
     if torch.cuda.device_count() < world:
         pytest.skip(f"needs {world} GPUs (RCCL refuses two ranks on one GPU)")
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     L = Layout(n=2 << 20, block_size=B)
     K = min(rounds, 3)
     out = str(tmp_path / "rankRANK.npz")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
-           "--master-addr", "127.0.0.1", "--master-port", str(port), WORKER, "--transport", "rccl",
+           "--standalone", "--local-addr", "127.0.0.1", WORKER, "--transport", "rccl",
            "--floats", str(L.n), "--block", str(B), "--density", str(density), "--mode", str(mode), "--pipe", pipe,
            "--rounds", str(rounds), "--cycle", str(K), "--out", out]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
