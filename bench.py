@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--cpu-warmups", type=int, default=10)
     p.add_argument("--cpu-threads", type=int, default=8)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-round", action="store_true",
+                   help="N=1: skip the round_world1 object (the N>1 round at world 1, measured after the headline)")
     p.add_argument("--pmc", default="",
                    help="rocprofv3 PMC summary giving HBM traffic per launch (default: the profiles/pmc_*.json "
                         "measured on this workload)")
@@ -192,6 +194,51 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
         "one_thread": {"value": round(L.nbytes / t1 / 1e9, 3), "unit": "GB/s", "ms_per_round": round(t1 * 1e3, 3)},
         "host": {"nproc": os.cpu_count(), "cpu_model": cpu_model},
     }
+
+
+def round_world1(args, L: Layout, sets, dev, stream):
+    """The N>1 step's own code path at N=1, measured after the headline's timed region (which it does not touch): the
+    C++ round (worker scan, mask all-gather, plan, exchange with no peers, shard sum over the whole tensor, deferred
+    pipeline as bench picks at world 1) over a one-rank RCCL communicator made in this process.  Its per-round time is
+    the like-for-like N=1 point of the 1 -> 8 curve, whose N>=2 lines time the same round."""
+    from omr import cdist
+    try:
+        eng = cdist.CppSparseAllreduce(L, dev, transport="rccl1")
+    except Exception as e:  # noqa: BLE001  (reported, the headline line still prints)
+        return {"error": str(e)[:300]}
+    outs = []
+    for xs, out in sets:
+        out.copy_(xs[0])  # out-of-place: the shard sums land in `out`, x stays the input
+        outs.append(out)
+    every = max(1, args.event_every)
+
+    def step(i, timed=False):
+        eng.run(sets[i % len(sets)][0][0], out=outs[i % len(sets)], mode=1, async_=True, defer=True,
+                time_exchange=timed and i % every == 0)
+
+    for i in range(args.warmup):
+        step(i)
+    eng.join(stream)
+    torch.cuda.synchronize()
+    eng.stage_timings()  # (discard the warm-up records)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, timed=True)
+    eng.join(stream)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    stages, _, _, n_timed = eng.stage_timings()
+    eng.close()
+    scan_ms = stages["scan"]
+    sb = scan_only_bytes(L)
+    return {"ms_per_round": round(dt * 1e3, 5), "value": round(L.nbytes / dt / 1e9, 2), "unit": "GB/s",
+            "mode": "reduce-scatter (the N>1 bench default), deferred pipeline (OMR_ROUND_DEFER)",
+            "transport": "RCCL, one-rank communicator in this process (no peers: nothing crosses xGMI)",
+            "scan_in_round": {"kernel_ms": round(scan_ms, 5), "algorithmic_bytes_per_launch": sb,
+                              "frac": round(sb / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if scan_ms > 0 else None},
+            "stages_ms": {k: round(v, 5) for k, v in stages.items()}, "timed_rounds": n_timed,
+            "note": ("the N=1 anchor of the per-GPU scaling fraction: the same round as the N>=2 lines (value = "
+                     "tensor bytes per round time), measured after the headline's timed region")}
 
 
 def host_resident(args, ws, rank, local):
@@ -522,6 +569,8 @@ def main():
         line["exchange"]["pipe"] = pipe
         if pipe_probe is not None:
             line["exchange"]["pipe_probe_ms_per_round"] = pipe_probe
+    if not dist_mode and m == 1 and not args.no_round:
+        line["round_world1"] = round_world1(args, L, sets, dev, stream)
     if not dist_mode and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(L, bitmaps[0], args)
     print(json.dumps(line), flush=True)

@@ -45,8 +45,10 @@ int omr_dist_create_rccl(const void* id, int rank, int world, omr_dist** out);
  * rank calls omr_dist_ipc_unique_id and shares the id out of band (the ./omr_server rendezvous does); every rank
  * then calls omr_dist_create_ipc, which returns once all have joined.  Data moves device to device (each receiver
  * copies out of the sender's IPC-mapped buffer); ordering is carried on the device by IPC events, so calls return
- * without synchronising any stream, as with RCCL.  Buffers handed to a round must stay allocated while the
- * transport lives (their IPC mappings are cached).  Destroy is collective. */
+ * without synchronising any stream, as with RCCL.  The transport caches IPC handles and peer mappings per allocation:
+ * a plan's own buffers are dropped from the cache when the plan is destroyed (a new plan on the same transport is
+ * mapped afresh), but buffers the caller hands to a round must stay allocated while the transport lives.  Destroy is
+ * collective. */
 int omr_dist_ipc_unique_id(void* id /* OMR_UNIQUE_ID_BYTES */);
 int omr_dist_create_ipc(const void* id, int rank, int world, omr_dist** out);
 
@@ -58,11 +60,26 @@ int omr_dist_rank(const omr_dist* d);
 int omr_dist_world(const omr_dist* d);
 int omr_dist_destroy(omr_dist* d);
 
+/* The transport's two operations, as the round uses them (every rank of the group calls them in the same order).
+ * omr_dist_allgather: out[p*bytes .. (p+1)*bytes) = rank p's `in` (device buffers).  omr_dist_exchange: send[p]
+ * (send_bytes[p]) to peer p and recv[p] (recv_bytes[p]) from peer p for every p != rank, entries at p == rank
+ * ignored, zero-byte pieces skipped; sizes must match the peer's.  Over RCCL these are ncclAllGather and one group of
+ * ncclSend/ncclRecv (the reference's post_send / post_receive loop, common.cc:374-476, on the communication channel).
+ * Both return with the transfer enqueued on `stream`. */
+int omr_dist_allgather(omr_dist* d, const void* in, void* out, size_t bytes, omr_stream_t stream);
+int omr_dist_exchange(omr_dist* d, void* const* send, const size_t* send_bytes, void* const* recv,
+                      const size_t* recv_bytes, omr_stream_t stream);
+/* Test hook: the next exchange on `d` (omr_dist_exchange or a round's) fails with OMR_EINVAL once it has issued
+ * `after_pieces` non-empty pieces (0: before the first; a negative value disarms).  The transport stays usable: the
+ * RCCL group is closed (the pieces already issued still run), the loopback and IPC transports still meet their
+ * peers.  Used to test that a failed exchange leaves no RCCL group open. */
+int omr_dist_inject_fault(omr_dist* d, int64_t after_pieces);
+
 /* Workspaces for tensors of n floats on the layout (block_size, num_lanes, num_parts); allocated on the current
  * HIP device, which must be the device the rank's tensors live on. */
 int omr_ar_plan_create(omr_dist* d, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
                        omr_ar_plan** out);
-int omr_ar_plan_destroy(omr_ar_plan* plan);
+int omr_ar_plan_destroy(omr_ar_plan* plan); /* before its transport (omr_dist_destroy) */
 /* The same with roles (the reference's m workers and n aggregators, README.md:13-22): ranks [0, num_workers) are
  * workers; if num_workers < world the other ranks are dedicated aggregators — the ./omr_server processes, holding no
  * tensor — aggregator j = rank num_workers + j owning row shard j of n = world - num_workers (rows [j*rows/n,

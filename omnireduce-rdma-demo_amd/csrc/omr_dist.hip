@@ -73,6 +73,15 @@ using Slices = std::vector<Slice>;  // several pieces to or from one peer, match
 
 struct omr_dist {
   int rank = 0, world = 1;
+  // omr_dist_inject_fault (test hook): the next exchange fails once it has issued `fault_after` non-empty pieces
+  int64_t fault_after = -1;
+  // called before each non-empty piece of an exchange (k = pieces issued so far) and once after the last (k = their
+  // count): fails the armed exchange at its k-th piece
+  int fault(int64_t k) {
+    if (fault_after < 0 || k < fault_after) return 0;
+    fault_after = -1;
+    return derr(OMR_EINVAL, "exchange: fault injected after %lld pieces (omr_dist_inject_fault)", static_cast<long long>(k));
+  }
   virtual ~omr_dist() = default;
   // out[p*bytes .. (p+1)*bytes) = rank p's `in`; `in` may alias out + rank*bytes
   virtual int allgather(const void* in, void* out, size_t bytes, hipStream_t st) = 0;
@@ -81,6 +90,8 @@ struct omr_dist {
   virtual int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) = 0;
   // out[0 .. count) = sum over ranks p of in_p[rank*count .. (rank+1)*count)  (dense stand-in)
   virtual int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) = 0;
+  // the allocation holding `ptr` is about to be freed: drop anything cached about it (called before hipFree)
+  virtual void forget(const void* ptr) { (void)ptr; }
 };
 
 namespace {
@@ -100,14 +111,23 @@ struct RcclDist final : omr_dist {
   }
   int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
     TRY(nccl_check(ncclGroupStart(), "ncclGroupStart"));
-    for (int p = 0; p < world; ++p) {
+    // The group is closed on every path: a group left open would capture every later RCCL call of this thread (the
+    // next round's all-gather and exchange would be queued into it and never launched).  After a failed piece the
+    // pieces already issued still go out with the group; the first error is returned.
+    int rc = 0;
+    int64_t k = 0;
+    for (int p = 0; p < world && rc == 0; ++p) {
       if (p == rank) continue;
       for (const Slice& r : recvs[p])
-        if (r.bytes) TRY(nccl_check(ncclRecv(r.ptr, r.bytes, ncclUint8, p, xcomm, st), "ncclRecv"));
+        if (r.bytes && rc == 0 && (rc = fault(k++)) == 0)
+          rc = nccl_check(ncclRecv(r.ptr, r.bytes, ncclUint8, p, xcomm, st), "ncclRecv");
       for (const Slice& t : sends[p])
-        if (t.bytes) TRY(nccl_check(ncclSend(t.ptr, t.bytes, ncclUint8, p, xcomm, st), "ncclSend"));
+        if (t.bytes && rc == 0 && (rc = fault(k++)) == 0)
+          rc = nccl_check(ncclSend(t.ptr, t.bytes, ncclUint8, p, xcomm, st), "ncclSend");
     }
-    return nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    if (rc == 0) rc = fault(k);
+    const int rc_end = nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    return rc ? rc : rc_end;
   }
   int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
     return nccl_check(ncclReduceScatter(in, out, count, ncclFloat32, ncclSum, xcomm, st), "ncclReduceScatter");
@@ -165,12 +185,14 @@ struct LocalDist final : omr_dist {
     b->posted_sends[rank] = sends;
     b->barrier();
     int rc = 0;
+    int64_t pieces = 0;
     for (int p = 0; p < world && rc == 0; ++p) {
       if (p == rank) continue;
       const Slices& from = b->posted_sends[p][rank];
       size_t k = 0;
       for (const Slice& r : recvs[p]) {
         if (r.bytes == 0) continue;
+        if ((rc = fault(pieces++)) != 0) break;
         while (k < from.size() && from[k].bytes == 0) ++k;
         if (k == from.size() || from[k].bytes != r.bytes) {
           rc = derr(OMR_EINVAL, "local exchange: rank %d expects %zu bytes from %d, peer posted %zu", rank, r.bytes, p,
@@ -182,7 +204,9 @@ struct LocalDist final : omr_dist {
         ++k;
       }
     }
+    if (rc == 0) rc = fault(pieces);
     if (rc == 0) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    else (void)hipStreamSynchronize(st);  // copies already queued finish before the peers move on
     b->barrier();  // every rank leaves together, even on an error (no peer is left waiting)
     return rc;
   }
@@ -233,6 +257,7 @@ struct IpcEntry {
 struct IpcPost {
   uint32_t nent, nh;
   hipIpcMemHandle_t h[kIpcMaxHandles];
+  uint64_t hid[kIpcMaxHandles];  // the poster's id of each handle's allocation (new after the allocation is forgotten)
   IpcEntry e[kIpcMaxEntries];
 };
 struct IpcRank {
@@ -281,8 +306,19 @@ struct IpcDist final : omr_dist {
   std::vector<std::array<IpcEvents, kIpcChans * 2>> peer;  // peers' events, opened, [p][c * 2 + g % 2]
   std::vector<hipEvent_t> retired;                         // events of old generations, destroyed in batches
   uint64_t seq[kIpcChans] = {0, 0};
-  std::map<std::pair<uintptr_t, size_t>, hipIpcMemHandle_t> own;  // allocation (base, size) -> its handle
-  std::map<std::string, char*> opened;                               // peer handle bytes -> mapped base
+  // allocation (base, size) -> its handle and this rank's id for it.  forget() drops an entry before the allocation is
+  // freed, so a later allocation at the same range is posted under a new id and the peers map it afresh
+  struct OwnHandle {
+    hipIpcMemHandle_t h;
+    uint64_t id;
+  };
+  std::map<std::pair<uintptr_t, size_t>, OwnHandle> own;
+  uint64_t next_id = 1;
+  struct Mapping {
+    uint64_t id;
+    char* base;
+  };
+  std::map<std::pair<int, std::string>, Mapping> opened;  // (peer, handle bytes) -> the mapping of its current id
 
   static void release(IpcEvents& e, std::vector<hipEvent_t>& to) {
     for (int k = 0; k < kIpcRing; ++k) {
@@ -300,7 +336,7 @@ struct IpcDist final : omr_dist {
       b->rank[rank].left.store(1, std::memory_order_release);
       for (int p = 0; p < world; ++p)
         (void)ipc_spin([&] { return b->rank[p].left.load(std::memory_order_acquire) != 0; }, "peers to leave", rank);
-      for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
+      for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second.base);
     }
     for (auto& v : peer)
       for (IpcEvents& e : v) release(e, retired);
@@ -406,34 +442,57 @@ struct IpcDist final : omr_dist {
   const IpcEvents& mine_of(int c, uint64_t s) const { return mine[c][gen_of(s) % 2]; }
   const IpcEvents& peer_of(int c, uint64_t s, int p) const { return peer[p][c * 2 + gen_of(s) % 2]; }
 
-  // the IPC handle of the allocation holding `ptr`, and ptr's offset in it
-  int handle_of(const void* ptr, hipIpcMemHandle_t* h, uint64_t* off) {
+  // the IPC handle of the allocation holding `ptr`, its id, and ptr's offset in it
+  int handle_of(const void* ptr, hipIpcMemHandle_t* h, uint64_t* id, uint64_t* off) {
     hipDeviceptr_t base = nullptr;
     size_t size = 0;
     TRY(hip_check(hipMemGetAddressRange(&base, &size, const_cast<void*>(ptr)), "hipMemGetAddressRange"));
     const auto key = std::make_pair(reinterpret_cast<uintptr_t>(base), size);
     auto it = own.find(key);
     if (it == own.end()) {
-      hipIpcMemHandle_t nh;
-      TRY(hip_check(hipIpcGetMemHandle(&nh, base), "hipIpcGetMemHandle"));
-      it = own.emplace(key, nh).first;
+      OwnHandle oh;
+      TRY(hip_check(hipIpcGetMemHandle(&oh.h, base), "hipIpcGetMemHandle"));
+      oh.id = next_id++;
+      it = own.emplace(key, oh).first;
     }
-    *h = it->second;
+    *h = it->second.h;
+    *id = it->second.id;
     *off = static_cast<uint64_t>(static_cast<const char*>(ptr) - static_cast<const char*>(base));
     return 0;
   }
 
-  int map(const IpcPost& post, const IpcEntry& e, char** out) {
+  void forget(const void* ptr) override {
+    if (ptr == nullptr) return;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, const_cast<void*>(ptr)) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    own.erase(std::make_pair(reinterpret_cast<uintptr_t>(base), size));
+  }
+
+  // peer p's piece: its allocation mapped once per id (a new id for the same handle bytes replaces the old mapping,
+  // whose allocation the peer has freed)
+  int map(int p, const IpcPost& post, const IpcEntry& e, char** out) {
     if (e.hidx >= post.nh) return derr(OMR_EINVAL, "ipc transport: bad handle index");
     const hipIpcMemHandle_t& h = post.h[e.hidx];
-    std::string key(reinterpret_cast<const char*>(&h), sizeof(h));
+    const uint64_t id = post.hid[e.hidx];
+    const auto key = std::make_pair(p, std::string(reinterpret_cast<const char*>(&h), sizeof(h)));
     auto it = opened.find(key);
-    if (it == opened.end()) {
-      void* p = nullptr;
-      TRY(hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle"));
-      it = opened.emplace(key, static_cast<char*>(p)).first;
+    if (it != opened.end() && it->second.id != id) {
+      // the stale mapping's last reads were queued behind this rank's earlier operations: let them finish first
+      TRY(hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize"));
+      (void)hipIpcCloseMemHandle(it->second.base);
+      opened.erase(it);
+      it = opened.end();
     }
-    *out = it->second + e.off;
+    if (it == opened.end()) {
+      void* mp = nullptr;
+      TRY(hip_check(hipIpcOpenMemHandle(&mp, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle"));
+      it = opened.emplace(key, Mapping{id, static_cast<char*>(mp)}).first;
+    }
+    *out = it->second.base + e.off;
     return 0;
   }
 
@@ -452,13 +511,14 @@ struct IpcDist final : omr_dist {
       if (it.second.bytes == 0) continue;
       if (P.nent == kIpcMaxEntries) return derr(OMR_EINVAL, "ipc transport: more than %d pieces", kIpcMaxEntries);
       hipIpcMemHandle_t h;
-      uint64_t off = 0;
-      TRY(handle_of(it.second.ptr, &h, &off));
+      uint64_t hid = 0, off = 0;
+      TRY(handle_of(it.second.ptr, &h, &hid, &off));
       uint32_t hi = 0;
-      while (hi < P.nh && memcmp(&P.h[hi], &h, sizeof(h)) != 0) ++hi;
+      while (hi < P.nh && P.hid[hi] != hid) ++hi;
       if (hi == P.nh) {
         if (P.nh == kIpcMaxHandles) return derr(OMR_EINVAL, "ipc transport: more than %d buffers", kIpcMaxHandles);
-        P.h[P.nh++] = h;
+        P.h[P.nh] = h;
+        P.hid[P.nh++] = hid;
       }
       P.e[P.nent++] = IpcEntry{it.first, hi, off, it.second.bytes};
     }
@@ -506,7 +566,7 @@ struct IpcDist final : omr_dist {
         rc = derr(OMR_EINVAL, "ipc allgather: rank %d offered %u pieces", p, P.nent);
         break;
       }
-      rc = map(P, P.e[0], &src);
+      rc = map(p, P, P.e[0], &src);
       if (rc == 0) rc = wait_ready(0, s, p, st);
       if (rc == 0) rc = hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
     }
@@ -522,6 +582,7 @@ struct IpcDist final : omr_dist {
     uint64_t s = 0;
     TRY(begin(1, st, items, &s));
     int rc = 0;
+    int64_t pieces = 0;
     for (int p = 0; p < world && rc == 0; ++p) {
       if (p == rank) continue;
       const IpcPost& P = post_of(1, s, p);
@@ -529,6 +590,7 @@ struct IpcDist final : omr_dist {
       bool waited = false;
       for (const Slice& r : recvs[p]) {
         if (r.bytes == 0) continue;
+        if ((rc = fault(pieces++)) != 0) break;
         while (k < P.nent && P.e[k].peer != static_cast<uint32_t>(rank)) ++k;
         if (k == P.nent || P.e[k].bytes != r.bytes) {
           rc = derr(OMR_EINVAL, "ipc exchange: rank %d expects %zu bytes from %d, peer offered %llu", rank, r.bytes,
@@ -536,7 +598,7 @@ struct IpcDist final : omr_dist {
           break;
         }
         char* src = nullptr;
-        rc = map(P, P.e[k], &src);
+        rc = map(p, P, P.e[k], &src);
         if (rc == 0 && !waited) {
           rc = wait_ready(1, s, p, st);
           waited = true;
@@ -546,7 +608,8 @@ struct IpcDist final : omr_dist {
         ++k;
       }
     }
-    const int rc2 = end(1, s, st);
+    if (rc == 0) rc = fault(pieces);
+    const int rc2 = end(1, s, st);  // always: peers wait for it
     return rc ? rc : rc2;
   }
 
@@ -566,7 +629,7 @@ struct IpcDist final : omr_dist {
         rc = derr(OMR_EINVAL, "ipc reduce_scatter: rank %d offered %u pieces", p, P.nent);
         break;
       }
-      rc = map(P, P.e[0], &src);
+      rc = map(p, P, P.e[0], &src);
       if (rc == 0) rc = wait_ready(1, s, p, st);
       ptrs[p] = reinterpret_cast<const float*>(src) + static_cast<size_t>(rank) * count;
     }
@@ -704,6 +767,7 @@ struct omr_ar_plan {
     // sums [, sums back, unpack] (communication stream)
     hipEvent_t s0 = nullptr, s1 = nullptr, x0 = nullptr, x1 = nullptr, q0 = nullptr, q1 = nullptr, a1 = nullptr;
     bool scan = false, xchg = false, prep = false, agg = false;
+    bool open = false;  // the round's second half has not run yet (deferred): the record is left unread
     uint64_t out = 0, in = 0;
   };
   static constexpr int kTimed = 64;
@@ -856,6 +920,30 @@ int omr_dist_destroy(omr_dist* d) {
   return 0;
 }
 
+int omr_dist_inject_fault(omr_dist* d, int64_t after_pieces) {
+  if (d == nullptr) return derr(OMR_EINVAL, "inject_fault: NULL");
+  d->fault_after = after_pieces < 0 ? -1 : after_pieces;
+  return 0;
+}
+
+int omr_dist_allgather(omr_dist* d, const void* in, void* out, size_t bytes, omr_stream_t stream) {
+  if (d == nullptr || (bytes > 0 && (in == nullptr || out == nullptr))) return derr(OMR_EINVAL, "allgather: NULL");
+  return d->allgather(in, out, bytes, reinterpret_cast<hipStream_t>(stream));
+}
+
+int omr_dist_exchange(omr_dist* d, void* const* send, const size_t* send_bytes, void* const* recv,
+                      const size_t* recv_bytes, omr_stream_t stream) {
+  if (d == nullptr || send == nullptr || send_bytes == nullptr || recv == nullptr || recv_bytes == nullptr)
+    return derr(OMR_EINVAL, "exchange: NULL");
+  std::vector<Slices> sends(d->world), recvs(d->world);
+  for (int p = 0; p < d->world; ++p) {
+    if (p == d->rank) continue;
+    sends[p] = {Slice{send[p], send_bytes[p]}};
+    recvs[p] = {Slice{recv[p], recv_bytes[p]}};
+  }
+  return d->exchange(sends, recvs, reinterpret_cast<hipStream_t>(stream));
+}
+
 int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p == nullptr) return 0;
   (void)thread_drain(p);
@@ -869,17 +957,25 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     (void)flush_pending(p, p->cs, nullptr, nullptr);
     (void)hipDeviceSynchronize();
   }
+  // (the transport forgets what it cached about each buffer first: its IPC handle)
   void* devs[] = {p->bounds_dev, p->recv, p->results, p->flags_ws, p->next_ws, p->unext_ws, p->scan_ws};
-  for (void* v : devs) (void)hipFree(v);
+  for (void* v : devs) {
+    if (v) p->d->forget(v);
+    (void)hipFree(v);
+  }
   for (auto& st : p->set) {
     void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed};
-    for (void* v : sv) (void)hipFree(v);
+    for (void* v : sv) {
+      if (v) p->d->forget(v);
+      (void)hipFree(v);
+    }
     for (hipEvent_t e : {st.scanned, st.planned, st.ready, st.done})
       if (e) (void)hipEventDestroy(e);
   }
   if (p->ps) (void)hipStreamDestroy(p->ps);
   if (p->cs) (void)hipStreamDestroy(p->cs);
   for (int r = 0; r < omr_ar_plan::kStage; ++r) {
+    if (p->stage[r]) p->d->forget(p->stage[r]);
     (void)hipFree(p->stage[r]);
     for (hipEvent_t e : {p->ev_in[r], p->ev_round[r], p->ev_out[r]})
       if (e) (void)hipEventDestroy(e);
@@ -1020,6 +1116,7 @@ int timed_slot(omr_ar_plan* p, int* slot) {
     for (hipEvent_t* e : {&t.s0, &t.s1, &t.x0, &t.x1, &t.q0, &t.q1, &t.a1})
       TRY(hip_check(hipEventCreate(e), "hipEventCreate"));
   t.scan = t.xchg = t.prep = t.agg = false;
+  t.open = true;
   *slot = k;
   return 0;
 }
@@ -1036,6 +1133,13 @@ int timed_exchange(omr_ar_plan* p, int slot) {
 
 int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, bool async, bool timed, uint32_t seq,
                  hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks, int tslot) {
+  struct CloseRecord {  // the timing record is complete (or abandoned) once this second half returns
+    omr_ar_plan* p;
+    int slot;
+    ~CloseRecord() {
+      if (slot >= 0) p->timed[slot].open = false;
+    }
+  } close_record{p, timed ? tslot : -1};
   omr_ar_plan::Set& S = p->set[si];
   const int N = p->N, M = p->M, NA = p->A, me = p->me, sh = p->shard;
   const uint64_t rows = p->rows, B = p->B;
@@ -1572,7 +1676,13 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   }
   TRY(hip_check(hipStreamSynchronize(p->s_out), "hipStreamSynchronize"));  // the host buffer holds the result
   TRY(omr_ar_plan_join(p, stream));
-  if (zc) TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));  // (written by the rounds themselves)
+  if (zc) {
+    // written by the rounds themselves through the buffer's device mapping: wait for the event recorded (with the
+    // default system-scope release) after the last bucket's second half on the communication stream, so the host
+    // sees every store on return, then for the caller's stream
+    TRY(hip_check(hipEventSynchronize(p->ev_out[(K - 1) % R]), "hipEventSynchronize"));
+    TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
+  }
   if (sent_blocks) *sent_blocks = sent;
   if (union_blocks) *union_blocks = uni;
   return 0;
@@ -1627,8 +1737,12 @@ int omr_ar_plan_stage_timings(omr_ar_plan* p, float* stage_ms, uint64_t* bytes_o
     ++cnt[k];
     return 0;
   };
-  for (uint32_t i = p->timed_first; i < p->timed_next; ++i) {
+  // (a deferred round whose exchange has not been issued yet stops the read: it and the later records stay unread
+  // until a later call, so their stages are never counted without their exchange)
+  uint32_t i = p->timed_first;
+  for (; i < p->timed_next; ++i) {
     omr_ar_plan::Timed& t = p->timed[i % omr_ar_plan::kTimed];
+    if (t.open) break;
     if (t.scan) TRY(add(0, t.s0, t.s1));
     if (t.prep) TRY(add(1, t.q0, t.q1));
     if (t.xchg) {
@@ -1638,7 +1752,7 @@ int omr_ar_plan_stage_timings(omr_ar_plan* p, float* stage_ms, uint64_t* bytes_o
     }
     if (t.agg) TRY(add(3, t.x1, t.a1));
   }
-  p->timed_first = p->timed_next;
+  p->timed_first = i;
   if (stage_ms)
     for (int k = 0; k < OMR_ROUND_STAGES; ++k) stage_ms[k] = cnt[k] ? static_cast<float>(sum[k] / cnt[k]) : 0.f;
   if (bytes_out) *bytes_out = cnt[2] ? bo / cnt[2] : 0;
@@ -1706,13 +1820,18 @@ namespace {
 constexpr uint32_t kMsgW = 2 * OMR_MESSAGE_SIZE;
 
 void msgd_free_logs(omr_msgd_plan* p) {
-  (void)hipFree(p->sched);
-  (void)hipFree(p->msgs);
-  (void)hipFree(p->imm);
-  (void)hipFree(p->reply);
-  (void)hipFree(p->rimm);
-  for (float* v : p->wmsgs) (void)hipFree(v);
-  for (uint32_t* v : p->wimm) (void)hipFree(v);
+  // the transport forgets the logs' IPC handles first (a regrown log may land at a freed one's addresses)
+  auto release = [&](void* v) {
+    if (v) p->d->forget(v);
+    (void)hipFree(v);
+  };
+  release(p->sched);
+  release(p->msgs);
+  release(p->imm);
+  release(p->reply);
+  release(p->rimm);
+  for (float* v : p->wmsgs) release(v);
+  for (uint32_t* v : p->wimm) release(v);
   p->sched = nullptr;
   p->msgs = nullptr;
   p->imm = nullptr;
@@ -1773,7 +1892,10 @@ int omr_msgd_plan_destroy(omr_msgd_plan* p) {
   (void)hipDeviceSynchronize();
   msgd_free_logs(p);
   void* devs[] = {p->own_masks, p->masks_all, p->umask, p->unext, p->flags, p->next, p->scan_ws, p->rounds, p->maxr};
-  for (void* v : devs) (void)hipFree(v);
+  for (void* v : devs) {
+    if (v) p->d->forget(v);
+    (void)hipFree(v);
+  }
   (void)hipHostFree(p->host_r);
   delete p;
   return 0;

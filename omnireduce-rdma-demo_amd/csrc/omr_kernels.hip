@@ -201,13 +201,9 @@ __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
 // the buffer range check.  The number of memory operations per batch is then static, so the compiler's vmcnt
 // wait for a load never includes a younger, data-dependent store (tools/tune_fused.py: 2-4 % faster than
 // branching around the stores; write-through sc0 sc1 beat plain, sc1-only and nt stores).
-// ABL (timing-only builds, csrc/tune/): bit 0 drops the data stores, bit 1 the flag/next stores, bit 2 sends every
-// data store of a batch to the same block at the start of `out` (the same store count, no scattered HBM writes), bit 3
-// records per-workgroup timestamps {start, loop end, end with stores acknowledged, XCC} in place of the row masks
-// (tools/wg_timeline.py), bit 4 rotates the workgroup -> column map by one XCD.  MINW: the
-// amdgpu_waves_per_eu floor (occupancy study; 1 = the compiler's choice).  SAUX: the block stores' cache policy
-// (store-policy study; the product's is kStoreAux).  SKIP: a batch with no block to write skips its (dropped) data
-// stores through a wave-uniform branch (the product's choice at B = 1024).
+// SKIP (the product's choice at B = 1024): a batch with no block to write skips its (dropped) data stores through a
+// wave-uniform branch.  (The timing-study form of this kernel, with its ablation / store-policy / timeline knobs, is
+// tools/tune/scan1f_study.h; it is not built into libomr.so.)
 struct FusedArgs {
   const float* x;
   float* out;
@@ -222,9 +218,8 @@ struct FusedArgs {
 
 constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
 
-template <int VEC, int WAVES, int LOADS = 16, int ABL = 0, int MINW = 1, int SAUX = kStoreAux, int SKIP = 0,
-          int MAUX = -1>
-__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW))) void k_scan1f(FusedArgs a) {
+template <int VEC, int WAVES, int LOADS = 16, int SKIP = 0>
+__global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
   constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
   static_assert(RB >= 1 && RB <= 32, "batch bits are 32-bit");
   __shared__ uint32_t s_wfirst[WAVES], s_wlast[WAVES];
@@ -234,15 +229,12 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t T = gridDim.x, bid = blockIdx.x;
-  const uint32_t lin0 = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
-  const uint32_t lin = (ABL & 16) ? (lin0 + T / 8) % T : lin0;  // ABL bit 4: every XCD takes the next XCD's columns
+  const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
   const uint32_t k = lin % a.K, col = lin / a.K + a.part0 * a.lanes;  // col: global (partition, lane) index
   const uint32_t l = col % a.lanes, p = col / a.lanes;
   const uint32_t r0 = k * a.S;                                  // segment's first row within the partition
   const uint64_t row0 = static_cast<uint64_t>(p) * a.rpp + r0;  // its global row
-  uint64_t* const tl = (ABL & 8) ? a.masks : nullptr;           // timing-only: per-workgroup timestamps
-  uint64_t* const masks = (ABL & 8) ? nullptr : a.masks;
-  if ((ABL & 8) && threadIdx.x == 0) tl[bid * 4] = __builtin_amdgcn_s_memrealtime();
+  uint64_t* const masks = a.masks;
   const uint32_t row_bytes = a.lanes * a.block * 4;
   const uint32_t lane_b = l * a.block;
   const uint32_t row_stride = a.lanes * a.block;
@@ -264,9 +256,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
       for (int q = 0; q < VEC; ++q)
         v[s][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
                                               src, s * row_bytes + (q * 64 + lane) * 16, 0, kLoadAux));
-    const __amdgpu_buffer_rsrc_t dst =
-        chunk_rsrc((ABL & 4) ? a.out : a.out + blk0 * a.block, (a.out != nullptr && !(ABL & 1)) ? nrow * row_bytes : 0u);
-    const uint32_t row_step = (ABL & 4) ? 0u : row_bytes;  // ABL bit 2: every row's store to the same block
+    const __amdgpu_buffer_rsrc_t dst = chunk_rsrc(a.out + blk0 * a.block, a.out != nullptr ? nrow * row_bytes : 0u);
+    const uint32_t row_step = row_bytes;
     uint32_t bits = 0;
 #pragma unroll
     for (int s = 0; s < RB; ++s) {
@@ -282,7 +273,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
 #pragma unroll
         for (int q = 0; q < VEC; ++q)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
-                                                 dst, (s * row_step + (q * 64 + lane) * 16) | drop, 0, SAUX);
+                                                 dst, (s * row_step + (q * 64 + lane) * 16) | drop, 0, kStoreAux);
       }
     }
     if constexpr (SKIP) {
@@ -295,26 +286,17 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
 #pragma unroll
           for (int q = 0; q < VEC; ++q)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, add4(v4f{0.f, 0.f, 0.f, 0.f}, v[s][q])),
-                                                   dst, (s * row_step + (q * 64 + lane) * 16) | drop, 0, SAUX);
+                                                   dst, (s * row_step + (q * 64 + lane) * 16) | drop, 0, kStoreAux);
         }
       }
     }
-    if (!(ABL & 2) && static_cast<uint32_t>(lane) < nrow) {
+    if (static_cast<uint32_t>(lane) < nrow) {
       const uint64_t blk = blk0 + static_cast<uint64_t>(lane) * a.lanes;
       // successor of row rr+lane: next set bit above it in this batch, else the carry (client.cc:19-31)
       const uint32_t above = static_cast<uint32_t>(static_cast<uint64_t>(bits) >> (lane + 1));
       const uint32_t nr = above != 0 ? rr + lane + 1 + static_cast<uint32_t>(__builtin_ctz(above)) : carry;
-      if constexpr (MAUX < 0) {
-        if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>((bits >> lane) & 1u);
-        if (nr != kNone) a.next[blk] = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
-      } else {  // study: the flag / next stores with cache policy MAUX (byte offsets < 2^31 in the study's sizes)
-        const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc(a.flags, 0, a.flags ? 0x7FFFFFFF : 0, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(a.next, 0, 0x7FFFFFFF, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32((bits >> lane) & 1u, rf, static_cast<uint32_t>(blk * 4), 0, MAUX);
-        if (nr != kNone)
-          __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(row0 + nr) * row_stride + lane_b, rn,
-                                                static_cast<uint32_t>(blk * 4), 0, MAUX);
-      }
+      if (a.flags != nullptr) a.flags[blk] = static_cast<int32_t>((bits >> lane) & 1u);
+      if (nr != kNone) a.next[blk] = static_cast<uint32_t>(row0 + nr) * row_stride + lane_b;
       if (masks != nullptr && ((bits >> lane) & 1u))
         (void)__hip_atomic_fetch_or(&masks[row0 + rr + lane], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -328,7 +310,6 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
     s_wlast[wave] = wlast;   // last one
   }
   __syncthreads();
-  if ((ABL & 8) && threadIdx.x == 0) tl[bid * 4 + 1] = __builtin_amdgcn_s_memrealtime();
   // tail rows [wlast or lo, hi): successor = first non-zero row of a later wave, else of a later segment
   uint32_t succ = kNone;
   for (uint32_t w2 = wave + 1; w2 < WAVES; ++w2)
@@ -336,17 +317,9 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(MINW
       succ = s_wfirst[w2];
       break;
     }
-  if (!(ABL & 2) && (succ != kNone || last_seg)) {
+  if (succ != kNone || last_seg) {
     const uint32_t val = succ != kNone ? static_cast<uint32_t>(row0 + succ) * row_stride + lane_b : a.sentinel + lane_b;
     for (uint32_t i = (wlast == kNone ? lo : wlast) + lane; i < hi; i += 64) a.next[(row0 + i) * a.lanes + l] = val;
-  }
-  if constexpr ((ABL & 8) != 0) {  // every store of the workgroup acknowledged
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      tl[bid * 4 + 2] = __builtin_amdgcn_s_memrealtime();
-      tl[bid * 4 + 3] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg((15 << 11) | 20));  // HW_REG_XCC_ID
-    }
   }
   if (a.K == 1) return;
   // multi-segment column: publish {first, last}, count arrivals; the last arriver fixes every tail row
@@ -421,7 +394,8 @@ __global__ __launch_bounds__(kWGThreads) void k_scanm(ScanArgs a) {
   static_assert(G % SUB == 0 && G <= 64 && SUB <= 32, "a unit is whole SUB-groups of one row");
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t gl = a.lanes < static_cast<uint32_t>(G) ? a.lanes : static_cast<uint32_t>(G);  // lanes per unit
+  // lanes per unit; the host picks SUB <= lanes (launch_scan), so a group never reaches into the next row
+  const uint32_t gl = a.lanes < static_cast<uint32_t>(G) ? a.lanes : static_cast<uint32_t>(G);
   const uint32_t upr = a.lanes / gl;  // units per row (1 or 2)
   const uint64_t units = a.rows * upr;
   const uint32_t T = gridDim.x, bid = blockIdx.x;
@@ -1340,7 +1314,7 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
     // B = 1024 (1 % non-zero at config 3): a batch of 4 rows rarely has a block to write, and skipping its
     // dropped-store issue altogether measured 1-2 % faster (profiles/r02/fused/tune_c3_skip*.log); at B = 256 the
     // static schedule is faster (most 16-row batches write something)
-    default: k_scan1f<4, kFusedWaves, kFusedLoads, 0, 1, kStoreAux, 1><<<grid, T, 0, st>>>(a); break;
+    default: k_scan1f<4, kFusedWaves, kFusedLoads, 1><<<grid, T, 0, st>>>(a); break;
   }
   return launch_status("k_scan1f");
 }
@@ -1369,9 +1343,18 @@ int launch_scan(const Layout& L, const ScanArgs& a, hipStream_t st) {
   const uint64_t units = L.rows * (L.lanes / gl);
   const unsigned gm = static_cast<unsigned>((units + kWavesPerWG - 1) / kWavesPerWG);
   (void)g;
+  // a group of SUB blocks must lie inside one row: rows narrower than the default group (B=256 with 16 lanes, B=512
+  // with 8) take the half-width group (make_layout admits them)
+  const bool narrow = L.lanes < static_cast<uint32_t>(32 / L.vec);
   switch (L.vec) {
-    case 1: k_scanm<1, 32, kScanmUnitLanes><<<gm, kWGThreads, 0, st>>>(a); break;
-    case 2: k_scanm<2, 16, kScanmUnitLanes><<<gm, kWGThreads, 0, st>>>(a); break;
+    case 1:
+      if (narrow) k_scanm<1, 16, kScanmUnitLanes><<<gm, kWGThreads, 0, st>>>(a);
+      else k_scanm<1, 32, kScanmUnitLanes><<<gm, kWGThreads, 0, st>>>(a);
+      break;
+    case 2:
+      if (narrow) k_scanm<2, 8, kScanmUnitLanes><<<gm, kWGThreads, 0, st>>>(a);
+      else k_scanm<2, 16, kScanmUnitLanes><<<gm, kWGThreads, 0, st>>>(a);
+      break;
     default: k_scanm<4, 8, kScanmUnitLanes><<<gm, kWGThreads, 0, st>>>(a); break;
   }
   return launch_status("k_scanm");

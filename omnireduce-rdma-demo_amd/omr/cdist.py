@@ -44,6 +44,9 @@ def load():
         "omr_dist_rank": (i, [vp]),
         "omr_dist_world": (i, [vp]),
         "omr_dist_destroy": (i, [vp]),
+        "omr_dist_allgather": (i, [vp, vp, vp, ctypes.c_size_t, vp]),
+        "omr_dist_exchange": (i, [vp, vp, vp, vp, vp, vp]),
+        "omr_dist_inject_fault": (i, [vp, ctypes.c_int64]),
         "omr_ar_plan_create": (i, [vp, u64, u32, u32, u32, vp]),
         "omr_ar_plan_destroy": (i, [vp]),
         "omr_ar_plan_create_roles": (i, [vp, u32, u64, u32, u32, u32, vp]),
@@ -83,7 +86,9 @@ class CppSparseAllreduce:
     """One rank of the C++ round.  transport "rccl" (default): one process per GPU, the torch.distributed default
     group supplies rank/world and the unique-id broadcast.  transport "ipc": ranks are processes of one node sharing
     any GPUs (omr_dist_create_ipc); rank, world and the id (ipc_unique_id() of one rank) are passed in.  transport
-    "local1": a group of one rank (the round with no peers), e.g. for the single-GPU host-resident bench."""
+    "local1": a group of one rank (the round with no peers), e.g. for the single-GPU host-resident bench.  transport
+    "rccl1": a one-rank RCCL communicator made in this process (no torch.distributed group): the N>1 bench path's
+    round with no peers, e.g. bench.py's world-1 round line."""
 
     def __init__(self, L: Layout, device, group=None, transport: str = "rccl", uid: Optional[bytes] = None,
                  rank: Optional[int] = None, world: Optional[int] = None, num_workers: Optional[int] = None):
@@ -98,6 +103,11 @@ class CppSparseAllreduce:
             rank, world = 0, 1
             self._board = D.omr_local_board_create(1)
             _check(D.omr_dist_create_local(self._board, 0, ctypes.byref(self._d)), "omr_dist_create_local")
+        elif transport == "rccl1":
+            rank, world = 0, 1
+            uid = (ctypes.c_ubyte * UNIQUE_ID_BYTES)()
+            _check(D.omr_dist_unique_id(uid), "omr_dist_unique_id")
+            _check(D.omr_dist_create_rccl(uid, 0, 1, ctypes.byref(self._d)), "omr_dist_create_rccl")
         elif transport == "ipc":
             if uid is None or rank is None or world is None:
                 raise ValueError("the ipc transport needs uid, rank and world")
@@ -115,9 +125,21 @@ class CppSparseAllreduce:
             _check(D.omr_dist_create_rccl(uidt.data_ptr(), rank, world, ctypes.byref(self._d)), "omr_dist_create_rccl")
         self._p = ctypes.c_void_p()
         nw = world if num_workers is None else num_workers
-        _check(D.omr_ar_plan_create_roles(self._d, nw, L.n, L.block_size, L.num_lanes, L.num_threads,
-                                          ctypes.byref(self._p)), "omr_ar_plan_create_roles")
         self.rank, self.world, self.num_workers = rank, world, nw
+        self._plan()
+
+    def _plan(self):
+        L = self.L
+        _check(load().omr_ar_plan_create_roles(self._d, self.num_workers, L.n, L.block_size, L.num_lanes,
+                                               L.num_threads, ctypes.byref(self._p)), "omr_ar_plan_create_roles")
+
+    def replan(self):
+        """Destroy the plan and make a new one of the same shape on the same transport (collective: every rank calls
+        it).  The new plan's buffers may land at the old ones' addresses: the transport must not reuse what it cached
+        about the freed ones (the IPC transport's handles)."""
+        load().omr_ar_plan_destroy(self._p)
+        self._p = ctypes.c_void_p()
+        self._plan()
 
     ALLREDUCE, REDUCE_SCATTER, DENSE_REDUCE_SCATTER, ASYNC, TIME_EXCHANGE, DEFER = 0, 1, 2, 0x100, 0x200, 0x400
     THREAD = 0x800
@@ -208,6 +230,30 @@ class CppSparseAllreduce:
         """Make `stream` (default: the current stream) wait for every asynchronous round issued so far."""
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         _check(load().omr_ar_plan_join(self._p, st.cuda_stream), "omr_ar_plan_join")
+
+    def inject_fault(self, after_pieces: int = 0):
+        """Test hook (omr_dist_inject_fault): the next exchange fails after issuing `after_pieces` pieces."""
+        _check(load().omr_dist_inject_fault(self._d, after_pieces), "omr_dist_inject_fault")
+
+    def allgather(self, src: torch.Tensor, dst: torch.Tensor, stream=None):
+        """The transport's all-gather of src.nbytes per rank into dst (omr_dist_allgather)."""
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(load().omr_dist_allgather(self._d, src.data_ptr(), dst.data_ptr(), src.numel() * src.element_size(),
+                                         st.cuda_stream), "omr_dist_allgather")
+
+    def exchange(self, sends, recvs, stream=None) -> int:
+        """One grouped exchange (omr_dist_exchange): sends[p] to peer p, recvs[p] from peer p (tensors or None).
+        Returns the C return code instead of raising (the fault-injection tests look at it)."""
+        W = self.world
+        sp, sb = (ctypes.c_void_p * W)(), (ctypes.c_size_t * W)()
+        rp, rb = (ctypes.c_void_p * W)(), (ctypes.c_size_t * W)()
+        for p in range(W):
+            if sends[p] is not None:
+                sp[p], sb[p] = sends[p].data_ptr(), sends[p].numel() * sends[p].element_size()
+            if recvs[p] is not None:
+                rp[p], rb[p] = recvs[p].data_ptr(), recvs[p].numel() * recvs[p].element_size()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return load().omr_dist_exchange(self._d, sp, sb, rp, rb, st.cuda_stream)
 
     def close(self):
         D = load()

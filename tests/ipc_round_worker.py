@@ -34,6 +34,9 @@ def main():
                     help="round r runs input (and output buffer) r mod cycle (0: one of each per round); a long run "
                          "thus reuses its buffers as a training loop does")
     ap.add_argument("--workers", type=int, default=0, help="ranks >= this are dedicated aggregators (0: all workers)")
+    ap.add_argument("--replan", action="store_true",
+                    help="run the rounds, destroy the plan, make a new one on the same transport and run them again "
+                         "(the saved outputs are the second plan's)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     L = Layout(n=a.n, block_size=a.block)
@@ -69,6 +72,19 @@ def main():
     nxt = torch.zeros(L.nb, dtype=torch.int32, device=dev)
     unx = torch.empty(L.nb, dtype=torch.int32, device=dev)
     sums = {}
+    if a.replan:
+        for r in range(a.rounds):
+            eng.run(xs[r % K], out=outs[r % K], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
+                    async_=a.pipe != "sync", defer=a.pipe in ("defer", "thread"), thread=a.pipe.startswith("thread"))
+        eng.join()
+        torch.cuda.synchronize()
+        eng.replan()
+        for r in range(K):
+            if outs[r] is not None:
+                outs[r].copy_(xs[r])
+        flags.zero_()
+        nxt.zero_()
+        unx.zero_()
     for r in range(a.rounds):
         eng.run(xs[r % K], out=outs[r % K], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
                 async_=a.pipe != "sync", defer=a.pipe in ("defer", "thread"), thread=a.pipe.startswith("thread"))

@@ -19,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "ipc_round_worker.py")
 
 
-def run_ranks(tmp_path, world, n, B, density, mode, pipe, rounds=3, workers=0, cycle=0):
+def run_ranks(tmp_path, world, n, B, density, mode, pipe, rounds=3, workers=0, cycle=0, extra=()):
     uid = cdist.ipc_unique_id().hex()
     procs, outs = [], []
     for r in range(world):
@@ -27,7 +27,7 @@ def run_ranks(tmp_path, world, n, B, density, mode, pipe, rounds=3, workers=0, c
         outs.append(out)
         cmd = [sys.executable, WORKER, "--rank", str(r), "--world", str(world), "--uid", uid, "--n", str(n),
                "--block", str(B), "--density", str(density), "--mode", str(mode), "--pipe", pipe,
-               "--rounds", str(rounds), "--workers", str(workers), "--cycle", str(cycle), "--out", out]
+               "--rounds", str(rounds), "--workers", str(workers), "--cycle", str(cycle), "--out", out] + list(extra)
         procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     logs = []
     for p in procs:
@@ -64,6 +64,16 @@ def test_cpp_round_processes(gpu, tmp_path, world, pipe, mode, B, density, round
     K = min(rounds, 3)
     res = run_ranks(tmp_path, world, L.n, B, density, mode, pipe, rounds, cycle=K)
     check_rounds(res, L, world, B, density, mode, rounds, K)
+
+
+@pytest.mark.parametrize("world,pipe,mode", [(2, "sync", 0), (3, "defer", 1)])
+def test_cpp_round_processes_replan(gpu, tmp_path, world, pipe, mode):
+    """A plan destroyed and re-created on the same IPC transport: the new plan's buffers may reuse the old ones'
+    addresses, so the transport must post them under new ids and its peers must map them afresh (a
+    stale cached handle or mapping would move the old allocation's bytes without an error)."""
+    L = Layout(n=2 << 20, block_size=256)
+    res = run_ranks(tmp_path, world, L.n, 256, 0.2, mode, pipe, 3, cycle=3, extra=["--replan"])
+    check_rounds(res, L, world, 256, 0.2, mode, 3, 3)
 
 
 def check_rounds(res, L, world, B, density, mode, rounds, K):

@@ -104,6 +104,18 @@ def test_random_values_parity(gpu, B, m):
     assert_parity(_rand_sparse(L, 0.3, 11 * m + B, m), L)
 
 
+@pytest.mark.parametrize("B,slots,m", [(256, 4, 2), (512, 4, 2), (256, 4, 5), (512, 4, 8), (1024, 8, 3)])
+def test_narrow_rows_multi_worker(gpu, B, slots, m):
+    """Rows narrower than k_scanm's default block group (16 lanes at B=256, 8 at B=512: layouts the C ABI admits) take
+    the half-width group, so no group reaches into the next row; the last row is checked too."""
+    L = Layout(n=1 << 19, block_size=B, num_slots=slots)
+    assert L.num_lanes == slots * 1024 // B
+    bufs = _rand_sparse(L, 0.4, 7 * m + B, m)
+    for b in bufs:  # the last block of the tensor non-zero on every worker
+        b[-B:] = 1.0
+    assert_parity(bufs, L)
+
+
 def test_all_zero(gpu):
     L = Layout(n=1 << 20)
     res, out = assert_parity([np.zeros(L.n, dtype=np.float32)], L)

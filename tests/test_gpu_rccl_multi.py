@@ -41,3 +41,29 @@ def test_cpp_round_rccl_processes(gpu, tmp_path, world, pipe, mode, B, density, 
     assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
     res = [np.load(out.replace("RANK", str(r))) for r in range(world)]
     check_rounds(res, L, world, B, density, mode, rounds, K)
+
+
+C4_WORKER = os.path.join(HERE, "rccl_c4_worker.py")
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("case,extra", [
+    ("c4", ["--rounds", "5"]),                 # BASELINE config 4: 8 x 256 MiB, -r 0.095, reduce-scatter + all-reduce
+    ("buckets", ["--total-mib", "1024"]),      # config 5's path: pinned host, 256 MiB buckets, -r 0.49
+])
+def test_rccl_world8_full_size(gpu, tmp_path, case, extra):
+    """The round over RCCL at BASELINE config 4's own size (256 MiB per rank, world 8, deferred rounds), every summed
+    block checked against the known answer ka[count] and the chains against the oracle; and the bucketed
+    pinned-host path at world 8.  Skipped below 8 GPUs."""
+    world = 8
+    if torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs (RCCL refuses two ranks on one GPU)")
+    out = str(tmp_path / "rankRANK.txt")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--standalone", "--local-addr", "127.0.0.1", C4_WORKER, "--case", case, "--out", out] + extra
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, (p.stdout + p.stderr)[-4000:]
+    for r in range(world):
+        with open(out.replace("RANK", str(r))) as f:
+            msg = f.read()
+        assert msg == "ok", f"rank {r}: {msg[-3000:]}"

@@ -11,7 +11,8 @@
 // per-workgroup timestamps, rotated XCD map), flag/next store policies (MAUX), the pure read of the geometry and
 // flat mixed read/write probes.
 #define OMR_NO_CAPI
-#include "../omr_kernels.hip"
+#include "../../omnireduce-rdma-demo_amd/csrc/omr_kernels.hip"
+#include "scan1f_study.h"
 
 namespace {
 // k_scan1d — k_scan1f with decoupled stores (study; slower on MI355X: profiles/r02/tune_r02_*.log).
@@ -1144,12 +1145,12 @@ unsigned occ_lds(K kern) {
 }
 template <int VEC, int W, int LD, int ABL, int SAUX = kStoreAux, int SKIP = 0>
 void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
-  const unsigned lds = occ_lds(&k_scan1f<VEC, W, LD, ABL, 1, SAUX, SKIP>);
-  k_scan1f<VEC, W, LD, ABL, 1, SAUX, SKIP><<<grid_of(L, f), 64 * W, lds, st>>>(a);
+  const unsigned lds = occ_lds(&k_scan1f_study<VEC, W, LD, ABL, 1, SAUX, SKIP>);
+  k_scan1f_study<VEC, W, LD, ABL, 1, SAUX, SKIP><<<grid_of(L, f), 64 * W, lds, st>>>(a);
 }
 template <int VEC, int W, int SKIP, int MAUX>
 void go_fm(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
-  k_scan1f<VEC, W, 16, 0, 1, kStoreAux, SKIP, MAUX><<<grid_of(L, f), 64 * W, 0, st>>>(a);
+  k_scan1f_study<VEC, W, 16, 0, 1, kStoreAux, SKIP, MAUX><<<grid_of(L, f), 64 * W, 0, st>>>(a);
 }
 template <int VEC, int W, int LD, int P, int ABL>
 void go_d(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {

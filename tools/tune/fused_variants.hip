@@ -3,7 +3,8 @@
 // source, and the split-batch study kernel k_scan1s, timed side by side by tools/tune_fused.py
 // (profiles/r01/tune_round1_session4.md).
 #define OMR_NO_CAPI
-#include "../omr_kernels.hip"
+#include "../../omnireduce-rdma-demo_amd/csrc/omr_kernels.hip"
+#include "scan1f_study.h"
 
 namespace {
 // k_scan1s — k_scan1f with SPLIT batch ownership (study): batch j (RB rows of the column segment) belongs to wave
@@ -328,7 +329,7 @@ namespace {
 template <int VEC, int W, int LOADS, int ABL, int MINW = 1, int SAUX = kStoreAux>
 void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(L.parts) * L.lanes * f.K);
-  k_scan1f<VEC, W, LOADS, ABL, MINW, SAUX><<<grid, 64 * W, 0, st>>>(a);
+  k_scan1f_study<VEC, W, LOADS, ABL, MINW, SAUX><<<grid, 64 * W, 0, st>>>(a);
 }
 
 struct Variant {

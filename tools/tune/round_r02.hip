@@ -7,7 +7,8 @@
 // tools/tune_round_r02.py times both (and the product's pack, k_move) at an 8-worker shard and at world 1, and checks
 // the variant against the product bit for bit.
 #define OMR_NO_CAPI
-#include "../omr_kernels.hip"
+#include "../../omnireduce-rdma-demo_amd/csrc/omr_kernels.hip"
+#include "scan1f_study.h"
 
 namespace {
 

@@ -8,7 +8,8 @@
 // as a G/8-byte store.  tools/tune_scanm_r02.py times the variants side by side (and with worker buffers staggered
 // inside one allocation, the channel-contention test) and checks every variant against the product bit for bit.
 #define OMR_NO_CAPI
-#include "../omr_kernels.hip"
+#include "../../omnireduce-rdma-demo_amd/csrc/omr_kernels.hip"
+#include "scan1f_study.h"
 
 namespace {
 

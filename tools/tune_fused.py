@@ -15,7 +15,7 @@ import torch  # noqa: E402
 
 from omr import Layout, ops  # noqa: E402
 
-SRC = os.path.join(ROOT, "omnireduce-rdma-demo_amd", "csrc", "tune", "fused_variants.hip")
+SRC = os.path.join(ROOT, "tools", "tune", "fused_variants.hip")
 LIB = os.path.join(ROOT, "build", "libtune_fused.so")
 
 

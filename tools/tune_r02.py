@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Round-2 single-pass kernel study: time csrc/tune/fused_r02.hip variants (decoupled stores k_scan1d vs the product
+"""Round-2 single-pass kernel study: time tools/tune/fused_r02.hip variants (decoupled stores k_scan1d vs the product
 k_scan1f, ablations, the pure read of the same geometry) side by side in one process, interleaved rounds, in place as
 bench.py runs.  Every full-output variant is first checked against the product kernel (flags, next offsets and the
 out-of-place aggregated blocks, bit for bit).
@@ -17,7 +17,7 @@ import torch  # noqa: E402
 
 from omr import Layout, ops  # noqa: E402
 
-SRC = os.path.join(ROOT, "omnireduce-rdma-demo_amd", "csrc", "tune", "fused_r02.hip")
+SRC = os.path.join(ROOT, "tools", "tune", "fused_r02.hip")
 LIB = os.path.join(ROOT, "build", "libtune_r02.so")
 
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""The multi-rank round's aggregator-side kernels at config-4 shapes on one MI355X (csrc/tune/round_r02.hip): the
+"""The multi-rank round's aggregator-side kernels at config-4 shapes on one MI355X (tools/tune/round_r02.hip): the
 shard sum of shard 0 of 8 with 8 workers' contributions (8 x 256 MiB, -r 0.095, worker 0 aggregating, its own
 blocks read in place), and the world-1 shard sum (the whole tensor, one worker); the product's k_shard_sum against
 variants that issue every contributor's loads at once; plus the product's pack (k_move) of worker 0's blocks of
@@ -18,7 +18,7 @@ import torch  # noqa: E402
 
 from omr import Layout, _lib, ops  # noqa: E402
 
-SRC = os.path.join(ROOT, "omnireduce-rdma-demo_amd", "csrc", "tune", "round_r02.hip")
+SRC = os.path.join(ROOT, "tools", "tune", "round_r02.hip")
 LIB = os.path.join(ROOT, "build", "libtune_round_r02.so")
 
 

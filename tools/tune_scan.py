@@ -2,7 +2,7 @@
 """Time k_scan1 shape variants and HBM calibration kernels side by side (one process, interleaved rounds).
 
 usage: python tools/tune_scan.py [--size-mib 256] [--rounds 20] [--reps 5]
-Builds omnireduce-rdma-demo_amd/csrc/tune/scan_variants.hip into build/libtune.so (hipcc, gfx950)."""
+Builds omnireduce-rdma-demo_amd/tools/tune/scan_variants.hip into build/libtune.so (hipcc, gfx950)."""
 import argparse
 import ctypes
 import json
@@ -17,7 +17,7 @@ import torch  # noqa: E402
 
 from omr import Layout, ops  # noqa: E402
 
-SRC = os.path.join(ROOT, "omnireduce-rdma-demo_amd", "csrc", "tune", "scan_variants.hip")
+SRC = os.path.join(ROOT, "tools", "tune", "scan_variants.hip")
 LIB = os.path.join(ROOT, "build", "libtune.so")
 
 

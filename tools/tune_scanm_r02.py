@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Round-2 study of the m-worker one-device sum (csrc/tune/scanm_r02.hip): finer work units, XCD-contiguous unit
+"""Round-2 study of the m-worker one-device sum (tools/tune/scanm_r02.hip): finer work units, XCD-contiguous unit
 order, worker-pipelined loads, and the channel-contention test (the m worker buffers placed inside one allocation
 at offsets staggered by --stagger-kib, against separate allocations).  Every variant is first checked against the
 product k_scanm bit for bit (sums, flags, row masks).  Each launch is timed alone (one event pair per launch,
@@ -20,7 +20,7 @@ import torch  # noqa: E402
 
 from omr import Layout, ops  # noqa: E402
 
-SRC = os.path.join(ROOT, "omnireduce-rdma-demo_amd", "csrc", "tune", "scanm_r02.hip")
+SRC = os.path.join(ROOT, "tools", "tune", "scanm_r02.hip")
 LIB = os.path.join(ROOT, "build", "libtune_scanm_r02.so")
 
 

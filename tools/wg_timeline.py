@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-workgroup timeline of one k_scan1f launch (csrc/tune/fused_r02.hip "timeline" variants: the product kernel
+"""Per-workgroup timeline of one k_scan1f launch (tools/tune/fused_r02.hip "timeline" variants: the product kernel
 built with ABL bit 3, which records s_memrealtime (100 MHz) at each workgroup's start, after its stream loop and
 once every store it issued is acknowledged).  Prints the launch's event time next to the spread of those
 timestamps, so a kernel's time above its pure read can be placed: in the streams, in the workgroups' tails, or
