@@ -132,6 +132,23 @@ def scan_only_bytes(L: Layout) -> int:
     return L.nbytes + L.nb * 8 + L.rows * 8
 
 
+def scan_pack_bytes(L: Layout, bm: np.ndarray, rank: int, world: int) -> int:
+    """The round's worker scan with the fused pack (omr_worker_scan_pack_f32): scan_only_bytes plus the rank's
+    non-zero blocks of the other shards written to their send streams, and the position-table entries of the
+    segments it packs (uint32 per (segment, 64-row group, lane))."""
+    bounds = [s * L.rows // world for s in range(world + 1)]
+    rowmask = np.ones(L.rows, dtype=bool)
+    rowmask[bounds[rank]:bounds[rank + 1]] = False
+    packed = int(np.count_nonzero(bm.reshape(L.rows, L.num_lanes)[rowmask]))
+    from omr import _lib
+    import ctypes
+    S, gps, ent = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
+    _lib.load().omr_pack_geometry(L.n, L.block_size, L.num_lanes, L.num_threads, ctypes.byref(S), ctypes.byref(gps),
+                                  ctypes.byref(ent))
+    table = ent.value * 4 * (world - 1) // world
+    return scan_only_bytes(L) + packed * L.block_size * 4 + table
+
+
 def step_algorithmic_bytes(L: Layout, bitmaps, m: int) -> int:
     """m*S + d_union*S + m*nb*8 (flag + next per block per worker)."""
     nb = L.nb
@@ -202,10 +219,17 @@ def round_world1(args, L: Layout, sets, dev, stream):
     pipeline as bench picks at world 1) over a one-rank RCCL communicator made in this process.  Its per-round time is
     the like-for-like N=1 point of the 1 -> 8 curve, whose N>=2 lines time the same round."""
     from omr import cdist
+    # RCCL prints a version banner on stdout when the communicator is made: keep stdout for the one JSON line
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
     try:
         eng = cdist.CppSparseAllreduce(L, dev, transport="rccl1")
     except Exception as e:  # noqa: BLE001  (reported, the headline line still prints)
         return {"error": str(e)[:300]}
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
     outs = []
     for xs, out in sets:
         out.copy_(xs[0])  # out-of-place: the shard sums land in `out`, x stays the input
@@ -354,6 +378,7 @@ def main():
             engine = cdist.CppSparseAllreduce(L, dev, transport="ipc", uid=uid[0], rank=rank, world=ws)
         else:
             engine = cdist.CppSparseAllreduce(L, device=dev)
+        engine_fused = engine.fused_pack  # the worker scan packs the exchange's blocks itself
         for xs, out in sets:  # out-of-place result buffers keep every step's input pristine
             out.copy_(xs[0])
 
@@ -461,7 +486,8 @@ def main():
     kernel_name = ("k_scan1f (single pass: scan + sum + next)" if (m == 1 and args.kernel == "fused") else
                    ("k_scan1" if m == 1 else "k_scanm"))
     if dist_mode:
-        kernel_name = "k_scan1f (round worker scan: flags + next + row masks, no out)"
+        kernel_name = ("k_scan1f (round worker scan: flags + next + row masks + the fused pack of the other shards' "
+                       "blocks)" if engine_fused else "k_scan1f (round worker scan: flags + next + row masks, no out)")
     scan_ms_dist = None
     if dist_mode:
         # the timed rounds' own events (every `every`-th timed step): its worker scan kernel on the caller's stream,
@@ -491,7 +517,7 @@ def main():
         kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
     if True:
         if dist_mode:
-            kbytes = scan_only_bytes(L)
+            kbytes = (scan_pack_bytes(L, bitmaps[0], rank, n_gpus) if engine_fused else scan_only_bytes(L))
         elif m == 1 and args.kernel == "fused":
             kbytes = fused_bytes(L, bitmaps[0])
         else:

@@ -209,6 +209,32 @@ int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint3
                         int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out, void* workspace,
                         size_t workspace_bytes, omr_stream_t stream);
 
+/* The round's worker scan with the worker's pack fused in (the multi-rank round's form; common.cc:399-407): as
+ * omr_worker_scan_f32, and every non-zero block of a row of shard s != own_shard is also written to `send`, so no
+ * separate pass re-reads the blocks to pack them.  Shards: rows [shard_bounds[s], shard_bounds[s+1]) (HOST uint64,
+ * num_shards + 1 entries, 0 .. rows), each made of whole column segments of the scan (omr_pack_supported says
+ * whether a set of bounds is; a ragged shard packs with omr_move_blocks_f32 instead).  Shard s's stream starts at
+ * send + shard_bounds[s] * num_lanes * block_size floats (send: n floats, device) and holds its non-zero blocks
+ * segment by segment (column segments of omr_pack_geometry's seg_rows rows), each segment's in row order; segments
+ * take their places in completion order through shard_counters (device uint32[num_shards], zero on entry: after the
+ * call counter s = the stream's block count).  pos_table (device uint32[table_entries]) receives for each
+ * (segment, 64-row group g, lane l) the stream position of the first block of lane l at or after row 64 g of the
+ * segment: the aggregator's address of block (row r, lane l) is pos + the lane's set bits in the group below r
+ * (omr_shard_sum_cols_f32).  Entries of segments with no non-zero block, and of own_shard's, are not written.
+ * own_shard: -1 packs every shard (a worker that aggregates none). */
+int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                             int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out,
+                             const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard, float* send,
+                             uint32_t* shard_counters, uint32_t* pos_table, void* workspace, size_t workspace_bytes,
+                             omr_stream_t stream);
+/* The fused pack's geometry on this layout: rows per column segment, 64-row groups per segment, position-table
+ * entries (num_parts * segments per partition * groups * num_lanes); and whether shard bounds (HOST) are whole
+ * segments (0, else OMR_EINVAL with the reason). */
+int omr_pack_geometry(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, uint32_t* seg_rows,
+                      uint32_t* groups_per_seg, uint64_t* table_entries);
+int omr_pack_supported(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                       const uint64_t* shard_bounds, uint32_t num_shards);
+
 /* The aggregator bookkeeping of a round in ONE launch (server.cc:83-96, for the whole tensor at once), from
  * `count` workers' row masks (device, stride rows):
  *   union_masks[r] = OR of the workers' masks (the domain of the min_next chain, server.cc:86-96);
@@ -234,6 +260,15 @@ int omr_round_plan_chain(const uint64_t* row_masks, uint32_t count, uint64_t row
                          uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
                          uint32_t* arrive, uint32_t* done_flag, uint32_t seq, uint32_t* union_next,
                          uint32_t block_size, omr_stream_t stream);
+/* omr_round_plan_chain with worker c's masks at row_masks + c * mask_stride (mask_stride >= rows: the all-gathered
+ * arrays of the fused pack carry each worker's position table after its masks), and zero_counters (device
+ * uint32[num_zero_counters <= 1024], or NULL) cleared: the next round's pack counters. */
+int omr_round_plan_ex(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                      uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                      uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
+                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
+                      uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                      omr_stream_t stream);
 
 /* Block movement addressed by a row mask and its prefix (no block list): the k-th set bit of `row_masks` over
  * rows [0, rows) minus [skip_begin, skip_end) is block k of the packed stream.
@@ -253,6 +288,16 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
                       const uint64_t* row_masks, uint32_t count, const uint32_t* prefix, const uint64_t* write_set,
                       uint64_t rows, uint64_t row_begin, uint64_t row_end, uint32_t num_lanes, uint32_t block_size,
                       int packed_out, float* out, omr_stream_t stream);
+/* The same over the fused pack's column-ordered streams (omr_worker_scan_pack_f32): worker a's stream of these rows
+ * at recv + recv_offsets[a] blocks, a block's place from worker a's position table, which sits at word pos_offset
+ * (uint32 words) of its array row_masks + a * mask_stride (after its masks: pos_offset >= 2 * rows).  Rows
+ * [row_begin, row_end) must be whole column segments of the layout (n, block_size, num_lanes, num_parts); `prefix`
+ * is used for the write set's entry (packed_out) only. */
+int omr_shard_sum_cols_f32(const float* own, uint32_t me, const float* recv, const uint64_t* recv_offsets,
+                           const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t pos_offset,
+                           const uint32_t* prefix, const uint64_t* write_set, uint64_t n, uint32_t block_size,
+                           uint32_t num_lanes, uint32_t num_parts, uint64_t row_begin, uint64_t row_end,
+                           int packed_out, float* out, omr_stream_t stream);
 
 /* ---------------------------------------------------------------- message-level round (wire format) */
 

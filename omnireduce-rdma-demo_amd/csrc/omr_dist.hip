@@ -720,12 +720,20 @@ struct omr_ar_plan {
   bool worker() const { return me < M; }
   std::vector<uint64_t> bounds;   // shard s = rows [bounds[s], bounds[s+1])
   uint64_t shard_nb = 0;          // blocks of the largest shard
+  // Fused pack (omr_worker_scan_pack_f32): the worker scan writes its blocks of the other shards into their send
+  // streams itself (no pack pass).  Needs every shard to be whole column segments of the scan (world 1, 2, 4, 8 of a
+  // power-of-two layout); otherwise (ragged shards, or OMR_PACK_MOVE=1) the round packs with omr_move_blocks_f32.
+  // Each rank's all-gathered array is then its masks followed by its position table: mstride words per rank.
+  bool fused_pack = false;
+  uint64_t mstride = 0;           // uint64 words per rank in masks_all (rows without the fused pack)
   // per-round state, kSets sets used in turn: an asynchronous round's bookkeeping and exchange still read their
   // set while the next rounds' scans fill the others
   static constexpr int kSets = 3;
   struct Set {
-    uint64_t* own = nullptr;        // [rows] this rank's masks (the scan ORs into them; the plan kernel re-zeroes them)
-    uint64_t* masks_all = nullptr;  // [N][rows] every worker's masks (all-gather)
+    uint64_t* own = nullptr;        // [mstride] this rank's masks (the scan ORs into them; the plan kernel re-zeroes
+                                    // them), then (fused pack) its position table
+    uint64_t* masks_all = nullptr;  // [N][mstride] every rank's `own` (all-gather)
+    uint32_t* pack_cnt = nullptr;   // fused pack: [A] the scan's per-shard stream counters (the plan re-zeroes them)
     uint64_t* wset = nullptr;       // [rows] write set: union + lane heads
     uint64_t* umask = nullptr;      // [rows] union of the workers' masks
     uint32_t* prefix = nullptr;     // [N+1][rows+1] popcount prefixes: workers, then the write set
@@ -832,6 +840,7 @@ struct omr_ar_plan {
 };
 
 namespace {
+int32_t me_shard(const omr_ar_plan* p) { return p->shard; }
 int flush_pending(omr_ar_plan* p, hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks);
 int thread_drain(omr_ar_plan* p);
 void thread_stop(omr_ar_plan* p);
@@ -964,7 +973,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     (void)hipFree(v);
   }
   for (auto& st : p->set) {
-    void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed};
+    void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed, st.pack_cnt};
     for (void* v : sv) {
       if (v) p->d->forget(v);
       (void)hipFree(v);
@@ -1033,6 +1042,15 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   uint64_t max_rows = 0;
   for (int s = 0; s < NA; ++s) max_rows = std::max(max_rows, p->bounds[s + 1] - p->bounds[s]);
   p->shard_nb = max_rows * num_lanes;
+  p->mstride = p->rows;
+  if (N > 1 && getenv("OMR_PACK_MOVE") == nullptr &&
+      omr_pack_supported(n, block_size, num_lanes, num_parts, p->bounds.data(), static_cast<uint32_t>(NA)) == 0) {
+    uint64_t entries = 0;
+    TRY(omr_check(omr_pack_geometry(n, block_size, num_lanes, num_parts, nullptr, nullptr, &entries),
+                  "omr_pack_geometry"));
+    p->fused_pack = true;
+    p->mstride = p->rows + (entries + 1) / 2;
+  }
   int rc = 0;
   auto A = [&](int r) {
     if (rc == 0) rc = r;
@@ -1042,8 +1060,9 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   const char* sf = getenv("OMR_EVENT_SYSFENCE");
   const unsigned evflags = hipEventDisableTiming | ((sf != nullptr && atoi(sf) != 0) ? 0u : hipEventDisableSystemFence);
   for (auto& st : p->set) {
-    A(dev_alloc(&st.own, p->rows));
-    A(dev_alloc(&st.masks_all, static_cast<size_t>(N) * p->rows));
+    A(dev_alloc(&st.own, p->mstride));
+    A(dev_alloc(&st.masks_all, static_cast<size_t>(N) * p->mstride));
+    if (p->fused_pack) A(dev_alloc(&st.pack_cnt, NA));
     A(dev_alloc(&st.wset, p->rows));
     A(dev_alloc(&st.umask, p->rows));
     A(dev_alloc(&st.prefix, static_cast<size_t>(M + 1) * (p->rows + 1)));
@@ -1086,7 +1105,9 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   }
   if (rc == 0) A(hip_check(hipMemset(p->arrive, 0, sizeof(uint32_t)), "hipMemset arrive"));
   for (auto& st : p->set)
-    if (rc == 0) A(hip_check(hipMemset(st.own, 0, p->rows * sizeof(uint64_t)), "hipMemset own masks"));
+    if (rc == 0) A(hip_check(hipMemset(st.own, 0, p->mstride * sizeof(uint64_t)), "hipMemset own masks"));
+  for (auto& st : p->set)
+    if (rc == 0 && st.pack_cnt) A(hip_check(hipMemset(st.pack_cnt, 0, NA * sizeof(uint32_t)), "hipMemset pack counters"));
   if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset scan ws"));
   if (rc == 0)
     A(hip_check(hipMemcpy(p->bounds_dev, p->bounds.data(), (NA + 1) * sizeof(uint64_t), hipMemcpyHostToDevice),
@@ -1196,7 +1217,10 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       for (int s = 0; s < NA; ++s) {
         const int ar = p->agg_rank(s);
         if (ar == me) continue;
-        const uint64_t k0 = cnt(me, s) - (p->colocated && s > me ? own_shard : 0);
+        // the fused pack's stream of shard s starts at the shard's first block; the pack pass's streams follow one
+        // another in block order without this rank's own shard
+        const uint64_t k0 = p->fused_pack ? p->bounds[s] * p->lanes
+                                          : cnt(me, s) - (p->colocated && s > me ? own_shard : 0);
         sends[ar] = {Slice{S.packed + k0 * B, per(me, s) * B * sizeof(float)}};
       }
     if (sh >= 0)
@@ -1225,11 +1249,17 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     const bool dense_out = rs_mode && p->colocated;
     // (a dedicated aggregator keeps only its own shard's sums: at the start of `results`)
     sums = dense_out ? out : p->results + (wk ? cnt(M, sh) * B : 0);
-    TRY(omr_check(omr_shard_sum_f32(p->colocated ? x : nullptr, p->colocated ? static_cast<uint32_t>(me)
-                                                                             : static_cast<uint32_t>(M),
-                                    p->recv, roff.data(), S.masks_all, static_cast<uint32_t>(M), S.prefix, S.wset,
-                                    rows, r0, r1, p->lanes, p->B, dense_out ? 0 : 1, sums, xstream),
-                  "omr_shard_sum_f32"));
+    const float* own = p->colocated ? x : nullptr;
+    const uint32_t own_idx = p->colocated ? static_cast<uint32_t>(me) : static_cast<uint32_t>(M);
+    if (p->fused_pack)  // the workers' streams are column-ordered: positions from their all-gathered tables
+      TRY(omr_check(omr_shard_sum_cols_f32(own, own_idx, p->recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
+                                           p->mstride, 2 * rows, S.prefix, S.wset, p->n, p->B, p->lanes, p->parts,
+                                           r0, r1, dense_out ? 0 : 1, sums, xstream),
+                    "omr_shard_sum_cols_f32"));
+    else
+      TRY(omr_check(omr_shard_sum_f32(own, own_idx, p->recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
+                                      S.prefix, S.wset, rows, r0, r1, p->lanes, p->B, dense_out ? 0 : 1, sums, xstream),
+                    "omr_shard_sum_f32"));
     if (!p->colocated) p->last_sums_blocks = per(M, sh);
   }
   ht_of(p).lap("2:shard sum");
@@ -1318,17 +1348,18 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
   // 2. every worker's row masks
   ht.lap("1:refill wait");
   if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].q0, qs), "hipEventRecord"));
-  TRY(p->d->allgather(S.own, S.masks_all, rows * sizeof(uint64_t), qs));
+  TRY(p->d->allgather(S.own, S.masks_all, p->mstride * sizeof(uint64_t), qs));
   ht.lap("1:allgather");
   // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for its next round
   //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
   const uint32_t seq = ++p->seq;
   //    ... and, by extra workgroups of the same launch, the aggregator chain (server.cc:86-96 min_next) over the union
-  TRY(omr_check(omr_round_plan_chain(S.masks_all, static_cast<uint32_t>(M), rows, p->rpp, p->lanes, p->bounds_dev,
-                                     NS, S.wset, S.umask, S.prefix,
-                                     p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, p->arrive,
-                                     p->flag_map + si, seq, j.un, p->B, qstream),
-                "omr_round_plan_chain"));
+  TRY(omr_check(omr_round_plan_ex(S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes,
+                                  p->bounds_dev, NS, S.wset, S.umask, S.prefix,
+                                  p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, S.pack_cnt,
+                                  S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->arrive, p->flag_map + si, seq,
+                                  j.un, p->B, qstream),
+                "omr_round_plan_ex"));
   if (async) {
     TRY(hip_check(hipEventRecord(S.planned, qs), "hipEventRecord"));
     S.plan_pending = true;
@@ -1337,9 +1368,9 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
   // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407): addressed by
   //     device-side data only, so it is queued before the host learns the counts and runs while it waits.  (Every
   //     host API call costs microseconds; a round that spends them on side streams and events is host-bound.)
-  if (N > 1 && mode != OMR_ROUND_DENSE_REDUCE_SCATTER && p->worker()) {
+  if (N > 1 && mode != OMR_ROUND_DENSE_REDUCE_SCATTER && p->worker() && !p->fused_pack) {
     const uint64_t r0 = p->colocated ? p->bounds[me] : 0, r1 = p->colocated ? p->bounds[me + 1] : 0;
-    TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * rows,
+    TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * p->mstride,
                                       S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
                                       r1, qstream), "omr_move_blocks_f32 pack"));
   }
@@ -1500,9 +1531,18 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   }
   if (p->worker()) {
     if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
-    TRY(omr_check(omr_worker_scan_f32(p->scan_from ? p->scan_from : x, p->n, p->B, p->lanes, p->parts, fl, nx, S.own,
-                                      p->scan_from ? const_cast<float*>(x) : nullptr, p->scan_ws, p->scan_ws_bytes,
-                                      stream), "omr_worker_scan_f32"));
+    const float* src = p->scan_from ? p->scan_from : x;
+    float* sout = p->scan_from ? const_cast<float*>(x) : nullptr;
+    const bool pack = p->fused_pack && (mode & 0xFF) != OMR_ROUND_DENSE_REDUCE_SCATTER;
+    if (pack)  // the scan also writes this worker's blocks of the other shards into their send streams
+      TRY(omr_check(omr_worker_scan_pack_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout, p->bounds.data(),
+                                             static_cast<uint32_t>(p->A), p->colocated ? me_shard(p) : -1, S.packed,
+                                             S.pack_cnt, reinterpret_cast<uint32_t*>(S.own + p->rows), p->scan_ws,
+                                             p->scan_ws_bytes, stream),
+                    "omr_worker_scan_pack_f32"));
+    else
+      TRY(omr_check(omr_worker_scan_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout, p->scan_ws,
+                                        p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
     if (timed) {
       TRY(hip_check(hipEventRecord(p->timed[tslot].s1, st), "hipEventRecord"));
       p->timed[tslot].scan = true;
@@ -1699,6 +1739,8 @@ int omr_ar_plan_shard(omr_ar_plan* p, int* shard, uint64_t* row_begin, uint64_t*
   if (num_blocks) *num_blocks = p->colocated ? 0 : p->last_sums_blocks;
   return 0;
 }
+
+int omr_ar_plan_fused_pack(const omr_ar_plan* p) { return p != nullptr && p->fused_pack ? 1 : 0; }
 
 int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_join: NULL");

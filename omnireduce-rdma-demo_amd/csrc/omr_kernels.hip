@@ -204,6 +204,16 @@ __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
 // SKIP (the product's choice at B = 1024): a batch with no block to write skips its (dropped) data stores through a
 // wave-uniform branch.  (The timing-study form of this kernel, with its ablation / store-policy / timeline knobs, is
 // tools/tune/scan1f_study.h; it is not built into libomr.so.)
+//
+// PACK (the multi-rank round's worker scan): the scan also packs the worker's non-zero blocks of the other shards
+// for their aggregators (common.cc:399-407), so no separate pack pass re-reads them from HBM.  A shard is a row range
+// made of whole column segments; its send stream is its segments' non-zero blocks, segment by segment, each segment's
+// blocks in row order.  A segment's place in the stream is taken by ONE device atomic on the shard's counter once the
+// workgroup knows its count (segments land in completion order, not in a fixed order: no workgroup ever waits for
+// another).  Until then the blocks stay on chip: each wave keeps its range's non-zero blocks, highest row first, in
+// `wcap` LDS slots of its own (the rest, its lowest rows, are re-read at the end: none at config 4's density).  The
+// aggregator finds a block from pos[(segment, 64-row group), lane] = its stream position of the group's first block
+// in that column, plus the column's set bits of the group below the row.
 struct FusedArgs {
   const float* x;
   float* out;
@@ -214,18 +224,33 @@ struct FusedArgs {
   uint64_t* masks;     // [rows] row masks, zero on entry, non-zero blocks OR-ed in (multi-rank round), or null
   uint32_t lanes, rpp, K, S, block, sentinel;
   uint32_t part0;      // first partition of the launch (a per-partition call scans partitions [part0, part0 + grid))
+  // PACK
+  float* send;         // shard s's stream starts at float bounds[s] * lanes * block (a buffer of n floats)
+  uint32_t* shard_cnt; // [nshards] blocks taken so far in each shard's stream (zero on entry)
+  uint32_t* pos;       // [parts * K * gps * lanes] stream position of (segment, group, lane)'s first block
+  uint32_t bounds[OMR_MAX_WORKERS + 1];  // shard s = rows [bounds[s], bounds[s + 1]), whole segments
+  uint32_t nshards, gps, wcap;
+  int32_t own_shard;   // this rank's own shard (read in place by its aggregator, not packed); -1: none
 };
+
+constexpr uint32_t kPackLdsBytes = 128u << 10;  // the waves' stash slots: 8 blocks per wave at B = 256 (16 waves)
+constexpr uint32_t kPackGroupRows = 64;         // the position table's row granularity (one wave of row masks)
 
 constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
 
-template <int VEC, int WAVES, int LOADS = 16, int SKIP = 0>
+template <int VEC, int WAVES, int LOADS = 16, int SKIP = 0, bool PACK = false>
 __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
   constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
-  static_assert(RB >= 1 && RB <= 32, "batch bits are 32-bit");
+  static_assert(RB >= 1 && RB <= 32 && 32 % RB == 0, "a batch's bits lie inside one 32-bit word");
+  [[maybe_unused]] constexpr uint32_t B4 = 64 * VEC;  // 16-byte vectors per block
   __shared__ uint32_t s_wfirst[WAVES], s_wlast[WAVES];
   __shared__ int s_fix;
   __shared__ uint32_t s_carry[64];
   __shared__ uint32_t s_seg_last[64];
+  // PACK: dynamic LDS = the segment's non-zero-row bits [ceil(S / 32) words, 16-byte aligned] + the stash slots
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+  __shared__ uint32_t s_wcnt[PACK ? WAVES : 1], s_wpre[PACK ? WAVES : 1];
+  __shared__ uint32_t s_base, s_total;
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t T = gridDim.x, bid = blockIdx.x;
@@ -244,6 +269,21 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
   const uint32_t lo = wave * rw < a.S ? wave * rw : a.S;
   const uint32_t hi = lo + rw < a.S ? lo + rw : a.S;
   uint32_t carry = kNone, wlast = kNone;
+  // PACK: this segment's shard (the host checked that a segment never straddles two) and whether it is packed
+  [[maybe_unused]] uint32_t shard = 0;
+  [[maybe_unused]] bool pack = false;
+  [[maybe_unused]] uint32_t* const s_bits = s_dyn;
+  [[maybe_unused]] const uint32_t bits_words = ((a.S + 31) / 32 + 3) & ~3u;
+  [[maybe_unused]] v4f* const stash = reinterpret_cast<v4f*>(s_dyn + bits_words);
+  [[maybe_unused]] uint32_t cnt_w = 0, taken = 0;  // the wave's non-zero rows, and how many of them (the highest) it stashed
+  if constexpr (PACK) {
+    while (shard + 1 < a.nshards && row0 >= a.bounds[shard + 1]) ++shard;
+    pack = static_cast<int32_t>(shard) != a.own_shard;
+    if (pack) {
+      for (uint32_t i = threadIdx.x; i < bits_words; i += 64 * WAVES) s_bits[i] = 0;
+      __syncthreads();
+    }
+  }
   for (uint32_t nb_ = (hi - lo + RB - 1) / RB; nb_ > 0; --nb_) {
     const uint32_t rr = lo + (nb_ - 1) * RB;
     const uint32_t nrow = (hi - rr < static_cast<uint32_t>(RB)) ? hi - rr : RB;
@@ -300,6 +340,23 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
       if (masks != nullptr && ((bits >> lane) & 1u))
         (void)__hip_atomic_fetch_or(&masks[row0 + rr + lane], 1ull << l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if constexpr (PACK) {
+      if (pack && bits != 0) {
+        cnt_w += static_cast<uint32_t>(__builtin_popcount(bits));
+        if (lane == 0) (void)__hip_atomic_fetch_or(&s_bits[rr >> 5], bits << (rr & 31), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        // the batch's non-zero blocks into the wave's free slots, highest row first (slot j = j-th from the top)
+#pragma unroll
+        for (int s = RB - 1; s >= 0; --s) {
+          if (((bits >> s) & 1u) && taken < a.wcap) {
+            v4f* const slot = stash + (static_cast<uint64_t>(wave) * a.wcap + taken) * B4;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) slot[q * 64 + lane] = v[s][q];
+            ++taken;
+          }
+        }
+      }
+    }
     if (bits != 0) {
       if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
       carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
@@ -320,6 +377,61 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
   if (succ != kNone || last_seg) {
     const uint32_t val = succ != kNone ? static_cast<uint32_t>(row0 + succ) * row_stride + lane_b : a.sentinel + lane_b;
     for (uint32_t i = (wlast == kNone ? lo : wlast) + lane; i < hi; i += 64) a.next[(row0 + i) * a.lanes + l] = val;
+  }
+  if constexpr (PACK) {
+    if (pack) {
+      if (lane == 0) s_wcnt[wave] = cnt_w;
+      __syncthreads();  // (also orders every wave's s_bits updates before the reads below)
+      if (threadIdx.x == 0) {  // the segment's place in its shard's stream: one device atomic
+        uint32_t t = 0;
+        for (uint32_t w2 = 0; w2 < WAVES; ++w2) {
+          s_wpre[w2] = t;
+          t += s_wcnt[w2];
+        }
+        s_total = t;
+        s_base = t ? __hip_atomic_fetch_add(&a.shard_cnt[shard], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      }
+      __syncthreads();
+      if (s_total != 0) {
+        const uint32_t base = s_base;
+        // position table: group j's first block = base + the segment's non-zero rows before row 64 j
+        const uint64_t seg = static_cast<uint64_t>(p) * a.K + k;
+        for (uint32_t j = threadIdx.x; j < a.gps; j += 64 * WAVES) {
+          uint32_t c = 0;
+          for (uint32_t wd = 0; wd < j * (kPackGroupRows / 32); ++wd) c += static_cast<uint32_t>(__builtin_popcount(s_bits[wd]));
+          a.pos[(seg * a.gps + j) * a.lanes + l] = base + c;
+        }
+        // the wave's blocks: its range's non-zero rows take stream places base + s_wpre[wave] + (rank among them)
+        float* const sbase = a.send + static_cast<uint64_t>(a.bounds[shard]) * row_stride;
+        const uint64_t wb = static_cast<uint64_t>(base) + s_wpre[wave];
+        for (uint32_t j = 0; j < taken; ++j) {  // stashed: the j-th from the top has rank cnt_w - 1 - j
+          const v4f* const slot = stash + (static_cast<uint64_t>(wave) * a.wcap + j) * B4;
+          v4f* const d = reinterpret_cast<v4f*>(sbase + (wb + cnt_w - 1 - j) * a.block);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = slot[q * 64 + lane];
+        }
+        // the rest (the wave's lowest cnt_w - taken non-zero rows, in order): re-read, from `out` when the scan wrote
+        // 0.0f + x there (the same bits), else from x
+        const float* const rsrc = a.out != nullptr ? a.out : a.x;
+        uint32_t idx = 0;
+        const uint32_t over = cnt_w - taken;
+        for (uint32_t wd = lo >> 5; idx < over && wd * 32 < hi; ++wd) {
+          uint32_t m = s_bits[wd];
+          const uint32_t b0 = wd * 32;
+          if (b0 < lo) m &= ~0u << (lo - b0);
+          if (hi - b0 < 32) m &= (1u << (hi - b0)) - 1u;
+          while (m != 0 && idx < over) {
+            const uint32_t r = b0 + static_cast<uint32_t>(__builtin_ctz(m));
+            m &= m - 1;
+            const v4f* const sp = reinterpret_cast<const v4f*>(rsrc + ((row0 + r) * a.lanes + l) * a.block);
+            v4f* const d = reinterpret_cast<v4f*>(sbase + (wb + idx) * a.block);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = sp[q * 64 + lane];
+            ++idx;
+          }
+        }
+      }
+    }
   }
   if (a.K == 1) return;
   // multi-segment column: publish {first, last}, count arrivals; the last arriver fixes every tail row
@@ -834,10 +946,6 @@ template <int VEC>
 constexpr int move_slots() {  // blocks per batch for a pure move
   return 16 / VEC;
 }
-template <int VEC>
-constexpr int sum_slots() {  // blocks per batch for the shard sum (accumulators + one worker's loads)
-  return (8 / VEC) < 2 ? 2 : 8 / VEC;
-}
 
 __device__ __forceinline__ uint64_t below(uint32_t l) { return l >= 64 ? ~0ull : ((1ull << l) - 1ull); }
 
@@ -876,19 +984,21 @@ __device__ __forceinline__ uint32_t take_bits(uint64_t& rem, uint32_t (&lj)[SL],
 constexpr int kPlanThreads = 1024;
 constexpr uint64_t kPlanLdsRows = 8192;  // 64 KiB of dynamic LDS
 
-__device__ __forceinline__ uint64_t plan_row(const uint64_t* masks, uint32_t a, uint32_t count, uint64_t rows,
+__device__ __forceinline__ uint64_t plan_row(const uint64_t* masks, uint32_t a, uint32_t count, uint64_t mstride,
                                              uint64_t r, uint32_t rpp, uint64_t all_lanes, uint64_t* uni) {
-  if (a < count) return masks[static_cast<uint64_t>(a) * rows + r];
+  if (a < count) return masks[static_cast<uint64_t>(a) * mstride + r];
   uint64_t u = 0;
-  for (uint32_t c = 0; c < count; ++c) u |= masks[static_cast<uint64_t>(c) * rows + r];
+  for (uint32_t c = 0; c < count; ++c) u |= masks[static_cast<uint64_t>(c) * mstride + r];
   *uni = u;
   return (r % rpp == 0) ? (u | all_lanes) : u;
 }
 
 struct PlanArgs {
-  const uint64_t* masks;
+  const uint64_t* masks;  // worker c's row masks at masks + c * mstride
   uint32_t count, rpp, lanes, nbounds;
-  uint64_t rows;
+  uint64_t rows, mstride;
+  uint32_t* zero_cnt;     // [zero_cnt_n] cleared by the write-set workgroup (the next round's pack counters), or null
+  uint32_t zero_cnt_n;
   const uint64_t* bounds;
   uint64_t* write_set;
   uint64_t* union_masks;
@@ -905,10 +1015,10 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
   if (blockIdx.x > a.count) {  // the aggregator chain (server.cc:86-96 min_next) over the union, one segment each
     const uint64_t* m = a.masks;
     const uint32_t cnt = a.count;
-    const uint64_t rows = a.rows;
+    const uint64_t ms = a.mstride;
     next_segment<kPlanThreads / 64>(a.chain, blockIdx.x - a.count - 1, [&](uint64_t r) {
       uint64_t u = 0;
-      for (uint32_t c = 0; c < cnt; ++c) u |= m[static_cast<uint64_t>(c) * rows + r];
+      for (uint32_t c = 0; c < cnt; ++c) u |= m[static_cast<uint64_t>(c) * ms + r];
       return u;
     }, a.chain.next);
     return;
@@ -921,13 +1031,14 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
   const bool ws = arr == a.count;
   const bool keep = a.rows <= kPlanLdsRows;
   if (t < a.nbounds) s_bounds[t] = a.bounds[t];
+  if (ws && a.zero_cnt != nullptr && t < a.zero_cnt_n) a.zero_cnt[t] = 0;
   // pass 1: coalesced row reads, 4 rows per thread per step
   for (uint64_t r0 = t; r0 < a.rows; r0 += 4 * kPlanThreads) {
     uint64_t v[4], u[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const uint64_t r = r0 + static_cast<uint64_t>(i) * kPlanThreads;
-      v[i] = r < a.rows ? plan_row(a.masks, arr, a.count, a.rows, r, a.rpp, all_lanes, &u[i]) : 0;
+      v[i] = r < a.rows ? plan_row(a.masks, arr, a.count, a.mstride, r, a.rpp, all_lanes, &u[i]) : 0;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -948,7 +1059,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
   auto row = [&](uint64_t r) -> uint64_t {
     if (keep) return s_val[r];
     if (ws) return a.write_set[r];
-    return a.masks[static_cast<uint64_t>(arr) * a.rows + r];
+    return a.masks[static_cast<uint64_t>(arr) * a.mstride + r];
   };
   uint32_t sum = 0;
   for (uint64_t r = rb; r < re; ++r) sum += static_cast<uint32_t>(__builtin_popcountll(row(r)));
@@ -1063,100 +1174,186 @@ __global__ __launch_bounds__(kWGThreads) void k_move(MoveArgs a) {
 }
 
 // Aggregator shard sum over rows [r0, r1) of the write set (server.cc:83-99 with the RDMA hop replaced by the
-// transport): for every write-set block, ((0.0f + x_a0) + x_a1) + ... over the workers whose mask has it, in
-// rank order.  Worker `me`'s contribution is read in place from its dense tensor `own`; worker a's from its
-// received stream at recv + recv_off[a] blocks (its shard blocks in block order).  Output dense (block
-// position, in place) or packed (write-set order of the shard, for the sums' return trip).
-struct ShardArgs {
+// transport): for every write-set block, ((0.0f + x_a0) + x_a1) + ... over the workers whose mask has it, in rank
+// order (a write-set block no worker has, a lane head: +0.0f).  Worker `me`'s contribution is read in place from its
+// dense tensor `own`; worker a's from its received stream at recv + recv_off[a] blocks, which is either
+//   row-ordered (pos_off == kRowStreams): its blocks of these rows in block order, position from the prefix arrays; or
+//   column-ordered (k_scan1f's fused pack): segment by segment, position from its position table.
+// Output dense (block position, in place) or packed (write-set order of the shard, for the sums' return trip).
+//
+// Work unit = 32 rows x one lane column (column streams: one half of a segment's 64-row group).  Lane i holds row i
+// of the rows it loads: ONE round trip fetches the unit's index data (write-set row, every worker's mask row and
+// stream prefix or position).  Ballots over the lanes give each worker's column bits, so every (block, contributor)
+// pair's stream position is computed in registers; a wave-wide exclusive scan lays the pairs out in LDS in
+// (block, rank) order.  The pairs are then streamed P at a time: all P loads in flight (P * VEC dwordx4 per lane),
+// then a segmented sum in rank order whose last pair of each block stores it.  So a unit costs one index round trip
+// plus one per P pairs, whatever the number of contributors (the round-2 kernel paid a round trip per contributor
+// per batch of blocks behind a prefix round trip: 2.9 TB/s at an 8-worker shard).
+struct SumArgs {
   const float* own;
   const float* recv;
   uint64_t recv_off[OMR_MAX_WORKERS];
-  const uint64_t* masks;  // [count][rows]
-  const uint32_t* prefix;  // [count + 1][rows + 1]; index count = write set
+  const uint64_t* masks;   // worker c's row masks at masks + c * mstride
+  uint64_t mstride;
+  const uint32_t* prefix;  // [count + 1][rows + 1]: the workers' row-stream prefixes, then the write set's
+  uint64_t pos_off;        // column streams: worker c's position table at (const uint32_t*)(masks + c * mstride) + pos_off
   const uint64_t* write_set;
   float* out;
   uint64_t rows, r0, r1;
-  uint32_t count, me, lanes, block, packed_out, lg;
+  uint32_t count, me, lanes, block, packed_out;
+  uint32_t S, gps;         // column streams: segment rows (shards are whole segments), 64-row groups per segment
 };
 
+constexpr uint64_t kRowStreams = ~0ull;
+constexpr uint32_t kSumUnitRows = 32;
+// a pair record: source block (bits 0-31: in `own` or in `recv`), destination block (32-59), flags
+constexpr uint64_t kRecOwn = 1ull << 60, kRecZero = 1ull << 61, kRecFirst = 1ull << 62, kRecLast = 1ull << 63;
+
 template <int VEC>
-__global__ __launch_bounds__(kWGThreads) void k_shard_sum(ShardArgs a) {
-  constexpr int SL = sum_slots<VEC>();
+__global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
+  constexpr int P = 32 / VEC;  // pair slots per window
+  constexpr int kSlotGroup = P < 8 ? P : 8;
+  constexpr uint32_t kRecCap = kSumUnitRows * OMR_MAX_WORKERS;
+  __shared__ uint64_t s_rec[kWavesPerWG][kRecCap];
   const int lane = threadIdx.x & 63;
-  const uint32_t groups = a.lanes / a.lg;
-  const uint32_t bbytes = a.block * 4;
-  const uint64_t units = (a.r1 - a.r0) * groups;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool cols = a.pos_off != kRowStreams;
+  const uint64_t srows = a.r1 - a.r0;
+  const uint64_t units = cols ? (srows / a.S) * a.gps * 2 * a.lanes
+                              : ((srows + kSumUnitRows - 1) / kSumUnitRows) * a.lanes;
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
-  const uint32_t* pws = a.prefix + static_cast<uint64_t>(a.count) * (a.rows + 1);
-  const uint64_t cmask = a.count >= 64 ? ~0ull : ((1ull << a.count) - 1ull);
-  for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-       u < units; u += nw) {
-    const uint64_t r = a.r0 + u / groups;
-    const uint32_t g0 = static_cast<uint32_t>(u % groups) * a.lg;
-    // every index load of the unit issued together (one round trip before the data loads): the write-set row and
-    // its prefix, and on lane c < count worker c's mask and stream prefixes
+  const uint32_t* const pws = a.prefix + static_cast<uint64_t>(a.count) * (a.rows + 1);
+  const uint32_t wpre0 = a.packed_out ? pws[a.r0] : 0u;
+  const uint32_t bbytes = a.block * 4;
+  for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + wave; u < units; u += nw) {
+    const uint32_t l = static_cast<uint32_t>(u % a.lanes);
+    uint64_t g0, gidx = 0;  // first row the lanes load (lane i: row g0 + i); column streams: the group's table index
+    uint32_t nload, h0, h1;  // rows loaded; the unit's rows are lanes [h0, h1)
+    if (cols) {
+      uint64_t t = u / a.lanes;
+      const uint32_t h = static_cast<uint32_t>(t & 1u);
+      t >>= 1;
+      const uint32_t j = static_cast<uint32_t>(t % a.gps);
+      const uint64_t seg = a.r0 / a.S + t / a.gps;
+      g0 = seg * a.S + static_cast<uint64_t>(j) * kPackGroupRows;
+      nload = a.S - j * kPackGroupRows < kPackGroupRows ? a.S - j * kPackGroupRows : kPackGroupRows;
+      h0 = h * kSumUnitRows;
+      h1 = nload < h0 + kSumUnitRows ? nload : h0 + kSumUnitRows;
+      gidx = seg * a.gps + j;
+      if (h0 >= h1) continue;
+    } else {
+      g0 = a.r0 + (u / a.lanes) * kSumUnitRows;
+      nload = a.r1 - g0 < kSumUnitRows ? static_cast<uint32_t>(a.r1 - g0) : kSumUnitRows;
+      h0 = 0;
+      h1 = nload;
+    }
+    // ---- index loads, all issued together (one round trip)
+    const bool rl = static_cast<uint32_t>(lane) < nload;
+    const uint64_t r = g0 + (rl ? static_cast<uint32_t>(lane) : 0u);
+    const uint64_t w = rl ? a.write_set[r] : 0ull;
+    const uint32_t wpre = (rl && a.packed_out) ? pws[r] : 0u;
+    uint64_t mk[OMR_MAX_WORKERS];
+    uint32_t pre[OMR_MAX_WORKERS];
+#pragma unroll
+    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) {
+      mk[c] = (c < a.count && rl) ? a.masks[c * a.mstride + r] : 0ull;
+      pre[c] = (!cols && c < a.count && rl) ? a.prefix[c * (a.rows + 1) + r] : 0u;
+    }
+    // lane c < count: worker c's group position (column streams) or its stream prefix at r0 (row streams)
     const bool cl = static_cast<uint32_t>(lane) < a.count;
-    const uint32_t* pc = a.prefix + static_cast<uint64_t>(cl ? lane : 0) * (a.rows + 1);
-    const uint64_t w = a.write_set[r];
-    const uint64_t mc = cl ? a.masks[static_cast<uint64_t>(lane) * a.rows + r] : 0ull;
-    const uint32_t pcr = pc[r], pcr0 = pc[a.r0];
-    const uint32_t pwr = pws[r], pwr0 = pws[a.r0];
-    uint64_t rem = w & (below(g0 + a.lg) & ~below(g0));
-    if (rem == 0) continue;
-    // lane c: the first block of row r in worker c's stream
-    const uint64_t kc0 = cl ? a.recv_off[lane] + (pcr - pcr0) : 0ull;
-    uint64_t kw = pwr - pwr0 + static_cast<uint64_t>(__builtin_popcountll(w & below(g0)));
-    float* orow = a.out + r * a.lanes * a.block;
-    while (rem != 0) {
-      uint32_t lj[SL];
-      uint64_t bm;
-      const uint32_t nv = take_bits<SL>(rem, lj, bm);
-      v4f acc[SL][VEC];
+    const uint32_t base_c =
+        !cl ? 0u
+            : cols ? reinterpret_cast<const uint32_t*>(a.masks + lane * a.mstride)[a.pos_off + gidx * a.lanes + l]
+                   : a.prefix[static_cast<uint64_t>(lane) * (a.rows + 1) + a.r0];
+    // ---- (block, contributor) pairs of the unit's write-set blocks, rank order within a block
+    const bool mine = static_cast<uint32_t>(lane) >= h0 && static_cast<uint32_t>(lane) < h1;
+    const bool wb = mine && ((w >> l) & 1ull);
+    uint32_t cb = 0;
 #pragma unroll
-      for (int j = 0; j < SL; ++j)
+    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) cb |= static_cast<uint32_t>((mk[c] >> l) & 1ull) << c;
+    const uint32_t np = wb ? (cb ? static_cast<uint32_t>(__builtin_popcount(cb)) : 1u) : 0u;
+    uint32_t inc = np;
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) acc[j][q] = v4f{0.f, 0.f, 0.f, 0.f};
-      // contributors of the batch in rank order; each worker's (up to SL) blocks loaded at once
-      uint64_t cont = __ballot((mc & bm) != 0) & cmask;
-      while (cont != 0) {
-        const uint32_t c = static_cast<uint32_t>(__builtin_ctzll(cont));
-        cont &= cont - 1;
-        const uint64_t m_c = readlane64(mc, c);
-        const bool mine = c == a.me;
-        const __amdgpu_buffer_rsrc_t src =
-            mine ? chunk_rsrc(a.own + r * a.lanes * a.block, a.lanes * bbytes)
-                 : chunk_rsrc(a.recv + readlane64(kc0, c) * a.block,
-                              static_cast<uint32_t>(__builtin_popcountll(m_c)) * bbytes);
-        v4f v[SL][VEC];
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+    if (total == 0) continue;
+    uint64_t ccol[OMR_MAX_WORKERS];  // column streams: worker c's bits of column l over the loaded rows
 #pragma unroll
-        for (int j = 0; j < SL; ++j) {
-          const bool has = static_cast<uint32_t>(j) < nv && ((m_c >> lj[j]) & 1u);
-          const uint32_t off = (mine ? lj[j] : static_cast<uint32_t>(__builtin_popcountll(m_c & below(lj[j])))) * bbytes;
+    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) ccol[c] = (cols && c < a.count) ? __ballot((mk[c] >> l) & 1ull) : 0ull;
+    if (np != 0) {
+      uint32_t k = inc - np;
+      const uint32_t first = k, last = inc - 1;
+      const uint64_t dst = a.packed_out ? static_cast<uint64_t>(wpre - wpre0) +
+                                              static_cast<uint64_t>(__builtin_popcountll(w & below(l)))
+                                        : r * a.lanes + l;
+      const uint64_t hdr = dst << 32;
+      if (cb == 0) {
+        s_rec[wave][k] = hdr | kRecZero | kRecFirst | kRecLast;
+      } else {
 #pragma unroll
-          for (int q = 0; q < VEC; ++q)
-            v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  src, (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0,
-                                                  kLoadAux));
-        }
-#pragma unroll
-        for (int j = 0; j < SL; ++j)
-          if (static_cast<uint32_t>(j) < nv && ((m_c >> lj[j]) & 1u)) {
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) acc[j][q] = add4(acc[j][q], v[j][q]);
+        for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) {
+          if (!((cb >> c) & 1u)) continue;
+          uint64_t rec;
+          if (c == a.me) {
+            rec = (r * a.lanes + l) | kRecOwn;
+          } else {
+            const uint32_t bc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_c), c));
+            const uint64_t pos = cols ? static_cast<uint64_t>(bc) + static_cast<uint64_t>(__builtin_popcountll(
+                                                                        ccol[c] & below(static_cast<uint32_t>(lane))))
+                                      : static_cast<uint64_t>(pre[c] - bc) +
+                                            static_cast<uint64_t>(__builtin_popcountll(mk[c] & below(l)));
+            rec = (a.recv_off[c] + pos) & 0xFFFFFFFFull;
           }
+          rec |= hdr | (k == first ? kRecFirst : 0ull) | (k == last ? kRecLast : 0ull);
+          s_rec[wave][k++] = rec;
+        }
       }
-      const __amdgpu_buffer_rsrc_t dst = a.packed_out ? chunk_rsrc(a.out + kw * a.block, nv * bbytes)
-                                                      : chunk_rsrc(orow, a.lanes * bbytes);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the wave's record stores land before its reads
+    // ---- the pairs, P at a time: every load of the window in flight, then the segmented rank-order sum
+    v4f acc[VEC];
 #pragma unroll
-      for (int j = 0; j < SL; ++j) {
-        const uint32_t off = (a.packed_out ? static_cast<uint32_t>(j) : lj[j]) * bbytes;
-        const uint32_t drop = static_cast<uint32_t>(j) < nv ? 0u : kDropStore;
+    for (int q = 0; q < VEC; ++q) acc[q] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (uint32_t wbase = 0; wbase < total; wbase += P) {
+      const uint32_t nv = total - wbase < static_cast<uint32_t>(P) ? total - wbase : static_cast<uint32_t>(P);
+      const uint64_t myrec = static_cast<uint32_t>(lane) < nv ? s_rec[wave][wbase + lane] : 0ull;
+      v4f v[P][VEC];
+      // every load of the window issued before the first use; slots in groups of kSlotGroup, a group past the
+      // window's last pair skipped by a wave-uniform branch (a sparse unit issues only what it needs)
 #pragma unroll
-        for (int q = 0; q < VEC; ++q)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[j][q]), dst,
-                                                 (off + (q * 64 + lane) * 16) | drop, 0, 0);
+      for (int g = 0; g < P; g += kSlotGroup) {
+        if (static_cast<uint32_t>(g) < nv) {
+#pragma unroll
+          for (int j = g; j < g + kSlotGroup; ++j) {
+            const uint64_t rc = readlane64(myrec, j);
+            const bool load = static_cast<uint32_t>(j) < nv && !(rc & kRecZero);
+            const float* const sb = (rc & kRecOwn) ? a.own : a.recv;
+            const __amdgpu_buffer_rsrc_t src =
+                chunk_rsrc(sb + static_cast<uint64_t>(static_cast<uint32_t>(rc)) * a.block, load ? bbytes : 0u);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q)
+              v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (q * 64 + lane) * 16, 0,
+                                                                                     kLoadAux));
+          }
+        }
       }
-      kw += nv;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        if (static_cast<uint32_t>(j) < nv) {  // (wave-uniform)
+          const uint64_t rc = readlane64(myrec, j);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q)  // (0.0f + x_first) + ...: a block's first pair restarts from +0.0f
+            acc[q] = add4((rc & kRecFirst) ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
+          if (rc & kRecLast) {
+            v4f* const d = reinterpret_cast<v4f*>(a.out + ((rc >> 32) & 0x0FFFFFFFull) * a.block);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = acc[q];
+          }
+        }
+      }
     }
   }
 }
@@ -1285,9 +1482,59 @@ size_t fused_workspace_bytes(const Layout& L, const FusedShape& f) {
   return cols * sizeof(uint32_t) + cols * f.K * sizeof(uint64_t) + 16;
 }
 
+// The fused pack of the multi-rank worker scan (k_scan1f<..., PACK>): where the other shards' blocks go.
+struct PackSpec {
+  float* send;
+  uint32_t* shard_cnt;
+  uint32_t* pos;
+  const uint64_t* bounds;  // host, nshards + 1
+  uint32_t nshards;
+  int32_t own_shard;
+};
+
+uint32_t pack_groups(const FusedShape& f) { return (f.S + kPackGroupRows - 1) / kPackGroupRows; }
+
+uint64_t pack_table_entries(const Layout& L, const FusedShape& f) {
+  return static_cast<uint64_t>(L.parts) * f.K * pack_groups(f) * L.lanes;
+}
+
+// a fused pack needs every shard to be whole column segments (a segment's blocks go to one shard's stream)
+int pack_check(const Layout& L, const FusedShape& f, const uint64_t* bounds, uint32_t nshards) {
+  if (nshards == 0 || nshards > OMR_MAX_WORKERS) return fail("pack: %u shards (1..%d)", nshards, OMR_MAX_WORKERS);
+  if (bounds == nullptr) return fail("pack: NULL shard bounds");
+  if (bounds[0] != 0 || bounds[nshards] != L.rows) return fail("pack: shard bounds must cover rows [0, %llu)",
+                                                                static_cast<unsigned long long>(L.rows));
+  for (uint32_t s = 0; s < nshards; ++s) {
+    if (bounds[s] > bounds[s + 1]) return fail("pack: shard bounds must not decrease");
+    if (bounds[s] % f.S != 0)
+      return fail("pack: shard bound %llu is not a multiple of the scan's %u-row column segments (a ragged shard: "
+                  "pack with omr_move_blocks_f32 instead)", static_cast<unsigned long long>(bounds[s]), f.S);
+  }
+  return 0;
+}
+
+template <int VEC, int SKIP>
+int launch_fused_pack(const FusedArgs& a, const Layout& L, const FusedShape& f, unsigned grid, hipStream_t st) {
+  const uint32_t bits_words = ((f.S + 31) / 32 + 3) & ~3u;
+  const size_t lds = bits_words * sizeof(uint32_t) + static_cast<size_t>(kFusedWaves) * a.wcap * L.block * 4;
+  auto* fn = &k_scan1f<VEC, kFusedWaves, kFusedLoads, SKIP, true>;
+  static bool attr = false;  // (dynamic LDS beyond 64 KiB is opted into once per instantiation)
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return fail("k_scan1f pack: cannot reserve %zu bytes of LDS: %s", lds, hipGetErrorString(e));
+    }
+    attr = true;
+  }
+  fn<<<grid, 64 * kFusedWaves, lds, st>>>(a);
+  return launch_status("k_scan1f (pack)");
+}
+
 int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* out, int32_t* flags, uint32_t* next,
                  void* ws, hipStream_t st, uint64_t* masks = nullptr, uint32_t part_begin = 0,
-                 uint32_t part_count = 0) {
+                 uint32_t part_count = 0, const PackSpec* pk = nullptr) {
   if (part_count == 0) part_count = L.parts - part_begin;
   FusedArgs a{};
   a.part0 = part_begin;
@@ -1308,6 +1555,21 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
   a.masks = masks;
   const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(part_count) * L.lanes * f.K);
   constexpr int T = 64 * kFusedWaves;
+  if (pk != nullptr) {
+    a.send = pk->send;
+    a.shard_cnt = pk->shard_cnt;
+    a.pos = pk->pos;
+    for (uint32_t s = 0; s <= pk->nshards; ++s) a.bounds[s] = static_cast<uint32_t>(pk->bounds[s]);
+    a.nshards = pk->nshards;
+    a.own_shard = pk->own_shard;
+    a.gps = pack_groups(f);
+    a.wcap = kPackLdsBytes / (kFusedWaves * L.block * 4);
+    switch (L.vec) {
+      case 1: return launch_fused_pack<1, 0>(a, L, f, grid, st);
+      case 2: return launch_fused_pack<2, 0>(a, L, f, grid, st);
+      default: return launch_fused_pack<4, 1>(a, L, f, grid, st);
+    }
+  }
   switch (L.vec) {
     case 1: k_scan1f<1, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
     case 2: k_scan1f<2, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
@@ -1748,11 +2010,67 @@ int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint3
   return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks);
 }
 
+int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                             int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out,
+                             const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard, float* send,
+                             uint32_t* shard_counters, uint32_t* pos_table, void* workspace, size_t workspace_bytes,
+                             omr_stream_t stream) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  if (buf == nullptr || next_offsets == nullptr || row_masks == nullptr || send == nullptr ||
+      shard_counters == nullptr || pos_table == nullptr)
+    return fail("worker_scan_pack: buf, next_offsets, row_masks, send, shard_counters and pos_table are required");
+  if (reinterpret_cast<uintptr_t>(buf) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(send) % 16 != 0)
+    return fail("worker_scan_pack: buffers must be 16-byte aligned");
+  const FusedShape f = fused_shape(L);
+  if (int rc = pack_check(L, f, shard_bounds, num_shards)) return rc;
+  if (own_shard < -1 || own_shard >= static_cast<int32_t>(num_shards))
+    return fail("worker_scan_pack: own_shard %d out of range", own_shard);
+  const size_t need = fused_workspace_bytes(L, f);
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need))
+    return fail("worker_scan_pack: needs a zero-initialised workspace of %zu bytes", need);
+  const PackSpec pk{send, shard_counters, pos_table, shard_bounds, num_shards, own_shard};
+  return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks, 0, 0, &pk);
+}
+
+int omr_pack_geometry(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, uint32_t* seg_rows,
+                      uint32_t* groups_per_seg, uint64_t* table_entries) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  const FusedShape f = fused_shape(L);
+  if (seg_rows) *seg_rows = f.S;
+  if (groups_per_seg) *groups_per_seg = pack_groups(f);
+  if (table_entries) *table_entries = pack_table_entries(L, f);
+  return 0;
+}
+
+int omr_pack_supported(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                       const uint64_t* shard_bounds, uint32_t num_shards) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  return pack_check(L, fused_shape(L), shard_bounds, num_shards);
+}
+
 int omr_round_plan_chain(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                          uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
                          uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
                          uint32_t* arrive, uint32_t* done_flag, uint32_t seq, uint32_t* union_next,
                          uint32_t block_size, omr_stream_t stream) {
+  return omr_round_plan_ex(row_masks, count, rows, rows, rows_per_part, num_lanes, bounds, num_bounds, write_set,
+                           union_masks, prefix, counts, zero_masks, nullptr, 0, arrive, done_flag, seq, union_next,
+                           block_size, stream);
+}
+
+int omr_round_plan_ex(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                      uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                      uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
+                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
+                      uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                      omr_stream_t stream) {
+  if (mask_stride < rows) return fail("round_plan: mask_stride %llu < rows", static_cast<unsigned long long>(mask_stride));
+  if (num_zero_counters > kPlanThreads || (num_zero_counters > 0 && zero_counters == nullptr))
+    return fail("round_plan: zero_counters");
   if (count == 0 || count > OMR_MAX_WORKERS) return fail("round_plan: count %u out of range", count);
   if (rows == 0 || rows_per_part == 0 || rows % rows_per_part != 0) return fail("round_plan: bad rows");
   if (num_lanes == 0 || num_lanes > 64) return fail("round_plan: num_lanes %u out of range", num_lanes);
@@ -1763,6 +2081,9 @@ int omr_round_plan_chain(const uint64_t* row_masks, uint32_t count, uint64_t row
   if (num_bounds > OMR_MAX_WORKERS + 2) return fail("round_plan: %u bounds > %d", num_bounds, OMR_MAX_WORKERS + 2);
   PlanArgs a;
   a.masks = row_masks;
+  a.mstride = mask_stride;
+  a.zero_cnt = zero_counters;
+  a.zero_cnt_n = num_zero_counters;
   a.count = count;
   a.rpp = rows_per_part;
   a.lanes = num_lanes;
@@ -1845,30 +2166,52 @@ int omr_move_blocks_f32(const float* src, float* dst, int dir, const uint64_t* r
   return launch_status("k_move");
 }
 
+}  // extern "C"
+
+namespace {
+int launch_shard_sum(const SumArgs& a0, const uint64_t* recv_offsets, hipStream_t st) {
+  SumArgs a = a0;
+  if (a.count == 0 || a.count > OMR_MAX_WORKERS) return fail("shard_sum: count %u out of range", a.count);
+  if (a.block != 256 && a.block != 512 && a.block != 1024) return fail("shard_sum: block_size %u unsupported", a.block);
+  if (a.lanes == 0 || a.lanes > 64 || (a.lanes & (a.lanes - 1)) != 0) return fail("shard_sum: num_lanes %u", a.lanes);
+  if (a.r0 > a.r1 || a.r1 > a.rows) return fail("shard_sum: bad row range");
+  if (a.r1 == a.r0) return 0;
+  if (a.masks == nullptr || a.prefix == nullptr || a.write_set == nullptr || a.out == nullptr ||
+      (a.me < a.count && a.own == nullptr) || (a.count > 1 && a.recv == nullptr) || recv_offsets == nullptr)
+    return fail("shard_sum: NULL pointer");
+  if (reinterpret_cast<uintptr_t>(a.out) % 16 != 0 || reinterpret_cast<uintptr_t>(a.own) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(a.recv) % 16 != 0)
+    return fail("shard_sum: buffers must be 16-byte aligned");
+  for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) {
+    a.recv_off[c] = c < a.count ? recv_offsets[c] : 0;
+    if (c < a.count && c != a.me && a.recv_off[c] > 0xFFFFFFFFull) return fail("shard_sum: recv offset beyond 2^32 blocks");
+  }
+  const uint64_t srows = a.r1 - a.r0;
+  const uint64_t units = a.pos_off != kRowStreams ? (srows / a.S) * a.gps * 2 * a.lanes
+                                                 : ((srows + kSumUnitRows - 1) / kSumUnitRows) * a.lanes;
+  const unsigned g = grid_for(units);
+  switch (a.block / 256) {
+    case 1: k_shard_sum<1><<<g, kWGThreads, 0, st>>>(a); break;
+    case 2: k_shard_sum<2><<<g, kWGThreads, 0, st>>>(a); break;
+    default: k_shard_sum<4><<<g, kWGThreads, 0, st>>>(a); break;
+  }
+  return launch_status("k_shard_sum");
+}
+}  // namespace
+
+extern "C" {
+
 int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const uint64_t* recv_offsets,
                       const uint64_t* row_masks, uint32_t count, const uint32_t* prefix, const uint64_t* write_set,
                       uint64_t rows, uint64_t row_begin, uint64_t row_end, uint32_t num_lanes, uint32_t block_size,
                       int packed_out, float* out, omr_stream_t stream) {
-  if (count == 0 || count > OMR_MAX_WORKERS) return fail("shard_sum: count %u out of range", count);
-  if (block_size != 256 && block_size != 512 && block_size != 1024)
-    return fail("shard_sum: block_size %u unsupported", block_size);
-  const uint32_t vec = block_size / 256;
-  if (num_lanes == 0 || num_lanes > 64 || (num_lanes & (num_lanes - 1)) != 0)
-    return fail("shard_sum: num_lanes %u", num_lanes);
-  if (row_begin > row_end || row_end > rows) return fail("shard_sum: bad row range");
-  if (row_end == row_begin) return 0;
-  if (row_masks == nullptr || prefix == nullptr || write_set == nullptr || out == nullptr ||
-      (me < count && own == nullptr) || (count > 1 && recv == nullptr) || recv_offsets == nullptr)
-    return fail("shard_sum: NULL pointer");
-  if (reinterpret_cast<uintptr_t>(out) % 16 != 0 || reinterpret_cast<uintptr_t>(own) % 16 != 0 ||
-      reinterpret_cast<uintptr_t>(recv) % 16 != 0)
-    return fail("shard_sum: buffers must be 16-byte aligned");
-  ShardArgs a;
+  SumArgs a{};
   a.own = own;
   a.recv = recv;
-  for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) a.recv_off[c] = c < count ? recv_offsets[c] : 0;
   a.masks = row_masks;
+  a.mstride = rows;
   a.prefix = prefix;
+  a.pos_off = kRowStreams;
   a.write_set = write_set;
   a.out = out;
   a.rows = rows;
@@ -1879,15 +2222,44 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
   a.lanes = num_lanes;
   a.block = block_size;
   a.packed_out = packed_out ? 1u : 0u;
-  a.lg = unit_lanes(row_end - row_begin, num_lanes, count > 1 ? 4096 : 8192);
-  const unsigned g = grid_for((row_end - row_begin) * (num_lanes / a.lg));
-  hipStream_t st = S(stream);
-  switch (vec) {
-    case 1: k_shard_sum<1><<<g, kWGThreads, 0, st>>>(a); break;
-    case 2: k_shard_sum<2><<<g, kWGThreads, 0, st>>>(a); break;
-    default: k_shard_sum<4><<<g, kWGThreads, 0, st>>>(a); break;
-  }
-  return launch_status("k_shard_sum");
+  return launch_shard_sum(a, recv_offsets, S(stream));
+}
+
+int omr_shard_sum_cols_f32(const float* own, uint32_t me, const float* recv, const uint64_t* recv_offsets,
+                           const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t pos_offset,
+                           const uint32_t* prefix, const uint64_t* write_set, uint64_t n, uint32_t block_size,
+                           uint32_t num_lanes, uint32_t num_parts, uint64_t row_begin, uint64_t row_end,
+                           int packed_out, float* out, omr_stream_t stream) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  const FusedShape f = fused_shape(L);
+  if (row_begin % f.S != 0 || row_end % f.S != 0)
+    return fail("shard_sum_cols: rows [%llu, %llu) are not whole %u-row column segments",
+                static_cast<unsigned long long>(row_begin), static_cast<unsigned long long>(row_end), f.S);
+  const uint64_t words = mask_stride * 2;  // the position table must lie inside each worker's array
+  if (mask_stride < L.rows || pos_offset < L.rows * 2 || pos_offset + pack_table_entries(L, f) > words)
+    return fail("shard_sum_cols: position table outside the mask arrays (stride %llu, offset %llu)",
+                static_cast<unsigned long long>(mask_stride), static_cast<unsigned long long>(pos_offset));
+  SumArgs a{};
+  a.own = own;
+  a.recv = recv;
+  a.masks = row_masks;
+  a.mstride = mask_stride;
+  a.prefix = prefix;
+  a.pos_off = pos_offset;
+  a.write_set = write_set;
+  a.out = out;
+  a.rows = L.rows;
+  a.r0 = row_begin;
+  a.r1 = row_end;
+  a.count = count;
+  a.me = me;
+  a.lanes = L.lanes;
+  a.block = L.block;
+  a.packed_out = packed_out ? 1u : 0u;
+  a.S = f.S;
+  a.gps = pack_groups(f);
+  return launch_shard_sum(a, recv_offsets, S(stream));
 }
 
 }  // extern "C"

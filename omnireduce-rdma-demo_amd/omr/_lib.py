@@ -59,6 +59,14 @@ SIGNATURES = {
     "omr_move_blocks_f32": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_u64, c_u32, c_u32, c_u64, c_u64, c_vp]),
     "omr_shard_sum_f32": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, c_vp, c_vp, c_u64, c_u64, c_u64, c_u32,
                                   c_u32, c_int, c_vp, c_vp]),
+    "omr_worker_scan_pack_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32,
+                                         ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
+    "omr_pack_geometry": (c_int, [c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp]),
+    "omr_pack_supported": (c_int, [c_u64, c_u32, c_u32, c_u32, c_vp, c_u32]),
+    "omr_round_plan_ex": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp, c_vp, c_u32, c_vp, c_vp, c_u32, c_vp, c_u32, c_vp]),
+    "omr_shard_sum_cols_f32": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, c_u64, c_u64, c_vp, c_vp, c_u64, c_u32,
+                                       c_u32, c_u32, c_u64, c_u64, c_int, c_vp, c_vp]),
     "omr_msg_plan_create": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u32, c_vp]),
     "omr_msg_plan_destroy": (c_int, [c_vp]),
     "omr_msg_round_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -54,6 +54,7 @@ def load():
         "omr_sparse_allreduce_f32": (i, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "omr_sparse_round_f32": (i, [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]),
         "omr_ar_plan_join": (i, [vp, vp]),
+        "omr_ar_plan_fused_pack": (i, [vp]),
         "omr_sparse_buckets_f32": (i, [vp, vp, u64, i, vp, vp, vp]),
         "omr_msgd_plan_create": (i, [vp, u32, u64, u32, u32, u32, vp]),
         "omr_msgd_plan_destroy": (i, [vp]),
@@ -132,6 +133,11 @@ class CppSparseAllreduce:
         L = self.L
         _check(load().omr_ar_plan_create_roles(self._d, self.num_workers, L.n, L.block_size, L.num_lanes,
                                                L.num_threads, ctypes.byref(self._p)), "omr_ar_plan_create_roles")
+
+    @property
+    def fused_pack(self) -> bool:
+        """The worker scan packs the exchange's blocks itself (omr_ar_plan_fused_pack)."""
+        return bool(load().omr_ar_plan_fused_pack(self._p))
 
     def replan(self):
         """Destroy the plan and make a new one of the same shape on the same transport (collective: every rank calls

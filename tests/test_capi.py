@@ -105,3 +105,27 @@ def test_dist_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     bound = set(re.findall(r'"(omr_[a-z0-9_]+)"', inspect.getsource(cdist.load)))
     assert sorted(set(declared) - bound) == [], "omr_dist.h entry points without a ctypes binding"
+
+
+@pytest.mark.parametrize("mib,B,S,gps,entries", [(256, 256, 512, 8, 4096), (256, 1024, 256, 4, 1024),
+                                                 (8, 256, 16, 1, 512)])
+def test_pack_geometry(mib, B, S, gps, entries):
+    """The fused pack's column segments and position table (host-only logic of omr_pack_geometry): config 4's
+    256 MiB at B=256 scans one 512-row segment per (partition, lane) column; B=1024 has two per column."""
+    lib = _lib.load()
+    L = Layout.from_bytes(mib << 20, B)
+    s, g, e = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
+    assert lib.omr_pack_geometry(L.n, B, L.num_lanes, L.num_threads, ctypes.byref(s), ctypes.byref(g),
+                                 ctypes.byref(e)) == 0
+    assert (s.value, g.value, e.value) == (S, gps, entries)
+
+
+@pytest.mark.parametrize("world", range(1, 9))
+def test_pack_supported_worlds(world):
+    """Shards must be whole column segments: worlds 1, 2, 4, 8 of config 4 pack in the scan; 3, 5, 6, 7 (ragged
+    shards) keep the separate pack pass."""
+    lib = _lib.load()
+    L = Layout.from_bytes(256 << 20, 256)
+    b = np.array([s * L.rows // world for s in range(world + 1)], dtype=np.uint64)
+    rc = lib.omr_pack_supported(L.n, 256, L.num_lanes, L.num_threads, b.ctypes.data_as(ctypes.c_void_p), world)
+    assert (rc == 0) == (world in (1, 2, 4, 8)), (world, rc)

@@ -11,6 +11,110 @@
 #include "scan1f_study.h"
 
 namespace {
+// The round-2 product shard sum (kept here as the comparison point; the product's k_shard_sum since round 3 builds a
+// flat (block, contributor) list per unit and issues all its loads at once).
+// Aggregator shard sum over rows [r0, r1) of the write set (server.cc:83-99 with the RDMA hop replaced by the
+// transport): for every write-set block, ((0.0f + x_a0) + x_a1) + ... over the workers whose mask has it, in
+// rank order.  Worker `me`'s contribution is read in place from its dense tensor `own`; worker a's from its
+// received stream at recv + recv_off[a] blocks (its shard blocks in block order).  Output dense (block
+// position, in place) or packed (write-set order of the shard, for the sums' return trip).
+struct ShardArgs {
+  const float* own;
+  const float* recv;
+  uint64_t recv_off[OMR_MAX_WORKERS];
+  const uint64_t* masks;  // [count][rows]
+  const uint32_t* prefix;  // [count + 1][rows + 1]; index count = write set
+  const uint64_t* write_set;
+  float* out;
+  uint64_t rows, r0, r1;
+  uint32_t count, me, lanes, block, packed_out, lg;
+};
+
+template <int VEC>
+__global__ __launch_bounds__(kWGThreads) void k_shard_sum_r02(ShardArgs a) {
+  constexpr int SL = (8 / VEC) < 2 ? 2 : 8 / VEC;  // blocks per batch
+  const int lane = threadIdx.x & 63;
+  const uint32_t groups = a.lanes / a.lg;
+  const uint32_t bbytes = a.block * 4;
+  const uint64_t units = (a.r1 - a.r0) * groups;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
+  const uint32_t* pws = a.prefix + static_cast<uint64_t>(a.count) * (a.rows + 1);
+  const uint64_t cmask = a.count >= 64 ? ~0ull : ((1ull << a.count) - 1ull);
+  for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+       u < units; u += nw) {
+    const uint64_t r = a.r0 + u / groups;
+    const uint32_t g0 = static_cast<uint32_t>(u % groups) * a.lg;
+    // every index load of the unit issued together (one round trip before the data loads): the write-set row and
+    // its prefix, and on lane c < count worker c's mask and stream prefixes
+    const bool cl = static_cast<uint32_t>(lane) < a.count;
+    const uint32_t* pc = a.prefix + static_cast<uint64_t>(cl ? lane : 0) * (a.rows + 1);
+    const uint64_t w = a.write_set[r];
+    const uint64_t mc = cl ? a.masks[static_cast<uint64_t>(lane) * a.rows + r] : 0ull;
+    const uint32_t pcr = pc[r], pcr0 = pc[a.r0];
+    const uint32_t pwr = pws[r], pwr0 = pws[a.r0];
+    uint64_t rem = w & (below(g0 + a.lg) & ~below(g0));
+    if (rem == 0) continue;
+    // lane c: the first block of row r in worker c's stream
+    const uint64_t kc0 = cl ? a.recv_off[lane] + (pcr - pcr0) : 0ull;
+    uint64_t kw = pwr - pwr0 + static_cast<uint64_t>(__builtin_popcountll(w & below(g0)));
+    float* orow = a.out + r * a.lanes * a.block;
+    while (rem != 0) {
+      uint32_t lj[SL];
+      uint64_t bm;
+      const uint32_t nv = take_bits<SL>(rem, lj, bm);
+      v4f acc[SL][VEC];
+#pragma unroll
+      for (int j = 0; j < SL; ++j)
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[j][q] = v4f{0.f, 0.f, 0.f, 0.f};
+      // contributors of the batch in rank order; each worker's (up to SL) blocks loaded at once
+      uint64_t cont = __ballot((mc & bm) != 0) & cmask;
+      while (cont != 0) {
+        const uint32_t c = static_cast<uint32_t>(__builtin_ctzll(cont));
+        cont &= cont - 1;
+        const uint64_t m_c = readlane64(mc, c);
+        const bool mine = c == a.me;
+        const __amdgpu_buffer_rsrc_t src =
+            mine ? chunk_rsrc(a.own + r * a.lanes * a.block, a.lanes * bbytes)
+                 : chunk_rsrc(a.recv + readlane64(kc0, c) * a.block,
+                              static_cast<uint32_t>(__builtin_popcountll(m_c)) * bbytes);
+        v4f v[SL][VEC];
+#pragma unroll
+        for (int j = 0; j < SL; ++j) {
+          const bool has = static_cast<uint32_t>(j) < nv && ((m_c >> lj[j]) & 1u);
+          const uint32_t off = (mine ? lj[j] : static_cast<uint32_t>(__builtin_popcountll(m_c & below(lj[j])))) * bbytes;
+#pragma unroll
+          for (int q = 0; q < VEC; ++q)
+            v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  src, (off + (q * 64 + lane) * 16) | (has ? 0u : kDropStore), 0,
+                                                  kLoadAux));
+        }
+#pragma unroll
+        for (int j = 0; j < SL; ++j)
+          if (static_cast<uint32_t>(j) < nv && ((m_c >> lj[j]) & 1u)) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) acc[j][q] = add4(acc[j][q], v[j][q]);
+          }
+      }
+      const __amdgpu_buffer_rsrc_t dst = a.packed_out ? chunk_rsrc(a.out + kw * a.block, nv * bbytes)
+                                                      : chunk_rsrc(orow, a.lanes * bbytes);
+#pragma unroll
+      for (int j = 0; j < SL; ++j) {
+        const uint32_t off = (a.packed_out ? static_cast<uint32_t>(j) : lj[j]) * bbytes;
+        const uint32_t drop = static_cast<uint32_t>(j) < nv ? 0u : kDropStore;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[j][q]), dst,
+                                                 (off + (q * 64 + lane) * 16) | drop, 0, 0);
+      }
+      kw += nv;
+    }
+  }
+}
+
+}  // namespace
+
+namespace {
 
 template <int VEC, int MC, int SL>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum_all(ShardArgs a) {
@@ -183,7 +287,7 @@ void go_all(ShardArgs a, uint32_t lg, hipStream_t st) {
 void go_prod(ShardArgs a, uint32_t lg, hipStream_t st) {
   const Shape s = shape_of(a, lg);
   a.lg = s.lg;
-  k_shard_sum<1><<<s.grid, kWGThreads, 0, st>>>(a);
+  k_shard_sum_r02<1><<<s.grid, kWGThreads, 0, st>>>(a);
 }
 
 struct Variant {
@@ -192,7 +296,7 @@ struct Variant {
   uint32_t max_count;
 };
 const Variant kVariants[] = {
-    {"product k_shard_sum", go_prod, 16},
+    {"round-2 k_shard_sum", go_prod, 16},
     {"all-contributors MC8 SL4", go_all<8, 4>, 8},
     {"all-contributors MC8 SL2", go_all<8, 2>, 8},
     {"all-contributors MC1 SL16", go_all<1, 16>, 1},

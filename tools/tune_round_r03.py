@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Round 3: the multi-rank round's worker and aggregator kernels at config-4 shapes on one MI355X (8 workers x 256 MiB,
+-r 0.095, seeds 1..8; rank 0's view: worker 0 and aggregator of shard 0 of 8).
+
+Worker side, per launch (algorithmic bytes in brackets):
+  scan       omr_worker_scan_f32             [S + nb*8 + rows*8]
+  scan+pack  omr_worker_scan_pack_f32        [+ the other shards' non-zero blocks written + table]   (the product)
+  pack       omr_move_blocks_f32 (round 2's separate pack pass)  [its blocks read + written]
+Aggregator side, shard 0's sums from 8 contributions (own in place + 7 received streams) [received + own + write-set
+blocks, as tools/tune_round_r02.py counts them]:
+  round-2 k_shard_sum (tools/tune/round_r02.hip), the product's k_shard_sum over row-ordered streams
+  (omr_shard_sum_f32) and over the fused pack's column-ordered streams (omr_shard_sum_cols_f32).
+Every variant's output is checked bit for bit against the others.  Batch-timed with events, interleaved.
+usage: python tools/tune_round_r03.py [--rounds 10] [--reps 20]"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "omnireduce-rdma-demo_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from omr import Layout, _lib, ops  # noqa: E402
+import tune_round_r02 as r02  # noqa: E402
+
+
+def popc(a):
+    return int(sum(bin(int(v) & 0xFFFFFFFFFFFFFFFF).count("1") for v in a))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--density", type=float, default=0.095)
+    ap.add_argument("--only", default="", help="time only the cases whose name contains this (PMC passes)")
+    ap.add_argument("--json", default="", help="also write {case: {us, bytes}} here")
+    a = ap.parse_args()
+    torch.cuda.init()
+    tl = r02.load()
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    L = Layout.from_bytes(256 << 20, 256)
+    m = naggs = a.workers
+    rows, B, NB = L.rows, 256, L.num_lanes
+    S_, gps, ent = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
+    assert lib.omr_pack_geometry(L.n, B, NB, L.num_threads, ctypes.byref(S_), ctypes.byref(gps), ctypes.byref(ent)) == 0
+    ent = ent.value
+    mstride = rows + (ent + 1) // 2
+    bounds = np.array([s * rows // naggs for s in range(naggs + 1)], dtype=np.uint64)
+    bptr = bounds.ctypes.data_as(ctypes.c_void_p)
+    xs = [ops.fill_blocks(torch.from_numpy(ops.gen_bitmap(w, a.density, L.nb)).to(dev), L) for w in range(m)]
+    wsb = lib.omr_scan_workspace_bytes(L.n, B, NB, L.num_threads)
+    ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=dev)
+    flags = torch.empty(L.nb, dtype=torch.int32, device=dev)
+    nxt = torch.empty(L.nb, dtype=torch.int32, device=dev)
+    # every worker's scan + fused pack into its slot of the all-gathered array, and its send buffer
+    masks_all = torch.zeros(m * mstride, dtype=torch.int64, device=dev)
+    sends, cnts = [], []
+    for w in range(m):
+        slot = masks_all[w * mstride:(w + 1) * mstride]
+        send = torch.empty(L.n, dtype=torch.float32, device=dev)
+        cnt = torch.zeros(naggs, dtype=torch.int32, device=dev)
+        _lib.check(lib.omr_worker_scan_pack_f32(xs[w].data_ptr(), L.n, B, NB, L.num_threads, flags.data_ptr(),
+                                                nxt.data_ptr(), slot.data_ptr(), None, bptr, naggs, w, send.data_ptr(),
+                                                cnt.data_ptr(), slot[rows:].data_ptr(), ws.data_ptr(), wsb, st),
+                   "omr_worker_scan_pack_f32")
+        sends.append(send)
+        cnts.append(cnt)
+    torch.cuda.synchronize()
+    cnts = [c.cpu().numpy() for c in cnts]
+    wset = torch.empty(rows, dtype=torch.int64, device=dev)
+    umask = torch.empty(rows, dtype=torch.int64, device=dev)
+    prefix = torch.empty((m + 1) * (rows + 1), dtype=torch.int32, device=dev)
+    counts = torch.empty((m + 1) * (naggs + 1), dtype=torch.int32, device=dev)
+    bdev = torch.from_numpy(bounds.astype(np.int64)).to(dev)
+    _lib.check(lib.omr_round_plan_ex(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                     naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                     counts.data_ptr(), None, None, 0, None, None, 0, None, B, st), "plan")
+    # the round-2 layout: masks [m][rows] contiguous, row-ordered streams packed by k_move
+    masks = torch.stack([masks_all[w * mstride:w * mstride + rows] for w in range(m)]).contiguous()
+    torch.cuda.synchronize()
+    r0, r1 = int(bounds[0]), int(bounds[1])
+    pre = prefix.view(m + 1, rows + 1)
+    per = [cnts[w][0] for w in range(m)]
+    roff = np.zeros(m, dtype=np.uint64)
+    acc = 0
+    for w in range(1, m):
+        roff[w] = acc
+        acc += int(per[w])
+    recv_c = torch.empty(max(acc, 1) * B, dtype=torch.float32, device=dev)  # column-ordered (fused pack) streams
+    recv_r = torch.empty(max(acc, 1) * B, dtype=torch.float32, device=dev)  # row-ordered (k_move) streams
+    for w in range(1, m):
+        k0, k = int(roff[w]), int(per[w])
+        recv_c[k0 * B:(k0 + k) * B].copy_(sends[w][r0 * NB * B:(r0 * NB + k) * B])
+        _lib.check(lib.omr_move_blocks_f32(xs[w].data_ptr(), recv_r[k0 * B:].data_ptr(), 0, masks[w].data_ptr(),
+                                           pre[w].data_ptr(), rows, NB, B, r1, rows, st), "pack")
+    torch.cuda.synchronize()
+    roff_c = roff.ctypes.data_as(ctypes.c_void_p)
+    roff_t = (ctypes.c_uint64 * m)(*[int(v) for v in roff])
+
+    def sum_r02(out):
+        return tl.tune_shard_sum(0, xs[0].data_ptr(), 0, recv_r.data_ptr(), roff_t, masks.data_ptr(), m,
+                                 prefix.data_ptr(), wset.data_ptr(), rows, r0, r1, NB, 0, out.data_ptr(), 0, st)
+
+    def sum_rows(out):
+        return lib.omr_shard_sum_f32(xs[0].data_ptr(), 0, recv_r.data_ptr(), roff_c, masks.data_ptr(), m,
+                                     prefix.data_ptr(), wset.data_ptr(), rows, r0, r1, NB, B, 0, out.data_ptr(), st)
+
+    def sum_cols(out):
+        return lib.omr_shard_sum_cols_f32(xs[0].data_ptr(), 0, recv_c.data_ptr(), roff_c, masks_all.data_ptr(), m,
+                                          mstride, 2 * rows, prefix.data_ptr(), wset.data_ptr(), L.n, B, NB,
+                                          L.num_threads, r0, r1, 0, out.data_ptr(), st)
+
+    sums = {"round-2 k_shard_sum (rows)": sum_r02, "product k_shard_sum (rows)": sum_rows,
+            "product k_shard_sum (cols)": sum_cols}
+    ref = None
+    for name, fn in sums.items():
+        o = xs[0].clone()
+        assert fn(o) == 0, name
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = o
+        assert torch.equal(o.view(torch.int32), ref.view(torch.int32)), f"{name} differs"
+    # worker side: worker 0's scan alone, scan + fused pack, and the separate pack pass
+    own_masks = torch.zeros(mstride, dtype=torch.int64, device=dev)
+    send0 = torch.empty(L.n, dtype=torch.float32, device=dev)
+    cntbig = torch.zeros(a.reps * naggs, dtype=torch.int32, device=dev)  # one fresh counter set per launch
+    packed = torch.empty(L.n, dtype=torch.float32, device=dev)
+
+    def scan():
+        return lib.omr_worker_scan_f32(xs[0].data_ptr(), L.n, B, NB, L.num_threads, flags.data_ptr(), nxt.data_ptr(),
+                                       own_masks.data_ptr(), None, ws.data_ptr(), wsb, st)
+
+    def scan_pack(i=0):
+        return lib.omr_worker_scan_pack_f32(xs[0].data_ptr(), L.n, B, NB, L.num_threads, flags.data_ptr(),
+                                            nxt.data_ptr(), own_masks.data_ptr(), None, bptr, naggs, 0,
+                                            send0.data_ptr(), cntbig[i * naggs:].data_ptr(),
+                                            own_masks[rows:].data_ptr(), ws.data_ptr(), wsb, st)
+
+    def pack():
+        return lib.omr_move_blocks_f32(xs[0].data_ptr(), packed.data_ptr(), 0, masks[0].data_ptr(), pre[0].data_ptr(),
+                                       rows, NB, B, r0, r1, st)
+
+    unext = torch.empty(L.nb, dtype=torch.int32, device=dev)
+
+    def plan():  # the round's bookkeeping launch: union, write set, prefixes, counts, aggregator chain
+        return lib.omr_round_plan_ex(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                     naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                     counts.data_ptr(), None, None, 0, None, None, 0, unext.data_ptr(), B, st)
+
+    workers = {"scan (omr_worker_scan_f32)": scan, "scan + fused pack (product)": scan_pack,
+               "pack pass (k_move, round 2)": pack, "round plan + chain (k_round_plan)": plan}
+    cases = {**sums, **workers}
+    if a.only:
+        cases = {k: v for k, v in cases.items() if a.only in k}
+    outs = [xs[0].clone() for _ in range(2)]
+    times = {k: [] for k in cases}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for r in range(a.rounds):
+        for name, fn in cases.items():
+            cntbig.zero_()
+            e0.record()
+            for i in range(a.reps):
+                if name in sums:
+                    fn(outs[i % 2])
+                elif fn is scan_pack:
+                    fn(i)
+                else:
+                    fn()
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                times[name].append(e0.elapsed_time(e1) / a.reps)
+    mk = masks.cpu().numpy().view(np.uint64)
+    own_blocks = popc(mk[0][r0:r1])
+    ub = popc(wset.cpu().numpy().view(np.uint64)[r0:r1])
+    nc = int(acc)
+    sbytes = (nc + own_blocks + ub) * B * 4
+    other = popc(mk[0]) - own_blocks
+    scan_b = L.nbytes + L.nb * 8 + rows * 8
+    table_b = ent * 4 * (naggs - 1) // naggs
+    wbytes = {"scan (omr_worker_scan_f32)": scan_b, "scan + fused pack (product)": scan_b + other * B * 4 + table_b,
+              "pack pass (k_move, round 2)": 2 * other * B * 4,
+              # reads every worker's masks; writes write set, union, m + 1 prefix arrays, counts, the union chain
+              "round plan + chain (k_round_plan)": m * rows * 8 + 2 * rows * 8 + (m + 1) * (rows + 1) * 4 +
+              L.nb * 4}
+    report = {}
+    print(f"## config 4 shapes, {m} workers, -r {a.density}: shard 0 write set {ub} blocks, received {nc}, own {own_blocks}: "
+          f"{sbytes} B per shard sum; worker 0 packs {other} blocks", flush=True)
+    for name in cases:
+        t = np.median(times[name]) * 1e-3
+        b = sbytes if name in sums else wbytes[name]
+        report[name] = {"us": round(t * 1e6, 3), "algorithmic_bytes": int(b), "GBps": round(b / t / 1e9, 1)}
+        print(f"{name:34s} median {t * 1e6:8.2f} us  {b:>11d} B  {b / t / 1e9:7.1f} GB/s  ({b / t / 8e12:.3f} of 8 TB/s)",
+              flush=True)
+    if all(k in times and times[k] for k in list(workers)[:3]):
+        ts, tsp, tp = (np.median(times[k]) * 1e3 for k in list(workers)[:3])
+        print(f"worker side per round: scan + pack pass {ts + tp:.2f} us -> fused {tsp:.2f} us", flush=True)
+    if a.json:
+        import json
+        with open(a.json, "w") as f:
+            json.dump(report, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
