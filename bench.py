@@ -213,7 +213,7 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
     }
 
 
-def round_world1(args, L: Layout, sets, dev, stream):
+def round_world1(args, L: Layout, sets, dev, stream, bm=None):
     """The N>1 step's own code path at N=1, measured after the headline's timed region (which it does not touch): the
     C++ round (worker scan, mask all-gather, plan, exchange with no peers, shard sum over the whole tensor, deferred
     pipeline as bench picks at world 1) over a one-rank RCCL communicator made in this process.  Its per-round time is
@@ -254,7 +254,8 @@ def round_world1(args, L: Layout, sets, dev, stream):
     stages, _, _, n_timed = eng.stage_timings()
     eng.close()
     scan_ms = stages["scan"]
-    sb = scan_only_bytes(L)
+    # a one-rank round's worker scan writes the shard sums itself (0.0f + x over the write set: omr_sparse_round_f32)
+    sb = (fused_bytes(L, bm) + L.rows * 8) if bm is not None else scan_only_bytes(L)
     return {"ms_per_round": round(dt * 1e3, 5), "value": round(L.nbytes / dt / 1e9, 2), "unit": "GB/s",
             "mode": "reduce-scatter (the N>1 bench default), deferred pipeline (OMR_ROUND_DEFER)",
             "transport": "RCCL, one-rank communicator in this process (no peers: nothing crosses xGMI)",
@@ -487,7 +488,10 @@ def main():
                    ("k_scan1" if m == 1 else "k_scanm"))
     if dist_mode:
         kernel_name = ("k_scan1f (round worker scan: flags + next + row masks + the fused pack of the other shards' "
-                       "blocks)" if engine_fused else "k_scan1f (round worker scan: flags + next + row masks, no out)")
+                       "blocks)" if engine_fused else
+                       "k_scan1f (one-rank round's worker scan: flags + next + row masks + the shard sums)"
+                       if n_gpus == 1 and args.dist_mode != "dense" else
+                       "k_scan1f (round worker scan: flags + next + row masks, no out)")
     scan_ms_dist = None
     if dist_mode:
         # the timed rounds' own events (every `every`-th timed step): its worker scan kernel on the caller's stream,
@@ -517,7 +521,10 @@ def main():
         kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
     if True:
         if dist_mode:
-            kbytes = (scan_pack_bytes(L, bitmaps[0], rank, n_gpus) if engine_fused else scan_only_bytes(L))
+            if n_gpus == 1 and args.dist_mode != "dense":  # one rank: the scan writes the shard sums itself
+                kbytes = fused_bytes(L, bitmaps[0]) + L.rows * 8
+            else:
+                kbytes = (scan_pack_bytes(L, bitmaps[0], rank, n_gpus) if engine_fused else scan_only_bytes(L))
         elif m == 1 and args.kernel == "fused":
             kbytes = fused_bytes(L, bitmaps[0])
         else:
@@ -596,7 +603,7 @@ def main():
         if pipe_probe is not None:
             line["exchange"]["pipe_probe_ms_per_round"] = pipe_probe
     if not dist_mode and m == 1 and not args.no_round:
-        line["round_world1"] = round_world1(args, L, sets, dev, stream)
+        line["round_world1"] = round_world1(args, L, sets, dev, stream, bitmaps[0])
     if not dist_mode and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(L, bitmaps[0], args)
     print(json.dumps(line), flush=True)

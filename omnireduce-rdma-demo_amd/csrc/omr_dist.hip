@@ -837,6 +837,7 @@ struct omr_ar_plan {
   // buffer, over PCIe) and writes its non-zero blocks and lane heads (0.0f + x) into the round's x, the staging
   // buffer the rest of the round reads (a sum of 0.0f + x_w equals a sum of x_w bit for bit)
   const float* scan_from = nullptr;
+  bool in_buckets = false;  // omr_sparse_buckets_f32 is issuing the rounds
 };
 
 namespace {
@@ -1152,8 +1153,13 @@ int timed_exchange(omr_ar_plan* p, int slot) {
   return 0;
 }
 
+// (internal bit in a round's mode: a one-rank round whose worker scan wrote the sums itself, see omr_sparse_round_f32)
+constexpr int kModeSolo = 0x10000;
+
 int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, bool async, bool timed, uint32_t seq,
                  hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks, int tslot) {
+  const bool solo = (mode & kModeSolo) != 0;
+  mode &= ~kModeSolo;
   struct CloseRecord {  // the timing record is complete (or abandoned) once this second half returns
     omr_ar_plan* p;
     int slot;
@@ -1244,7 +1250,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
   // 5. aggregator: rank-order shard sums (server.cc:97-98); a co-located rank reads its own blocks in place.
   //    Co-located reduce-scatter writes them in place (dense); otherwise packed in write-set order
   float* sums = nullptr;
-  if (sh >= 0) {
+  if (sh >= 0 && !solo) {
     const uint64_t r0 = p->bounds[sh], r1 = p->bounds[sh + 1];
     const bool dense_out = rs_mode && p->colocated;
     // (a dedicated aggregator keeps only its own shard's sums: at the start of `results`)
@@ -1277,7 +1283,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
         }
       TRY(p->d->exchange(ss, sr, xs));
     }
-    if (wk && out != nullptr)
+    if (wk && out != nullptr && !solo)
       TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, S.wset, S.prefix + static_cast<uint64_t>(M) * (rows + 1),
                                         rows, p->lanes, p->B, 0, 0, xstream), "omr_move_blocks_f32 unpack"));
   }
@@ -1514,6 +1520,13 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   const int si = p->cur;
   omr_ar_plan::Set& S = p->set[si];
   p->cur = (p->cur + 1) % omr_ar_plan::kSets;
+  // A one-rank group's aggregator sums one worker's blocks: its shard sum is 0.0f + x over the write set (the worker's
+  // non-zero blocks and the lane heads), exactly what the worker scan writes when it is given `out` (k_scan1f, as
+  // the single-GPU step).  So the scan writes the sums, and the second half skips the shard sum and the unpack.  (Not
+  // in the bucket pipeline, whose `out` may be a pinned host buffer's mapping: there the write-back stays beside the
+  // next bucket's scan instead of inside it.)
+  const bool solo = p->N == 1 && p->worker() && p->colocated && p->scan_from == nullptr && !p->in_buckets &&
+                    mode != OMR_ROUND_DENSE_REDUCE_SCATTER;
   // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass (a dedicated aggregator
   //    offers its all-zero mask buffer to the all-gather).  The set's own masks must have been consumed and
   //    re-zeroed by the plan of the round kSets calls back.
@@ -1532,7 +1545,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   if (p->worker()) {
     if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
     const float* src = p->scan_from ? p->scan_from : x;
-    float* sout = p->scan_from ? const_cast<float*>(x) : nullptr;
+    float* sout = p->scan_from ? const_cast<float*>(x) : (solo ? out : nullptr);
     const bool pack = p->fused_pack && (mode & 0xFF) != OMR_ROUND_DENSE_REDUCE_SCATTER;
     if (pack)  // the scan also writes this worker's blocks of the other shards into their send streams
       TRY(omr_check(omr_worker_scan_pack_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout, p->bounds.data(),
@@ -1554,7 +1567,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   p->ht.lap("1:scan events");
   omr_ar_plan::Job j;
   j.si = si;
-  j.mode = mode;
+  j.mode = mode | (solo ? kModeSolo : 0);
   j.tslot = tslot;
   j.async = async;
   j.defer = defer;
@@ -1591,6 +1604,11 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
                            uint64_t* union_blocks, omr_stream_t stream) {
   if (p == nullptr || buf == nullptr) return derr(OMR_EINVAL, "sparse_buckets: NULL");
   TRY(thread_drain(p));
+  struct InBuckets {  // (the rounds of this call keep their shard sum off the scan: see omr_sparse_round_f32)
+    omr_ar_plan* p;
+    ~InBuckets() { p->in_buckets = false; }
+  } in_buckets{p};
+  p->in_buckets = true;
   if (total_n == 0 || total_n % p->n != 0)
     return derr(OMR_EINVAL, "sparse_buckets: total_n %llu is not a multiple of the plan's bucket of %llu floats",
                 static_cast<unsigned long long>(total_n), static_cast<unsigned long long>(p->n));

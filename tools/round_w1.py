@@ -41,7 +41,7 @@ def main():
             launches[i % 4]()
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res = bench.round_world1(a, L, sets, dev, stream)
+    res = bench.round_world1(a, L, sets, dev, stream, bm)
     res["wall_s"] = round(time.perf_counter() - t0, 3)
     res["GPU_MAX_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES")
     res["headline_first"] = a.headline
