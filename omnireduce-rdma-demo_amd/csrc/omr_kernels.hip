@@ -17,6 +17,7 @@
 //   exchange kernels  : mask union, popcount prefixes, compaction, block gather/scatter, sparse shard sum.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -1518,15 +1519,18 @@ int launch_fused_pack(const FusedArgs& a, const Layout& L, const FusedShape& f, 
   const uint32_t bits_words = ((f.S + 31) / 32 + 3) & ~3u;
   const size_t lds = bits_words * sizeof(uint32_t) + static_cast<size_t>(kFusedWaves) * a.wcap * L.block * 4;
   auto* fn = &k_scan1f<VEC, kFusedWaves, kFusedLoads, SKIP, true>;
-  static bool attr = false;  // (dynamic LDS beyond 64 KiB is opted into once per instantiation)
-  if (!attr) {
+  // dynamic LDS beyond 64 KiB is opted into per instantiation, raised when a layout needs more (S sizes the bits)
+  static std::atomic<size_t> attr{0};
+  if (lds > attr.load()) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     if (e != hipSuccess) {
       (void)hipGetLastError();
       return fail("k_scan1f pack: cannot reserve %zu bytes of LDS: %s", lds, hipGetErrorString(e));
     }
-    attr = true;
+    size_t cur = attr.load();
+    while (lds > cur && !attr.compare_exchange_weak(cur, lds)) {
+    }
   }
   fn<<<grid, 64 * kFusedWaves, lds, st>>>(a);
   return launch_status("k_scan1f (pack)");
