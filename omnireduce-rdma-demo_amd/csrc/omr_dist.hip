@@ -744,6 +744,8 @@ struct omr_ar_plan {
     hipEvent_t done = nullptr;      // recorded on the communication stream once the round is through with it
     bool pending = false;           // `done` recorded and not yet waited for by a refill
     bool plan_pending = false;      // `planned` recorded and not yet waited for by a scan
+    bool scan_wait = false;         // fused pack: `done` recorded and not yet waited for by the scan that refills
+                                    // `packed` (guarded by mu: the progress thread sets it)
   } set[kSets];
   int cur = 0;                      // the set the next round fills
   int last_async = -1;              // set of the last asynchronous round (for join)
@@ -819,6 +821,7 @@ struct omr_ar_plan {
   std::condition_variable cv_job, cv_done;
   std::deque<Job> jobs;
   uint64_t rounds_begun = 0, first_halves = 0;  // rounds whose scan is queued / whose bookkeeping is issued
+  uint64_t second_halves = 0;  // rounds whose exchange and aggregation are issued (or abandoned on an error)
   bool busy = false, stop = false;
   int thread_rc = 0;
   std::string thread_err;
@@ -1167,6 +1170,16 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       if (slot >= 0) p->timed[slot].open = false;
     }
   } close_record{p, timed ? tslot : -1};
+  struct CountHalf {  // (a fused-pack scan that refills this set waits until this second half is issued)
+    omr_ar_plan* p;
+    ~CountHalf() {
+      {
+        std::lock_guard<std::mutex> g(p->mu);
+        ++p->second_halves;
+      }
+      p->cv_done.notify_all();
+    }
+  } count_half{p};
   omr_ar_plan::Set& S = p->set[si];
   const int N = p->N, M = p->M, NA = p->A, me = p->me, sh = p->shard;
   const uint64_t rows = p->rows, B = p->B;
@@ -1200,6 +1213,8 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
       S.pending = true;
       p->last_async = si;
+      std::lock_guard<std::mutex> g(p->mu);
+      S.scan_wait = true;
     }
     if (sent_blocks != nullptr || union_blocks != nullptr) TRY(wait_flag(flag, seq, st));
     if (sent_blocks) *sent_blocks = (r1 - r0) * p->lanes * static_cast<uint64_t>(N - 1);
@@ -1295,6 +1310,8 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
     S.pending = true;
     p->last_async = si;
+    std::lock_guard<std::mutex> g(p->mu);
+    S.scan_wait = true;
   }
   ht_of(p).lap("2:rest");
   if (sent_blocks) *sent_blocks = total_send;
@@ -1432,7 +1449,7 @@ void progress_main(omr_ar_plan* p) {
       p->thread_rc = rc;
       p->thread_err = g_derr;
     }
-    if (p->thread_rc != 0) p->first_halves = p->rounds_begun;
+    if (p->thread_rc != 0) p->first_halves = p->second_halves = p->rounds_begun;
     p->busy = false;
     p->cv_done.notify_all();
   }
@@ -1541,6 +1558,20 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   if (S.plan_pending) {
     TRY(wait_ev(st, S.planned));
     S.plan_pending = false;
+  }
+  // A fused-pack scan refills the set's send streams: the exchange of the round kSets calls back, which reads them
+  // (issued up to kDeferDepth calls later, on the communication stream), must be through first.  The progress thread
+  // may not have issued it yet: wait until it has (at most one call behind then), then for it on the device.
+  const bool pack_scan = p->fused_pack && p->worker() && mode != OMR_ROUND_DENSE_REDUCE_SCATTER;
+  if (pack_scan) {
+    std::unique_lock<std::mutex> lk(p->mu);
+    const uint64_t need = p->rounds_begun >= omr_ar_plan::kSets ? p->rounds_begun - (omr_ar_plan::kSets - 1) : 0;
+    if (threaded) p->cv_done.wait(lk, [&] { return p->second_halves >= need || p->thread_rc != 0; });
+    if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
+    const bool w = S.scan_wait;
+    S.scan_wait = false;
+    lk.unlock();
+    if (w) TRY(wait_ev(st, S.done));
   }
   if (p->worker()) {
     if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));

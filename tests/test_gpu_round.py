@@ -189,9 +189,14 @@ def test_move_blocks_pack_unpack(gpu, B, rows, skip):
     assert (dense.cpu().numpy().view(np.uint32) == want.ravel().view(np.uint32)).all()
 
 
-@pytest.mark.parametrize("count,me,B,packed_out", [(1, 0, 256, 0), (3, 1, 256, 0), (3, 2, 256, 1), (8, 5, 256, 1),
-                                                   (4, 0, 1024, 0), (2, 1, 512, 1), (16, 7, 256, 0)])
-def test_shard_sum(gpu, count, me, B, packed_out):
+@pytest.mark.parametrize("count,me,B,packed_out,span", [
+    (1, 0, 256, 0, None), (3, 1, 256, 0, None), (3, 2, 256, 1, None), (8, 5, 256, 1, None), (4, 0, 1024, 0, None),
+    (2, 1, 512, 1, None), (16, 7, 256, 0, None),
+    (3, 3, 256, 1, None),        # a dedicated aggregator (me == count): no own contribution
+    (5, 2, 256, 0, (5, 70)),     # a row range that is not whole 32-row units (ragged shards)
+    (4, 4, 512, 1, (1, 2)),      # one row
+])
+def test_shard_sum(gpu, count, me, B, packed_out, span):
     L = Layout(n=(2 << 20) if B == 256 else (4 << 20), block_size=B)
     lanes, rows = L.num_lanes, L.rows
     xs = [oracle.fill(oracle.gen_bitmap(c, 0.2, L.nb), B, mode=1, seed=11 + c) for c in range(count)]
@@ -199,7 +204,7 @@ def test_shard_sum(gpu, count, me, B, packed_out):
     masks = np.stack([oracle.row_masks(f, lanes) for f in flags])
     u, wset = np_write_set(masks, L.rows_per_part, lanes)
     N = 4
-    r0, r1 = rows // N, 3 * rows // N  # a two-shard-wide row range
+    r0, r1 = span if span else (rows // N, 3 * rows // N)  # default: a two-shard-wide row range
     # worker c != me sends its non-zero blocks of [r0, r1) in block order; streams concatenated in rank order
     streams, roff, acc = [], [], 0
     for c in range(count):
@@ -211,7 +216,7 @@ def test_shard_sum(gpu, count, me, B, packed_out):
     recv = np.concatenate(streams).ravel() if streams and acc else np.zeros(B, np.float32)
     prefix = np.concatenate([np_prefix(masks[c]) for c in range(count)] + [np_prefix(wset)])
     lib = _lib.load()
-    own = torch.from_numpy(xs[me]).to(gpu)
+    own = torch.from_numpy(xs[me] if me < count else np.zeros(L.n, np.float32)).to(gpu)
     recvd = torch.from_numpy(recv.astype(np.float32)).to(gpu)
     md = torch.from_numpy(masks.view(np.int64).ravel()).to(gpu)
     pd = torch.from_numpy(prefix.view(np.int32)).to(gpu)
@@ -222,8 +227,8 @@ def test_shard_sum(gpu, count, me, B, packed_out):
         out = torch.full((len(wblocks) * B,), np.nan, dtype=torch.float32, device=gpu)
     else:
         out = own.clone()  # dense, in place semantics: other blocks keep x_me
-    assert lib.omr_shard_sum_f32(P(own), me, P(recvd), roff_h, P(md), count, P(pd), P(wd), rows, r0, r1, lanes, B,
-                                 packed_out, P(out), stream()) == 0, lib.omr_last_error()
+    assert lib.omr_shard_sum_f32(P(own) if me < count else None, me, P(recvd), roff_h, P(md), count, P(pd), P(wd),
+                                 rows, r0, r1, lanes, B, packed_out, P(out), stream()) == 0, lib.omr_last_error()
     torch.cuda.synchronize()
     # expected: rank-order sums from +0.0 over the workers that flag the block (server.cc:97-98, :148-150)
     exp_blocks = np.zeros((len(wblocks), B), dtype=np.float32)
@@ -237,6 +242,6 @@ def test_shard_sum(gpu, count, me, B, packed_out):
     if packed_out:
         assert (got.view(np.uint32) == exp_blocks.ravel().view(np.uint32)).all()
     else:
-        want = xs[me].copy().reshape(-1, B)
+        want = (xs[me].copy() if me < count else np.zeros(L.n, np.float32)).reshape(-1, B)
         want[wblocks] = exp_blocks
         assert (got.view(np.uint32) == want.ravel().view(np.uint32)).all()

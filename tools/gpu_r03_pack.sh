@@ -10,6 +10,7 @@ cd $R
 timeout -k 10 300 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu tests/test_gpu_pack.py \
   > $O/tests_pack.log 2>&1 && \
 timeout -k 10 300 python3 tools/tune_round_r03.py > $O/tune_round_r03.log 2>&1 && \
+timeout -k 10 300 python3 tools/tune_shard_r03.py > $O/tune_shard_r03.log 2>&1 && \
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu tests/test_gpu_round.py \
   tests/test_cpp_dist.py tests/test_gpu_ipc.py tests/test_gpu_fault.py > $O/tests.log 2>&1 && \
 timeout -k 10 300 python3 bench.py --no-cpu > $O/c2.json 2> $O/c2.err && \

@@ -31,7 +31,7 @@ def popc(a):
     return int(sum(bin(int(v) & 0xFFFFFFFFFFFFFFFF).count("1") for v in a))
 
 
-def main():
+def parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workers", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=10)
@@ -39,9 +39,12 @@ def main():
     ap.add_argument("--density", type=float, default=0.095)
     ap.add_argument("--only", default="", help="time only the cases whose name contains this (PMC passes)")
     ap.add_argument("--json", default="", help="also write {case: {us, bytes}} here")
-    a = ap.parse_args()
-    torch.cuda.init()
-    tl = r02.load()
+    return ap
+
+
+def setup(a):
+    """Config-4 shapes on one device: m workers' scans with the fused pack, the plan over the all-gathered arrays, and
+    shard 0's received streams in both layouts (column-ordered from the fused pack, row-ordered from k_move)."""
     lib = _lib.load()
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
@@ -101,6 +104,25 @@ def main():
         _lib.check(lib.omr_move_blocks_f32(xs[w].data_ptr(), recv_r[k0 * B:].data_ptr(), 0, masks[w].data_ptr(),
                                            pre[w].data_ptr(), rows, NB, B, r1, rows, st), "pack")
     torch.cuda.synchronize()
+    return dict(L=L, m=m, naggs=naggs, rows=rows, B=B, NB=NB, ent=ent, mstride=mstride, bounds=bounds, bptr=bptr,
+                xs=xs, wsb=wsb, ws=ws, flags=flags, nxt=nxt, masks_all=masks_all, sends=sends, cnts=cnts, wset=wset,
+                umask=umask, prefix=prefix, counts=counts, bdev=bdev, masks=masks, r0=r0, r1=r1, pre=pre, roff=roff,
+                acc=acc, recv_c=recv_c, recv_r=recv_r, S=S_.value, gps=gps.value, dev=dev, st=st)
+
+
+def main():
+    a = parser().parse_args()
+    torch.cuda.init()
+    tl = r02.load()
+    lib = _lib.load()
+    D = setup(a)
+    L, m, naggs, rows, B, NB, ent, mstride = (D[k] for k in ("L", "m", "naggs", "rows", "B", "NB", "ent", "mstride"))
+    bounds, bptr, xs, wsb, ws, flags, nxt = (D[k] for k in ("bounds", "bptr", "xs", "wsb", "ws", "flags", "nxt"))
+    masks_all, wset, umask, prefix, counts, bdev = (D[k] for k in ("masks_all", "wset", "umask", "prefix", "counts",
+                                                                     "bdev"))
+    masks, r0, r1, pre, roff, acc, recv_c, recv_r = (D[k] for k in ("masks", "r0", "r1", "pre", "roff", "acc",
+                                                                   "recv_c", "recv_r"))
+    dev, st = D["dev"], D["st"]
     roff_c = roff.ctypes.data_as(ctypes.c_void_p)
     roff_t = (ctypes.c_uint64 * m)(*[int(v) for v in roff])
 
