@@ -451,7 +451,10 @@ struct IpcDist final : omr_dist {
     auto it = own.find(key);
     if (it == own.end()) {
       OwnHandle oh;
-      TRY(hip_check(hipIpcGetMemHandle(&oh.h, base), "hipIpcGetMemHandle"));
+      const hipError_t e = hipIpcGetMemHandle(&oh.h, base);
+      if (e != hipSuccess)
+        return derr(static_cast<int>(e), "hipIpcGetMemHandle: %s (pointer %p in allocation %p of %zu bytes)",
+                    hipGetErrorString(e), ptr, reinterpret_cast<void*>(base), size);
       oh.id = next_id++;
       it = own.emplace(key, oh).first;
     }
