@@ -45,10 +45,11 @@ int omr_dist_create_rccl(const void* id, int rank, int world, omr_dist** out);
  * rank calls omr_dist_ipc_unique_id and shares the id out of band (the ./omr_server rendezvous does); every rank
  * then calls omr_dist_create_ipc, which returns once all have joined.  Data moves device to device (each receiver
  * copies out of the sender's IPC-mapped buffer); ordering is carried on the device by IPC events, so calls return
- * without synchronising any stream, as with RCCL.  The transport caches IPC handles and peer mappings per allocation:
- * a plan's own buffers are dropped from the cache when the plan is destroyed (a new plan on the same transport is
- * mapped afresh), but buffers the caller hands to a round must stay allocated while the transport lives.  Destroy is
- * collective. */
+ * without synchronising any stream, as with RCCL.  The transport caches IPC handles and peer mappings per allocation.
+ * Plans allocate their device buffers through the transport, which keeps every buffer it exported alive until it is
+ * destroyed itself and hands it to the next plan that asks for the same size (a freed allocation a peer still maps
+ * may come back from hipMalloc at the same address, and ROCm then refuses to export it).  Buffers the caller hands
+ * to a round must stay allocated while the transport lives.  Destroy is collective. */
 int omr_dist_ipc_unique_id(void* id /* OMR_UNIQUE_ID_BYTES */);
 int omr_dist_create_ipc(const void* id, int rank, int world, omr_dist** out);
 

@@ -90,8 +90,11 @@ struct omr_dist {
   virtual int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) = 0;
   // out[0 .. count) = sum over ranks p of in_p[rank*count .. (rank+1)*count)  (dense stand-in)
   virtual int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) = 0;
-  // the allocation holding `ptr` is about to be freed: drop anything cached about it (called before hipFree)
-  virtual void forget(const void* ptr) { (void)ptr; }
+  // Device memory of the plans that run on this transport goes through it: a transport that exports buffers to
+  // other processes (HIP IPC) keeps every exported allocation alive until it is destroyed itself and hands it back
+  // to the next alloc of the same size, so an address a peer has mapped is never freed and re-allocated under it.
+  virtual int alloc(void** ptr, size_t bytes) { return hip_check(hipMalloc(ptr, bytes), "hipMalloc"); }
+  virtual void release(void* ptr) { (void)hipFree(ptr); }
 };
 
 namespace {
@@ -306,8 +309,9 @@ struct IpcDist final : omr_dist {
   std::vector<std::array<IpcEvents, kIpcChans * 2>> peer;  // peers' events, opened, [p][c * 2 + g % 2]
   std::vector<hipEvent_t> retired;                         // events of old generations, destroyed in batches
   uint64_t seq[kIpcChans] = {0, 0};
-  // allocation (base, size) -> its handle and this rank's id for it.  forget() drops an entry before the allocation is
-  // freed, so a later allocation at the same range is posted under a new id and the peers map it afresh
+  // allocation (base, size) -> its handle and this rank's id for it.  The plans' exported allocations are never freed
+  // while the transport lives (release() parks them), so an entry never outlives its allocation.  A
+  // caller's buffer (an input or output tensor) must stay allocated while the transport lives, as omr_dist.h says.
   struct OwnHandle {
     hipIpcMemHandle_t h;
     uint64_t id;
@@ -319,6 +323,8 @@ struct IpcDist final : omr_dist {
     char* base;
   };
   std::map<std::pair<int, std::string>, Mapping> opened;  // (peer, handle bytes) -> the mapping of its current id
+  std::map<void*, size_t> sized;                           // live allocations made through alloc(): their sizes
+  std::multimap<size_t, void*> parked;                     // released exported allocations, by size
 
   static void release(IpcEvents& e, std::vector<hipEvent_t>& to) {
     for (int k = 0; k < kIpcRing; ++k) {
@@ -338,6 +344,8 @@ struct IpcDist final : omr_dist {
         (void)ipc_spin([&] { return b->rank[p].left.load(std::memory_order_acquire) != 0; }, "peers to leave", rank);
       for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second.base);
     }
+    // every peer has left (closed its mappings of them): the parked allocations can go now
+    for (auto& kv : parked) (void)hipFree(kv.second);
     for (auto& v : peer)
       for (IpcEvents& e : v) release(e, retired);
     for (auto& row : mine)
@@ -464,15 +472,33 @@ struct IpcDist final : omr_dist {
     return 0;
   }
 
-  void forget(const void* ptr) override {
-    if (ptr == nullptr) return;
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    if (hipMemGetAddressRange(&base, &size, const_cast<void*>(ptr)) != hipSuccess) {
-      (void)hipGetLastError();
-      return;
+  // Plans' allocations.  An exported one is parked, not freed, when its plan goes: on ROCm 7 a freed allocation that
+  // a peer still maps can come back from hipMalloc at the same address, and hipIpcGetMemHandle then refuses it
+  // ("invalid argument"; seen when a plan was destroyed and re-created on the transport).  A parked allocation keeps
+  // its handle and id, so the peers' mappings of it stay right when the next plan reuses it.
+  int alloc(void** ptr, size_t bytes) override {
+    auto it = parked.find(bytes);
+    if (it != parked.end()) {
+      *ptr = it->second;
+      parked.erase(it);
+    } else {
+      TRY(hip_check(hipMalloc(ptr, bytes), "hipMalloc"));
     }
-    own.erase(std::make_pair(reinterpret_cast<uintptr_t>(base), size));
+    sized[*ptr] = bytes;
+    return 0;
+  }
+  void release(void* ptr) override {
+    if (ptr == nullptr) return;
+    auto s = sized.find(ptr);
+    const auto o = own.lower_bound(std::make_pair(reinterpret_cast<uintptr_t>(ptr), size_t{0}));
+    const bool exported = o != own.end() && o->first.first == reinterpret_cast<uintptr_t>(ptr);
+    if (s != sized.end() && exported) {
+      parked.emplace(s->second, ptr);
+    } else {
+      if (exported) own.erase(o);
+      (void)hipFree(ptr);
+    }
+    if (s != sized.end()) sized.erase(s);
   }
 
   // peer p's piece: its allocation mapped once per id (a new id for the same handle bytes replaces the old mapping,
@@ -701,9 +727,10 @@ struct HostTrace {
   }
 };
 
+// a plan's device buffer, through its transport (omr_dist::alloc)
 template <typename T>
-int dev_alloc(T** p, size_t count) {
-  return hip_check(hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(count, 1) * sizeof(T)), "hipMalloc");
+int dev_alloc(omr_dist* d, T** p, size_t count) {
+  return d->alloc(reinterpret_cast<void**>(p), std::max<size_t>(count, 1) * sizeof(T));
 }
 
 }  // namespace
@@ -969,30 +996,22 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     fprintf(stderr, "[omr host trace rank %d] progress thread:\n", p->me);
     p->ht_thread.print(p->me);
   }
-  if (p->npend > 0) {  // deferred rounds still owe their exchanges to the peers: issue them and let them drain
+  if (p->npend > 0)  // deferred rounds still owe their exchanges to the peers: issue them and let them drain
     (void)flush_pending(p, p->cs, nullptr, nullptr);
-    (void)hipDeviceSynchronize();
-  }
-  // (the transport forgets what it cached about each buffer first: its IPC handle)
-  void* devs[] = {p->bounds_dev, p->recv, p->results, p->flags_ws, p->next_ws, p->unext_ws, p->scan_ws};
-  for (void* v : devs) {
-    if (v) p->d->forget(v);
-    (void)hipFree(v);
-  }
+  (void)hipDeviceSynchronize();
+  // back to the transport, which keeps the exported ones alive for the next plan (omr_dist::alloc)
+  void* devs[] = {p->bounds_dev, p->recv, p->results, p->flags_ws, p->next_ws, p->unext_ws, p->scan_ws, p->arrive};
+  for (void* v : devs) p->d->release(v);
   for (auto& st : p->set) {
     void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed, st.pack_cnt};
-    for (void* v : sv) {
-      if (v) p->d->forget(v);
-      (void)hipFree(v);
-    }
+    for (void* v : sv) p->d->release(v);
     for (hipEvent_t e : {st.scanned, st.planned, st.ready, st.done})
       if (e) (void)hipEventDestroy(e);
   }
   if (p->ps) (void)hipStreamDestroy(p->ps);
   if (p->cs) (void)hipStreamDestroy(p->cs);
   for (int r = 0; r < omr_ar_plan::kStage; ++r) {
-    if (p->stage[r]) p->d->forget(p->stage[r]);
-    (void)hipFree(p->stage[r]);
+    p->d->release(p->stage[r]);
     for (hipEvent_t e : {p->ev_in[r], p->ev_round[r], p->ev_out[r]})
       if (e) (void)hipEventDestroy(e);
   }
@@ -1004,7 +1023,6 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
       if (e) (void)hipEventDestroy(e);
   (void)hipHostFree(p->counts_host);
   (void)hipHostFree(p->flag_host);
-  (void)hipFree(p->arrive);
   delete p;
   return 0;
 }
@@ -1067,13 +1085,13 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   const char* sf = getenv("OMR_EVENT_SYSFENCE");
   const unsigned evflags = hipEventDisableTiming | ((sf != nullptr && atoi(sf) != 0) ? 0u : hipEventDisableSystemFence);
   for (auto& st : p->set) {
-    A(dev_alloc(&st.own, p->mstride));
-    A(dev_alloc(&st.masks_all, static_cast<size_t>(N) * p->mstride));
-    if (p->fused_pack) A(dev_alloc(&st.pack_cnt, NA));
-    A(dev_alloc(&st.wset, p->rows));
-    A(dev_alloc(&st.umask, p->rows));
-    A(dev_alloc(&st.prefix, static_cast<size_t>(M + 1) * (p->rows + 1)));
-    if (N > 1 && p->worker()) A(dev_alloc(&st.packed, n));
+    A(dev_alloc(p->d, &st.own, p->mstride));
+    A(dev_alloc(p->d, &st.masks_all, static_cast<size_t>(N) * p->mstride));
+    if (p->fused_pack) A(dev_alloc(p->d, &st.pack_cnt, NA));
+    A(dev_alloc(p->d, &st.wset, p->rows));
+    A(dev_alloc(p->d, &st.umask, p->rows));
+    A(dev_alloc(p->d, &st.prefix, static_cast<size_t>(M + 1) * (p->rows + 1)));
+    if (N > 1 && p->worker()) A(dev_alloc(p->d, &st.packed, n));
     for (hipEvent_t* e : {&st.scanned, &st.planned, &st.ready, &st.done})
       A(hip_check(hipEventCreateWithFlags(e, evflags), "hipEventCreate"));
   }
@@ -1088,21 +1106,21 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     A(hip_check(hipStreamCreateWithPriority(&p->cs, hipStreamNonBlocking, prio), "hipStreamCreate"));
   }
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, evflags), "hipEventCreate"));
-  A(dev_alloc(&p->bounds_dev, NA + 1));
-  if (N > 1 && p->shard >= 0) A(dev_alloc(&p->recv, static_cast<size_t>(M) * p->shard_nb * block_size));
-  A(dev_alloc(&p->results, n));
-  A(dev_alloc(&p->flags_ws, p->nb));
-  A(dev_alloc(&p->next_ws, p->nb));
-  A(dev_alloc(&p->unext_ws, p->nb));
+  A(dev_alloc(p->d, &p->bounds_dev, NA + 1));
+  if (N > 1 && p->shard >= 0) A(dev_alloc(p->d, &p->recv, static_cast<size_t>(M) * p->shard_nb * block_size));
+  A(dev_alloc(p->d, &p->results, n));
+  A(dev_alloc(p->d, &p->flags_ws, p->nb));
+  A(dev_alloc(p->d, &p->next_ws, p->nb));
+  A(dev_alloc(p->d, &p->unext_ws, p->nb));
   p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
-  A(dev_alloc(reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
+  A(dev_alloc(p->d, reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
   constexpr int NSETS = omr_ar_plan::kSets;
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), NSETS * (M + 1) * (NA + 1) * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0)
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->counts_map), p->counts_host, 0),
                 "hipHostGetDevicePointer"));
-  A(dev_alloc(&p->arrive, 1));
+  A(dev_alloc(p->d, &p->arrive, 1));
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), NSETS * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0) {
@@ -1685,7 +1703,7 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   constexpr int R = omr_ar_plan::kStage;
   if (p->s_in == nullptr) {
     for (int r = 0; r < R; ++r) {
-      TRY(dev_alloc(&p->stage[r], p->n));
+      TRY(dev_alloc(p->d, &p->stage[r], p->n));
       TRY(hip_check(hipEventCreateWithFlags(&p->ev_in[r], hipEventDisableTiming), "hipEventCreate"));
       TRY(hip_check(hipEventCreateWithFlags(&p->ev_round[r], hipEventDisableTiming), "hipEventCreate"));
       TRY(hip_check(hipEventCreateWithFlags(&p->ev_out[r], hipEventDisableTiming), "hipEventCreate"));
@@ -1914,11 +1932,9 @@ namespace {
 constexpr uint32_t kMsgW = 2 * OMR_MESSAGE_SIZE;
 
 void msgd_free_logs(omr_msgd_plan* p) {
-  // the transport forgets the logs' IPC handles first (a regrown log may land at a freed one's addresses)
-  auto release = [&](void* v) {
-    if (v) p->d->forget(v);
-    (void)hipFree(v);
-  };
+  // through the transport, which keeps exported logs alive for reuse (a regrown log may otherwise land at a freed
+  // one's addresses while a peer still maps it)
+  auto release = [&](void* v) { p->d->release(v); };
   release(p->sched);
   release(p->msgs);
   release(p->imm);
@@ -1938,18 +1954,18 @@ void msgd_free_logs(omr_msgd_plan* p) {
 int msgd_alloc_logs(omr_msgd_plan* p, uint32_t rcap) {
   msgd_free_logs(p);
   const uint64_t units = static_cast<uint64_t>(p->G) * rcap;
-  TRY(dev_alloc(&p->sched, units * omr_msg_sched_bytes()));
+  TRY(dev_alloc(p->d, &p->sched, units * omr_msg_sched_bytes()));
   if (p->worker()) {
-    TRY(dev_alloc(&p->msgs, units * kMsgW));
-    TRY(dev_alloc(&p->imm, units));
+    TRY(dev_alloc(p->d, &p->msgs, units * kMsgW));
+    TRY(dev_alloc(p->d, &p->imm, units));
   }
-  TRY(dev_alloc(&p->reply, units * kMsgW));
-  TRY(dev_alloc(&p->rimm, units));
+  TRY(dev_alloc(p->d, &p->reply, units * kMsgW));
+  TRY(dev_alloc(p->d, &p->rimm, units));
   if (p->agg >= 0)
     for (int w = 0; w < p->M; ++w) {
       if (w == p->me) continue;  // a co-located aggregator reads its own worker's log in place
-      TRY(dev_alloc(&p->wmsgs[w], units * kMsgW));
-      TRY(dev_alloc(&p->wimm[w], units));
+      TRY(dev_alloc(p->d, &p->wmsgs[w], units * kMsgW));
+      TRY(dev_alloc(p->d, &p->wimm[w], units));
     }
   p->rcap = rcap;
   return 0;
@@ -1986,10 +2002,7 @@ int omr_msgd_plan_destroy(omr_msgd_plan* p) {
   (void)hipDeviceSynchronize();
   msgd_free_logs(p);
   void* devs[] = {p->own_masks, p->masks_all, p->umask, p->unext, p->flags, p->next, p->scan_ws, p->rounds, p->maxr};
-  for (void* v : devs) {
-    if (v) p->d->forget(v);
-    (void)hipFree(v);
-  }
+  for (void* v : devs) p->d->release(v);
   (void)hipHostFree(p->host_r);
   delete p;
   return 0;
@@ -2025,16 +2038,16 @@ int omr_msgd_plan_create(omr_dist* d, uint32_t num_workers, uint64_t n, uint32_t
   auto A = [&](int r) {
     if (rc == 0) rc = r;
   };
-  A(dev_alloc(&p->own_masks, p->rows));
-  A(dev_alloc(&p->masks_all, static_cast<size_t>(p->N) * p->rows));
-  A(dev_alloc(&p->umask, p->rows));
-  A(dev_alloc(&p->unext, p->nb));
-  A(dev_alloc(&p->flags, p->nb));
-  A(dev_alloc(&p->next, p->nb));
+  A(dev_alloc(p->d, &p->own_masks, p->rows));
+  A(dev_alloc(p->d, &p->masks_all, static_cast<size_t>(p->N) * p->rows));
+  A(dev_alloc(p->d, &p->umask, p->rows));
+  A(dev_alloc(p->d, &p->unext, p->nb));
+  A(dev_alloc(p->d, &p->flags, p->nb));
+  A(dev_alloc(p->d, &p->next, p->nb));
   p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
-  A(dev_alloc(reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
-  A(dev_alloc(&p->rounds, p->G));
-  A(dev_alloc(&p->maxr, 1));
+  A(dev_alloc(p->d, reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
+  A(dev_alloc(p->d, &p->rounds, p->G));
+  A(dev_alloc(p->d, &p->maxr, 1));
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->host_r), (p->G + 1) * sizeof(uint32_t)), "hipHostMalloc"));
   if (rc == 0) A(hip_check(hipMemset(p->own_masks, 0, p->rows * sizeof(uint64_t)), "hipMemset"));
   if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset"));
