@@ -24,8 +24,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--event-every", type=int, default=10)
     ap.add_argument("--headline", action="store_true", help="run the headline's k_scan1f launches first, as bench does")
+    ap.add_argument("--pg", action="store_true",
+                    help="make a one-rank torch.distributed nccl group first, as bench.py --force-dist does")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
+    if a.pg:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29547")
+        torch.cuda.set_device(0)
+        torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     L = Layout.from_bytes(256 << 20, 256)
     bm = ops.gen_bitmap(0, 0.095, L.nb)
     sets = []
@@ -45,6 +52,8 @@ def main():
     res["wall_s"] = round(time.perf_counter() - t0, 3)
     res["GPU_MAX_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES")
     res["headline_first"] = a.headline
+    res["torch_group"] = a.pg
+    res["env"] = {k: os.environ.get(k) for k in ("OMR_SIDE_QUEUES", "OMR_SIDE_PRIORITY")}
     print(json.dumps(res), flush=True)
 
 
