@@ -213,19 +213,30 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
     }
 
 
-def round_world1(args, L: Layout, sets, dev, stream, bm=None):
+def round_world1(args, L: Layout, sets, dev, stream, bm=None, torch_group=True):
     """The N>1 step's own code path at N=1, measured after the headline's timed region (which it does not touch): the
-    C++ round (worker scan, mask all-gather, plan, exchange with no peers, shard sum over the whole tensor, deferred
-    pipeline as bench picks at world 1) over a one-rank RCCL communicator made in this process.  Its per-round time is
-    the like-for-like N=1 point of the 1 -> 8 curve, whose N>=2 lines time the same round."""
+    C++ round (worker scan, mask all-gather, plan, exchange with no peers, the one-rank round's sums written by its
+    worker scan, deferred pipeline as bench picks at world 1) over a one-rank RCCL communicator.  Its per-round time is
+    the like-for-like N=1 point of the 1 -> 8 curve, whose N>=2 lines time the same round.
+    torch_group: made as the N>1 lines make it, behind a torch.distributed nccl group (here a one-rank group on an
+    in-process HashStore, destroyed afterwards).  Without that group the same round ran 133-154 us instead of 59 on
+    MI355X (profiles/r03/round/queues/): the process's streams then share hardware queues differently."""
     from omr import cdist
+    import torch.distributed as tdist
+    made_group = False
     # RCCL prints a version banner on stdout when the communicator is made: keep stdout for the one JSON line
     sys.stdout.flush()
     saved = os.dup(1)
     os.dup2(2, 1)
     try:
-        eng = cdist.CppSparseAllreduce(L, dev, transport="rccl1")
+        if torch_group and not tdist.is_initialized():
+            tdist.init_process_group("nccl", store=tdist.HashStore(), rank=0, world_size=1, device_id=dev)
+            made_group = True
+        eng = (cdist.CppSparseAllreduce(L, dev) if torch_group else
+               cdist.CppSparseAllreduce(L, dev, transport="rccl1"))
     except Exception as e:  # noqa: BLE001  (reported, the headline line still prints)
+        if made_group:
+            tdist.destroy_process_group()
         return {"error": str(e)[:300]}
     finally:
         os.dup2(saved, 1)
@@ -253,12 +264,15 @@ def round_world1(args, L: Layout, sets, dev, stream, bm=None):
     dt = (time.perf_counter() - t0) / args.steps
     stages, _, _, n_timed = eng.stage_timings()
     eng.close()
+    if made_group:
+        tdist.destroy_process_group()
     scan_ms = stages["scan"]
     # a one-rank round's worker scan writes the shard sums itself (0.0f + x over the write set: omr_sparse_round_f32)
     sb = (fused_bytes(L, bm) + L.rows * 8) if bm is not None else scan_only_bytes(L)
     return {"ms_per_round": round(dt * 1e3, 5), "value": round(L.nbytes / dt / 1e9, 2), "unit": "GB/s",
             "mode": "reduce-scatter (the N>1 bench default), deferred pipeline (OMR_ROUND_DEFER)",
-            "transport": "RCCL, one-rank communicator in this process (no peers: nothing crosses xGMI)",
+            "transport": ("RCCL, one-rank communicator (no peers: nothing crosses xGMI)"
+                          + (", behind a one-rank torch.distributed nccl group as at N>1" if torch_group else "")),
             "scan_in_round": {"kernel_ms": round(scan_ms, 5), "algorithmic_bytes_per_launch": sb,
                               "frac": round(sb / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if scan_ms > 0 else None},
             "stages_ms": {k: round(v, 5) for k, v in stages.items()}, "timed_rounds": n_timed,

@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--workdir", default=os.path.join(ROOT, "gpurun_out", "pmc_round"))
     a = ap.parse_args()
     a.out, a.workdir = os.path.abspath(a.out), os.path.abspath(a.workdir)
+    os.makedirs(a.workdir, exist_ok=True)
     res = {}
     for case, kernel in CASES:
         tag = case.split()[0] + "_" + str(abs(hash(case)) % 1000)

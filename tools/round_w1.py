@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--headline", action="store_true", help="run the headline's k_scan1f launches first, as bench does")
     ap.add_argument("--pg", action="store_true",
                     help="make a one-rank torch.distributed nccl group first, as bench.py --force-dist does")
+    ap.add_argument("--no-group", action="store_true",
+                    help="bench.round_world1 without its own one-rank torch group (the in-process rccl1 transport)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     if a.pg:
@@ -48,7 +50,7 @@ def main():
             launches[i % 4]()
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res = bench.round_world1(a, L, sets, dev, stream, bm)
+    res = bench.round_world1(a, L, sets, dev, stream, bm, torch_group=not a.no_group)
     res["wall_s"] = round(time.perf_counter() - t0, 3)
     res["GPU_MAX_HW_QUEUES"] = os.environ.get("GPU_MAX_HW_QUEUES")
     res["headline_first"] = a.headline
