@@ -269,6 +269,16 @@ int omr_round_plan_ex(const uint64_t* row_masks, uint32_t count, uint64_t mask_s
                       uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
                       uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
                       omr_stream_t stream);
+struct omr_sum_list;
+/* omr_round_plan_ex plus, by further workgroups of the same launch, an aggregator's shard-sum pair list
+ * (omr_sum_list below; NULL: none), over column streams of the layout (rows * num_lanes * block_size floats,
+ * rows / rows_per_part partitions). */
+int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                        uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
+                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
+                        uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                        const struct omr_sum_list* list, omr_stream_t stream);
 
 /* Block movement addressed by a row mask and its prefix (no block list): the k-th set bit of `row_masks` over
  * rows [0, rows) minus [skip_begin, skip_end) is block k of the packed stream.
@@ -298,6 +308,35 @@ int omr_shard_sum_cols_f32(const float* own, uint32_t me, const float* recv, con
                            const uint32_t* prefix, const uint64_t* write_set, uint64_t n, uint32_t block_size,
                            uint32_t num_lanes, uint32_t num_parts, uint64_t row_begin, uint64_t row_end,
                            int packed_out, float* out, omr_stream_t stream);
+
+/* The same shard sum in two steps (the multi-rank round's form since round 3): its (block, contributor) pair list,
+ * which depends only on the all-gathered masks and position tables and on where each worker's stream will land in
+ * `recv`, is built before the exchange (by the plan launch: omr_round_plan_list); the sum then streams the pairs'
+ * blocks (server.cc:97-98, rank order from +0.0f, bit-exact with omr_shard_sum_cols_f32).
+ *   records  device uint64[units * capacity] (omr_sum_list_geometry), counts device uint32[units];
+ *   rows [row_begin, row_end): the shard, whole column segments of the layout;
+ *   pos_offset: word offset of each worker's position table in its array (2 * rows in the round);
+ *   me: the worker whose blocks are read in place from `own` (< count), or count (none: a dedicated aggregator);
+ *   recv_offsets[a]: worker a's stream of these rows starts at recv + recv_offsets[a] blocks (< 2^32). */
+typedef struct omr_sum_list {
+  uint64_t* records;
+  uint32_t* counts;
+  uint64_t row_begin, row_end;
+  uint64_t pos_offset;
+  uint32_t me;
+  uint64_t recv_offsets[OMR_MAX_WORKERS];
+} omr_sum_list;
+int omr_sum_list_geometry(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, uint64_t row_begin,
+                          uint64_t row_end, uint32_t count, uint64_t* units, uint32_t* capacity);
+/* Build the list in a launch of its own (worker c's array at row_masks + c * mask_stride, as omr_round_plan_ex). */
+int omr_sum_list_build(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t n,
+                       uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, const omr_sum_list* list,
+                       omr_stream_t stream);
+/* The sum over a built list.  packed_out 0: out dense (may alias own); 1: out packed in write-set order of the shard's
+ * rows, from write_set and its row prefix write_prefix (omr_round_plan's prefix + count * (rows + 1)). */
+int omr_shard_sum_list_f32(const float* own, const float* recv, const omr_sum_list* list, uint32_t count, uint64_t n,
+                           uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, const uint64_t* write_set,
+                           const uint32_t* write_prefix, int packed_out, float* out, omr_stream_t stream);
 
 /* ---------------------------------------------------------------- message-level round (wire format) */
 

@@ -755,6 +755,9 @@ struct omr_ar_plan {
   // power-of-two layout); otherwise (ragged shards, or OMR_PACK_MOVE=1) the round packs with omr_move_blocks_f32.
   // Each rank's all-gathered array is then its masks followed by its position table: mstride words per rank.
   bool fused_pack = false;
+  bool sum_list = false;            // the shard sum's pairs built by the plan launch (fused pack, N > 1, an aggregator)
+  uint64_t list_units = 0;
+  uint32_t list_cap = 0;
   uint64_t mstride = 0;           // uint64 words per rank in masks_all (rows without the fused pack)
   // per-round state, kSets sets used in turn: an asynchronous round's bookkeeping and exchange still read their
   // set while the next rounds' scans fill the others
@@ -768,6 +771,8 @@ struct omr_ar_plan {
     uint64_t* umask = nullptr;      // [rows] union of the workers' masks
     uint32_t* prefix = nullptr;     // [N+1][rows+1] popcount prefixes: workers, then the write set
     float* packed = nullptr;        // own non-zero blocks of the other shards, block order
+    uint64_t* list_rec = nullptr;   // sum list: the shard sum's pair records, built by the plan launch
+    uint32_t* list_cnt = nullptr;   //   and their count per unit
     hipEvent_t scanned = nullptr;   // async: recorded on the caller's stream after the worker scan
     hipEvent_t planned = nullptr;   // async: recorded on the plan stream once `own` is consumed and re-zeroed
     hipEvent_t ready = nullptr;     // recorded once the set is filled (the plan stream for async rounds)
@@ -1003,7 +1008,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   void* devs[] = {p->bounds_dev, p->recv, p->results, p->flags_ws, p->next_ws, p->unext_ws, p->scan_ws, p->arrive};
   for (void* v : devs) p->d->release(v);
   for (auto& st : p->set) {
-    void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed, st.pack_cnt};
+    void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed, st.pack_cnt, st.list_rec, st.list_cnt};
     for (void* v : sv) p->d->release(v);
     for (hipEvent_t e : {st.scanned, st.planned, st.ready, st.done})
       if (e) (void)hipEventDestroy(e);
@@ -1075,6 +1080,14 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
                   "omr_pack_geometry"));
     p->fused_pack = true;
     p->mstride = p->rows + (entries + 1) / 2;
+    // OMR_SUM_LIST=0 (A/B knob): the shard sum builds its pairs itself (omr_shard_sum_cols_f32)
+    const char* le = getenv("OMR_SUM_LIST");
+    if (p->shard >= 0 && (le == nullptr || atoi(le) != 0)) {
+      TRY(omr_check(omr_sum_list_geometry(n, block_size, num_lanes, num_parts, p->bounds[p->shard],
+                                          p->bounds[p->shard + 1], static_cast<uint32_t>(p->M), &p->list_units,
+                                          &p->list_cap), "omr_sum_list_geometry"));
+      p->sum_list = p->list_units > 0;
+    }
   }
   int rc = 0;
   auto A = [&](int r) {
@@ -1092,6 +1105,10 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     A(dev_alloc(p->d, &st.umask, p->rows));
     A(dev_alloc(p->d, &st.prefix, static_cast<size_t>(M + 1) * (p->rows + 1)));
     if (N > 1 && p->worker()) A(dev_alloc(p->d, &st.packed, n));
+    if (p->sum_list) {
+      A(dev_alloc(p->d, &st.list_rec, p->list_units * p->list_cap));
+      A(dev_alloc(p->d, &st.list_cnt, p->list_units));
+    }
     for (hipEvent_t* e : {&st.scanned, &st.planned, &st.ready, &st.done})
       A(hip_check(hipEventCreateWithFlags(e, evflags), "hipEventCreate"));
   }
@@ -1192,6 +1209,22 @@ int timed_exchange(omr_ar_plan* p, int slot) {
   return 0;
 }
 
+// Worker w's stream of this rank's shard lands at a fixed region of `recv` (w * shard_nb blocks), so the shard sum's
+// pairs can be addressed before the exchange (the plan launch builds them: omr_round_plan_list).
+uint64_t recv_slot(const omr_ar_plan* p, int w) { return static_cast<uint64_t>(w) * p->shard_nb; }
+
+omr_sum_list list_desc(const omr_ar_plan* p, const omr_ar_plan::Set& S) {
+  omr_sum_list l{};
+  l.records = S.list_rec;
+  l.counts = S.list_cnt;
+  l.row_begin = p->bounds[p->shard];
+  l.row_end = p->bounds[p->shard + 1];
+  l.pos_offset = 2 * p->rows;  // each worker's position table follows its masks (omr_worker_scan_pack_f32)
+  l.me = p->colocated ? static_cast<uint32_t>(p->me) : static_cast<uint32_t>(p->M);
+  for (int w = 0; w < p->M; ++w) l.recv_offsets[w] = recv_slot(p, w);
+  return l;
+}
+
 // (internal bit in a round's mode: a one-rank round whose worker scan wrote the sums itself, see omr_sparse_round_f32)
 constexpr int kModeSolo = 0x10000;
 
@@ -1283,8 +1316,8 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     if (sh >= 0)
       for (int w = 0; w < M; ++w) {
         if (w == me) continue;
-        roff[w] = in_blocks;
-        recvs[w] = {Slice{p->recv + in_blocks * B, per(w, sh) * B * sizeof(float)}};
+        roff[w] = recv_slot(p, w);
+        recvs[w] = {Slice{p->recv + roff[w] * B, per(w, sh) * B * sizeof(float)}};
         in_blocks += per(w, sh);
       }
     TRY(p->d->exchange(sends, recvs, xs));
@@ -1308,7 +1341,13 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     sums = dense_out ? out : p->results + (wk ? cnt(M, sh) * B : 0);
     const float* own = p->colocated ? x : nullptr;
     const uint32_t own_idx = p->colocated ? static_cast<uint32_t>(me) : static_cast<uint32_t>(M);
-    if (p->fused_pack)  // the workers' streams are column-ordered: positions from their all-gathered tables
+    if (p->sum_list) {  // the pairs were built by this round's plan launch
+      const omr_sum_list l = list_desc(p, S);
+      TRY(omr_check(omr_shard_sum_list_f32(own, p->recv, &l, static_cast<uint32_t>(M), p->n, p->B, p->lanes, p->parts,
+                                           S.wset, S.prefix + static_cast<uint64_t>(M) * (rows + 1), dense_out ? 0 : 1,
+                                           sums, xstream),
+                    "omr_shard_sum_list_f32"));
+    } else if (p->fused_pack)  // the workers' streams are column-ordered: positions from their all-gathered tables
       TRY(omr_check(omr_shard_sum_cols_f32(own, own_idx, p->recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
                                            p->mstride, 2 * rows, S.prefix, S.wset, p->n, p->B, p->lanes, p->parts,
                                            r0, r1, dense_out ? 0 : 1, sums, xstream),
@@ -1413,12 +1452,14 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
   //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
   const uint32_t seq = ++p->seq;
   //    ... and, by extra workgroups of the same launch, the aggregator chain (server.cc:86-96 min_next) over the union
-  TRY(omr_check(omr_round_plan_ex(S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes,
-                                  p->bounds_dev, NS, S.wset, S.umask, S.prefix,
-                                  p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, S.pack_cnt,
-                                  S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->arrive, p->flag_map + si, seq,
-                                  j.un, p->B, qstream),
-                "omr_round_plan_ex"));
+  //    ... and the shard sum's pair list, by more workgroups (sum_list)
+  const omr_sum_list sl = p->sum_list ? list_desc(p, S) : omr_sum_list{};
+  TRY(omr_check(omr_round_plan_list(S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes,
+                                    p->bounds_dev, NS, S.wset, S.umask, S.prefix,
+                                    p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, S.pack_cnt,
+                                    S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->arrive, p->flag_map + si, seq,
+                                    j.un, p->B, p->sum_list ? &sl : nullptr, qstream),
+                "omr_round_plan_list"));
   if (async) {
     TRY(hip_check(hipEventRecord(S.planned, qs), "hipEventRecord"));
     S.plan_pending = true;

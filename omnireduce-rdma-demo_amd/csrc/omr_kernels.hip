@@ -994,6 +994,114 @@ __device__ __forceinline__ uint64_t plan_row(const uint64_t* masks, uint32_t a, 
   return (r % rpp == 0) ? (u | all_lanes) : u;
 }
 
+constexpr uint64_t kRowStreams = ~0ull;
+constexpr uint32_t kSumUnitRows = 32;
+// a pair record: source block (bits 0-31: in `own` or in `recv`), destination block (32-59), flags
+constexpr uint64_t kRecOwn = 1ull << 60, kRecZero = 1ull << 61, kRecFirst = 1ull << 62, kRecLast = 1ull << 63;
+
+// ---------------------------------------------------------------- the shard sum's pair list, built before the exchange
+// (round 3, second session).  The aggregator's shard sum over the fused pack's column streams (k_shard_sum below) spent
+// most of its time before its first data load: at an 8-worker shard every wave fetched its unit's index data (one
+// round trip), built its (block, contributor) pairs, and only then loaded blocks -- 7.3 of 12 us per wave, the chip's
+// 1024 waves in lock step (profiles/r03/round/tune_shard_r03.log).  Everything those pairs depend on is known before
+// the exchange: the workers' masks and position tables (all-gathered) and where each worker's stream will land in
+// `recv` (a fixed region per worker).  So the pairs are built by extra workgroups of the round's plan launch, hidden
+// behind the exchange, and the sum (k_shard_sum_list) starts with one coalesced load of its unit's records.
+struct ListArgs {
+  const uint64_t* masks;  // worker c's row masks at masks + c * mstride, its position table at word pos_off
+  uint64_t mstride, pos_off;
+  uint64_t recv_off[OMR_MAX_WORKERS];
+  uint64_t rows, r0, r1, all_lanes;
+  uint32_t count, me, lanes, rpp, S, gps, cap;
+  uint64_t* records;  // unit u's records at records + u * cap, in (block, rank) order
+  uint32_t* counts;   // unit u's record count
+};
+
+__device__ __forceinline__ uint64_t list_units(const ListArgs& a) {
+  return ((a.r1 - a.r0) / a.S) * a.gps * 2 * a.lanes;
+}
+
+// Units [u0, units) step ustride, one wave each: unit = 32 rows x one lane (one half of a segment's 64-row group), as
+// k_shard_sum's column-stream units.  Lane i holds row i of the group: ONE round trip fetches every worker's mask row
+// and position-table entry; ballots give each worker's column bits; a wave-wide exclusive scan places each lane's
+// pairs; records go straight to global memory.
+__device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, uint64_t ustride) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t units = list_units(a);
+  for (uint64_t u = u0; u < units; u += ustride) {
+    const uint32_t l = static_cast<uint32_t>(u % a.lanes);
+    uint64_t t = u / a.lanes;
+    const uint32_t h = static_cast<uint32_t>(t & 1u);
+    t >>= 1;
+    const uint32_t j = static_cast<uint32_t>(t % a.gps);
+    const uint64_t seg = a.r0 / a.S + t / a.gps;
+    const uint64_t g0 = seg * a.S + static_cast<uint64_t>(j) * kPackGroupRows;
+    const uint32_t nload = a.S - j * kPackGroupRows < kPackGroupRows ? a.S - j * kPackGroupRows : kPackGroupRows;
+    const uint32_t h0 = h * kSumUnitRows;
+    const uint32_t h1 = nload < h0 + kSumUnitRows ? nload : h0 + kSumUnitRows;
+    const uint64_t gidx = seg * a.gps + j;
+    if (h0 >= h1) {
+      if (lane == 0) a.counts[u] = 0;
+      continue;
+    }
+    const bool rl = static_cast<uint32_t>(lane) < nload;
+    const uint64_t r = g0 + (rl ? static_cast<uint32_t>(lane) : 0u);
+    uint64_t mk[OMR_MAX_WORKERS];
+#pragma unroll
+    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) mk[c] = (c < a.count && rl) ? a.masks[c * a.mstride + r] : 0ull;
+    const bool cl = static_cast<uint32_t>(lane) < a.count;
+    const uint32_t base_c =
+        cl ? reinterpret_cast<const uint32_t*>(a.masks + lane * a.mstride)[a.pos_off + gidx * a.lanes + l] : 0u;
+    uint64_t un = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) un |= mk[c];
+    const uint64_t w = (rl && r % a.rpp == 0) ? (un | a.all_lanes) : un;  // write set: union + lane heads
+    const bool mine = static_cast<uint32_t>(lane) >= h0 && static_cast<uint32_t>(lane) < h1;
+    const bool wb = mine && ((w >> l) & 1ull);
+    uint32_t cb = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) cb |= static_cast<uint32_t>((mk[c] >> l) & 1ull) << c;
+    const uint32_t np = wb ? (cb ? static_cast<uint32_t>(__builtin_popcount(cb)) : 1u) : 0u;
+    uint32_t inc = np;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+    if (lane == 0) a.counts[u] = total;
+    if (total == 0) continue;
+    uint64_t ccol[OMR_MAX_WORKERS];  // worker c's bits of column l over the group's rows
+#pragma unroll
+    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) ccol[c] = c < a.count ? __ballot((mk[c] >> l) & 1ull) : 0ull;
+    if (np != 0) {
+      uint64_t* const rec = a.records + u * a.cap;
+      uint32_t k = inc - np;
+      const uint32_t first = k, last = inc - 1;
+      const uint64_t hdr = (r * a.lanes + l) << 32;  // the block's dense index (the sum converts it when packing)
+      if (cb == 0) {
+        rec[k] = hdr | kRecZero | kRecFirst | kRecLast;
+      } else {
+#pragma unroll
+        for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) {
+          if (!((cb >> c) & 1u)) continue;
+          uint64_t v;
+          if (c == a.me) {
+            v = (r * a.lanes + l) | kRecOwn;
+          } else {
+            const uint32_t bc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_c), c));
+            const uint64_t pos = static_cast<uint64_t>(bc) +
+                                 static_cast<uint64_t>(__builtin_popcountll(ccol[c] & below(static_cast<uint32_t>(lane))));
+            v = (a.recv_off[c] + pos) & 0xFFFFFFFFull;
+          }
+          v |= hdr | (k == first ? kRecFirst : 0ull) | (k == last ? kRecLast : 0ull);
+          rec[k++] = v;
+        }
+      }
+    }
+  }
+}
+
 struct PlanArgs {
   const uint64_t* masks;  // worker c's row masks at masks + c * mstride
   uint32_t count, rpp, lanes, nbounds;
@@ -1010,9 +1118,19 @@ struct PlanArgs {
   uint32_t* done_flag;  // receives `seq` once every workgroup's counts are visible system-wide, or null
   uint32_t seq;
   NextArgs chain;       // union_next: the aggregator chain over the union, by workgroups count+1.. (chain.next null: none)
+  uint32_t chain_wgs;
+  uint32_t list_wgs;    // the shard sum's pair list, by the workgroups after the chain's (0: none)
+  ListArgs list;
 };
 
 __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
+  if (blockIdx.x > a.count + a.chain_wgs) {  // the shard sum's pair list, one unit per wave
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr uint32_t kW = kPlanThreads / 64;
+    build_sum_list(a.list, static_cast<uint64_t>(blockIdx.x - a.count - 1 - a.chain_wgs) * kW + w,
+                   static_cast<uint64_t>(a.list_wgs) * kW);
+    return;
+  }
   if (blockIdx.x > a.count) {  // the aggregator chain (server.cc:86-96 min_next) over the union, one segment each
     const uint64_t* m = a.masks;
     const uint32_t cnt = a.count;
@@ -1205,10 +1323,6 @@ struct SumArgs {
   uint32_t S, gps;         // column streams: segment rows (shards are whole segments), 64-row groups per segment
 };
 
-constexpr uint64_t kRowStreams = ~0ull;
-constexpr uint32_t kSumUnitRows = 32;
-// a pair record: source block (bits 0-31: in `own` or in `recv`), destination block (32-59), flags
-constexpr uint64_t kRecOwn = 1ull << 60, kRecZero = 1ull << 61, kRecFirst = 1ull << 62, kRecLast = 1ull << 63;
 
 template <int VEC>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
@@ -1350,6 +1464,90 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
             acc[q] = add4((rc & kRecFirst) ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
           if (rc & kRecLast) {
             v4f* const d = reinterpret_cast<v4f*>(a.out + ((rc >> 32) & 0x0FFFFFFFull) * a.block);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = acc[q];
+          }
+        }
+      }
+    }
+  }
+}
+
+// The shard sum over a pair list (build_sum_list): per unit, ONE coalesced load of its count and first 64 records,
+// then the records' blocks streamed P at a time (every load of a window in flight) into the segmented rank-order sum
+// of k_shard_sum.  Packed output: a record's dense block index becomes its write-set position (the write set's row
+// prefix and row, loaded beside the window's blocks).
+struct ListSumArgs {
+  const float* own;
+  const float* recv;
+  const uint64_t* records;
+  const uint32_t* counts;
+  const uint64_t* write_set;  // packed output: the write set's rows and row prefix (omr_round_plan's prefix[count])
+  const uint32_t* wprefix;
+  float* out;
+  uint64_t units, r0;
+  uint32_t cap, lanes, block, packed_out;
+};
+
+template <int VEC>
+__global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
+  constexpr int P = 32 / VEC;  // pair slots per window
+  constexpr int kSlotGroup = P < 8 ? P : 8;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
+  const uint32_t bbytes = a.block * 4;
+  const uint32_t wpre0 = a.packed_out ? a.wprefix[a.r0] : 0u;
+  for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + wave; u < a.units; u += nw) {
+    const uint64_t* const rec = a.records + u * a.cap;
+    const uint32_t total = __builtin_amdgcn_readfirstlane(a.counts[u]);
+    uint64_t chunk = static_cast<uint32_t>(lane) < a.cap ? rec[lane] : 0ull;  // (issued with the count's load)
+    if (total == 0) continue;
+    uint64_t pdst = 0;  // packed output: chunk record `lane`'s write-set position
+    v4f acc[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) acc[q] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (uint32_t wbase = 0; wbase < total; wbase += P) {
+      const uint32_t cb = wbase & 63u;  // the window's first record in the chunk
+      if (cb == 0) {
+        if (wbase != 0) chunk = wbase + lane < a.cap ? rec[wbase + lane] : 0ull;
+        if (a.packed_out && wbase + lane < total) {
+          const uint64_t d = (chunk >> 32) & 0x0FFFFFFFull;
+          const uint64_t r = d / a.lanes;
+          const uint32_t l = static_cast<uint32_t>(d - r * a.lanes);
+          pdst = static_cast<uint64_t>(a.wprefix[r] - wpre0) +
+                 static_cast<uint64_t>(__builtin_popcountll(a.write_set[r] & below(l)));
+        }
+      }
+      const uint32_t nv = total - wbase < static_cast<uint32_t>(P) ? total - wbase : static_cast<uint32_t>(P);
+      v4f v[P][VEC];
+#pragma unroll
+      for (int g = 0; g < P; g += kSlotGroup) {
+        if (static_cast<uint32_t>(g) < nv) {
+#pragma unroll
+          for (int j = g; j < g + kSlotGroup; ++j) {
+            const uint64_t rc = readlane64(chunk, cb + j);
+            const bool load = static_cast<uint32_t>(j) < nv && !(rc & kRecZero);
+            const float* const sb = (rc & kRecOwn) ? a.own : a.recv;
+            const __amdgpu_buffer_rsrc_t src =
+                chunk_rsrc(sb + static_cast<uint64_t>(static_cast<uint32_t>(rc)) * a.block, load ? bbytes : 0u);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q)
+              v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (q * 64 + lane) * 16, 0,
+                                                                                     kLoadAux));
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        if (static_cast<uint32_t>(j) < nv) {  // (wave-uniform)
+          const uint64_t rc = readlane64(chunk, cb + j);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q)  // (0.0f + x_first) + ...: a block's first pair restarts from +0.0f
+            acc[q] = add4((rc & kRecFirst) ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
+          if (rc & kRecLast) {
+            const uint64_t dst = a.packed_out ? readlane64(pdst, cb + j) : ((rc >> 32) & 0x0FFFFFFFull);
+            v4f* const d = reinterpret_cast<v4f*>(a.out + dst * a.block);
 #pragma unroll
             for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = acc[q];
           }
@@ -1626,6 +1824,53 @@ int launch_scan(const Layout& L, const ScanArgs& a, hipStream_t st) {
   return launch_status("k_scanm");
 }
 
+
+// the pair list's arguments for the layout's column streams (shard rows [row_begin, row_end), whole segments)
+int make_list_args(const Layout& L, const uint64_t* masks, uint32_t count, uint64_t mstride, const omr_sum_list* sl,
+                   ListArgs* a) {
+  const FusedShape f = fused_shape(L);
+  if (sl == nullptr || sl->records == nullptr || sl->counts == nullptr || masks == nullptr)
+    return fail("sum_list: NULL pointer");
+  if (count == 0 || count > OMR_MAX_WORKERS) return fail("sum_list: count %u out of range", count);
+  if (sl->me > count) return fail("sum_list: me %u > count %u", sl->me, count);
+  if (sl->row_begin > sl->row_end || sl->row_end > L.rows || sl->row_begin % f.S != 0 || sl->row_end % f.S != 0)
+    return fail("sum_list: rows [%llu, %llu) are not whole %u-row column segments",
+                static_cast<unsigned long long>(sl->row_begin), static_cast<unsigned long long>(sl->row_end), f.S);
+  if (mstride < L.rows || sl->pos_offset < L.rows * 2 || sl->pos_offset + pack_table_entries(L, f) > mstride * 2)
+    return fail("sum_list: position table outside the mask arrays (stride %llu, offset %llu)",
+                static_cast<unsigned long long>(mstride), static_cast<unsigned long long>(sl->pos_offset));
+  if (L.nb > (1ull << 28)) return fail("sum_list: more than 2^28 blocks");
+  ListArgs& g = *a;
+  g = ListArgs{};
+  g.masks = masks;
+  g.mstride = mstride;
+  g.pos_off = sl->pos_offset;
+  for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) {
+    g.recv_off[c] = c < count ? sl->recv_offsets[c] : 0;
+    if (c < count && c != sl->me && g.recv_off[c] > 0xFFFFFFFFull) return fail("sum_list: recv offset beyond 2^32");
+  }
+  g.rows = L.rows;
+  g.r0 = sl->row_begin;
+  g.r1 = sl->row_end;
+  g.all_lanes = L.lanes >= 64 ? ~0ull : ((1ull << L.lanes) - 1ull);
+  g.count = count;
+  g.me = sl->me;
+  g.lanes = L.lanes;
+  g.rpp = L.rows_per_part;
+  g.S = f.S;
+  g.gps = pack_groups(f);
+  g.cap = kSumUnitRows * count;
+  g.records = sl->records;
+  g.counts = sl->counts;
+  return 0;
+}
+
+uint64_t list_units_host(const ListArgs& a) { return ((a.r1 - a.r0) / a.S) * a.gps * 2 * a.lanes; }
+
+__global__ __launch_bounds__(kWGThreads) void k_sum_list(ListArgs a) {
+  build_sum_list(a, static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+                 static_cast<uint64_t>(gridDim.x) * kWavesPerWG);
+}
 }  // namespace
 
 // internal, not in omr.h: the other translation units of libomr.so report through omr_last_error() with this
@@ -2072,6 +2317,17 @@ int omr_round_plan_ex(const uint64_t* row_masks, uint32_t count, uint64_t mask_s
                       uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
                       uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
                       omr_stream_t stream) {
+  return omr_round_plan_list(row_masks, count, mask_stride, rows, rows_per_part, num_lanes, bounds, num_bounds,
+                             write_set, union_masks, prefix, counts, zero_masks, zero_counters, num_zero_counters,
+                             arrive, done_flag, seq, union_next, block_size, nullptr, stream);
+}
+
+int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                        uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
+                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
+                        uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                        const omr_sum_list* list, omr_stream_t stream) {
   if (mask_stride < rows) return fail("round_plan: mask_stride %llu < rows", static_cast<unsigned long long>(mask_stride));
   if (num_zero_counters > kPlanThreads || (num_zero_counters > 0 && zero_counters == nullptr))
     return fail("round_plan: zero_counters");
@@ -2120,8 +2376,22 @@ int omr_round_plan_ex(const uint64_t* row_masks, uint32_t count, uint64_t mask_s
     a.chain.sentinel = omr_sentinel(block_size, num_lanes);
     chain_wgs = static_cast<uint32_t>(parts * a.chain.segs_per_part);
   }
+  a.chain_wgs = chain_wgs;
+  a.list_wgs = 0;
+  if (list != nullptr) {
+    if (block_size != 256 && block_size != 512 && block_size != 1024)
+      return fail("round_plan: block_size %u unsupported", block_size);
+    Layout L;
+    if (int rc = make_layout(rows * num_lanes * block_size, block_size, num_lanes,
+                             static_cast<uint32_t>(rows / rows_per_part), &L))
+      return rc;
+    if (int rc = make_list_args(L, row_masks, count, mask_stride, list, &a.list)) return rc;
+    const uint64_t units = list_units_host(a.list);
+    const uint64_t wgs = (units + kPlanThreads / 64 - 1) / (kPlanThreads / 64);
+    a.list_wgs = static_cast<uint32_t>(wgs < 512 ? wgs : 512);
+  }
   const size_t lds = rows <= kPlanLdsRows ? rows * sizeof(uint64_t) : 0;
-  k_round_plan<<<count + 1 + chain_wgs, kPlanThreads, lds, S(stream)>>>(a);
+  k_round_plan<<<count + 1 + chain_wgs + a.list_wgs, kPlanThreads, lds, S(stream)>>>(a);
   return launch_status("k_round_plan");
 }
 
@@ -2264,6 +2534,72 @@ int omr_shard_sum_cols_f32(const float* own, uint32_t me, const float* recv, con
   a.S = f.S;
   a.gps = pack_groups(f);
   return launch_shard_sum(a, recv_offsets, S(stream));
+}
+
+int omr_sum_list_geometry(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, uint64_t row_begin,
+                          uint64_t row_end, uint32_t count, uint64_t* units, uint32_t* capacity) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  const FusedShape f = fused_shape(L);
+  if (count == 0 || count > OMR_MAX_WORKERS) return fail("sum_list: count %u out of range", count);
+  if (row_begin > row_end || row_end > L.rows || row_begin % f.S != 0 || row_end % f.S != 0)
+    return fail("sum_list: rows [%llu, %llu) are not whole %u-row column segments",
+                static_cast<unsigned long long>(row_begin), static_cast<unsigned long long>(row_end), f.S);
+  if (units) *units = ((row_end - row_begin) / f.S) * pack_groups(f) * 2 * L.lanes;
+  if (capacity) *capacity = kSumUnitRows * count;
+  return 0;
+}
+
+int omr_sum_list_build(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t n,
+                       uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, const omr_sum_list* list,
+                       omr_stream_t stream) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  ListArgs a;
+  if (int rc = make_list_args(L, row_masks, count, mask_stride, list, &a)) return rc;
+  const uint64_t units = list_units_host(a);
+  if (units == 0) return 0;
+  k_sum_list<<<grid_for(units), kWGThreads, 0, S(stream)>>>(a);
+  return launch_status("k_sum_list");
+}
+
+int omr_shard_sum_list_f32(const float* own, const float* recv, const omr_sum_list* list, uint32_t count, uint64_t n,
+                           uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, const uint64_t* write_set,
+                           const uint32_t* write_prefix, int packed_out, float* out, omr_stream_t stream) {
+  uint64_t units = 0;
+  uint32_t cap = 0;
+  if (list == nullptr) return fail("shard_sum_list: NULL list");
+  if (int rc = omr_sum_list_geometry(n, block_size, num_lanes, num_parts, list->row_begin, list->row_end, count,
+                                     &units, &cap))
+    return rc;
+  if (units == 0) return 0;
+  if (list->records == nullptr || list->counts == nullptr || out == nullptr || (list->me < count && own == nullptr) ||
+      (count > 1 && recv == nullptr) || (packed_out && (write_set == nullptr || write_prefix == nullptr)))
+    return fail("shard_sum_list: NULL pointer");
+  if (reinterpret_cast<uintptr_t>(out) % 16 != 0 || reinterpret_cast<uintptr_t>(own) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(recv) % 16 != 0)
+    return fail("shard_sum_list: buffers must be 16-byte aligned");
+  ListSumArgs a{};
+  a.own = own;
+  a.recv = recv;
+  a.records = list->records;
+  a.counts = list->counts;
+  a.write_set = write_set;
+  a.wprefix = write_prefix;
+  a.out = out;
+  a.units = units;
+  a.r0 = list->row_begin;
+  a.cap = cap;
+  a.lanes = num_lanes;
+  a.block = block_size;
+  a.packed_out = packed_out ? 1u : 0u;
+  const unsigned g = grid_for(units);
+  switch (block_size / 256) {
+    case 1: k_shard_sum_list<1><<<g, kWGThreads, 0, S(stream)>>>(a); break;
+    case 2: k_shard_sum_list<2><<<g, kWGThreads, 0, S(stream)>>>(a); break;
+    default: k_shard_sum_list<4><<<g, kWGThreads, 0, S(stream)>>>(a); break;
+  }
+  return launch_status("k_shard_sum_list");
 }
 
 }  // extern "C"

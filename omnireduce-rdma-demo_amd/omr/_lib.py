@@ -67,6 +67,12 @@ SIGNATURES = {
                                   c_vp, c_vp, c_u32, c_vp, c_vp, c_u32, c_vp, c_u32, c_vp]),
     "omr_shard_sum_cols_f32": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, c_u64, c_u64, c_vp, c_vp, c_u64, c_u32,
                                        c_u32, c_u32, c_u64, c_u64, c_int, c_vp, c_vp]),
+    "omr_round_plan_list": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
+                                    c_vp, c_vp, c_u32, c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_vp]),
+    "omr_sum_list_geometry": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u64, c_u64, c_u32, c_vp, c_vp]),
+    "omr_sum_list_build": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp]),
+    "omr_shard_sum_list_f32": (c_int, [c_vp, c_vp, c_vp, c_u32, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_int, c_vp,
+                                       c_vp]),
     "omr_msg_plan_create": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u32, c_vp]),
     "omr_msg_plan_destroy": (c_int, [c_vp]),
     "omr_msg_round_f32": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -89,6 +95,12 @@ SIGNATURES = {
 }
 
 _lib = None
+
+
+class SumList(ctypes.Structure):
+    """struct omr_sum_list (include/omr.h): an aggregator's shard-sum pair list."""
+    _fields_ = [("records", c_vp), ("counts", c_vp), ("row_begin", c_u64), ("row_end", c_u64),
+                ("pos_offset", c_u64), ("me", ctypes.c_uint32), ("recv_offsets", c_u64 * OMR_MAX_WORKERS)]
 
 
 class OmrError(RuntimeError):

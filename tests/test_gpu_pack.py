@@ -197,10 +197,36 @@ def test_shard_sum_cols(gpu, n, B, density, m, naggs, colocated, packed_out):
         else:
             out = xds[me].clone() if colocated else torch.zeros(L.n, device=gpu)
         own = xds[me] if colocated else None
+        out0 = out.clone()
         rc = lib.omr_shard_sum_cols_f32(P(own), me, P(recv), offs.ctypes.data_as(ctypes.c_void_p), P(masks_all), m,
                                         mstride, 2 * rows, P(prefix), P(wset), L.n, B, L.num_lanes, L.num_threads, r0,
                                         r1, packed_out, P(out), stream())
         assert rc == 0, lib.omr_last_error()
+        # the same sums through the pair list: built by the plan launch (omr_round_plan_list) and in a launch of its
+        # own (omr_sum_list_build); each must equal the one-kernel form bit for bit
+        units, cap = ctypes.c_uint64(), ctypes.c_uint32()
+        assert lib.omr_sum_list_geometry(L.n, B, L.num_lanes, L.num_threads, r0, r1, m, ctypes.byref(units),
+                                         ctypes.byref(cap)) == 0, lib.omr_last_error()
+        for how in ("plan", "build"):
+            rec = torch.full((max(1, units.value * cap.value),), -1, dtype=torch.int64, device=gpu)
+            cnt = torch.full((max(1, units.value),), 7, dtype=torch.int32, device=gpu)
+            sl = _lib.SumList(P(rec), P(cnt), r0, r1, 2 * rows, me)
+            for w in range(m):
+                sl.recv_offsets[w] = int(offs[w])
+            if how == "plan":
+                rc = lib.omr_round_plan_list(P(masks_all), m, mstride, rows, L.rows_per_part, L.num_lanes, P(bdev),
+                                             naggs + 1, P(wset), P(umask), P(prefix), P(counts), None, None, 0, None,
+                                             None, 0, None, B, ctypes.byref(sl), stream())
+            else:
+                rc = lib.omr_sum_list_build(P(masks_all), m, mstride, L.n, B, L.num_lanes, L.num_threads,
+                                            ctypes.byref(sl), stream())
+            assert rc == 0, lib.omr_last_error()
+            out2 = out0.clone()
+            rc = lib.omr_shard_sum_list_f32(P(own), P(recv), ctypes.byref(sl), m, L.n, B, L.num_lanes, L.num_threads,
+                                            P(wset), P(prefix[m * (rows + 1):]), packed_out, P(out2), stream())
+            assert rc == 0, lib.omr_last_error()
+            torch.cuda.synchronize()
+            assert torch.equal(out2.view(torch.int32), out.view(torch.int32)), f"shard {s}: pair list ({how})"
         torch.cuda.synchronize()
         o = out.cpu().numpy()
         if packed_out:

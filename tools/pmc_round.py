@@ -14,10 +14,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = [  # (tune_round_r03 case filter, kernel name in the trace)
     ("product k_shard_sum (cols)", "::k_shard_sum<"),
+    ("product k_shard_sum_list", "::k_shard_sum_list<"),
     ("scan + fused pack", "::k_scan1f<"),
     ("scan (omr_worker_scan_f32)", "::k_scan1f<"),
     ("pack pass", "::k_move<"),
-    ("round plan", "::k_round_plan("),
+    ("round plan + chain (k_round_plan)", "::k_round_plan("),
+    ("round plan + chain + pair list", "::k_round_plan("),
 ]
 TIMED = 10  # the case's own launches (--rounds 2 --reps 5): the last ones of its kernel in the trace
 

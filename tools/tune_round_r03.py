@@ -139,8 +139,25 @@ def main():
                                           mstride, 2 * rows, prefix.data_ptr(), wset.data_ptr(), L.n, B, NB,
                                           L.num_threads, r0, r1, 0, out.data_ptr(), st)
 
+    # the pair list of shard 0 (built once here; the round builds it in its plan launch, timed below)
+    units, cap = ctypes.c_uint64(), ctypes.c_uint32()
+    _lib.check(lib.omr_sum_list_geometry(L.n, B, NB, L.num_threads, r0, r1, m, ctypes.byref(units), ctypes.byref(cap)),
+               "geometry")
+    lrec = torch.empty(units.value * cap.value, dtype=torch.int64, device=dev)
+    lcnt = torch.empty(units.value, dtype=torch.int32, device=dev)
+    sl = _lib.SumList(lrec.data_ptr(), lcnt.data_ptr(), r0, r1, 2 * rows, 0)
+    for w in range(m):
+        sl.recv_offsets[w] = int(roff[w])
+    _lib.check(lib.omr_sum_list_build(masks_all.data_ptr(), m, mstride, L.n, B, NB, L.num_threads, ctypes.byref(sl),
+                                      st), "omr_sum_list_build")
+
+    def sum_list(out):
+        return lib.omr_shard_sum_list_f32(xs[0].data_ptr(), recv_c.data_ptr(), ctypes.byref(sl), m, L.n, B, NB,
+                                          L.num_threads, wset.data_ptr(), prefix[m * (rows + 1):].data_ptr(), 0,
+                                          out.data_ptr(), st)
+
     sums = {"round-2 k_shard_sum (rows)": sum_r02, "product k_shard_sum (rows)": sum_rows,
-            "product k_shard_sum (cols)": sum_cols}
+            "product k_shard_sum (cols)": sum_cols, "product k_shard_sum_list (pairs from the plan)": sum_list}
     ref = None
     for name, fn in sums.items():
         o = xs[0].clone()
@@ -176,8 +193,19 @@ def main():
                                      naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
                                      counts.data_ptr(), None, None, 0, None, None, 0, unext.data_ptr(), B, st)
 
+    def plan_list():  # ... with shard 0's pair list built by the same launch (the round since round 3)
+        return lib.omr_round_plan_list(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                       naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                       counts.data_ptr(), None, None, 0, None, None, 0, unext.data_ptr(), B,
+                                       ctypes.byref(sl), st)
+
+    def list_only():  # the pair list in a launch of its own
+        return lib.omr_sum_list_build(masks_all.data_ptr(), m, mstride, L.n, B, NB, L.num_threads, ctypes.byref(sl),
+                                      st)
+
     workers = {"scan (omr_worker_scan_f32)": scan, "scan + fused pack (product)": scan_pack,
-               "pack pass (k_move, round 2)": pack, "round plan + chain (k_round_plan)": plan}
+               "pack pass (k_move, round 2)": pack, "round plan + chain (k_round_plan)": plan,
+               "round plan + chain + pair list": plan_list, "pair list alone (k_sum_list)": list_only}
     cases = {**sums, **workers}
     if a.only:
         cases = {k: v for k, v in cases.items() if a.only in k}
@@ -212,6 +240,11 @@ def main():
               # reads every worker's masks; writes write set, union, m + 1 prefix arrays, counts, the union chain
               "round plan + chain (k_round_plan)": m * rows * 8 + 2 * rows * 8 + (m + 1) * (rows + 1) * 4 +
               L.nb * 4}
+    # the pair list: reads every worker's mask rows of the shard and position-table entries, writes the records
+    nrec = int(lcnt.sum().item())
+    lbytes = m * (r1 - r0) * 8 + m * (ent // naggs) * 4 + nrec * 8 + units.value * 4
+    wbytes["round plan + chain + pair list"] = wbytes["round plan + chain (k_round_plan)"] + lbytes
+    wbytes["pair list alone (k_sum_list)"] = lbytes
     report = {}
     print(f"## config 4 shapes, {m} workers, -r {a.density}: shard 0 write set {ub} blocks, received {nc}, own {own_blocks}: "
           f"{sbytes} B per shard sum; worker 0 packs {other} blocks", flush=True)
