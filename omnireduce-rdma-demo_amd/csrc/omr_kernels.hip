@@ -1712,11 +1712,11 @@ int pack_check(const Layout& L, const FusedShape& f, const uint64_t* bounds, uin
   return 0;
 }
 
-template <int VEC, int SKIP>
+template <int VEC, int SKIP, int WAVES = kFusedWaves>
 int launch_fused_pack(const FusedArgs& a, const Layout& L, const FusedShape& f, unsigned grid, hipStream_t st) {
   const uint32_t bits_words = ((f.S + 31) / 32 + 3) & ~3u;
-  const size_t lds = bits_words * sizeof(uint32_t) + static_cast<size_t>(kFusedWaves) * a.wcap * L.block * 4;
-  auto* fn = &k_scan1f<VEC, kFusedWaves, kFusedLoads, SKIP, true>;
+  const size_t lds = bits_words * sizeof(uint32_t) + static_cast<size_t>(WAVES) * a.wcap * L.block * 4;
+  auto* fn = &k_scan1f<VEC, WAVES, kFusedLoads, SKIP, true>;
   // dynamic LDS beyond 64 KiB is opted into per instantiation, raised when a layout needs more (S sizes the bits)
   static std::atomic<size_t> attr{0};
   if (lds > attr.load()) {
@@ -1730,7 +1730,7 @@ int launch_fused_pack(const FusedArgs& a, const Layout& L, const FusedShape& f, 
     while (lds > cur && !attr.compare_exchange_weak(cur, lds)) {
     }
   }
-  fn<<<grid, 64 * kFusedWaves, lds, st>>>(a);
+  fn<<<grid, 64 * WAVES, lds, st>>>(a);
   return launch_status("k_scan1f (pack)");
 }
 
@@ -1765,6 +1765,18 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
     a.nshards = pk->nshards;
     a.own_shard = pk->own_shard;
     a.gps = pack_groups(f);
+    // OMR_PACK_WAVES=8 (study knob): 8-wave workgroups with half the stash (64 KiB), so two of them share a CU and one
+    // streams while the other takes its stream place and writes its blocks out
+    const char* pw = getenv("OMR_PACK_WAVES");
+    const int pack_waves = (pw != nullptr && atoi(pw) == 8) ? 8 : kFusedWaves;
+    if (pack_waves == 8) {
+      a.wcap = (kPackLdsBytes / 2) / (8 * L.block * 4);
+      switch (L.vec) {
+        case 1: return launch_fused_pack<1, 0, 8>(a, L, f, grid, st);
+        case 2: return launch_fused_pack<2, 0, 8>(a, L, f, grid, st);
+        default: return launch_fused_pack<4, 1, 8>(a, L, f, grid, st);
+      }
+    }
     a.wcap = kPackLdsBytes / (kFusedWaves * L.block * 4);
     switch (L.vec) {
       case 1: return launch_fused_pack<1, 0>(a, L, f, grid, st);

@@ -203,7 +203,15 @@ def main():
         return lib.omr_sum_list_build(masks_all.data_ptr(), m, mstride, L.n, B, NB, L.num_threads, ctypes.byref(sl),
                                       st)
 
+    def scan_pack8(i=0):  # OMR_PACK_WAVES=8: 8-wave workgroups, two per CU, half the stash each
+        os.environ["OMR_PACK_WAVES"] = "8"
+        try:
+            return scan_pack(i)
+        finally:
+            del os.environ["OMR_PACK_WAVES"]
+
     workers = {"scan (omr_worker_scan_f32)": scan, "scan + fused pack (product)": scan_pack,
+               "scan + fused pack (8-wave workgroups)": scan_pack8,
                "pack pass (k_move, round 2)": pack, "round plan + chain (k_round_plan)": plan,
                "round plan + chain + pair list": plan_list, "pair list alone (k_sum_list)": list_only}
     cases = {**sums, **workers}
@@ -219,7 +227,7 @@ def main():
             for i in range(a.reps):
                 if name in sums:
                     fn(outs[i % 2])
-                elif fn is scan_pack:
+                elif fn is scan_pack or fn is scan_pack8:
                     fn(i)
                 else:
                     fn()
@@ -236,6 +244,7 @@ def main():
     scan_b = L.nbytes + L.nb * 8 + rows * 8
     table_b = ent * 4 * (naggs - 1) // naggs
     wbytes = {"scan (omr_worker_scan_f32)": scan_b, "scan + fused pack (product)": scan_b + other * B * 4 + table_b,
+              "scan + fused pack (8-wave workgroups)": scan_b + other * B * 4 + table_b,
               "pack pass (k_move, round 2)": 2 * other * B * 4,
               # reads every worker's masks; writes write set, union, m + 1 prefix arrays, counts, the union chain
               "round plan + chain (k_round_plan)": m * rows * 8 + 2 * rows * 8 + (m + 1) * (rows + 1) * 4 +
@@ -254,8 +263,9 @@ def main():
         report[name] = {"us": round(t * 1e6, 3), "algorithmic_bytes": int(b), "GBps": round(b / t / 1e9, 1)}
         print(f"{name:34s} median {t * 1e6:8.2f} us  {b:>11d} B  {b / t / 1e9:7.1f} GB/s  ({b / t / 8e12:.3f} of 8 TB/s)",
               flush=True)
-    if all(k in times and times[k] for k in list(workers)[:3]):
-        ts, tsp, tp = (np.median(times[k]) * 1e3 for k in list(workers)[:3])
+    trio = ["scan (omr_worker_scan_f32)", "scan + fused pack (product)", "pack pass (k_move, round 2)"]
+    if all(k in times and times[k] for k in trio):
+        ts, tsp, tp = (np.median(times[k]) * 1e3 for k in trio)
         print(f"worker side per round: scan + pack pass {ts + tp:.2f} us -> fused {tsp:.2f} us", flush=True)
     if a.json:
         import json
