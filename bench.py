@@ -175,6 +175,20 @@ def read_pmc(path: str, workload: str, dist_mode: bool):
     return None, None
 
 
+def read_pmc_round(world: int, L: Layout):
+    """(HBM bytes per launch, source) of the N>1 round's worker scan with the fused pack, from tools/pmc_round.py's
+    summary: measured at config 4's shapes as rank 0 of 8, so it describes only a world-8 line over 256 MiB, B=256."""
+    path = os.path.join(ROOT, "profiles", "pmc_round_r03.json")
+    if world != 8 or L.nbytes != 256 << 20 or L.block_size != 256:
+        return None, None
+    try:
+        with open(path) as f:
+            k = json.load(f)["kernels"]
+        return k["scan + fused pack (product)"]["hbm_bytes_per_launch"], path
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
 def cpu_baseline(L: Layout, bm: np.ndarray, args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker / CPU baseline only (never the product path)
@@ -216,27 +230,22 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
 def round_world1(args, L: Layout, sets, dev, stream, bm=None, torch_group=True):
     """The N>1 step's own code path at N=1, measured after the headline's timed region (which it does not touch): the
     C++ round (worker scan, mask all-gather, plan, exchange with no peers, the one-rank round's sums written by its
-    worker scan, deferred pipeline as bench picks at world 1) over a one-rank RCCL communicator.  Its per-round time is
-    the like-for-like N=1 point of the 1 -> 8 curve, whose N>=2 lines time the same round.
-    torch_group: made as the N>1 lines make it, behind a torch.distributed nccl group (here a one-rank group on an
-    in-process HashStore, destroyed afterwards).  Without that group the same round ran 133-154 us instead of 59 on
-    MI355X (profiles/r03/round/queues/): the process's streams then share hardware queues differently."""
+    worker scan, deferred pipeline as bench picks) over a one-rank RCCL communicator.  Its per-round time is the
+    like-for-like N=1 point of the 1 -> 8 curve, whose N>=2 lines time the same round.
+    torch_group (default): exactly the N>1 lines' measurement -- this bench run as one rank under
+    torch.distributed.run (--force-dist), in a child process; its line's figures are returned.  Made in-process
+    instead (torch_group False: a one-rank communicator with no torch group, after the headline) the same round ran
+    118-154 us instead of 59 on MI355X (profiles/r03/round/queues/), so the process set-up of the N>1 lines is kept."""
+    if torch_group:
+        return round_world1_child(args)
     from omr import cdist
-    import torch.distributed as tdist
-    made_group = False
     # RCCL prints a version banner on stdout when the communicator is made: keep stdout for the one JSON line
     sys.stdout.flush()
     saved = os.dup(1)
     os.dup2(2, 1)
     try:
-        if torch_group and not tdist.is_initialized():
-            tdist.init_process_group("nccl", store=tdist.HashStore(), rank=0, world_size=1, device_id=dev)
-            made_group = True
-        eng = (cdist.CppSparseAllreduce(L, dev) if torch_group else
-               cdist.CppSparseAllreduce(L, dev, transport="rccl1"))
+        eng = cdist.CppSparseAllreduce(L, dev, transport="rccl1")
     except Exception as e:  # noqa: BLE001  (reported, the headline line still prints)
-        if made_group:
-            tdist.destroy_process_group()
         return {"error": str(e)[:300]}
     finally:
         os.dup2(saved, 1)
@@ -264,20 +273,47 @@ def round_world1(args, L: Layout, sets, dev, stream, bm=None, torch_group=True):
     dt = (time.perf_counter() - t0) / args.steps
     stages, _, _, n_timed = eng.stage_timings()
     eng.close()
-    if made_group:
-        tdist.destroy_process_group()
     scan_ms = stages["scan"]
     # a one-rank round's worker scan writes the shard sums itself (0.0f + x over the write set: omr_sparse_round_f32)
     sb = (fused_bytes(L, bm) + L.rows * 8) if bm is not None else scan_only_bytes(L)
     return {"ms_per_round": round(dt * 1e3, 5), "value": round(L.nbytes / dt / 1e9, 2), "unit": "GB/s",
             "mode": "reduce-scatter (the N>1 bench default), deferred pipeline (OMR_ROUND_DEFER)",
-            "transport": ("RCCL, one-rank communicator (no peers: nothing crosses xGMI)"
-                          + (", behind a one-rank torch.distributed nccl group as at N>1" if torch_group else "")),
+            "transport": "RCCL, one-rank communicator made in this process, no torch group (no peers)",
             "scan_in_round": {"kernel_ms": round(scan_ms, 5), "algorithmic_bytes_per_launch": sb,
                               "frac": round(sb / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if scan_ms > 0 else None},
-            "stages_ms": {k: round(v, 5) for k, v in stages.items()}, "timed_rounds": n_timed,
-            "note": ("the N=1 anchor of the per-GPU scaling fraction: the same round as the N>=2 lines (value = "
-                     "tensor bytes per round time), measured after the headline's timed region")}
+            "stages_ms": {k: round(v, 5) for k, v in stages.items()}, "timed_rounds": n_timed}
+
+
+def round_world1_child(args):
+    """bench.py --force-dist as one rank under torch.distributed.run, in a child process (started as a child, never
+    exec'd over this GPU process): the N>1 lines' own measurement at world 1.  Returns its figures."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes=1",
+           "--nproc-per-node", "1", os.path.join(ROOT, "bench.py"), "--force-dist", "--no-cpu",
+           "--steps", str(max(args.steps, 50)), "--warmup", str(max(args.warmup, 10)),
+           "--size-mib", str(args.size_mib), "--block-size", str(args.block_size), "--density", str(args.density)]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                           "MASTER_PORT")}
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    except subprocess.TimeoutExpired:
+        return {"error": "the world-1 round's child run timed out (240 s)"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"child exit {r.returncode}: " + (r.stderr or r.stdout)[-300:]}
+    d = json.loads(lines[-1])
+    ex = d.get("exchange", {})
+    rf = d.get("roofline", {})
+    return {"ms_per_round": d["ms_per_step"], "value": d["value"], "unit": d["unit"],
+            "rounds": d["steps"], "warmup": d["warmup"],
+            "mode": "reduce-scatter (the N>1 bench default), pipeline " + str(ex.get("pipe")),
+            "transport": "RCCL, one rank under torch.distributed.run (bench.py --force-dist; no peers)",
+            "scan_in_round": {"kernel_ms": rf.get("kernel_ms"), "algorithmic_bytes_per_launch":
+                              rf.get("algorithmic_bytes_per_launch"), "frac": rf.get("frac"),
+                              "traffic": rf.get("traffic"), "traffic_source": rf.get("traffic_source")},
+            "stages_ms": ex.get("stages_ms"), "host_ms_per_call": ex.get("host_ms_per_call"),
+            "note": ("the N=1 anchor of the per-GPU scaling fraction: the N>=2 lines' measurement at world 1 (a child "
+                     "process, run after the headline's timed region)")}
 
 
 def host_resident(args, ws, rank, local):
@@ -544,7 +580,10 @@ def main():
         else:
             kbytes = algorithmic_scan_bytes(L, bitmaps, m)
         achieved = kbytes / (kms * 1e-3) / 1e9
-        traffic, pmc_src = read_pmc(args.pmc, workload, dist_mode)
+        if dist_mode and n_gpus > 1 and engine_fused and args.dist_mode != "dense":
+            traffic, pmc_src = read_pmc_round(n_gpus, L)
+        else:
+            traffic, pmc_src = read_pmc(args.pmc, workload, dist_mode)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                     "kernel": kernel_name,

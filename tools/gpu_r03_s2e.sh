@@ -9,8 +9,8 @@ mkdir -p $O
 cd $R
 timeout -k 10 300 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider -m gpu \
   tests/test_gpu_pack.py > $O/tests_pack.log 2>&1 && \
-OMR_PACK_WAVES=8 timeout -k 10 300 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
-  -m gpu tests/test_gpu_pack.py > $O/tests_pack_w8.log 2>&1 && \
+OMR_PACK_WAVES=16 timeout -k 10 300 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
+  -m gpu tests/test_gpu_pack.py > $O/tests_pack_w16.log 2>&1 && \
 timeout -k 10 300 python3 tools/tune_round_r03.py > $O/tune_round_r03.log 2>&1 && \
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider -m gpu \
   tests/test_gpu_round.py tests/test_cpp_dist.py tests/test_gpu_ipc.py tests/test_gpu_fault.py > $O/tests_round.log 2>&1 && \

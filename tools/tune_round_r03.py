@@ -156,8 +156,21 @@ def main():
                                           L.num_threads, wset.data_ptr(), prefix[m * (rows + 1):].data_ptr(), 0,
                                           out.data_ptr(), st)
 
+    def env_case(fn, var, val):
+        def run(out):
+            os.environ[var] = val
+            try:
+                return fn(out)
+            finally:
+                del os.environ[var]
+        return run
+
     sums = {"round-2 k_shard_sum (rows)": sum_r02, "product k_shard_sum (rows)": sum_rows,
-            "product k_shard_sum (cols)": sum_cols, "product k_shard_sum_list (pairs from the plan)": sum_list}
+            "product k_shard_sum (cols)": sum_cols,
+            "k_shard_sum_list, one unit per wave": env_case(sum_list, "OMR_SUM_PIPE", "0"),
+            "k_shard_sum_pipe, 1 unit per wave": env_case(sum_list, "OMR_SUM_PIPE", "1"),
+            "k_shard_sum_pipe, 2 units per wave": env_case(sum_list, "OMR_SUM_PIPE", "2"),
+            "product k_shard_sum_pipe (4 units per wave)": sum_list}
     ref = None
     for name, fn in sums.items():
         o = xs[0].clone()
@@ -203,15 +216,15 @@ def main():
         return lib.omr_sum_list_build(masks_all.data_ptr(), m, mstride, L.n, B, NB, L.num_threads, ctypes.byref(sl),
                                       st)
 
-    def scan_pack8(i=0):  # OMR_PACK_WAVES=8: 8-wave workgroups, two per CU, half the stash each
-        os.environ["OMR_PACK_WAVES"] = "8"
+    def scan_pack16(i=0):  # OMR_PACK_WAVES=16: one 16-wave workgroup per CU (the product until round 3's 2nd session)
+        os.environ["OMR_PACK_WAVES"] = "16"
         try:
             return scan_pack(i)
         finally:
             del os.environ["OMR_PACK_WAVES"]
 
     workers = {"scan (omr_worker_scan_f32)": scan, "scan + fused pack (product)": scan_pack,
-               "scan + fused pack (8-wave workgroups)": scan_pack8,
+               "scan + fused pack (16-wave workgroups)": scan_pack16,
                "pack pass (k_move, round 2)": pack, "round plan + chain (k_round_plan)": plan,
                "round plan + chain + pair list": plan_list, "pair list alone (k_sum_list)": list_only}
     cases = {**sums, **workers}
@@ -227,7 +240,7 @@ def main():
             for i in range(a.reps):
                 if name in sums:
                     fn(outs[i % 2])
-                elif fn is scan_pack or fn is scan_pack8:
+                elif fn is scan_pack or fn is scan_pack16:
                     fn(i)
                 else:
                     fn()
@@ -244,7 +257,7 @@ def main():
     scan_b = L.nbytes + L.nb * 8 + rows * 8
     table_b = ent * 4 * (naggs - 1) // naggs
     wbytes = {"scan (omr_worker_scan_f32)": scan_b, "scan + fused pack (product)": scan_b + other * B * 4 + table_b,
-              "scan + fused pack (8-wave workgroups)": scan_b + other * B * 4 + table_b,
+              "scan + fused pack (16-wave workgroups)": scan_b + other * B * 4 + table_b,
               "pack pass (k_move, round 2)": 2 * other * B * 4,
               # reads every worker's masks; writes write set, union, m + 1 prefix arrays, counts, the union chain
               "round plan + chain (k_round_plan)": m * rows * 8 + 2 * rows * 8 + (m + 1) * (rows + 1) * 4 +
