@@ -313,7 +313,8 @@ int omr_shard_sum_cols_f32(const float* own, uint32_t me, const float* recv, con
  * which depends only on the all-gathered masks and position tables and on where each worker's stream will land in
  * `recv`, is built before the exchange (by the plan launch: omr_round_plan_list); the sum then streams the pairs'
  * blocks (server.cc:97-98, rank order from +0.0f, bit-exact with omr_shard_sum_cols_f32).
- *   records  device uint64[units * capacity] (omr_sum_list_geometry), counts device uint32[units];
+ *   records  device uint64[units * capacity] (omr_sum_list_geometry: a unit's records end with a terminator word),
+ *   counts   device uint32[units] (each unit's record count);
  *   rows [row_begin, row_end): the shard, whole column segments of the layout;
  *   pos_offset: word offset of each worker's position table in its array (2 * rows in the round);
  *   me: the worker whose blocks are read in place from `own` (< count), or count (none: a dedicated aggregator);

@@ -998,6 +998,9 @@ constexpr uint64_t kRowStreams = ~0ull;
 constexpr uint32_t kSumUnitRows = 32;
 // a pair record: source block (bits 0-31: in `own` or in `recv`), destination block (32-59), flags
 constexpr uint64_t kRecOwn = 1ull << 60, kRecZero = 1ull << 61, kRecFirst = 1ull << 62, kRecLast = 1ull << 63;
+// a pair list's unit ends with this word (no real record has every bit set: destinations are < 2^28 blocks), so the
+// sum finds its unit's length in the same load as its first records
+constexpr uint64_t kRecEnd = ~0ull;
 
 // ---------------------------------------------------------------- the shard sum's pair list, built before the exchange
 // (round 3, second session).  The aggregator's shard sum over the fused pack's column streams (k_shard_sum below) spent
@@ -1041,7 +1044,10 @@ __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, u
     const uint32_t h1 = nload < h0 + kSumUnitRows ? nload : h0 + kSumUnitRows;
     const uint64_t gidx = seg * a.gps + j;
     if (h0 >= h1) {
-      if (lane == 0) a.counts[u] = 0;
+      if (lane == 0) {
+        a.counts[u] = 0;
+        a.records[u * a.cap] = kRecEnd;
+      }
       continue;
     }
     const bool rl = static_cast<uint32_t>(lane) < nload;
@@ -1069,7 +1075,10 @@ __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, u
       if (lane >= d) inc += o;
     }
     const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
-    if (lane == 0) a.counts[u] = total;
+    if (lane == 0) {
+      a.counts[u] = total;
+      a.records[u * a.cap + total] = kRecEnd;
+    }
     if (total == 0) continue;
     uint64_t ccol[OMR_MAX_WORKERS];  // worker c's bits of column l over the group's rows
 #pragma unroll
@@ -1499,9 +1508,19 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
   const uint32_t bbytes = a.block * 4;
   const uint32_t wpre0 = a.packed_out ? a.wprefix[a.r0] : 0u;
   for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + wave; u < a.units; u += nw) {
+    // ONE load: the unit's first 64 words; its length is the first terminator's lane (more chunks only past 63)
     const uint64_t* const rec = a.records + u * a.cap;
-    const uint32_t total = __builtin_amdgcn_readfirstlane(a.counts[u]);
-    uint64_t chunk = static_cast<uint32_t>(lane) < a.cap ? rec[lane] : 0ull;  // (issued with the count's load)
+    uint64_t chunk = static_cast<uint32_t>(lane) < a.cap ? rec[lane] : kRecEnd;
+    uint32_t total = 0;
+    for (uint64_t e = __ballot(chunk == kRecEnd);; ) {
+      if (e != 0) {
+        total += static_cast<uint32_t>(__builtin_ctzll(e));
+        break;
+      }
+      total += 64;
+      const uint64_t nx = total + lane < a.cap ? rec[total + lane] : kRecEnd;
+      e = __ballot(nx == kRecEnd);
+    }
     if (total == 0) continue;
     uint64_t pdst = 0;  // packed output: chunk record `lane`'s write-set position
     v4f acc[VEC];
@@ -1554,128 +1573,6 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
         }
       }
     }
-  }
-}
-
-// The same sum, software-pipelined across windows (the product since round 3's second session).  With one unit per
-// wave the chip's 1024 waves at an 8-worker shard run in lock step: all load, then all store, with the latencies in
-// between exposed (k_shard_sum and k_shard_sum_list both take 15-17 us for 46 MB).  Here a wave takes several units
-// (the grid is a quarter of the units) and keeps two windows in flight: window i+1's loads are issued before window i
-// is summed and stored, and the next unit's records are fetched while the current one streams.  Every window issues
-// exactly P loads and P stores (unused slots: a zero-size descriptor / a store pointed past its range), so the
-// compiler's vmcnt waits count exactly the older window's loads and never a younger, data-dependent operation.
-template <int VEC>
-__global__ __launch_bounds__(kWGThreads) void k_shard_sum_pipe(ListSumArgs a) {
-  constexpr int P = 32 / VEC;  // pair slots per window
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
-  const uint32_t bbytes = a.block * 4;
-  const uint32_t wpre0 = a.packed_out ? a.wprefix[a.r0] : 0u;
-  struct Win {
-    uint64_t u;      // unit (>= units: none)
-    uint32_t wb;     // first record of the window within the unit
-    uint32_t total;  // the unit's records
-    uint64_t chunk;  // lane i: record (wb & ~63) + i of the unit
-    uint64_t pdst;   // packed output: that record's write-set position
-  };
-  auto fetch = [&](uint64_t u, uint32_t& tv, uint64_t& ch) {  // issued, not waited for
-    tv = u < a.units ? a.counts[u] : 0u;
-    ch = (u < a.units && static_cast<uint32_t>(lane) < a.cap) ? a.records[u * a.cap + lane] : 0ull;
-  };
-  auto packed_pos = [&](const Win& w) -> uint64_t {
-    if (!a.packed_out || (w.wb & ~63u) + lane >= w.total) return 0;
-    const uint64_t d = (w.chunk >> 32) & 0x0FFFFFFFull;
-    const uint64_t r = d / a.lanes;
-    const uint32_t l = static_cast<uint32_t>(d - r * a.lanes);
-    return static_cast<uint64_t>(a.wprefix[r] - wpre0) +
-           static_cast<uint64_t>(__builtin_popcountll(a.write_set[r] & below(l)));
-  };
-  // the next unit's records, prefetched one unit ahead
-  uint64_t un = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + wave;
-  uint32_t tn;
-  uint64_t chn;
-  fetch(un, tn, chn);
-  auto next_unit = [&](Win& w) {  // w := the first window of the next non-empty unit (w.u >= units: none)
-    for (;;) {
-      w.u = un;
-      w.total = __builtin_amdgcn_readfirstlane(tn);
-      w.chunk = chn;
-      w.wb = 0;
-      un += nw;
-      fetch(un, tn, chn);
-      if (w.u >= a.units || w.total != 0) break;
-    }
-    w.pdst = w.u < a.units ? packed_pos(w) : 0;
-  };
-  auto advance = [&](const Win& cur, Win& w) {  // w := the window after cur
-    w = cur;
-    w.wb = cur.wb + P;
-    if (w.wb >= cur.total) {
-      next_unit(w);
-    } else if ((w.wb & 63u) == 0) {  // a unit of more than 64 records: its next 64
-      w.chunk = w.wb + lane < a.cap ? a.records[w.u * a.cap + w.wb + lane] : 0ull;
-      w.pdst = packed_pos(w);
-    }
-  };
-  auto issue = [&](const Win& w, v4f (&v)[P][VEC]) {
-    const uint32_t cb = w.wb & 63u;
-    const uint32_t nv = w.total - w.wb < static_cast<uint32_t>(P) ? w.total - w.wb : static_cast<uint32_t>(P);
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-      const uint64_t rc = readlane64(w.chunk, cb + j);
-      const bool load = static_cast<uint32_t>(j) < nv && !(rc & kRecZero);
-      const float* const sb = (rc & kRecOwn) ? a.own : a.recv;
-      const __amdgpu_buffer_rsrc_t src =
-          chunk_rsrc(sb + (load ? static_cast<uint64_t>(static_cast<uint32_t>(rc)) * a.block : 0ull),
-                     load ? bbytes : 0u);
-#pragma unroll
-      for (int q = 0; q < VEC; ++q)
-        v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (q * 64 + lane) * 16, 0,
-                                                                               kLoadAux));
-    }
-  };
-  v4f acc[VEC];
-#pragma unroll
-  for (int q = 0; q < VEC; ++q) acc[q] = v4f{0.f, 0.f, 0.f, 0.f};
-  auto consume = [&](const Win& w, v4f (&v)[P][VEC]) {
-    const uint32_t cb = w.wb & 63u;
-    const uint32_t nv = w.total - w.wb < static_cast<uint32_t>(P) ? w.total - w.wb : static_cast<uint32_t>(P);
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-      const uint64_t rc = readlane64(w.chunk, cb + j);
-      const bool use = static_cast<uint32_t>(j) < nv;
-      const bool first = use && (rc & kRecFirst), last = use && (rc & kRecLast);
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) {  // (0.0f + x_first) + ...: a block's first pair restarts from +0.0f
-        const v4f s = add4(first ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
-        acc[q] = use ? s : acc[q];
-      }
-      const uint64_t dst = a.packed_out ? readlane64(w.pdst, cb + j) : ((rc >> 32) & 0x0FFFFFFFull);
-      const __amdgpu_buffer_rsrc_t d = chunk_rsrc(a.out + (last ? dst * a.block : 0ull), bbytes);
-      const uint32_t drop = last ? 0u : kDropStore;
-#pragma unroll
-      for (int q = 0; q < VEC; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[q]), d, ((q * 64 + lane) * 16) | drop, 0,
-                                               0);
-    }
-  };
-  Win wa, wb;
-  next_unit(wa);
-  if (wa.u >= a.units) return;
-  v4f va[P][VEC], vb[P][VEC];
-  issue(wa, va);
-  for (;;) {
-    advance(wa, wb);
-    const bool more_b = wb.u < a.units;
-    if (more_b) issue(wb, vb);
-    consume(wa, va);
-    if (!more_b) break;
-    advance(wb, wa);
-    const bool more_a = wa.u < a.units;
-    if (more_a) issue(wa, va);
-    consume(wb, vb);
-    if (!more_a) break;
   }
 }
 
@@ -1994,7 +1891,7 @@ int make_list_args(const Layout& L, const uint64_t* masks, uint32_t count, uint6
   g.rpp = L.rows_per_part;
   g.S = f.S;
   g.gps = pack_groups(f);
-  g.cap = kSumUnitRows * count;
+  g.cap = kSumUnitRows * count + 1;  // + the terminator
   g.records = sl->records;
   g.counts = sl->counts;
   return 0;
@@ -2681,7 +2578,7 @@ int omr_sum_list_geometry(uint64_t n, uint32_t block_size, uint32_t num_lanes, u
     return fail("sum_list: rows [%llu, %llu) are not whole %u-row column segments",
                 static_cast<unsigned long long>(row_begin), static_cast<unsigned long long>(row_end), f.S);
   if (units) *units = ((row_end - row_begin) / f.S) * pack_groups(f) * 2 * L.lanes;
-  if (capacity) *capacity = kSumUnitRows * count;
+  if (capacity) *capacity = kSumUnitRows * count + 1;  // + the terminator
   return 0;
 }
 
@@ -2728,26 +2625,13 @@ int omr_shard_sum_list_f32(const float* own, const float* recv, const omr_sum_li
   a.lanes = num_lanes;
   a.block = block_size;
   a.packed_out = packed_out ? 1u : 0u;
-  // OMR_SUM_PIPE: 0 = one unit per wave (k_shard_sum_list); else the pipelined kernel with units / OMR_SUM_PIPE waves
-  // (default 4 units per wave)
-  const char* pe = getenv("OMR_SUM_PIPE");
-  const int per_wave = pe != nullptr ? atoi(pe) : 4;
-  if (per_wave <= 0) {
-    const unsigned g = grid_for(units);
-    switch (block_size / 256) {
-      case 1: k_shard_sum_list<1><<<g, kWGThreads, 0, S(stream)>>>(a); break;
-      case 2: k_shard_sum_list<2><<<g, kWGThreads, 0, S(stream)>>>(a); break;
-      default: k_shard_sum_list<4><<<g, kWGThreads, 0, S(stream)>>>(a); break;
-    }
-    return launch_status("k_shard_sum_list");
-  }
-  const unsigned g = grid_for((units + per_wave - 1) / per_wave);
+  const unsigned g = grid_for(units);
   switch (block_size / 256) {
-    case 1: k_shard_sum_pipe<1><<<g, kWGThreads, 0, S(stream)>>>(a); break;
-    case 2: k_shard_sum_pipe<2><<<g, kWGThreads, 0, S(stream)>>>(a); break;
-    default: k_shard_sum_pipe<4><<<g, kWGThreads, 0, S(stream)>>>(a); break;
+    case 1: k_shard_sum_list<1><<<g, kWGThreads, 0, S(stream)>>>(a); break;
+    case 2: k_shard_sum_list<2><<<g, kWGThreads, 0, S(stream)>>>(a); break;
+    default: k_shard_sum_list<4><<<g, kWGThreads, 0, S(stream)>>>(a); break;
   }
-  return launch_status("k_shard_sum_pipe");
+  return launch_status("k_shard_sum_list");
 }
 
 }  // extern "C"

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = [  # (tune_round_r03 case filter, kernel name in the trace)
     ("product k_shard_sum (cols)", "::k_shard_sum<"),
-    ("product k_shard_sum_pipe", "::k_shard_sum_pipe<"),
+    ("product k_shard_sum_list", "::k_shard_sum_list<"),
     ("scan + fused pack", "::k_scan1f<"),
     ("scan (omr_worker_scan_f32)", "::k_scan1f<"),
     ("pack pass", "::k_move<"),

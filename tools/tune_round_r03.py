@@ -166,11 +166,7 @@ def main():
         return run
 
     sums = {"round-2 k_shard_sum (rows)": sum_r02, "product k_shard_sum (rows)": sum_rows,
-            "product k_shard_sum (cols)": sum_cols,
-            "k_shard_sum_list, one unit per wave": env_case(sum_list, "OMR_SUM_PIPE", "0"),
-            "k_shard_sum_pipe, 1 unit per wave": env_case(sum_list, "OMR_SUM_PIPE", "1"),
-            "k_shard_sum_pipe, 2 units per wave": env_case(sum_list, "OMR_SUM_PIPE", "2"),
-            "product k_shard_sum_pipe (4 units per wave)": sum_list}
+            "product k_shard_sum (cols)": sum_cols, "product k_shard_sum_list (pairs from the plan)": sum_list}
     ref = None
     for name, fn in sums.items():
         o = xs[0].clone()
