@@ -1080,9 +1080,11 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
                   "omr_pack_geometry"));
     p->fused_pack = true;
     p->mstride = p->rows + (entries + 1) / 2;
-    // OMR_SUM_LIST=0 (A/B knob): the shard sum builds its pairs itself (omr_shard_sum_cols_f32)
+    // OMR_SUM_LIST=1 (study knob): the plan launch builds the shard sum's pairs and omr_shard_sum_list_f32 sums them.
+    // At config 4's 8-worker shard that sum took 16.6-17.2 us against 15.5-16.1 for omr_shard_sum_cols_f32, which
+    // builds its pairs itself (profiles/r03/round/list_s2g/), so the round keeps the latter by default.
     const char* le = getenv("OMR_SUM_LIST");
-    if (p->shard >= 0 && (le == nullptr || atoi(le) != 0)) {
+    if (p->shard >= 0 && le != nullptr && atoi(le) != 0) {
       TRY(omr_check(omr_sum_list_geometry(n, block_size, num_lanes, num_parts, p->bounds[p->shard],
                                           p->bounds[p->shard + 1], static_cast<uint32_t>(p->M), &p->list_units,
                                           &p->list_cap), "omr_sum_list_geometry"));
