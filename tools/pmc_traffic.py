@@ -56,7 +56,8 @@ def main():
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     a.out, a.workdir = os.path.abspath(a.out), os.path.abspath(a.workdir)  # the passes run from /tmp
-    bench_args = [x for x in a.bench_args if x != "--"] or ["--steps", "20", "--warmup", "5", "--no-cpu"]
+    # (--no-round: bench's N=1 line would otherwise also run its world-1 round in a child process under the profiler)
+    bench_args = [x for x in a.bench_args if x != "--"] or ["--steps", "20", "--warmup", "5", "--no-cpu", "--no-round"]
     fetch_csv = run_pass("FETCH_SIZE", os.path.join(a.workdir, "fetch"), bench_args)
     write_csv = run_pass("WRITE_SIZE", os.path.join(a.workdir, "write"), bench_args)
     fetch_kib, nf = per_launch(fetch_csv, a.kernel, "FETCH_SIZE")
