@@ -1121,23 +1121,8 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     int least = 0, greatest = 0;
     A(hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange"));
     const int prio = (pe != nullptr && atoi(pe) != 0) ? greatest : least;
-    // OMR_SIDE_QUEUES (study knob): 1 = the two streams made with a CU mask of every CU, which gives each a hardware
-    // queue of its own instead of one shared round-robin with the caller's stream
-    const char* qe = getenv("OMR_SIDE_QUEUES");
-    if (qe != nullptr && atoi(qe) != 0) {
-      int cus = 0, dev = 0;
-      A(hip_check(hipGetDevice(&dev), "hipGetDevice"));
-      A(hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute"));
-      std::vector<uint32_t> mask((std::max(cus, 1) + 31) / 32, 0xFFFFFFFFu);
-      if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
-      A(hip_check(hipExtStreamCreateWithCUMask(&p->ps, static_cast<uint32_t>(mask.size()), mask.data()),
-                  "hipExtStreamCreateWithCUMask"));
-      A(hip_check(hipExtStreamCreateWithCUMask(&p->cs, static_cast<uint32_t>(mask.size()), mask.data()),
-                  "hipExtStreamCreateWithCUMask"));
-    } else {
-      A(hip_check(hipStreamCreateWithPriority(&p->ps, hipStreamNonBlocking, prio), "hipStreamCreate"));
-      A(hip_check(hipStreamCreateWithPriority(&p->cs, hipStreamNonBlocking, prio), "hipStreamCreate"));
-    }
+    A(hip_check(hipStreamCreateWithPriority(&p->ps, hipStreamNonBlocking, prio), "hipStreamCreate"));
+    A(hip_check(hipStreamCreateWithPriority(&p->cs, hipStreamNonBlocking, prio), "hipStreamCreate"));
   }
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, evflags), "hipEventCreate"));
   A(dev_alloc(p->d, &p->bounds_dev, NA + 1));
