@@ -215,6 +215,15 @@ def test_cpp_async_rounds_loopback(gpu, world, mode, round_flags):
             assert (outs[r][k].view(np.uint32) == exp.view(np.uint32)).all(), f"round {k} rank {r}"
 
 
+@pytest.mark.parametrize("world,mode,round_flags", [
+    (8, 1, (D_,) * 7), (4, 0, (A, D_, D_, A, D_, D_, D_)), (4, 0, (T | D_,) * 7), (8, 1, (0,) * 4)])
+def test_cpp_rounds_sum_list_loopback(gpu, monkeypatch, world, mode, round_flags):
+    """The same rounds with OMR_SUM_LIST=1: the plan launch builds each shard's pair list (omr_round_plan_list) and
+    the aggregator sums over it (omr_shard_sum_list_f32), every worker's stream received at its fixed region."""
+    monkeypatch.setenv("OMR_SUM_LIST", "1")
+    test_cpp_async_rounds_loopback(gpu, world, mode, round_flags)
+
+
 @pytest.mark.parametrize("world,flags", [(4, 0), (8, 0x100)])
 def test_cpp_dense_reduce_scatter_loopback(gpu, world, flags):
     """OMR_ROUND_DENSE_REDUCE_SCATTER (the dense stand-in): this rank's shard of the elementwise rank-order sum of
