@@ -22,3 +22,6 @@ for w in 2 4; do
     done
   done
 done
+# the loopback round tests with the pair-list shard sum (added after the final check)
+timeout -k 10 300 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider -m gpu \
+  tests/test_cpp_dist.py -k sum_list > $O/tests_sum_list.log 2>&1
