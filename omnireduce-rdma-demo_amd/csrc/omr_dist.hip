@@ -771,6 +771,8 @@ struct omr_ar_plan {
     uint64_t* umask = nullptr;      // [rows] union of the workers' masks
     uint32_t* prefix = nullptr;     // [N+1][rows+1] popcount prefixes: workers, then the write set
     float* packed = nullptr;        // own non-zero blocks of the other shards, block order
+    float* recv = nullptr;          // this shard's blocks from each peer, worker w's at w * shard_nb blocks
+    hipEvent_t xdone = nullptr;     // aggregation stream: recorded on the communication stream after the exchange
     uint64_t* list_rec = nullptr;   // sum list: the shard sum's pair records, built by the plan launch
     uint32_t* list_cnt = nullptr;   //   and their count per unit
     hipEvent_t scanned = nullptr;   // async: recorded on the caller's stream after the worker scan
@@ -786,10 +788,14 @@ struct omr_ar_plan {
   int last_async = -1;              // set of the last asynchronous round (for join)
   hipStream_t ps = nullptr;         // plan stream of asynchronous rounds: mask all-gather, plan, pack, union chain
   hipStream_t cs = nullptr;         // communication stream of asynchronous rounds: exchange, shard sums [, sums back]
+  hipStream_t as = nullptr;         // aggregation stream: an asynchronous co-located reduce-scatter round's shard sums,
+                                    // so round k+1's exchange on `cs` runs while round k's sums do (OMR_AGG_STREAM=0:
+                                    // off)
+  int as_last = -1;                 // set of the last round whose sums went on `as` (for join)
+  hipStream_t tail = nullptr;       // the stream of the last asynchronous round's last work (the bucket write-back)
   uint64_t* bounds_dev = nullptr;
   uint32_t* counts_host = nullptr;  // [kSets][M+1][A+1] per set: prefix[a][bounds[s]], pinned memory the plan kernel writes
   uint32_t* counts_map = nullptr;   // its device-side address
-  float* recv = nullptr;     // this shard's blocks from each peer, peer-major
   float* results = nullptr;  // all-reduce: every shard's sums, write-set order (a dedicated aggregator: its own)
   uint64_t last_sums_blocks = 0;  // a dedicated aggregator: blocks of its last round's shard sums in `results`
   int32_t* flags_ws = nullptr;
@@ -1005,16 +1011,18 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     (void)flush_pending(p, p->cs, nullptr, nullptr);
   (void)hipDeviceSynchronize();
   // back to the transport, which keeps the exported ones alive for the next plan (omr_dist::alloc)
-  void* devs[] = {p->bounds_dev, p->recv, p->results, p->flags_ws, p->next_ws, p->unext_ws, p->scan_ws, p->arrive};
+  void* devs[] = {p->bounds_dev, p->results, p->flags_ws, p->next_ws, p->unext_ws, p->scan_ws, p->arrive};
   for (void* v : devs) p->d->release(v);
   for (auto& st : p->set) {
-    void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed, st.pack_cnt, st.list_rec, st.list_cnt};
+    void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed, st.pack_cnt, st.list_rec, st.list_cnt,
+                  st.recv};
     for (void* v : sv) p->d->release(v);
-    for (hipEvent_t e : {st.scanned, st.planned, st.ready, st.done})
+    for (hipEvent_t e : {st.scanned, st.planned, st.ready, st.done, st.xdone})
       if (e) (void)hipEventDestroy(e);
   }
   if (p->ps) (void)hipStreamDestroy(p->ps);
   if (p->cs) (void)hipStreamDestroy(p->cs);
+  if (p->as) (void)hipStreamDestroy(p->as);
   for (int r = 0; r < omr_ar_plan::kStage; ++r) {
     p->d->release(p->stage[r]);
     for (hipEvent_t e : {p->ev_in[r], p->ev_round[r], p->ev_out[r]})
@@ -1111,7 +1119,7 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
       A(dev_alloc(p->d, &st.list_rec, p->list_units * p->list_cap));
       A(dev_alloc(p->d, &st.list_cnt, p->list_units));
     }
-    for (hipEvent_t* e : {&st.scanned, &st.planned, &st.ready, &st.done})
+    for (hipEvent_t* e : {&st.scanned, &st.planned, &st.ready, &st.done, &st.xdone})
       A(hip_check(hipEventCreateWithFlags(e, evflags), "hipEventCreate"));
   }
   {
@@ -1123,10 +1131,14 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     const int prio = (pe != nullptr && atoi(pe) != 0) ? greatest : least;
     A(hip_check(hipStreamCreateWithPriority(&p->ps, hipStreamNonBlocking, prio), "hipStreamCreate"));
     A(hip_check(hipStreamCreateWithPriority(&p->cs, hipStreamNonBlocking, prio), "hipStreamCreate"));
+    const char* ae = getenv("OMR_AGG_STREAM");
+    if (N > 1 && p->shard >= 0 && (ae == nullptr || atoi(ae) != 0))
+      A(hip_check(hipStreamCreateWithPriority(&p->as, hipStreamNonBlocking, prio), "hipStreamCreate"));
   }
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, evflags), "hipEventCreate"));
   A(dev_alloc(p->d, &p->bounds_dev, NA + 1));
-  if (N > 1 && p->shard >= 0) A(dev_alloc(p->d, &p->recv, static_cast<size_t>(M) * p->shard_nb * block_size));
+  if (N > 1 && p->shard >= 0)
+    for (auto& st : p->set) A(dev_alloc(p->d, &st.recv, static_cast<size_t>(M) * p->shard_nb * block_size));
   A(dev_alloc(p->d, &p->results, n));
   A(dev_alloc(p->d, &p->flags_ws, p->nb));
   A(dev_alloc(p->d, &p->next_ws, p->nb));
@@ -1304,7 +1316,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       for (int w = 0; w < M; ++w) {
         if (w == me) continue;
         roff[w] = recv_slot(p, w);
-        recvs[w] = {Slice{p->recv + roff[w] * B, per(w, sh) * B * sizeof(float)}};
+        recvs[w] = {Slice{S.recv + roff[w] * B, per(w, sh) * B * sizeof(float)}};
         in_blocks += per(w, sh);
       }
     TRY(p->d->exchange(sends, recvs, xs));
@@ -1318,6 +1330,16 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     TRY(timed_exchange(p, tslot));
   }
   const bool rs_mode = mode == OMR_ROUND_REDUCE_SCATTER;
+  // An asynchronous reduce-scatter round sums on the aggregation stream, behind this exchange only, so the next
+  // round's exchange on the communication stream need not wait for these sums (its blocks land in another set's
+  // `recv`).  The set's `done` then follows the sums, and with them the exchange.
+  hipStream_t ss = xs;
+  if (async && rs_mode && p->colocated && p->as != nullptr && sh >= 0 && !solo) {
+    TRY(hip_check(hipEventRecord(S.xdone, xs), "hipEventRecord"));
+    TRY(hip_check(hipStreamWaitEvent(p->as, S.xdone, 0), "hipStreamWaitEvent"));
+    ss = p->as;
+  }
+  const omr_stream_t sstream = reinterpret_cast<omr_stream_t>(ss);
   // 5. aggregator: rank-order shard sums (server.cc:97-98); a co-located rank reads its own blocks in place.
   //    Co-located reduce-scatter writes them in place (dense); otherwise packed in write-set order
   float* sums = nullptr;
@@ -1330,18 +1352,18 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     const uint32_t own_idx = p->colocated ? static_cast<uint32_t>(me) : static_cast<uint32_t>(M);
     if (p->sum_list) {  // the pairs were built by this round's plan launch
       const omr_sum_list l = list_desc(p, S);
-      TRY(omr_check(omr_shard_sum_list_f32(own, p->recv, &l, static_cast<uint32_t>(M), p->n, p->B, p->lanes, p->parts,
+      TRY(omr_check(omr_shard_sum_list_f32(own, S.recv, &l, static_cast<uint32_t>(M), p->n, p->B, p->lanes, p->parts,
                                            S.wset, S.prefix + static_cast<uint64_t>(M) * (rows + 1), dense_out ? 0 : 1,
-                                           sums, xstream),
+                                           sums, sstream),
                     "omr_shard_sum_list_f32"));
     } else if (p->fused_pack)  // the workers' streams are column-ordered: positions from their all-gathered tables
-      TRY(omr_check(omr_shard_sum_cols_f32(own, own_idx, p->recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
+      TRY(omr_check(omr_shard_sum_cols_f32(own, own_idx, S.recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
                                            p->mstride, 2 * rows, S.prefix, S.wset, p->n, p->B, p->lanes, p->parts,
-                                           r0, r1, dense_out ? 0 : 1, sums, xstream),
+                                           r0, r1, dense_out ? 0 : 1, sums, sstream),
                     "omr_shard_sum_cols_f32"));
     else
-      TRY(omr_check(omr_shard_sum_f32(own, own_idx, p->recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
-                                      S.prefix, S.wset, rows, r0, r1, p->lanes, p->B, dense_out ? 0 : 1, sums, xstream),
+      TRY(omr_check(omr_shard_sum_f32(own, own_idx, S.recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
+                                      S.prefix, S.wset, rows, r0, r1, p->lanes, p->B, dense_out ? 0 : 1, sums, sstream),
                     "omr_shard_sum_f32"));
     if (!p->colocated) p->last_sums_blocks = per(M, sh);
   }
@@ -1365,13 +1387,15 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
                                         rows, p->lanes, p->B, 0, 0, xstream), "omr_move_blocks_f32 unpack"));
   }
   if (timed && p->timed[tslot].xchg) {
-    TRY(hip_check(hipEventRecord(p->timed[tslot].a1, xs), "hipEventRecord"));
+    TRY(hip_check(hipEventRecord(p->timed[tslot].a1, ss), "hipEventRecord"));
     p->timed[tslot].agg = true;
   }
   if (async) {
-    TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
+    TRY(hip_check(hipEventRecord(S.done, ss), "hipEventRecord"));
     S.pending = true;
     p->last_async = si;
+    p->tail = ss;  // the stream this round's last work is on
+    if (ss == p->as) p->as_last = si;
     std::lock_guard<std::mutex> g(p->mu);
     S.scan_wait = true;
   }
@@ -1596,7 +1620,10 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   // last asynchronous round's `done` follows all of its plan-stream work)
   if (!async && p->last_async >= 0) {
     TRY(hip_check(hipStreamWaitEvent(st, p->set[p->last_async].done, 0), "hipStreamWaitEvent"));
+    if (p->as_last >= 0 && p->as_last != p->last_async)
+      TRY(hip_check(hipStreamWaitEvent(st, p->set[p->as_last].done, 0), "hipStreamWaitEvent"));
     p->last_async = -1;
+    p->as_last = -1;
   }
   const int si = p->cur;
   omr_ar_plan::Set& S = p->set[si];
@@ -1790,9 +1817,9 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
     const int r = static_cast<int>(k % R);
     if (zc) {  // the results are already in host memory: the staging buffer is free once the second half is through
       p->out_used[r] = true;
-      return hip_check(hipEventRecord(p->ev_out[r], p->cs), "hipEventRecord");
+      return hip_check(hipEventRecord(p->ev_out[r], p->tail ? p->tail : p->cs), "hipEventRecord");
     }
-    TRY(hip_check(hipEventRecord(p->ev_round[r], p->cs), "hipEventRecord"));
+    TRY(hip_check(hipEventRecord(p->ev_round[r], p->tail ? p->tail : p->cs), "hipEventRecord"));
     TRY(hip_check(hipStreamWaitEvent(p->s_out, p->ev_round[r], 0), "hipStreamWaitEvent"));
     if (back_n)
       TRY(hip_check(hipMemcpyAsync(hbuf + k * p->n + back0, p->stage[r] + back0, back_n * sizeof(float),
@@ -1860,9 +1887,13 @@ int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
   TRY(thread_drain(p));
   TRY(flush_pending(p, reinterpret_cast<hipStream_t>(stream), nullptr, nullptr));
   if (p->last_async < 0) return 0;
-  // the communication stream runs rounds in issue order: waiting for the last one covers every earlier one
+  // the communication and aggregation streams each run rounds in issue order: waiting for the last one on each
+  // covers every earlier one
   TRY(hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), p->set[p->last_async].done, 0),
                 "hipStreamWaitEvent"));
+  if (p->as_last >= 0 && p->as_last != p->last_async)
+    TRY(hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), p->set[p->as_last].done, 0),
+                  "hipStreamWaitEvent"));
   return 0;
 }
 
