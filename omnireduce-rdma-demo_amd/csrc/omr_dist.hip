@@ -789,8 +789,8 @@ struct omr_ar_plan {
   hipStream_t ps = nullptr;         // plan stream of asynchronous rounds: mask all-gather, plan, pack, union chain
   hipStream_t cs = nullptr;         // communication stream of asynchronous rounds: exchange, shard sums [, sums back]
   hipStream_t as = nullptr;         // aggregation stream: an asynchronous co-located reduce-scatter round's shard sums,
-                                    // so round k+1's exchange on `cs` runs while round k's sums do (OMR_AGG_STREAM=0:
-                                    // off)
+                                    // so round k+1's exchange on `cs` runs while round k's sums do (OMR_AGG_STREAM=1:
+                                    // on; off by default)
   int as_last = -1;                 // set of the last round whose sums went on `as` (for join)
   hipStream_t tail = nullptr;       // the stream of the last asynchronous round's last work (the bucket write-back)
   uint64_t* bounds_dev = nullptr;
@@ -1131,8 +1131,11 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     const int prio = (pe != nullptr && atoi(pe) != 0) ? greatest : least;
     A(hip_check(hipStreamCreateWithPriority(&p->ps, hipStreamNonBlocking, prio), "hipStreamCreate"));
     A(hip_check(hipStreamCreateWithPriority(&p->cs, hipStreamNonBlocking, prio), "hipStreamCreate"));
+    // OMR_AGG_STREAM=1 (opt-in): the aggregation stream.  Off by default: a fourth side stream exceeds the process's
+    // four hardware queues (GPU_MAX_HW_QUEUES), and its wait for the exchange can then block whatever shares its queue.
+    // As 4 IPC ranks on one GPU it took 27.5 ms per round against 1.47 ms without (profiles/r03/agg_stream/).
     const char* ae = getenv("OMR_AGG_STREAM");
-    if (N > 1 && p->shard >= 0 && (ae == nullptr || atoi(ae) != 0))
+    if (N > 1 && p->shard >= 0 && ae != nullptr && atoi(ae) != 0)
       A(hip_check(hipStreamCreateWithPriority(&p->as, hipStreamNonBlocking, prio), "hipStreamCreate"));
   }
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, evflags), "hipEventCreate"));
