@@ -224,6 +224,16 @@ def test_cpp_rounds_sum_list_loopback(gpu, monkeypatch, world, mode, round_flags
     test_cpp_async_rounds_loopback(gpu, world, mode, round_flags)
 
 
+@pytest.mark.parametrize("world,mode,round_flags", [
+    (8, 1, (D_,) * 7), (4, 1, (A, D_, 0, D_, A, D_, D_)), (4, 1, (T | D_,) * 7), (3, 0, (D_, D_, A, D_))])
+def test_cpp_rounds_agg_stream_loopback(gpu, monkeypatch, world, mode, round_flags):
+    """The same rounds with OMR_AGG_STREAM=1: asynchronous reduce-scatter rounds sum on the aggregation stream (each
+    set with its own receive buffer), mixed with synchronous rounds and all-reduce rounds that stay on the
+    communication stream."""
+    monkeypatch.setenv("OMR_AGG_STREAM", "1")
+    test_cpp_async_rounds_loopback(gpu, world, mode, round_flags)
+
+
 @pytest.mark.parametrize("world,flags", [(4, 0), (8, 0x100)])
 def test_cpp_dense_reduce_scatter_loopback(gpu, world, flags):
     """OMR_ROUND_DENSE_REDUCE_SCATTER (the dense stand-in): this rank's shard of the elementwise rank-order sum of
