@@ -1317,6 +1317,48 @@ __global__ __launch_bounds__(kWGThreads) void k_move(MoveArgs a) {
 // then a segmented sum in rank order whose last pair of each block stores it.  So a unit costs one index round trip
 // plus one per P pairs, whatever the number of contributors (the round-2 kernel paid a round trip per contributor
 // per batch of blocks behind a prefix round trip: 2.9 TB/s at an 8-worker shard).
+// One window of the shard sum: P (block, contributor) pairs, records `rec` lanes [cb, cb + P) (nv of them real).
+// Every window issues exactly P loads and then exactly P stores, whatever nv and whichever pairs end a block: an
+// unused slot loads through a zero-size descriptor, a store that does not end a block is pointed past its
+// descriptor's range and dropped.  On gfx9 `vmcnt` counts loads and stores together, so a data-dependent store
+// between two uses of loaded blocks made the compiler wait for every outstanding operation (s_waitcnt vmcnt(0)) before
+// each use -- one store's write latency per summed block.  With the static schedule each wait counts exactly the
+// younger operations and the window's loads stay in flight together.
+template <int VEC, int P>
+__device__ __forceinline__ void sum_window(uint64_t rec, uint32_t cb, uint32_t nv, uint64_t pdst, bool packed,
+                                           const float* own, const float* recv, float* out, uint32_t block,
+                                           uint32_t bbytes, int lane, v4f (&acc)[VEC]) {
+  v4f v[P][VEC];
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const uint64_t rc = readlane64(rec, cb + j);
+    const bool load = static_cast<uint32_t>(j) < nv && !(rc & kRecZero);
+    const float* const sb = (rc & kRecOwn) ? own : recv;
+    const __amdgpu_buffer_rsrc_t src =
+        chunk_rsrc(load ? sb + static_cast<uint64_t>(static_cast<uint32_t>(rc)) * block : recv, load ? bbytes : 0u);
+#pragma unroll
+    for (int q = 0; q < VEC; ++q)
+      v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (q * 64 + lane) * 16, 0, kLoadAux));
+  }
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    const uint64_t rc = readlane64(rec, cb + j);
+    const bool use = static_cast<uint32_t>(j) < nv;
+    const bool first = use && (rc & kRecFirst), last = use && (rc & kRecLast);
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {  // (0.0f + x_first) + ...: a block's first pair restarts from +0.0f
+      const v4f sum = add4(first ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
+      acc[q] = use ? sum : acc[q];
+    }
+    const uint64_t dst = packed ? readlane64(pdst, cb + j) : ((rc >> 32) & 0x0FFFFFFFull);
+    const __amdgpu_buffer_rsrc_t d = chunk_rsrc(out + (last ? dst * block : 0ull), bbytes);
+    const uint32_t drop = last ? 0u : kDropStore;
+#pragma unroll
+    for (int q = 0; q < VEC; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[q]), d, ((q * 64 + lane) * 16) | drop, 0, 0);
+  }
+}
+
 struct SumArgs {
   const float* own;
   const float* recv;
@@ -1336,7 +1378,6 @@ struct SumArgs {
 template <int VEC>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
   constexpr int P = 32 / VEC;  // pair slots per window
-  constexpr int kSlotGroup = P < 8 ? P : 8;
   constexpr uint32_t kRecCap = kSumUnitRows * OMR_MAX_WORKERS;
   __shared__ uint64_t s_rec[kWavesPerWG][kRecCap];
   const int lane = threadIdx.x & 63;
@@ -1444,40 +1485,7 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
     for (uint32_t wbase = 0; wbase < total; wbase += P) {
       const uint32_t nv = total - wbase < static_cast<uint32_t>(P) ? total - wbase : static_cast<uint32_t>(P);
       const uint64_t myrec = static_cast<uint32_t>(lane) < nv ? s_rec[wave][wbase + lane] : 0ull;
-      v4f v[P][VEC];
-      // every load of the window issued before the first use; slots in groups of kSlotGroup, a group past the
-      // window's last pair skipped by a wave-uniform branch (a sparse unit issues only what it needs)
-#pragma unroll
-      for (int g = 0; g < P; g += kSlotGroup) {
-        if (static_cast<uint32_t>(g) < nv) {
-#pragma unroll
-          for (int j = g; j < g + kSlotGroup; ++j) {
-            const uint64_t rc = readlane64(myrec, j);
-            const bool load = static_cast<uint32_t>(j) < nv && !(rc & kRecZero);
-            const float* const sb = (rc & kRecOwn) ? a.own : a.recv;
-            const __amdgpu_buffer_rsrc_t src =
-                chunk_rsrc(sb + static_cast<uint64_t>(static_cast<uint32_t>(rc)) * a.block, load ? bbytes : 0u);
-#pragma unroll
-            for (int q = 0; q < VEC; ++q)
-              v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (q * 64 + lane) * 16, 0,
-                                                                                     kLoadAux));
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < P; ++j) {
-        if (static_cast<uint32_t>(j) < nv) {  // (wave-uniform)
-          const uint64_t rc = readlane64(myrec, j);
-#pragma unroll
-          for (int q = 0; q < VEC; ++q)  // (0.0f + x_first) + ...: a block's first pair restarts from +0.0f
-            acc[q] = add4((rc & kRecFirst) ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
-          if (rc & kRecLast) {
-            v4f* const d = reinterpret_cast<v4f*>(a.out + ((rc >> 32) & 0x0FFFFFFFull) * a.block);
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = acc[q];
-          }
-        }
-      }
+      sum_window<VEC, P>(myrec, 0, nv, 0, false, a.own, a.recv, a.out, a.block, bbytes, lane, acc);
     }
   }
 }
@@ -1501,7 +1509,6 @@ struct ListSumArgs {
 template <int VEC>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
   constexpr int P = 32 / VEC;  // pair slots per window
-  constexpr int kSlotGroup = P < 8 ? P : 8;
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
@@ -1539,39 +1546,7 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
         }
       }
       const uint32_t nv = total - wbase < static_cast<uint32_t>(P) ? total - wbase : static_cast<uint32_t>(P);
-      v4f v[P][VEC];
-#pragma unroll
-      for (int g = 0; g < P; g += kSlotGroup) {
-        if (static_cast<uint32_t>(g) < nv) {
-#pragma unroll
-          for (int j = g; j < g + kSlotGroup; ++j) {
-            const uint64_t rc = readlane64(chunk, cb + j);
-            const bool load = static_cast<uint32_t>(j) < nv && !(rc & kRecZero);
-            const float* const sb = (rc & kRecOwn) ? a.own : a.recv;
-            const __amdgpu_buffer_rsrc_t src =
-                chunk_rsrc(sb + static_cast<uint64_t>(static_cast<uint32_t>(rc)) * a.block, load ? bbytes : 0u);
-#pragma unroll
-            for (int q = 0; q < VEC; ++q)
-              v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (q * 64 + lane) * 16, 0,
-                                                                                     kLoadAux));
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < P; ++j) {
-        if (static_cast<uint32_t>(j) < nv) {  // (wave-uniform)
-          const uint64_t rc = readlane64(chunk, cb + j);
-#pragma unroll
-          for (int q = 0; q < VEC; ++q)  // (0.0f + x_first) + ...: a block's first pair restarts from +0.0f
-            acc[q] = add4((rc & kRecFirst) ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
-          if (rc & kRecLast) {
-            const uint64_t dst = a.packed_out ? readlane64(pdst, cb + j) : ((rc >> 32) & 0x0FFFFFFFull);
-            v4f* const d = reinterpret_cast<v4f*>(a.out + dst * a.block);
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = acc[q];
-          }
-        }
-      }
+      sum_window<VEC, P>(chunk, cb, nv, pdst, a.packed_out != 0, a.own, a.recv, a.out, a.block, bbytes, lane, acc);
     }
   }
 }

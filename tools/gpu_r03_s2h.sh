@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 3, second session: the shard sums with a static per-window load / store schedule (sum_window) -- parity
+# tests, the round kernels at config-4 shapes, the round tests.
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-r03s2h}
+mkdir -p $O
+cd $R
+T="python3 -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider -m gpu"
+timeout -k 10 300 $T tests/test_gpu_pack.py tests/test_gpu_round.py > $O/tests_pack_round.log 2>&1 && \
+timeout -k 10 300 python3 tools/tune_round_r03.py > $O/tune_round_r03.log 2>&1 && \
+timeout -k 10 600 $T tests/test_cpp_dist.py tests/test_gpu_ipc.py tests/test_gpu_fault.py tests/test_gpu_buckets.py \
+  > $O/tests_round.log 2>&1
