@@ -1323,7 +1323,9 @@ __global__ __launch_bounds__(kWGThreads) void k_move(MoveArgs a) {
 // descriptor's range and dropped.  On gfx9 `vmcnt` counts loads and stores together, so a data-dependent store
 // between two uses of loaded blocks made the compiler wait for every outstanding operation (s_waitcnt vmcnt(0)) before
 // each use -- one store's write latency per summed block.  With the static schedule each wait counts exactly the
-// younger operations and the window's loads stay in flight together.
+// younger operations and the window's loads stay in flight together.  Used by the pair-list sum (17.2 -> 15.4 us at
+// config 4's 8-worker shard); k_shard_sum keeps its branchy window, which measured faster for it (15.5-16.1 against
+// 17.8-18.0 us with this one: profiles/r03/round/static_s2h/tune_round_r03.log).
 template <int VEC, int P>
 __device__ __forceinline__ void sum_window(uint64_t rec, uint32_t cb, uint32_t nv, uint64_t pdst, bool packed,
                                            const float* own, const float* recv, float* out, uint32_t block,
@@ -1378,6 +1380,7 @@ struct SumArgs {
 template <int VEC>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
   constexpr int P = 32 / VEC;  // pair slots per window
+  constexpr int kSlotGroup = P < 8 ? P : 8;
   constexpr uint32_t kRecCap = kSumUnitRows * OMR_MAX_WORKERS;
   __shared__ uint64_t s_rec[kWavesPerWG][kRecCap];
   const int lane = threadIdx.x & 63;
@@ -1485,7 +1488,40 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
     for (uint32_t wbase = 0; wbase < total; wbase += P) {
       const uint32_t nv = total - wbase < static_cast<uint32_t>(P) ? total - wbase : static_cast<uint32_t>(P);
       const uint64_t myrec = static_cast<uint32_t>(lane) < nv ? s_rec[wave][wbase + lane] : 0ull;
-      sum_window<VEC, P>(myrec, 0, nv, 0, false, a.own, a.recv, a.out, a.block, bbytes, lane, acc);
+      v4f v[P][VEC];
+      // every load of the window issued before the first use; slots in groups of kSlotGroup, a group past the
+      // window's last pair skipped by a wave-uniform branch (a sparse unit issues only what it needs)
+#pragma unroll
+      for (int g = 0; g < P; g += kSlotGroup) {
+        if (static_cast<uint32_t>(g) < nv) {
+#pragma unroll
+          for (int j = g; j < g + kSlotGroup; ++j) {
+            const uint64_t rc = readlane64(myrec, j);
+            const bool load = static_cast<uint32_t>(j) < nv && !(rc & kRecZero);
+            const float* const sb = (rc & kRecOwn) ? a.own : a.recv;
+            const __amdgpu_buffer_rsrc_t src =
+                chunk_rsrc(sb + static_cast<uint64_t>(static_cast<uint32_t>(rc)) * a.block, load ? bbytes : 0u);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q)
+              v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (q * 64 + lane) * 16, 0,
+                                                                                     kLoadAux));
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        if (static_cast<uint32_t>(j) < nv) {  // (wave-uniform)
+          const uint64_t rc = readlane64(myrec, j);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q)  // (0.0f + x_first) + ...: a block's first pair restarts from +0.0f
+            acc[q] = add4((rc & kRecFirst) ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
+          if (rc & kRecLast) {
+            v4f* const d = reinterpret_cast<v4f*>(a.out + ((rc >> 32) & 0x0FFFFFFFull) * a.block);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = acc[q];
+          }
+        }
+      }
     }
   }
 }
