@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Historical: k_shard_sum_pipe and OMR_SUM_PIPE were removed after this run.)
 # Round 3, second session: the pipelined pair-list shard sum (k_shard_sum_pipe) and the 8-wave pack scan as defaults --
 # their parity tests (and the variants behind OMR_SUM_PIPE / OMR_PACK_WAVES), the round kernels at config-4 shapes, the
 # round tests, bench with the driver's arguments (round_world1 as a torch.distributed.run child), PMC of the round.
