@@ -776,11 +776,11 @@ struct omr_ar_plan {
     uint64_t* list_rec = nullptr;   // sum list: the shard sum's pair records, built by the plan launch
     uint32_t* list_cnt = nullptr;   //   and their count per unit
     hipEvent_t scanned = nullptr;   // async: recorded on the caller's stream after the worker scan
-    hipEvent_t planned = nullptr;   // async: recorded on the plan stream once `own` is consumed and re-zeroed
     hipEvent_t ready = nullptr;     // recorded once the set is filled (the plan stream for async rounds)
     hipEvent_t done = nullptr;      // recorded on the communication stream once the round is through with it
     bool pending = false;           // `done` recorded and not yet waited for by a refill
-    bool plan_pending = false;      // `planned` recorded and not yet waited for by a scan
+    bool plan_pending = false;      // `ready` recorded (the plan has consumed and re-zeroed `own`) and not yet waited
+                                    // for by a scan
     bool scan_wait = false;         // fused pack: `done` recorded and not yet waited for by the scan that refills
                                     // `packed` (guarded by mu: the progress thread sets it)
   } set[kSets];
@@ -847,7 +847,7 @@ struct omr_ar_plan {
   HostTrace ht;
   // OMR_ROUND_THREAD: a progress thread issues each round's steps after the worker scan, in call order.  The
   // calling thread queues the scan, then a job; it runs at most kSets - 1 rounds ahead of the thread's first halves
-  // (a set's `planned` / `scanned` events must have been recorded / waited for before the set is reused).
+  // (a set's `ready` / `scanned` events must have been recorded / waited for before the set is reused).
   struct Job {
     int si = 0, mode = 0, tslot = -1;
     bool async = false, defer = false, timed = false, flush_first = false;
@@ -1017,7 +1017,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed, st.pack_cnt, st.list_rec, st.list_cnt,
                   st.recv};
     for (void* v : sv) p->d->release(v);
-    for (hipEvent_t e : {st.scanned, st.planned, st.ready, st.done, st.xdone})
+    for (hipEvent_t e : {st.scanned, st.ready, st.done, st.xdone})
       if (e) (void)hipEventDestroy(e);
   }
   if (p->ps) (void)hipStreamDestroy(p->ps);
@@ -1119,7 +1119,7 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
       A(dev_alloc(p->d, &st.list_rec, p->list_units * p->list_cap));
       A(dev_alloc(p->d, &st.list_cnt, p->list_units));
     }
-    for (hipEvent_t* e : {&st.scanned, &st.planned, &st.ready, &st.done, &st.xdone})
+    for (hipEvent_t* e : {&st.scanned, &st.ready, &st.done, &st.xdone})
       A(hip_check(hipEventCreateWithFlags(e, evflags), "hipEventCreate"));
   }
   {
@@ -1230,6 +1230,8 @@ omr_sum_list list_desc(const omr_ar_plan* p, const omr_ar_plan::Set& S) {
 // (internal bit in a round's mode: a one-rank round whose worker scan wrote the sums itself, see omr_sparse_round_f32)
 constexpr int kModeSolo = 0x10000;
 
+int wait_ev(hipStream_t on, hipEvent_t ev);
+
 int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, bool async, bool timed, uint32_t seq,
                  hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks, int tslot) {
   const bool solo = (mode & kModeSolo) != 0;
@@ -1260,7 +1262,8 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
   hipStream_t xs = st;
   ht_of(p).start();
   if (async) {
-    TRY(hip_check(hipStreamWaitEvent(p->cs, S.ready, 0), "hipStreamWaitEvent"));
+    // (a deferred round's `ready` fired long ago, as a rule: then no wait is queued at all)
+    TRY(wait_ev(p->cs, S.ready));
     xs = p->cs;
   }
   ht_of(p).lap("2:cs wait ready");
@@ -1474,10 +1477,6 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
                                     S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->arrive, p->flag_map + si, seq,
                                     j.un, p->B, p->sum_list ? &sl : nullptr, qstream),
                 "omr_round_plan_list"));
-  if (async) {
-    TRY(hip_check(hipEventRecord(S.planned, qs), "hipEventRecord"));
-    S.plan_pending = true;
-  }
   ht.lap("1:plan");
   // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407): addressed by
   //     device-side data only, so it is queued before the host learns the counts and runs while it waits.  (Every
@@ -1493,9 +1492,14 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
     p->timed[tslot].prep = true;
   }
   ht.lap("1:pack");
-  // the rest goes on the communication stream for an asynchronous round, behind everything queued so far
-  if (async) TRY(hip_check(hipEventRecord(S.ready, qs), "hipEventRecord"));
-  {  // the set's `planned` is recorded and its `scanned` waited for: the caller may reuse it
+  // the rest goes on the communication stream for an asynchronous round, behind everything queued so far.  The same
+  // event tells the scan that refills this set's own masks that the plan has consumed and re-zeroed them (one record
+  // per round instead of two: every host API call costs the round microseconds)
+  if (async) {
+    TRY(hip_check(hipEventRecord(S.ready, qs), "hipEventRecord"));
+    S.plan_pending = true;
+  }
+  {  // the set's `ready` is recorded and its `scanned` waited for: the caller may reuse it
     std::lock_guard<std::mutex> g(p->mu);
     ++p->first_halves;
   }
@@ -1650,7 +1654,7 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
     if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
   }
   if (S.plan_pending) {
-    TRY(wait_ev(st, S.planned));
+    TRY(wait_ev(st, S.ready));
     S.plan_pending = false;
   }
   // A fused-pack scan refills the set's send streams: the exchange of the round kSets calls back, which reads them
