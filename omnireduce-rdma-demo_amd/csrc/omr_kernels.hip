@@ -983,12 +983,6 @@ __device__ __forceinline__ uint32_t take_bits(uint64_t& rem, uint32_t (&lj)[SL],
 // exclusive scan -> prefix[a][r]; counts[a][s] = prefix[a][bounds[s]].  (Arrays of more than kPlanLdsRows rows
 // are re-read in pass 2 instead of kept in LDS.)
 constexpr int kPlanThreads = 1024;
-// OMR_PLAN_THREADS=256 (study knob): the plan launch in 256-thread workgroups (72 VGPRs), small enough to share a CU
-// with a running scan workgroup instead of waiting for the scan's workgroups to drain
-int plan_threads() {
-  const char* e = getenv("OMR_PLAN_THREADS");
-  return (e != nullptr && atoi(e) == 256) ? 256 : kPlanThreads;
-}
 constexpr uint64_t kPlanLdsRows = 8192;  // 64 KiB of dynamic LDS
 
 __device__ __forceinline__ uint64_t plan_row(const uint64_t* masks, uint32_t a, uint32_t count, uint64_t mstride,
@@ -1138,11 +1132,10 @@ struct PlanArgs {
   ListArgs list;
 };
 
-template <int T>
-__global__ __launch_bounds__(T) void k_round_plan(PlanArgs a) {
+__global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
   if (blockIdx.x > a.count + a.chain_wgs) {  // the shard sum's pair list, one unit per wave
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr uint32_t kW = T / 64;
+    constexpr uint32_t kW = kPlanThreads / 64;
     build_sum_list(a.list, static_cast<uint64_t>(blockIdx.x - a.count - 1 - a.chain_wgs) * kW + w,
                    static_cast<uint64_t>(a.list_wgs) * kW);
     return;
@@ -1151,7 +1144,7 @@ __global__ __launch_bounds__(T) void k_round_plan(PlanArgs a) {
     const uint64_t* m = a.masks;
     const uint32_t cnt = a.count;
     const uint64_t ms = a.mstride;
-    next_segment<T / 64>(a.chain, blockIdx.x - a.count - 1, [&](uint64_t r) {
+    next_segment<kPlanThreads / 64>(a.chain, blockIdx.x - a.count - 1, [&](uint64_t r) {
       uint64_t u = 0;
       for (uint32_t c = 0; c < cnt; ++c) u |= m[static_cast<uint64_t>(c) * ms + r];
       return u;
@@ -1159,7 +1152,7 @@ __global__ __launch_bounds__(T) void k_round_plan(PlanArgs a) {
     return;
   }
   extern __shared__ uint64_t s_val[];  // [rows] when rows <= kPlanLdsRows
-  __shared__ uint32_t s_wave[T / 64];
+  __shared__ uint32_t s_wave[kPlanThreads / 64];
   __shared__ uint64_t s_bounds[OMR_MAX_WORKERS + 2];
   const uint32_t arr = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint64_t all_lanes = a.lanes >= 64 ? ~0ull : ((1ull << a.lanes) - 1ull);
@@ -1168,16 +1161,16 @@ __global__ __launch_bounds__(T) void k_round_plan(PlanArgs a) {
   if (t < a.nbounds) s_bounds[t] = a.bounds[t];
   if (ws && a.zero_cnt != nullptr && t < a.zero_cnt_n) a.zero_cnt[t] = 0;
   // pass 1: coalesced row reads, 4 rows per thread per step
-  for (uint64_t r0 = t; r0 < a.rows; r0 += 4 * T) {
+  for (uint64_t r0 = t; r0 < a.rows; r0 += 4 * kPlanThreads) {
     uint64_t v[4], u[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint64_t r = r0 + static_cast<uint64_t>(i) * T;
+      const uint64_t r = r0 + static_cast<uint64_t>(i) * kPlanThreads;
       v[i] = r < a.rows ? plan_row(a.masks, arr, a.count, a.mstride, r, a.rpp, all_lanes, &u[i]) : 0;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint64_t r = r0 + static_cast<uint64_t>(i) * T;
+      const uint64_t r = r0 + static_cast<uint64_t>(i) * kPlanThreads;
       if (r >= a.rows) break;
       if (keep) s_val[r] = v[i];
       if (ws) {
@@ -1188,7 +1181,7 @@ __global__ __launch_bounds__(T) void k_round_plan(PlanArgs a) {
     }
   }
   __syncthreads();  // LDS rows (and, when re-read, this workgroup's write-set stores) visible to every thread
-  const uint64_t per = (a.rows + T - 1) / T;
+  const uint64_t per = (a.rows + kPlanThreads - 1) / kPlanThreads;
   const uint64_t rb = t * per < a.rows ? t * per : a.rows;
   const uint64_t re = rb + per < a.rows ? rb + per : a.rows;
   auto row = [&](uint64_t r) -> uint64_t {
@@ -1208,7 +1201,7 @@ __global__ __launch_bounds__(T) void k_round_plan(PlanArgs a) {
   if (lane == 63) s_wave[wave] = inc;
   __syncthreads();
   uint32_t wbase = 0, total = 0;
-  for (uint32_t w = 0; w < T / 64; ++w) {
+  for (uint32_t w = 0; w < kPlanThreads / 64; ++w) {
     if (w < wave) wbase += s_wave[w];
     total += s_wave[w];
   }
@@ -2441,12 +2434,7 @@ int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask
     a.list_wgs = static_cast<uint32_t>(wgs < 512 ? wgs : 512);
   }
   const size_t lds = rows <= kPlanLdsRows ? rows * sizeof(uint64_t) : 0;
-  if (plan_threads() == 256 && num_zero_counters <= 256) {
-    if (a.list_wgs) a.list_wgs = a.list_wgs * (kPlanThreads / 256) > 512 ? 512 : a.list_wgs * (kPlanThreads / 256);
-    k_round_plan<256><<<count + 1 + chain_wgs + a.list_wgs, 256, lds, S(stream)>>>(a);
-  } else {
-    k_round_plan<kPlanThreads><<<count + 1 + chain_wgs + a.list_wgs, kPlanThreads, lds, S(stream)>>>(a);
-  }
+  k_round_plan<<<count + 1 + chain_wgs + a.list_wgs, kPlanThreads, lds, S(stream)>>>(a);
   return launch_status("k_round_plan");
 }
 
