@@ -756,8 +756,6 @@ struct omr_ar_plan {
   // Each rank's all-gathered array is then its masks followed by its position table: mstride words per rank.
   bool fused_pack = false;
   bool sum_list = false;            // the shard sum's pairs built by the plan launch (fused pack, N > 1, an aggregator)
-  bool chain_split = false;         // OMR_CHAIN_SPLIT=1 (study knob): the union chain as a launch of its own (k_next,
-                                    // 256-thread workgroups that fit beside a scan workgroup) instead of in the plan's
   uint64_t list_units = 0;
   uint32_t list_cap = 0;
   uint64_t mstride = 0;           // uint64 words per rank in masks_all (rows without the fused pack)
@@ -1107,10 +1105,6 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   };
   // the round's events order work between streams of this device only: no system-scope fence (a record costs
   // its stream 1.2 us instead of 2.8, tools/event_cost.hip); what the host reads goes out as system-scope stores
-  {
-    const char* ce = getenv("OMR_CHAIN_SPLIT");
-    p->chain_split = ce != nullptr && atoi(ce) != 0;
-  }
   const char* sf = getenv("OMR_EVENT_SYSFENCE");
   const unsigned evflags = hipEventDisableTiming | ((sf != nullptr && atoi(sf) != 0) ? 0u : hipEventDisableSystemFence);
   for (auto& st : p->set) {
@@ -1481,10 +1475,8 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
                                     p->bounds_dev, NS, S.wset, S.umask, S.prefix,
                                     p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, S.pack_cnt,
                                     S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->arrive, p->flag_map + si, seq,
-                                    p->chain_split ? nullptr : j.un, p->B, p->sum_list ? &sl : nullptr, qstream),
+                                    j.un, p->B, p->sum_list ? &sl : nullptr, qstream),
                 "omr_round_plan_list"));
-  if (p->chain_split)  // the aggregator chain in 256-thread workgroups of its own launch, over the plan's union
-    TRY(omr_check(omr_next_offsets(S.umask, 1, p->n, p->B, p->lanes, p->parts, j.un, qstream), "omr_next_offsets"));
   ht.lap("1:plan");
   // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407): addressed by
   //     device-side data only, so it is queued before the host learns the counts and runs while it waits.  (Every
