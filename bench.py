@@ -39,9 +39,12 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-leve
 XGMI_LINK_GBPS = 153.0  # one of a GPU's 7 point-to-point xGMI links (the task's hardware notes; not in the guide)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs of this node, one rank each (default 1).  N > 1 without a launcher: bench.py starts "
+                        "torch.distributed.run with N ranks as a child process and relays rank 0's line; it exits "
+                        "non-zero when the node has fewer than N GPUs")
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--size-mib", type=int, default=256)
@@ -89,7 +92,59 @@ def parse():
                    help="N>1 round transport: RCCL over xGMI, one process per GPU (the product path), or HIP IPC "
                         "between processes that may share a GPU (a rehearsal of the N>1 path on one GPU; the "
                         "torch.distributed group is then gloo and only carries the id, barriers and timings)")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+def launch_plan(args, env, device_count: int):
+    """How this invocation runs ("how N>1 lines are launched"), decided before any GPU call:
+    ("run", n_gpus)     this process is the measurement (N=1, or one rank of a launched job); n_gpus is the number of
+                        GPUs whose ranks ran, the figure the line reports;
+    ("spawn", argv)     --gpus N > 1 without a launcher: start torch.distributed.run with N ranks as a child;
+    ("error", message)  refused: never report an N-GPU figure that N GPUs did not produce.
+    `value` is always the bytes all ranks processed over the max-over-ranks time, never N x one GPU's rate."""
+    launched = "WORLD_SIZE" in env
+    ws = int(env.get("WORLD_SIZE", "1"))
+    ipc = args.dist_transport == "ipc"
+    if not launched:
+        n = 1 if args.gpus is None else args.gpus
+        if n < 1:
+            return "error", f"--gpus {n}: at least one GPU"
+        if n == 1:
+            return "run", 1
+        if not args.host_resident and args.workers != 1:
+            return "error", "--workers > 1 is the single-GPU m-worker sum (N=1 only)"
+        if device_count < n:
+            return "error", (f"--gpus {n} but this node has {device_count} GPU(s): an N-GPU line needs N GPUs, one "
+                             f"rank each (nothing was measured)")
+        return "spawn", ["--nnodes=1", "--nproc-per-node", str(n), "--master-addr", "127.0.0.1"]
+    if args.gpus is not None and args.gpus != ws:
+        return "error", f"--gpus {args.gpus} but the launcher started {ws} rank(s)"
+    if ipc:  # ranks share the node's GPUs (a rehearsal): the line counts the GPUs, not the ranks
+        return "run", max(1, min(ws, device_count))
+    if ws > device_count and device_count > 0:
+        return "error", f"{ws} RCCL ranks on {device_count} GPU(s): RCCL runs one rank per GPU"
+    return "run", ws
+
+
+def spawn_ranks(torchrun_args, argv) -> int:
+    """Run this bench as `torchrun_args` ranks under torch.distributed.run, a child process started before this one
+    has made any GPU call (never exec'd over it); rank 0's JSON line is relayed on stdout, everything else on
+    stderr.  Returns the child's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:  # a free rendezvous port on the loopback address
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run"] + torchrun_args + ["--master-port", str(port),
+                                                                              os.path.abspath(__file__)] + list(argv)
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                           "MASTER_PORT")}
+    print(f"bench.py: launching {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+        (sys.stdout if line.startswith("{") else sys.stderr).flush()
+    return p.wait()
 
 
 def workload_string(args, m: int) -> str:
@@ -359,7 +414,7 @@ def host_resident(args, ws, rank, local):
     eng.close()
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        n_gpus = max(ws, 1)
+        n_gpus = max(ws, 1)  # RCCL: one rank per GPU (launch_plan)
         value = n_gpus * total.nbytes / (ms * 1e-3) / 1e9
         nz = float(bm.mean())
         print(json.dumps({
@@ -388,15 +443,23 @@ def host_resident(args, ws, rank, local):
 
 def main():
     args = parse()
+    if args.print_workload:
+        print(workload_string(args, args.workers if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 1))
+        return
+    # (torch.cuda.device_count() does not initialise the GPU on this image: a child may still be started after it)
+    how, what = launch_plan(args, os.environ, torch.cuda.device_count())
+    if how == "error":
+        print(f"bench.py: {what}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if how == "spawn":
+        sys.exit(spawn_ranks(what, sys.argv[1:]))
+    n_gpus = what
     ws, rank, local = dist_env()
+    ranks = ws  # ranks that run the step (each processes its own tensor); n_gpus = the GPUs they ran on
     if args.host_resident:
         host_resident(args, ws, rank, local)
         return
     dist_mode = ws > 1 or args.force_dist
-    if args.print_workload:
-        print(workload_string(args, args.workers if ws == 1 else 1))
-        return
-    n_gpus = ws if ws > 1 else args.gpus
     ipc = dist_mode and args.dist_transport == "ipc"
     if ipc:  # ranks may share GPUs: rank r on GPU r mod count; gloo for the id broadcast, barriers and timings
         local = local % max(1, torch.cuda.device_count())
@@ -540,7 +603,7 @@ def main():
         kernel_name = ("k_scan1f (round worker scan: flags + next + row masks + the fused pack of the other shards' "
                        "blocks)" if engine_fused else
                        "k_scan1f (one-rank round's worker scan: flags + next + row masks + the shard sums)"
-                       if n_gpus == 1 and args.dist_mode != "dense" else
+                       if ranks == 1 and args.dist_mode != "dense" else
                        "k_scan1f (round worker scan: flags + next + row masks, no out)")
     scan_ms_dist = None
     if dist_mode:
@@ -571,17 +634,17 @@ def main():
         kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
     if True:
         if dist_mode:
-            if n_gpus == 1 and args.dist_mode != "dense":  # one rank: the scan writes the shard sums itself
+            if ranks == 1 and args.dist_mode != "dense":  # one rank: the scan writes the shard sums itself
                 kbytes = fused_bytes(L, bitmaps[0]) + L.rows * 8
             else:
-                kbytes = (scan_pack_bytes(L, bitmaps[0], rank, n_gpus) if engine_fused else scan_only_bytes(L))
+                kbytes = (scan_pack_bytes(L, bitmaps[0], rank, ranks) if engine_fused else scan_only_bytes(L))
         elif m == 1 and args.kernel == "fused":
             kbytes = fused_bytes(L, bitmaps[0])
         else:
             kbytes = algorithmic_scan_bytes(L, bitmaps, m)
         achieved = kbytes / (kms * 1e-3) / 1e9
-        if dist_mode and n_gpus > 1 and engine_fused and args.dist_mode != "dense":
-            traffic, pmc_src = read_pmc_round(n_gpus, L)
+        if dist_mode and ranks > 1 and engine_fused and args.dist_mode != "dense":
+            traffic, pmc_src = read_pmc_round(ranks, L)
         else:
             traffic, pmc_src = read_pmc(args.pmc, workload, dist_mode)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -618,7 +681,7 @@ def main():
     transport_note = ("RCCL" if not ipc else
                       f"HIP IPC, {ws} ranks on {torch.cuda.device_count()} GPU(s): a rehearsal of the N>1 path, not a "
                       f"scaling figure")
-    total_bytes = n_gpus * m * L.nbytes
+    total_bytes = ranks * m * L.nbytes  # what every rank processed, over the max-over-ranks time
     value = total_bytes / (ms_per_step * 1e-3) / 1e9
     metric = "GB/s device-resident block scan+sum, 256 MiB fp32 @ 90% block-sparse"   # BASELINE.json
     nz = float(np.mean([bm.mean() for bm in bitmaps]))
@@ -631,6 +694,7 @@ def main():
         "value": round(value, 2),
         "unit": "GB/s",
         "n_gpus": n_gpus,
+        "ranks": ranks,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 5),
@@ -644,7 +708,7 @@ def main():
                    "nonzero_fraction": round(nz, 5),
                    "workers_per_gpu": m, "rotating_buffer_sets": len(sets),
                    "parallelism": "single GPU" if not dist_mode else
-                   f"dp{n_gpus} {dict(allreduce='sparse all-reduce', reduce='sparse reduce-scatter', dense='dense reduce-scatter (stand-in)')[args.dist_mode]} over "
+                   f"dp{ranks} {dict(allreduce='sparse all-reduce', reduce='sparse reduce-scatter', dense='dense reduce-scatter (stand-in)')[args.dist_mode]} over "
                    f"{transport_note} (C++ round driver, libomr_dist.so{pipe_note})"},
         "alg_bw_GiBps_reference_style": round(total_bytes / (ms_per_step * 1e-3) / 2 ** 30, 2),
         "roofline": roofline,
