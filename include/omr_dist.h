@@ -30,6 +30,11 @@ extern "C" {
 #endif
 
 #define OMR_UNIQUE_ID_BYTES 128
+/* Returned once a transport has been aborted (by an error, a deadline or omr_dist_abort), and by a plan whose
+ * earlier round failed. */
+#define OMR_EABORTED (-2)
+/* A host-side wait of the transport or of a round passed the transport's deadline (omr_dist_set_timeout). */
+#define OMR_ETIMEDOUT (-3)
 
 typedef struct omr_dist omr_dist;               /* a transport endpoint (one rank) */
 typedef struct omr_local_board omr_local_board; /* shared state of an in-process group */
@@ -70,11 +75,34 @@ int omr_dist_destroy(omr_dist* d);
 int omr_dist_allgather(omr_dist* d, const void* in, void* out, size_t bytes, omr_stream_t stream);
 int omr_dist_exchange(omr_dist* d, void* const* send, const size_t* send_bytes, void* const* recv,
                       const size_t* recv_bytes, omr_stream_t stream);
-/* Test hook: the next exchange on `d` (omr_dist_exchange or a round's) fails with OMR_EINVAL once it has issued
- * `after_pieces` non-empty pieces (0: before the first; a negative value disarms).  The transport stays usable: the
- * RCCL group is closed (the pieces already issued still run), the loopback and IPC transports still meet their
- * peers.  Used to test that a failed exchange leaves no RCCL group open. */
+/* Failure containment (the reference exits on a failed post, common.cc:450-451; a rank of a collective group must
+ * make sure its peers do not wait for it forever).
+ *   - Every host-side wait of a transport or of a round (a loopback barrier, an IPC rendezvous, a round's wait for
+ *     its block counts, omr_ar_plan_wait) ends after the transport's deadline: omr_dist_set_timeout (default 60 s, or
+ *     the environment's OMR_DIST_TIMEOUT_MS), with OMR_ETIMEDOUT.  The count wait also polls the group's failure
+ *     signals: RCCL's asynchronous errors (ncclCommGetAsyncError), a loopback or IPC peer's abort.
+ *   - Any error of a transport operation, an expired deadline, a failure signal, or omr_dist_abort ABORTS the
+ *     transport: RCCL's two communicators are aborted (ncclCommAbort cancels the operations queued on them, so this
+ *     rank's streams drain; peers' matching operations end at their own deadlines), the loopback and IPC groups
+ *     raise a flag that ends their peers' waits on this rank at once.  Every later operation fails with
+ *     OMR_EABORTED; the transport can only be destroyed (a recovery makes a new group).
+ *   - A round that fails after it has started (any error in omr_sparse_round_f32 past its argument checks, in
+ *     omr_sparse_buckets_f32, in join or wait) also marks its plan failed: later calls on the plan return
+ *     OMR_EABORTED; omr_ar_plan_destroy still releases it without waiting on peers.
+ * omr_dist_abort may be called from another thread while this rank waits.  omr_dist_poll returns the group's
+ * failure signals (0 while healthy). */
+int omr_dist_abort(omr_dist* d);
+int omr_dist_aborted(const omr_dist* d); /* 1 once aborted */
+int omr_dist_set_timeout(omr_dist* d, int64_t timeout_ms);
+int omr_dist_poll(omr_dist* d);
+/* Test hooks.  omr_dist_inject_fault: the next exchange on `d` (omr_dist_exchange or a round's) fails with OMR_EINVAL
+ * once it has issued `after_pieces` non-empty pieces (0: before the first; a negative value disarms): the RCCL group
+ * is closed (the pieces already issued still run, so no group is left open to capture later calls) and the
+ * transport is then aborted as above, standing in for a rank that stops issuing its part of an exchange.
+ * omr_dist_inject_allgather_fault: the next all-gather fails before it moves anything (a round failing in its first
+ * half). */
 int omr_dist_inject_fault(omr_dist* d, int64_t after_pieces);
+int omr_dist_inject_allgather_fault(omr_dist* d);
 
 /* Workspaces for tensors of n floats on the layout (block_size, num_lanes, num_parts); allocated on the current
  * HIP device, which must be the device the rank's tensors live on. */
@@ -194,6 +222,12 @@ int omr_ar_plan_stage_timings(omr_ar_plan* plan, float* stage_ms, uint64_t* byte
 int omr_ar_plan_fused_pack(const omr_ar_plan* plan);
 /* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
 int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
+/* Join, then wait on the host until `stream` has run every round issued so far: the bounded counterpart of a stream
+ * synchronise for a rank whose rounds wait on its peers.  Past the transport's deadline (or on a failure signal) the
+ * transport is aborted and OMR_ETIMEDOUT / the error is returned, instead of blocking on a peer that is gone. */
+int omr_ar_plan_wait(omr_ar_plan* plan, omr_stream_t stream);
+/* The plan's first failure (0: none); see failure containment above. */
+int omr_ar_plan_failed(omr_ar_plan* plan);
 
 /* ---------------------------------------------------------------- the round as wire messages between processes
  *

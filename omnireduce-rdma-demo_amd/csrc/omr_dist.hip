@@ -71,6 +71,12 @@ using Slices = std::vector<Slice>;  // several pieces to or from one peer, match
 
 // ---------------------------------------------------------------- transports
 
+int64_t default_timeout_ms() {
+  const char* e = getenv("OMR_DIST_TIMEOUT_MS");
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 ? v : 60000;
+}
+
 struct omr_dist {
   int rank = 0, world = 1;
   // omr_dist_inject_fault (test hook): the next exchange fails once it has issued `fault_after` non-empty pieces
@@ -82,14 +88,63 @@ struct omr_dist {
     fault_after = -1;
     return derr(OMR_EINVAL, "exchange: fault injected after %lld pieces (omr_dist_inject_fault)", static_cast<long long>(k));
   }
+  // Failure containment (the reference exits on a failed post, common.cc:450-451; a rank of a collective group must
+  // instead make sure its peers do not wait for it forever).  Every host-side wait of a transport or a round is bounded
+  // by this deadline; any error of an operation, an expired deadline or omr_dist_abort aborts the transport: RCCL's
+  // communicators are aborted (ncclCommAbort cancels the operations queued on them), the loopback and IPC groups
+  // raise a flag their peers' waits watch, and every later operation fails at once with OMR_EABORTED.
+  int64_t timeout_ms = default_timeout_ms();
+  std::atomic<bool> aborted{false};
+  std::atomic<bool> abort_started{false};
+  char abort_why[256] = {};
+  // abort the transport (once) and return rc; the caller's message (g_derr) is kept
+  int abort_with(int rc, const char* why) {
+    if (!abort_started.exchange(true)) {
+      snprintf(abort_why, sizeof(abort_why), "%s", why);
+      aborted.store(true, std::memory_order_release);
+      abort_group();
+    }
+    return rc;
+  }
+  int contain(int rc) { return rc == 0 ? 0 : abort_with(rc, g_derr); }
+  int check_open(const char* what) const {
+    if (!aborted.load(std::memory_order_acquire)) return 0;
+    return derr(OMR_EABORTED, "%s: rank %d's transport was aborted (%s)", what, rank, abort_why);
+  }
+  // the transport's group-wide failure signals: RCCL's asynchronous errors, a loopback or IPC peer's abort; an error
+  // aborts this rank's transport too
+  int poll() {
+    TRY(check_open("poll"));
+    return contain(do_poll());
+  }
+  // the operations the round uses (every rank of the group calls them in the same order); an error aborts
+  bool fault_allgather = false;  // omr_dist_inject_allgather_fault (test hook)
+  int allgather(const void* in, void* out, size_t bytes, hipStream_t st) {
+    TRY(check_open("allgather"));
+    if (fault_allgather) {
+      fault_allgather = false;
+      return contain(derr(OMR_EINVAL, "allgather: fault injected (omr_dist_inject_allgather_fault)"));
+    }
+    return contain(do_allgather(in, out, bytes, st));
+  }
+  int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) {
+    TRY(check_open("exchange"));
+    return contain(do_exchange(sends, recvs, st));
+  }
+  int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) {
+    TRY(check_open("reduce_scatter"));
+    return contain(do_reduce_scatter(in, out, count, st));
+  }
   virtual ~omr_dist() = default;
+  virtual void abort_group() {}
+  virtual int do_poll() { return 0; }
   // out[p*bytes .. (p+1)*bytes) = rank p's `in`; `in` may alias out + rank*bytes
-  virtual int allgather(const void* in, void* out, size_t bytes, hipStream_t st) = 0;
+  virtual int do_allgather(const void* in, void* out, size_t bytes, hipStream_t st) = 0;
   // sends[p] to peer p, recvs[p] from peer p, p != rank: the k-th non-empty send piece to a peer pairs with that
   // peer's k-th non-empty receive piece from this rank (equal sizes); every rank calls it, possibly with nothing
-  virtual int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) = 0;
+  virtual int do_exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) = 0;
   // out[0 .. count) = sum over ranks p of in_p[rank*count .. (rank+1)*count)  (dense stand-in)
-  virtual int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) = 0;
+  virtual int do_reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) = 0;
   // Device memory of the plans that run on this transport goes through it: a transport that exports buffers to
   // other processes (HIP IPC) keeps every exported allocation alive until it is destroyed itself and hands it back
   // to the next alloc of the same size, so an address a peer has mapped is never freed and re-allocated under it.
@@ -109,14 +164,31 @@ struct RcclDist final : omr_dist {
     if (xcomm) (void)ncclCommDestroy(xcomm);
     if (comm) (void)ncclCommDestroy(comm);
   }
-  int allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
+  // ncclCommAbort on both communicators (the split one first): the operations queued on them are cancelled on the
+  // device, so this rank's streams drain; the peers' matching operations are left to their own deadlines
+  void abort_group() override {
+    if (xcomm) (void)ncclCommAbort(xcomm);
+    if (comm) (void)ncclCommAbort(comm);
+    xcomm = comm = nullptr;
+  }
+  int do_poll() override {
+    for (ncclComm_t c : {comm, xcomm}) {
+      if (c == nullptr) continue;
+      ncclResult_t a = ncclSuccess;
+      TRY(nccl_check(ncclCommGetAsyncError(c, &a), "ncclCommGetAsyncError"));
+      if (a != ncclSuccess && a != ncclInProgress) return nccl_check(a, "RCCL asynchronous error");
+    }
+    return 0;
+  }
+  int do_allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
     return nccl_check(ncclAllGather(in, out, bytes, ncclUint8, comm, st), "ncclAllGather");
   }
-  int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
+  int do_exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
     TRY(nccl_check(ncclGroupStart(), "ncclGroupStart"));
     // The group is closed on every path: a group left open would capture every later RCCL call of this thread (the
     // next round's all-gather and exchange would be queued into it and never launched).  After a failed piece the
-    // pieces already issued still go out with the group; the first error is returned.
+    // pieces already issued still go out with the group, the first error is returned, and the caller (omr_dist::
+    // exchange) then aborts both communicators: the peers' pieces that this rank never posted can no longer match.
     int rc = 0;
     int64_t k = 0;
     for (int p = 0; p < world && rc == 0; ++p) {
@@ -132,7 +204,7 @@ struct RcclDist final : omr_dist {
     const int rc_end = nccl_check(ncclGroupEnd(), "ncclGroupEnd");
     return rc ? rc : rc_end;
   }
-  int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
+  int do_reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
     return nccl_check(ncclReduceScatter(in, out, count, ncclFloat32, ncclSum, xcomm, st), "ncclReduceScatter");
   }
 };
@@ -147,17 +219,43 @@ struct omr_local_board {
   uint64_t generation = 0;
   std::vector<const void*> posted;                // allgather inputs
   std::vector<std::vector<Slices>> posted_sends;  // [rank][peer]
+  bool aborted = false;  // a rank aborted its transport: every wait of the group ends with an error
+  int aborted_by = -1;
   explicit omr_local_board(int w) : world(w), posted(w), posted_sends(w, std::vector<Slices>(w)) {}
-  void barrier() {
+  // every rank's arrival, within the deadline; a rank that waits past it aborts the group (its peers then fail at
+  // once instead of each waiting out its own deadline)
+  int barrier(int rank, int64_t timeout_ms) {
     std::unique_lock<std::mutex> lk(mu);
+    if (aborted) return derr(OMR_EABORTED, "loopback: rank %d aborted the group", aborted_by);
     const uint64_t gen = generation;
     if (++arrived == world) {
       arrived = 0;
       ++generation;
       cv.notify_all();
-    } else {
-      cv.wait(lk, [&] { return generation != gen; });
+      return 0;
     }
+    const bool done = cv.wait_for(lk, std::chrono::milliseconds(timeout_ms),
+                                  [&] { return generation != gen || aborted; });
+    if (generation != gen) return 0;
+    if (aborted) return derr(OMR_EABORTED, "loopback: rank %d aborted the group", aborted_by);
+    (void)done;
+    abort_locked(rank);
+    return derr(OMR_ETIMEDOUT, "loopback: rank %d waited %lld ms for its peers at a barrier", rank,
+                static_cast<long long>(timeout_ms));
+  }
+  void abort_locked(int rank) {
+    if (!aborted) aborted_by = rank;
+    aborted = true;
+    cv.notify_all();
+  }
+  void abort(int rank) {
+    std::lock_guard<std::mutex> g(mu);
+    abort_locked(rank);
+  }
+  bool is_aborted(int* by) {
+    std::lock_guard<std::mutex> g(mu);
+    *by = aborted_by;
+    return aborted;
   }
 };
 
@@ -169,10 +267,18 @@ namespace {
 // and a peer must not touch its buffers again until every reader is through.
 struct LocalDist final : omr_dist {
   omr_local_board* b = nullptr;
-  int allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
+  // (an error return makes omr_dist abort the group: the peers' barriers then end at once, with an error)
+  void abort_group() override { b->abort(rank); }
+  int do_poll() override {
+    int by = -1;
+    if (b->is_aborted(&by)) return derr(OMR_EABORTED, "loopback: rank %d aborted the group", by);
+    return 0;
+  }
+  int barrier() { return b->barrier(rank, timeout_ms); }
+  int do_allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
     TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
     b->posted[rank] = in;
-    b->barrier();
+    TRY(barrier());
     int rc = 0;
     for (int p = 0; p < world && rc == 0; ++p) {
       char* dst = static_cast<char*>(out) + static_cast<size_t>(p) * bytes;
@@ -180,13 +286,14 @@ struct LocalDist final : omr_dist {
         rc = hip_check(hipMemcpyAsync(dst, b->posted[p], bytes, hipMemcpyDefault, st), "hipMemcpyAsync");
     }
     if (rc == 0) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
-    b->barrier();
-    return rc;
+    else (void)hipStreamSynchronize(st);  // copies already queued finish before the peers move on
+    TRY(rc);
+    return barrier();
   }
-  int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
+  int do_exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
     TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
     b->posted_sends[rank] = sends;
-    b->barrier();
+    TRY(barrier());
     int rc = 0;
     int64_t pieces = 0;
     for (int p = 0; p < world && rc == 0; ++p) {
@@ -210,21 +317,23 @@ struct LocalDist final : omr_dist {
     if (rc == 0) rc = fault(pieces);
     if (rc == 0) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
     else (void)hipStreamSynchronize(st);  // copies already queued finish before the peers move on
-    b->barrier();  // every rank leaves together, even on an error (no peer is left waiting)
-    return rc;
+    // on an error the group is aborted by the caller instead of met here: the peers' closing barrier ends at once
+    TRY(rc);
+    return barrier();
   }
-  int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
+  int do_reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
     // every rank's input is addressable here (threads of one process): sum the shard in rank order
     TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
     b->posted[rank] = in;
-    b->barrier();
+    TRY(barrier());
     std::vector<const float*> ptrs(world);
     for (int p = 0; p < world; ++p) ptrs[p] = static_cast<const float*>(b->posted[p]) + static_cast<size_t>(rank) * count;
-    TRY(omr_check(omr_dense_sum_f32(ptrs.data(), static_cast<uint32_t>(world), count, out,
-                                    reinterpret_cast<omr_stream_t>(st)), "omr_dense_sum_f32"));
-    TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));  // peers' inputs read before anyone moves on
-    b->barrier();
-    return 0;
+    int rc = omr_check(omr_dense_sum_f32(ptrs.data(), static_cast<uint32_t>(world), count, out,
+                                         reinterpret_cast<omr_stream_t>(st)), "omr_dense_sum_f32");
+    if (rc == 0) rc = hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");  // peers' inputs read first
+    else (void)hipStreamSynchronize(st);
+    TRY(rc);
+    return barrier();
   }
 };
 
@@ -266,6 +375,7 @@ struct IpcPost {
 struct IpcRank {
   std::atomic<uint64_t> posted[kIpcChans], done[kIpcChans];
   std::atomic<uint32_t> joined, left;
+  std::atomic<uint32_t> aborted;  // this rank aborted its transport (its peers' waits end with an error)
   std::atomic<uint64_t> evgen[kIpcChans][2];  // 1 + the generation whose handles slot [c][g % 2] holds (0: none)
   hipIpcEventHandle_t ready[kIpcChans][2][kIpcRing], rdone[kIpcChans][2][kIpcRing];
 };
@@ -284,15 +394,20 @@ std::string ipc_board_name(const void* id) {
   return buf;
 }
 
-// bounded spin on a host condition (peers are other processes: yield the core)
+// bounded spin on a host condition (peers are other processes: yield the core); ends early with an error when any
+// rank of the board has aborted its transport
 template <typename F>
-int ipc_spin(F ready, const char* what, int rank) {
+int ipc_spin(F ready, const char* what, int rank, int64_t timeout_ms, const IpcBoard* b = nullptr, int world = 0) {
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t i = 0;; ++i) {
     if (ready()) return 0;
     if ((i & 1023) == 1023) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
-        return derr(OMR_EINVAL, "ipc transport: rank %d waited 120 s for %s", rank, what);
+      for (int p = 0; b != nullptr && p < world; ++p)
+        if (b->rank[p].aborted.load(std::memory_order_acquire) != 0)
+          return derr(OMR_EABORTED, "ipc transport: rank %d aborted the group (rank %d waiting for %s)", p, rank, what);
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
+        return derr(OMR_ETIMEDOUT, "ipc transport: rank %d waited %lld ms for %s", rank,
+                    static_cast<long long>(timeout_ms), what);
       sched_yield();
     }
   }
@@ -326,6 +441,19 @@ struct IpcDist final : omr_dist {
   std::map<void*, size_t> sized;                           // live allocations made through alloc(): their sizes
   std::multimap<size_t, void*> parked;                     // released exported allocations, by size
 
+  template <typename F>
+  int spin(F ready, const char* what) { return ipc_spin(ready, what, rank, timeout_ms, b, world); }
+  // (an error return makes omr_dist abort: the flag ends the peers' waits on this rank at once)
+  void abort_group() override {
+    if (b != nullptr) b->rank[rank].aborted.store(1, std::memory_order_release);
+  }
+  int do_poll() override {
+    for (int p = 0; b != nullptr && p < world; ++p)
+      if (b->rank[p].aborted.load(std::memory_order_acquire) != 0)
+        return derr(OMR_EABORTED, "ipc transport: rank %d aborted the group", p);
+    return 0;
+  }
+
   static void release(IpcEvents& e, std::vector<hipEvent_t>& to) {
     for (int k = 0; k < kIpcRing; ++k) {
       if (e.ready[k]) to.push_back(e.ready[k]);
@@ -340,8 +468,12 @@ struct IpcDist final : omr_dist {
       // closes a mapping or an event
       (void)hipDeviceSynchronize();
       b->rank[rank].left.store(1, std::memory_order_release);
+      // (an aborted group does not wait: a peer may never leave; the driver keeps an exported allocation's memory
+      // alive while a peer still maps it)
       for (int p = 0; p < world; ++p)
-        (void)ipc_spin([&] { return b->rank[p].left.load(std::memory_order_acquire) != 0; }, "peers to leave", rank);
+        if (ipc_spin([&] { return b->rank[p].left.load(std::memory_order_acquire) != 0; }, "peers to leave", rank,
+                     timeout_ms, b, world) != 0)
+          break;
       for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second.base);
     }
     // every peer has left (closed its mappings of them): the parked allocations can go now
@@ -359,6 +491,14 @@ struct IpcDist final : omr_dist {
   }
 
   int attach(const void* id) {
+    // (the ranks meet here after starting up, which takes a process importing its runtime a minute or more on a cold
+    // machine: the rendezvous waits at least two minutes, the transport's own deadline applies afterwards)
+    struct Rendezvous {
+      int64_t& t;
+      int64_t keep;
+      ~Rendezvous() { t = keep; }
+    } rendezvous{timeout_ms, timeout_ms};
+    timeout_ms = std::max<int64_t>(timeout_ms, 120000);
     name = ipc_board_name(id);
     const size_t bytes = sizeof(IpcBoard);
     int fd = -1;
@@ -374,7 +514,7 @@ struct IpcDist final : omr_dist {
             if (fd < 0) fd = shm_open(name.c_str(), O_RDWR, 0600);
             struct stat stt;
             return fd >= 0 && fstat(fd, &stt) == 0 && static_cast<size_t>(stt.st_size) == bytes;
-          }, "the board", rank));
+          }, "the board", rank, timeout_ms));
     }
     void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);
@@ -384,7 +524,8 @@ struct IpcDist final : omr_dist {
       b->world = static_cast<uint32_t>(world);  // the rest is zero (a fresh shm object)
       b->magic.store(kIpcMagic, std::memory_order_release);
     }
-    TRY(ipc_spin([&] { return b->magic.load(std::memory_order_acquire) == kIpcMagic; }, "the board's owner", rank));
+    TRY(ipc_spin([&] { return b->magic.load(std::memory_order_acquire) == kIpcMagic; }, "the board's owner", rank,
+                 timeout_ms));
     if (b->world != static_cast<uint32_t>(world))
       return derr(OMR_EINVAL, "ipc transport: board world %u, this rank says %d", b->world, world);
     b->attached.fetch_add(1);
@@ -396,12 +537,12 @@ struct IpcDist final : omr_dist {
     me.joined.store(1, std::memory_order_release);
     if (rank == 0) {  // the name is only needed until every rank has mapped the board
       for (int p = 0; p < world; ++p)
-        TRY(ipc_spin([&] { return b->rank[p].joined.load(std::memory_order_acquire) != 0; }, "peers to join", rank));
+        TRY(spin([&] { return b->rank[p].joined.load(std::memory_order_acquire) != 0; }, "peers to join"));
       shm_unlink(name.c_str());
     }
     peer.assign(world, {});
     for (int p = 0; p < world; ++p)
-      TRY(ipc_spin([&] { return b->rank[p].joined.load(std::memory_order_acquire) != 0; }, "peers to join", rank));
+      TRY(spin([&] { return b->rank[p].joined.load(std::memory_order_acquire) != 0; }, "peers to join"));
     for (int c = 0; c < kIpcChans; ++c) TRY(open_gen(c, 0));
     return 0;
   }
@@ -430,8 +571,7 @@ struct IpcDist final : omr_dist {
     for (int p = 0; p < world; ++p) {
       if (p == rank) continue;
       const IpcRank& pr = b->rank[p];
-      TRY(ipc_spin([&] { return pr.evgen[c][g % 2].load(std::memory_order_acquire) == g + 1; },
-                   "a peer's events", rank));
+      TRY(spin([&] { return pr.evgen[c][g % 2].load(std::memory_order_acquire) == g + 1; }, "a peer's events"));
       IpcEvents& e = peer[p][c * 2 + g % 2];
       release(e, retired);
       for (int k = 0; k < kIpcRing; ++k) {
@@ -554,8 +694,7 @@ struct IpcDist final : omr_dist {
     TRY(hip_check(hipEventRecord(mine_of(c, s).ready[k], st), "hipEventRecord"));
     b->rank[rank].posted[c].store(s, std::memory_order_release);
     for (int p = 0; p < world; ++p)
-      TRY(ipc_spin([&] { return b->rank[p].posted[c].load(std::memory_order_acquire) >= s; }, "a peer's post",
-                   rank));
+      TRY(spin([&] { return b->rank[p].posted[c].load(std::memory_order_acquire) >= s; }, "a peer's post"));
     *s_out = s;
     return 0;
   }
@@ -570,15 +709,14 @@ struct IpcDist final : omr_dist {
     b->rank[rank].done[c].store(s, std::memory_order_release);
     for (int p = 0; p < world; ++p) {
       if (p == rank) continue;
-      TRY(ipc_spin([&] { return b->rank[p].done[c].load(std::memory_order_acquire) >= s; }, "a peer's copies",
-                   rank));
+      TRY(spin([&] { return b->rank[p].done[c].load(std::memory_order_acquire) >= s; }, "a peer's copies"));
       TRY(hip_check(hipStreamWaitEvent(st, peer_of(c, s, p).rdone[k], 0), "hipStreamWaitEvent"));
     }
     return 0;
   }
   const IpcPost& post_of(int c, uint64_t s, int p) const { return b->post[c][s % kIpcRing][p]; }
 
-  int allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
+  int do_allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
     uint64_t s = 0;
     TRY(begin(0, st, {{kIpcAll, Slice{const_cast<void*>(in), bytes}}}, &s));
     int rc = 0;
@@ -599,11 +737,12 @@ struct IpcDist final : omr_dist {
       if (rc == 0) rc = wait_ready(0, s, p, st);
       if (rc == 0) rc = hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
     }
-    const int rc2 = end(0, s, st);  // always: peers wait for it
-    return rc ? rc : rc2;
+    // (on an error this rank aborts instead of ending the operation: the peers' waits for it end at once)
+    TRY(rc);
+    return end(0, s, st);
   }
 
-  int exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
+  int do_exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
     std::vector<std::pair<uint32_t, Slice>> items;
     for (int p = 0; p < world; ++p)
       if (p != rank)
@@ -638,11 +777,11 @@ struct IpcDist final : omr_dist {
       }
     }
     if (rc == 0) rc = fault(pieces);
-    const int rc2 = end(1, s, st);  // always: peers wait for it
-    return rc ? rc : rc2;
+    TRY(rc);  // (aborted by the caller: see allgather)
+    return end(1, s, st);
   }
 
-  int reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
+  int do_reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
     uint64_t s = 0;
     TRY(begin(1, st, {{kIpcAll, Slice{const_cast<float*>(in), count * world * sizeof(float)}}}, &s));
     std::vector<const float*> ptrs(world);
@@ -666,27 +805,50 @@ struct IpcDist final : omr_dist {
     if (rc == 0)
       rc = omr_check(omr_dense_sum_f32(ptrs.data(), static_cast<uint32_t>(world), count, out,
                                        reinterpret_cast<omr_stream_t>(st)), "omr_dense_sum_f32");
-    const int rc2 = end(1, s, st);
-    return rc ? rc : rc2;
+    TRY(rc);
+    return end(1, s, st);
   }
 };
 
 // Spin until the plan kernel's completion notice (the round's sequence number) lands in pinned memory: the host
 // learns the block counts about a microsecond after the kernel ends, without an event or a stream sync.  Bails
-// out if the stream drains without the notice (a failed launch) or after a minute (a stuck peer).
-int wait_flag(const uint32_t* flag, uint32_t seq, hipStream_t st) {
+// out if the stream drains without the notice (a failed launch), on the transport's group-wide failure signals
+// (RCCL's asynchronous errors, a peer's abort) and after the transport's deadline (a stuck or dead peer: the mask
+// all-gather before the plan never completes); the transport is then aborted, so no peer waits on this rank.
+int wait_flag(omr_dist* d, const uint32_t* flag, uint32_t seq, hipStream_t st) {
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t spin = 1;; ++spin) {
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return 0;
     if ((spin & 4095) == 0) {
       const hipError_t q = hipStreamQuery(st);
-      if (q != hipSuccess && q != hipErrorNotReady) return hip_check(q, "round plan");
+      if (q != hipSuccess && q != hipErrorNotReady) return d->contain(hip_check(q, "round plan"));
       if (q == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq)
-        return derr(OMR_EINVAL, "round plan: stream idle but no completion notice (seq %u)", seq);
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
-        return derr(OMR_EINVAL, "round plan: no completion notice after 60 s (seq %u)", seq);
+        return d->contain(derr(OMR_EINVAL, "round plan: stream idle but no completion notice (seq %u)", seq));
+      TRY(d->poll());
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(d->timeout_ms))
+        return d->contain(derr(OMR_ETIMEDOUT, "round plan: rank %d had no completion notice after %lld ms (seq %u): "
+                                              "a peer is stuck or gone", d->rank,
+                               static_cast<long long>(d->timeout_ms), seq));
     }
     __builtin_ia32_pause();
+  }
+}
+
+// Wait on the host until `ev` has completed, within the transport's deadline and watching its failure signals (the
+// host-side counterpart of a device sync for a rank whose work may wait on its peers); aborts the transport on expiry.
+int wait_event_bounded(omr_dist* d, hipEvent_t ev, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 1;; ++spin) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return d->contain(hip_check(q, what));
+    if ((spin & 63) == 0) {
+      TRY(d->poll());
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(d->timeout_ms))
+        return d->contain(derr(OMR_ETIMEDOUT, "%s: rank %d's rounds did not complete within %lld ms: a peer is stuck or "
+                                              "gone", what, d->rank, static_cast<long long>(d->timeout_ms)));
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
 }
 
@@ -882,6 +1044,11 @@ struct omr_ar_plan {
   // buffer the rest of the round reads (a sum of 0.0f + x_w equals a sum of x_w bit for bit)
   const float* scan_from = nullptr;
   bool in_buckets = false;  // omr_sparse_buckets_f32 is issuing the rounds
+  // The first error of a round that had started (guarded by mu): the transport was aborted with it, and every later
+  // call on the plan fails at once (omr_ar_plan_destroy still releases everything).
+  int failed = 0;
+  std::string failed_why;
+  hipEvent_t wait_done = nullptr;  // omr_ar_plan_wait's event
 };
 
 namespace {
@@ -891,6 +1058,30 @@ int thread_drain(omr_ar_plan* p);
 void thread_stop(omr_ar_plan* p);
 thread_local bool t_progress = false;  // this thread is a plan's progress thread (OMR_ROUND_THREAD)
 HostTrace& ht_of(omr_ar_plan* p) { return t_progress ? p->ht_thread : p->ht; }
+
+// A round that had started failed: record it (first error wins) and abort the transport, so that no peer waits for
+// this rank's part of the round (the reference exits on a failed post, common.cc:450-451).  Returns rc.
+int plan_fail(omr_ar_plan* p, int rc) {
+  if (rc == 0) return 0;
+  const std::string why = g_derr;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    if (p->failed == 0) {
+      p->failed = rc;
+      p->failed_why = why;
+    }
+  }
+  (void)p->d->abort_with(rc, why.c_str());
+  snprintf(g_derr, sizeof(g_derr), "%s", why.c_str());  // (the caller's message, whatever abort_with did)
+  return rc;
+}
+
+// OMR_EABORTED if an earlier round of the plan failed
+int plan_check(omr_ar_plan* p, const char* what) {
+  std::lock_guard<std::mutex> g(p->mu);
+  if (p->failed == 0) return 0;
+  return derr(OMR_EABORTED, "%s: the plan failed in an earlier round (%s)", what, p->failed_why.c_str());
+}
 }  // namespace
 
 extern "C" {
@@ -974,9 +1165,34 @@ int omr_dist_destroy(omr_dist* d) {
   return 0;
 }
 
+int omr_dist_abort(omr_dist* d) {
+  if (d == nullptr) return derr(OMR_EINVAL, "dist_abort: NULL");
+  (void)d->abort_with(0, "omr_dist_abort");
+  return 0;
+}
+
+int omr_dist_aborted(const omr_dist* d) { return d != nullptr && d->aborted.load() ? 1 : 0; }
+
+int omr_dist_set_timeout(omr_dist* d, int64_t timeout_ms) {
+  if (d == nullptr || timeout_ms <= 0) return derr(OMR_EINVAL, "dist_set_timeout: NULL or a deadline <= 0");
+  d->timeout_ms = timeout_ms;
+  return 0;
+}
+
+int omr_dist_poll(omr_dist* d) {
+  if (d == nullptr) return derr(OMR_EINVAL, "dist_poll: NULL");
+  return d->poll();
+}
+
 int omr_dist_inject_fault(omr_dist* d, int64_t after_pieces) {
   if (d == nullptr) return derr(OMR_EINVAL, "inject_fault: NULL");
   d->fault_after = after_pieces < 0 ? -1 : after_pieces;
+  return 0;
+}
+
+int omr_dist_inject_allgather_fault(omr_dist* d) {
+  if (d == nullptr) return derr(OMR_EINVAL, "inject_allgather_fault: NULL");
+  d->fault_allgather = true;
   return 0;
 }
 
@@ -1007,9 +1223,11 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     fprintf(stderr, "[omr host trace rank %d] progress thread:\n", p->me);
     p->ht_thread.print(p->me);
   }
-  if (p->npend > 0)  // deferred rounds still owe their exchanges to the peers: issue them and let them drain
-    (void)flush_pending(p, p->cs, nullptr, nullptr);
-  (void)hipDeviceSynchronize();
+  // deferred rounds still owe their exchanges to the peers: issue them and let them drain (not after a failure: the
+  // transport is aborted, and their second halves would only fail)
+  if (p->npend > 0 && p->failed == 0 && !p->d->aborted.load()) (void)flush_pending(p, p->cs, nullptr, nullptr);
+  p->npend = 0;
+  (void)hipDeviceSynchronize();  // (an aborted RCCL communicator has cancelled its queued operations)
   // back to the transport, which keeps the exported ones alive for the next plan (omr_dist::alloc)
   void* devs[] = {p->bounds_dev, p->results, p->flags_ws, p->next_ws, p->unext_ws, p->scan_ws, p->arrive};
   for (void* v : devs) p->d->release(v);
@@ -1031,6 +1249,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p->s_in) (void)hipStreamDestroy(p->s_in);
   if (p->s_out) (void)hipStreamDestroy(p->s_out);
   if (p->st_ev) (void)hipEventDestroy(p->st_ev);
+  if (p->wait_done) (void)hipEventDestroy(p->wait_done);
   for (auto& t : p->timed)
     for (hipEvent_t e : {t.s0, t.s1, t.x0, t.x1, t.q0, t.q1, t.a1})
       if (e) (void)hipEventDestroy(e);
@@ -1290,12 +1509,12 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       std::lock_guard<std::mutex> g(p->mu);
       S.scan_wait = true;
     }
-    if (sent_blocks != nullptr || union_blocks != nullptr) TRY(wait_flag(flag, seq, st));
+    if (sent_blocks != nullptr || union_blocks != nullptr) TRY(wait_flag(p->d, flag, seq, st));
     if (sent_blocks) *sent_blocks = (r1 - r0) * p->lanes * static_cast<uint64_t>(N - 1);
     if (union_blocks) *union_blocks = per(M, me);
     return 0;
   }
-  TRY(wait_flag(flag, seq, st));
+  TRY(wait_flag(p->d, flag, seq, st));
   ht_of(p).lap("2:wait counts");
   const bool wk = p->worker();
   // a co-located rank keeps its own shard's blocks out of its packed stream (and reads them in place)
@@ -1539,6 +1758,8 @@ void progress_main(omr_ar_plan* p) {
     const bool failed = p->thread_rc != 0;
     lk.unlock();
     const int rc = failed ? 0 : round_rest(p, j, nullptr, nullptr);
+    if (rc != 0) (void)plan_fail(p, rc);  // (takes mu itself)
+    if (failed && j.tslot >= 0) p->timed[j.tslot].open = false;  // a skipped round's record is never read
     lk.lock();
     if (rc != 0) {
       p->thread_rc = rc;
@@ -1588,23 +1809,14 @@ extern "C" {
 // One round: scan -> mask all-gather -> one bookkeeping launch -> block counts to the host (the
 // round's single mid-round sync: the transport needs host-side sizes) -> pack -> send/recv -> shard sums
 // [-> sums back -> unpack].  Every block movement is addressed by masks and prefixes.
-int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
-                         uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
-                         omr_stream_t stream) {
-  if (p == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL plan");
-  if (p->worker() && (x == nullptr || out == nullptr)) return derr(OMR_EINVAL, "sparse_round: a worker needs x and out");
-  const bool threaded = (mode & OMR_ROUND_THREAD) != 0;
-  const bool defer = (mode & OMR_ROUND_DEFER) != 0;
-  const bool async = threaded || defer || (mode & OMR_ROUND_ASYNC) != 0;
-  const bool timed = (mode & OMR_ROUND_TIME_EXCHANGE) != 0;
-  mode &= ~(OMR_ROUND_ASYNC | OMR_ROUND_DEFER | OMR_ROUND_TIME_EXCHANGE | OMR_ROUND_THREAD);
-  if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
-    return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
-  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && !p->colocated)
-    return derr(OMR_EINVAL, "sparse_round: the dense reduce-scatter stand-in needs every rank to be a worker");
-  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && p->rows % p->N != 0)
-    return derr(OMR_EINVAL, "sparse_round: dense reduce-scatter needs equal shards (rows %llu, world %d)",
-                static_cast<unsigned long long>(p->rows), p->N);
+}  // extern "C"
+
+namespace {
+
+// omr_sparse_round_f32 after its argument checks (mode: the base mode; the flags separately)
+int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
+                       uint32_t* union_next, int mode, bool threaded, bool defer, bool async, bool timed,
+                       uint64_t* sent_blocks, uint64_t* union_blocks, omr_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // a threaded round hands its steps after the scan to the progress thread; any other call first lets the thread
   // issue everything queued (the plan's state is then this thread's alone)
@@ -1712,9 +1924,16 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
       ++p->rounds_begun;
     }
     const int rc = round_rest(p, j, sent_blocks, union_blocks);
-    if (rc != 0) {  // (a failed first half still counts as issued: no later threaded call waits on it)
-      std::lock_guard<std::mutex> g(p->mu);
-      p->first_halves = p->rounds_begun;
+    if (rc != 0) {
+      // a failed round counts as issued in both halves (a first-half failure left second_halves behind,
+      // and a later fused-pack threaded round waited for it forever), and its timing record is closed unread
+      {
+        std::lock_guard<std::mutex> g(p->mu);
+        p->first_halves = p->rounds_begun;
+        p->second_halves = std::max(p->second_halves, p->rounds_begun);
+      }
+      if (tslot >= 0) p->timed[tslot].open = false;
+      p->cv_done.notify_all();
     }
     return rc;
   }
@@ -1729,9 +1948,42 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
   return 0;
 }
 
-int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mode, uint64_t* sent_blocks,
-                           uint64_t* union_blocks, omr_stream_t stream) {
-  if (p == nullptr || buf == nullptr) return derr(OMR_EINVAL, "sparse_buckets: NULL");
+}  // namespace
+
+extern "C" {
+
+int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* flags, uint32_t* next_offsets,
+                         uint32_t* union_next, int mode, uint64_t* sent_blocks, uint64_t* union_blocks,
+                         omr_stream_t stream) {
+  if (p == nullptr) return derr(OMR_EINVAL, "sparse_round: NULL plan");
+  if (p->worker() && (x == nullptr || out == nullptr)) return derr(OMR_EINVAL, "sparse_round: a worker needs x and out");
+  const bool threaded = (mode & OMR_ROUND_THREAD) != 0;
+  const bool defer = (mode & OMR_ROUND_DEFER) != 0;
+  const bool async = threaded || defer || (mode & OMR_ROUND_ASYNC) != 0;
+  const bool timed = (mode & OMR_ROUND_TIME_EXCHANGE) != 0;
+  mode &= ~(OMR_ROUND_ASYNC | OMR_ROUND_DEFER | OMR_ROUND_TIME_EXCHANGE | OMR_ROUND_THREAD);
+  if (mode != OMR_ROUND_ALLREDUCE && mode != OMR_ROUND_REDUCE_SCATTER && mode != OMR_ROUND_DENSE_REDUCE_SCATTER)
+    return derr(OMR_EINVAL, "sparse_round: unknown mode %d", mode);
+  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && !p->colocated)
+    return derr(OMR_EINVAL, "sparse_round: the dense reduce-scatter stand-in needs every rank to be a worker");
+  if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER && p->rows % p->N != 0)
+    return derr(OMR_EINVAL, "sparse_round: dense reduce-scatter needs equal shards (rows %llu, world %d)",
+                static_cast<unsigned long long>(p->rows), p->N);
+  TRY(plan_check(p, "sparse_round"));
+  TRY(p->d->check_open("sparse_round"));
+  // from here on the round has started: any error fails the plan and aborts the transport (plan_fail)
+  return plan_fail(p, sparse_round_issue(p, x, out, flags, next_offsets, union_next, mode, threaded, defer, async, timed,
+                                         sent_blocks, union_blocks, stream));
+}
+
+}  // extern "C"
+
+namespace {
+
+// omr_sparse_buckets_f32; *started is set once the first round or copy has been issued (an error after that fails
+// the plan and aborts the transport)
+int sparse_buckets_issue(omr_ar_plan* p, float* buf, uint64_t total_n, int mode, uint64_t* sent_blocks,
+                         uint64_t* union_blocks, omr_stream_t stream, bool* started) {
   TRY(thread_drain(p));
   struct InBuckets {  // (the rounds of this call keep their shard sum off the scan: see omr_sparse_round_f32)
     omr_ar_plan* p;
@@ -1753,6 +2005,8 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
     return derr(OMR_EINVAL, "sparse_buckets: buf is neither device memory nor pinned host memory (memory type %d): "
                             "register it (omr_host_register / hipHostRegister)", static_cast<int>(attr.type));
   const bool host = attr.type == hipMemoryTypeHost;
+  if (host && !p->worker()) return derr(OMR_EINVAL, "sparse_buckets: a worker's call (this rank aggregates only)");
+  *started = true;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const uint64_t K = total_n / p->n, bytes = p->n * sizeof(float);
   const int rmode = mode | OMR_ROUND_DEFER;
@@ -1792,7 +2046,6 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   // reduce-scatter returns only this rank's shard: only those rows travel back
   const uint64_t row_floats = static_cast<uint64_t>(p->lanes) * p->B;
   const bool rs = mode == OMR_ROUND_REDUCE_SCATTER;
-  if (!p->worker()) return derr(OMR_EINVAL, "sparse_buckets: a worker's call (this rank aggregates only)");
   // Write-back.  When the pinned buffer has a device mapping, each round writes its results straight into it: the
   // unpack (all-reduce) or the shard sum (reduce-scatter) stores only the write-set blocks over PCIe, as the
   // reference's worker copies only the blocks it gets back (client.cc:89), and every other block already holds its
@@ -1875,6 +2128,20 @@ int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mod
   return 0;
 }
 
+}  // namespace
+
+extern "C" {
+
+int omr_sparse_buckets_f32(omr_ar_plan* p, float* buf, uint64_t total_n, int mode, uint64_t* sent_blocks,
+                           uint64_t* union_blocks, omr_stream_t stream) {
+  if (p == nullptr || buf == nullptr) return derr(OMR_EINVAL, "sparse_buckets: NULL");
+  TRY(plan_check(p, "sparse_buckets"));
+  TRY(p->d->check_open("sparse_buckets"));
+  bool started = false;
+  const int rc = sparse_buckets_issue(p, buf, total_n, mode, sent_blocks, union_blocks, stream, &started);
+  return started ? plan_fail(p, rc) : rc;
+}
+
 int omr_ar_plan_shard(omr_ar_plan* p, int* shard, uint64_t* row_begin, uint64_t* row_end, const float** sums,
                       uint64_t* num_blocks) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_shard: NULL");
@@ -1891,8 +2158,9 @@ int omr_ar_plan_fused_pack(const omr_ar_plan* p) { return p != nullptr && p->fus
 
 int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_join: NULL");
-  TRY(thread_drain(p));
-  TRY(flush_pending(p, reinterpret_cast<hipStream_t>(stream), nullptr, nullptr));
+  TRY(plan_check(p, "ar_plan_join"));
+  TRY(plan_fail(p, thread_drain(p)));
+  TRY(plan_fail(p, flush_pending(p, reinterpret_cast<hipStream_t>(stream), nullptr, nullptr)));
   if (p->last_async < 0) return 0;
   // the communication and aggregation streams each run rounds in issue order: waiting for the last one on each
   // covers every earlier one
@@ -1902,6 +2170,21 @@ int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
     TRY(hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), p->set[p->as_last].done, 0),
                   "hipStreamWaitEvent"));
   return 0;
+}
+
+int omr_ar_plan_wait(omr_ar_plan* p, omr_stream_t stream) {
+  if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_wait: NULL");
+  TRY(omr_ar_plan_join(p, stream));
+  if (p->wait_done == nullptr)
+    TRY(hip_check(hipEventCreateWithFlags(&p->wait_done, hipEventDisableTiming), "hipEventCreate"));
+  TRY(plan_fail(p, hip_check(hipEventRecord(p->wait_done, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord")));
+  return plan_fail(p, wait_event_bounded(p->d, p->wait_done, "ar_plan_wait"));
+}
+
+int omr_ar_plan_failed(omr_ar_plan* p) {
+  if (p == nullptr) return 0;
+  std::lock_guard<std::mutex> g(p->mu);
+  return p->failed;
 }
 
 int omr_ar_plan_exchange_time(omr_ar_plan* p, float* ms, uint64_t* bytes_out, uint64_t* bytes_in) {

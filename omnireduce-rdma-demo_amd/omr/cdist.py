@@ -47,6 +47,13 @@ def load():
         "omr_dist_allgather": (i, [vp, vp, vp, ctypes.c_size_t, vp]),
         "omr_dist_exchange": (i, [vp, vp, vp, vp, vp, vp]),
         "omr_dist_inject_fault": (i, [vp, ctypes.c_int64]),
+        "omr_dist_inject_allgather_fault": (i, [vp]),
+        "omr_dist_abort": (i, [vp]),
+        "omr_dist_aborted": (i, [vp]),
+        "omr_dist_set_timeout": (i, [vp, ctypes.c_int64]),
+        "omr_dist_poll": (i, [vp]),
+        "omr_ar_plan_wait": (i, [vp, vp]),
+        "omr_ar_plan_failed": (i, [vp]),
         "omr_ar_plan_create": (i, [vp, u64, u32, u32, u32, vp]),
         "omr_ar_plan_destroy": (i, [vp]),
         "omr_ar_plan_create_roles": (i, [vp, u32, u64, u32, u32, u32, vp]),
@@ -236,6 +243,36 @@ class CppSparseAllreduce:
         """Make `stream` (default: the current stream) wait for every asynchronous round issued so far."""
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         _check(load().omr_ar_plan_join(self._p, st.cuda_stream), "omr_ar_plan_join")
+
+    def wait(self, stream=None):
+        """Join every round issued so far into `stream` and wait on the host until it has run them, within the
+        transport's deadline (omr_ar_plan_wait): raises instead of blocking on a peer that is stuck or gone (the
+        transport is then aborted)."""
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(load().omr_ar_plan_wait(self._p, st.cuda_stream), "omr_ar_plan_wait")
+
+    def set_timeout(self, ms: int):
+        """The deadline of every host-side wait of the transport and its rounds (omr_dist_set_timeout)."""
+        _check(load().omr_dist_set_timeout(self._d, int(ms)), "omr_dist_set_timeout")
+
+    def abort(self):
+        """Abort the transport (omr_dist_abort): RCCL's communicators are aborted, loopback / IPC peers' waits on this
+        rank end at once; every later call fails.  For a rank that cannot finish its part of a round."""
+        if self._d:
+            _check(load().omr_dist_abort(self._d), "omr_dist_abort")
+
+    @property
+    def aborted(self) -> bool:
+        return bool(self._d) and bool(load().omr_dist_aborted(self._d))
+
+    @property
+    def failed(self) -> int:
+        """The plan's first failure code (0: none)."""
+        return int(load().omr_ar_plan_failed(self._p)) if self._p else 0
+
+    def inject_allgather_fault(self):
+        """Test hook (omr_dist_inject_allgather_fault): the next all-gather fails (a round failing in its first half)."""
+        _check(load().omr_dist_inject_allgather_fault(self._d), "omr_dist_inject_allgather_fault")
 
     def inject_fault(self, after_pieces: int = 0):
         """Test hook (omr_dist_inject_fault): the next exchange fails after issuing `after_pieces` pieces."""

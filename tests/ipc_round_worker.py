@@ -2,8 +2,10 @@
 tests/test_gpu_ipc.py (several of these share the one GPU), or over RCCL under torch.distributed.run, one rank per
 GPU (tests/test_gpu_rccl_multi.py, on nodes with enough GPUs).  Writes this rank's outputs to an .npz file."""
 import argparse
+import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "omnireduce-rdma-demo_amd"), os.path.join(ROOT, "oracle")):
@@ -37,6 +39,10 @@ def main():
     ap.add_argument("--replan", action="store_true",
                     help="run the rounds, destroy the plan, make a new one on the same transport and run them again "
                          "(the saved outputs are the second plan's)")
+    ap.add_argument("--timeout-ms", type=int, default=0, help="the transport's deadline (omr_dist_set_timeout)")
+    ap.add_argument("--fault-rank", type=int, default=-1, help="this rank's first exchange fails (omr_dist_inject_fault)")
+    ap.add_argument("--fault-after", type=int, default=0)
+    ap.add_argument("--status", default="", help="fault runs: write {error, seconds_to_error} here; exit 3 on an error")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     L = Layout(n=a.n, block_size=a.block)
@@ -56,6 +62,10 @@ def main():
         eng = cdist.CppSparseAllreduce(L, dev, transport="ipc", uid=bytes.fromhex(a.uid), rank=a.rank, world=a.world,
                                        num_workers=nw)
     worker = a.rank < nw
+    if a.timeout_ms:
+        eng.set_timeout(a.timeout_ms)
+    if a.fault_rank == a.rank:
+        eng.inject_fault(a.fault_after)
     # a different input per round (seed = rank, round): the pipelined rounds must not mix their buffers
     K = a.cycle or a.rounds
     xs, outs = [], []
@@ -85,18 +95,35 @@ def main():
         flags.zero_()
         nxt.zero_()
         unx.zero_()
-    for r in range(a.rounds):
-        eng.run(xs[r % K], out=outs[r % K], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
-                async_=a.pipe != "sync", defer=a.pipe in ("defer", "thread"), thread=a.pipe.startswith("thread"))
-        if not worker and a.pipe == "sync":  # a dedicated aggregator's shard sums of this round
-            torch.cuda.synchronize()
-            sh, r0, r1, ptr, nb = eng.shard()
-            t = (torch.as_tensor(ops._DeviceView(ptr, (nb * a.block,), "<f4"), device=dev).clone() if nb
-                 else torch.empty(0, device=dev))
-            sums[f"sums{r}"] = t.cpu().numpy()
-            sums["shard"] = np.array([sh, r0, r1])
-    eng.join()
+    t0 = time.monotonic()
+    try:
+        for r in range(a.rounds):
+            eng.run(xs[r % K], out=outs[r % K], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
+                    async_=a.pipe != "sync", defer=a.pipe in ("defer", "thread"), thread=a.pipe.startswith("thread"))
+            if not worker and a.pipe == "sync":  # a dedicated aggregator's shard sums of this round
+                torch.cuda.synchronize()
+                sh, r0, r1, ptr, nb = eng.shard()
+                t = (torch.as_tensor(ops._DeviceView(ptr, (nb * a.block,), "<f4"), device=dev).clone() if nb
+                     else torch.empty(0, device=dev))
+                sums[f"sums{r}"] = t.cpu().numpy()
+                sums["shard"] = np.array([sh, r0, r1])
+        eng.wait()  # (bounded by the transport's deadline: a stuck peer is an error, not a hang)
+    except cdist._lib.OmrError as e:
+        if not a.status:
+            raise
+        # a failed round: report, abort (the peers' waits on this rank end at once), leave without the collective
+        # clean-up a dead group cannot do
+        took = time.monotonic() - t0
+        eng.abort()
+        with open(a.status, "w") as f:
+            json.dump({"error": str(e), "seconds_to_error": took}, f)
+        print(f"rank {a.rank} failed after {took:.2f} s: {e}", flush=True)
+        eng.close()
+        os._exit(3)
     torch.cuda.synchronize()
+    if a.status:
+        with open(a.status, "w") as f:
+            json.dump({"error": "", "seconds_to_error": None}, f)
     arrs = dict(flags=flags.cpu().numpy(), next=nxt.cpu().numpy().view(np.uint32),
                 unext=unx.cpu().numpy().view(np.uint32), **sums)
     if worker:

@@ -12,6 +12,7 @@ server.cc:86-96).  Rank r writes "ok" (or the failure) to --out with RANK replac
 import argparse
 import os
 import sys
+import time
 import traceback
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -47,8 +48,7 @@ def check_c4(eng, L, rank, world, rounds, dev):
         for k in range(rounds):
             eng.run(x, out=outs[k % 3], flags=flags, next_offsets=nxt, union_next=unx, mode=mode, async_=True,
                     defer=True)
-        eng.join()
-        torch.cuda.synchronize()
+        eng.wait()  # bounded by the transport's deadline (a stuck peer is an error, not a hang)
         for out in outs[:min(rounds, 3)]:
             got = out.view(L.nb, L.block_size).view(torch.int32)
             exp = ka[:, None].expand(-1, L.block_size)
@@ -91,6 +91,12 @@ def main():
     ap.add_argument("--case", choices=("c4", "buckets"), required=True)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--total-mib", type=int, default=1024)
+    ap.add_argument("--fault-rank", type=int, default=-1,
+                    help="this rank's first exchange fails (omr_dist_inject_fault): the run must end at once, with "
+                         "the rank's error in its --out file and a non-zero exit, instead of hanging its peers")
+    ap.add_argument("--fault-op", choices=("exchange", "allgather"), default="exchange",
+                    help="which transport operation fails (at world 1 a round has no exchange: use allgather)")
+    ap.add_argument("--timeout-ms", type=int, default=0, help="the transport's deadline (default 60 s)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -100,19 +106,32 @@ def main():
     torch.distributed.init_process_group("nccl", device_id=dev)
     L = Layout.from_bytes(256 << 20, 256)
     eng = cdist.CppSparseAllreduce(L, dev)
-    msg = "ok"
+    if a.timeout_ms:
+        eng.set_timeout(a.timeout_ms)
+    if a.fault_rank == rank:
+        eng.inject_fault(0) if a.fault_op == "exchange" else eng.inject_allgather_fault()
+    out = a.out.replace("RANK", str(rank))
+    t0 = time.monotonic()
     try:
         if a.case == "c4":
             check_c4(eng, L, rank, world, a.rounds, dev)
         else:
             check_buckets(eng, L, rank, world, a.total_mib, dev)
-    except Exception:  # noqa: BLE001  (reported through the file; every rank still leaves collectively)
+    except Exception:  # noqa: BLE001
+        # fail fast: report, abort the transport (RCCL's communicators; the peers end at their deadlines or when the
+        # launcher stops them on this exit), and leave without the collective clean-up a broken group cannot do
         msg = traceback.format_exc()
+        with open(out, "w") as f:
+            f.write(f"rank {rank} failed after {time.monotonic() - t0:.2f} s\n{msg}")
+        print(f"rank {rank} FAILED after {time.monotonic() - t0:.2f} s: {msg.splitlines()[-1]}", file=sys.stderr,
+              flush=True)
+        eng.abort()
+        os._exit(1)
     eng.close()
     torch.distributed.destroy_process_group()
-    with open(a.out.replace("RANK", str(rank)), "w") as f:
-        f.write(msg)
-    print(f"rank {rank}: {msg.splitlines()[-1] if msg else ''}", flush=True)
+    with open(out, "w") as f:
+        f.write("ok")
+    print(f"rank {rank}: ok", flush=True)
 
 
 if __name__ == "__main__":

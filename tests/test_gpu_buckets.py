@@ -103,9 +103,28 @@ def test_buckets_loopback(gpu, world, mode, host, bucket_mib, total_mib):
         t.start()
     for t in th:
         t.join(timeout=240)
+    assert not any(t.is_alive() for t in th), "a rank is still running after 240 s"
     D.omr_local_board_destroy(board)
     assert not errs, errs
     check(bufs, bms, L, world, mode, gpu)
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("mode", [AR, RS])
+def test_buckets_config5_full_shape(gpu, mode):
+    """BASELINE config 5 at its own shape: 8 ranks, each with a 4 GiB fp32 gradient in PINNED
+    HOST memory (the reference's registered region res->buf, common.cc:873-914, filled by the generator at -r 0.49,
+    client.cc:396-421), reduced in place in 256 MiB buckets (16 rounds per rank through the four-buffer staging ring)
+    and written back (client.cc:89).  The union of 8 workers at 50 % is about 99.6 %, and 32 of a wave's 64 rows are
+    non-zero on average, past the fused pack's LDS stash (the overflow re-read path).  Ranks are loopback threads on
+    this GPU (the RCCL form of the same call is tests/test_gpu_rccl_multi.py's world-8 bucket case); every block of
+    every rank is checked against ka[count]."""
+    import time
+    t0 = time.monotonic()
+    test_buckets_loopback(gpu, 8, mode, True, 256, 4096)
+    print(f"\nconfig 5 full shape, mode {'AR' if mode == AR else 'RS'}: {time.monotonic() - t0:.1f} s wall "
+          f"(inputs, 16 buckets x 8 ranks, check)", flush=True)
 
 
 @pytest.mark.parametrize("world,mode", [(2, AR), (4, RS)])

@@ -67,3 +67,21 @@ def test_rccl_world8_full_size(gpu, tmp_path, case, extra):
         with open(out.replace("RANK", str(r))) as f:
             msg = f.read()
         assert msg == "ok", f"rank {r}: {msg[-3000:]}"
+
+
+def test_rccl_c4_worker_fault_ends_fast(gpu, tmp_path):
+    """a rank of the world-8 runs that fails must end the run at once (its error in its log, a
+    non-zero exit that makes the launcher stop the other ranks), not let it run into the test's timeout.  Exercised
+    at world 1 on this box: rank 0's first all-gather fails (omr_dist_inject_fault), its transport is aborted and the
+    worker leaves."""
+    out = str(tmp_path / "rankRANK.txt")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--standalone", "--local-addr", "127.0.0.1", C4_WORKER, "--case", "c4", "--rounds", "2",
+           "--fault-rank", "0", "--fault-op", "allgather", "--out", out]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
+    assert p.returncode != 0, (p.stdout + p.stderr)[-3000:]
+    with open(out.replace("RANK", "0")) as f:
+        msg = f.read()
+    assert "fault injected" in msg, msg[-3000:]
+    took = float(msg.split("failed after ", 1)[1].split(" s", 1)[0])
+    assert took < 30, msg[:200]
