@@ -1377,11 +1377,13 @@ struct SumArgs {
 };
 
 
-template <int VEC>
+// W >= count: the contributor loops are unrolled W times (the launch picks 2, 4, 8 or 16), so an 8-worker shard does
+// half the per-row work of a 16-way unroll.
+template <int VEC, int W>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
   constexpr int P = 32 / VEC;  // pair slots per window
   constexpr int kSlotGroup = P < 8 ? P : 8;
-  constexpr uint32_t kRecCap = kSumUnitRows * OMR_MAX_WORKERS;
+  constexpr uint32_t kRecCap = kSumUnitRows * W;
   __shared__ uint64_t s_rec[kWavesPerWG][kRecCap];
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1420,10 +1422,10 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
     const uint64_t r = g0 + (rl ? static_cast<uint32_t>(lane) : 0u);
     const uint64_t w = rl ? a.write_set[r] : 0ull;
     const uint32_t wpre = (rl && a.packed_out) ? pws[r] : 0u;
-    uint64_t mk[OMR_MAX_WORKERS];
-    uint32_t pre[OMR_MAX_WORKERS];
+    uint64_t mk[W];
+    uint32_t pre[W];
 #pragma unroll
-    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) {
+    for (uint32_t c = 0; c < W; ++c) {
       mk[c] = (c < a.count && rl) ? a.masks[c * a.mstride + r] : 0ull;
       pre[c] = (!cols && c < a.count && rl) ? a.prefix[c * (a.rows + 1) + r] : 0u;
     }
@@ -1438,7 +1440,7 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
     const bool wb = mine && ((w >> l) & 1ull);
     uint32_t cb = 0;
 #pragma unroll
-    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) cb |= static_cast<uint32_t>((mk[c] >> l) & 1ull) << c;
+    for (uint32_t c = 0; c < W; ++c) cb |= static_cast<uint32_t>((mk[c] >> l) & 1ull) << c;
     const uint32_t np = wb ? (cb ? static_cast<uint32_t>(__builtin_popcount(cb)) : 1u) : 0u;
     uint32_t inc = np;
 #pragma unroll
@@ -1448,9 +1450,9 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
     }
     const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
     if (total == 0) continue;
-    uint64_t ccol[OMR_MAX_WORKERS];  // column streams: worker c's bits of column l over the loaded rows
+    uint64_t ccol[W];  // column streams: worker c's bits of column l over the loaded rows
 #pragma unroll
-    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) ccol[c] = (cols && c < a.count) ? __ballot((mk[c] >> l) & 1ull) : 0ull;
+    for (uint32_t c = 0; c < W; ++c) ccol[c] = (cols && c < a.count) ? __ballot((mk[c] >> l) & 1ull) : 0ull;
     if (np != 0) {
       uint32_t k = inc - np;
       const uint32_t first = k, last = inc - 1;
@@ -1462,7 +1464,7 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
         s_rec[wave][k] = hdr | kRecZero | kRecFirst | kRecLast;
       } else {
 #pragma unroll
-        for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) {
+        for (uint32_t c = 0; c < W; ++c) {
           if (!((cb >> c) & 1u)) continue;
           uint64_t rec;
           if (c == a.me) {
@@ -1508,17 +1510,37 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
           }
         }
       }
+      // the segmented sums first, every pair's running sum kept in its slot's registers; then the stores of the blocks
+      // the window completed.  (A store between two adds makes every later wait count it: on gfx9 vmcnt counts loads
+      // and stores together, so the waits before the adds of the next slot group also waited for the stores' acks --
+      // up to four store round trips per window, measured as a 3 us tail at config 4's shard; round 4.)
+      // (every slot is consumed on every path, a slot past the window's last pair by a discarded add: a register whose
+      // load might still be pending on some path would make the compiler wait again before its store)
 #pragma unroll
       for (int j = 0; j < P; ++j) {
-        if (static_cast<uint32_t>(j) < nv) {  // (wave-uniform)
-          const uint64_t rc = readlane64(myrec, j);
+        const uint64_t rc = readlane64(myrec, j);
+        const bool use = static_cast<uint32_t>(j) < nv;
 #pragma unroll
-          for (int q = 0; q < VEC; ++q)  // (0.0f + x_first) + ...: a block's first pair restarts from +0.0f
-            acc[q] = add4((rc & kRecFirst) ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
+        for (int q = 0; q < VEC; ++q) {  // (0.0f + x_first) + ...: a block's first pair restarts from +0.0f
+          const v4f sum = add4((rc & kRecFirst) ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
+          acc[q] = use ? sum : acc[q];
+          v[j][q] = acc[q];
+        }
+      }
+      // (pins every add above the stores: left to itself the compiler sinks slot j+1's add below slot j's conditional
+      // store, and its wait then counts that store again)
+#pragma unroll
+      for (int j = 0; j < P; ++j)
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) asm volatile("" : "+v"(v[j][q]));
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        if (static_cast<uint32_t>(j) < nv) {
+          const uint64_t rc = readlane64(myrec, j);
           if (rc & kRecLast) {
             v4f* const d = reinterpret_cast<v4f*>(a.out + ((rc >> 32) & 0x0FFFFFFFull) * a.block);
 #pragma unroll
-            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = acc[q];
+            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = v[j][q];
           }
         }
       }
@@ -2486,6 +2508,15 @@ int omr_move_blocks_f32(const float* src, float* dst, int dir, const uint64_t* r
 }  // extern "C"
 
 namespace {
+template <int W>
+void launch_shard_sum_w(const SumArgs& a, unsigned g, hipStream_t st) {
+  switch (a.block / 256) {
+    case 1: k_shard_sum<1, W><<<g, kWGThreads, 0, st>>>(a); break;
+    case 2: k_shard_sum<2, W><<<g, kWGThreads, 0, st>>>(a); break;
+    default: k_shard_sum<4, W><<<g, kWGThreads, 0, st>>>(a); break;
+  }
+}
+
 int launch_shard_sum(const SumArgs& a0, const uint64_t* recv_offsets, hipStream_t st) {
   SumArgs a = a0;
   if (a.count == 0 || a.count > OMR_MAX_WORKERS) return fail("shard_sum: count %u out of range", a.count);
@@ -2507,11 +2538,10 @@ int launch_shard_sum(const SumArgs& a0, const uint64_t* recv_offsets, hipStream_
   const uint64_t units = a.pos_off != kRowStreams ? (srows / a.S) * a.gps * 2 * a.lanes
                                                  : ((srows + kSumUnitRows - 1) / kSumUnitRows) * a.lanes;
   const unsigned g = grid_for(units);
-  switch (a.block / 256) {
-    case 1: k_shard_sum<1><<<g, kWGThreads, 0, st>>>(a); break;
-    case 2: k_shard_sum<2><<<g, kWGThreads, 0, st>>>(a); break;
-    default: k_shard_sum<4><<<g, kWGThreads, 0, st>>>(a); break;
-  }
+  if (a.count <= 2) launch_shard_sum_w<2>(a, g, st);
+  else if (a.count <= 4) launch_shard_sum_w<4>(a, g, st);
+  else if (a.count <= 8) launch_shard_sum_w<8>(a, g, st);
+  else launch_shard_sum_w<OMR_MAX_WORKERS>(a, g, st);
   return launch_status("k_shard_sum");
 }
 }  // namespace
