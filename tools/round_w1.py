@@ -28,6 +28,10 @@ def main():
                     help="make a one-rank torch.distributed nccl group first, as bench.py --force-dist does")
     ap.add_argument("--no-group", action="store_true",
                     help="bench.round_world1 without its own one-rank torch group (the in-process rccl1 transport)")
+    # (bench.round_world1's child run reads the workload from these, as bench.py's own arguments)
+    ap.add_argument("--size-mib", type=int, default=256)
+    ap.add_argument("--block-size", type=int, default=256)
+    ap.add_argument("--density", type=float, default=0.095)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     if a.pg:
@@ -35,8 +39,8 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29547")
         torch.cuda.set_device(0)
         torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    L = Layout.from_bytes(256 << 20, 256)
-    bm = ops.gen_bitmap(0, 0.095, L.nb)
+    L = Layout.from_bytes(a.size_mib << 20, a.block_size)
+    bm = ops.gen_bitmap(0, a.density, L.nb)
     sets = []
     for _ in range(4):
         x = ops.fill_blocks(torch.from_numpy(bm).to(dev), L, mode=0)

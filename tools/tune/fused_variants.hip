@@ -8,7 +8,7 @@
 
 namespace {
 // k_scan1s — k_scan1f with SPLIT batch ownership (study): batch j (RB rows of the column segment) belongs to wave
-// j % WAVES, so the batches in flight at any moment are one contiguous stretch of every column (csrc/tune/
+// j % WAVES, so the batches in flight at any moment are one contiguous stretch of every column (tools/tune/
 // stream_probe.hip: "col split" read 2-3 % faster than the contiguous per-wave ranges).  In-batch successors
 // are stored in stream; every batch's tail (rows at and after its last non-zero row) gets its successor after
 // one barrier, from an LDS bitmap of non-empty batches (ds_or_b64) and the batches' 16-bit row masks.
@@ -170,7 +170,7 @@ void go_s(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
 
 namespace {
 // Pure read with k_scan1f's geometry and workgroup -> column mapping (no ballots, stores or barrier): the floor
-// the fused kernel's read stream could reach (csrc/tune/stream_probe.hip "col contig xcd").  Timing only.
+// the fused kernel's read stream could reach (tools/tune/stream_probe.hip "col contig xcd").  Timing only.
 template <int VEC, int W>
 __global__ __launch_bounds__(64 * W) void k_read_geom(FusedArgs a) {
   constexpr int RB = 16 / VEC;

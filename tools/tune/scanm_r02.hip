@@ -23,7 +23,7 @@ namespace {
 // write-through with a static store schedule (a block outside the write set is pointed past the row's
 // descriptor and dropped).  Lane w keeps worker w's row mask (no runtime-indexed register arrays).
 // tools/tune_scanm.py: SUB*VEC = 16 loads per worker, UW = 1 is fastest (8 x 256 MiB: 391.5 vs 410.8 us for the
-// previous plain-load form, csrc/tune/scanm_variants.hip).
+// previous plain-load form, tools/tune/scanm_variants.hip).
 template <int VEC, int SUB, int UW>
 __global__ __launch_bounds__(kWGThreads) void k_scanm_row(ScanArgs a) {
   constexpr uint32_t B4 = 64 * VEC;  // 16-byte vectors per block

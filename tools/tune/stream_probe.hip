@@ -2,7 +2,7 @@
 // register loads (buffer_load_dwordx4 nt, the k_scan1f load) versus LDS-DMA (global_load_lds_dwordx4 nt into a
 // per-wave LDS ring, then ds_read), at several occupancies and depths.  Every variant checksums all the words
 // it read, so a variant that skips or mis-orders data is caught.  Build: hipcc --offload-arch=gfx950 -O3
-// -std=c++17 -o build/stream_probe csrc/tune/stream_probe.hip; run: build/stream_probe [MiB] [rounds].
+// -std=c++17 -o build/stream_probe tools/tune/stream_probe.hip; run: build/stream_probe [MiB] [rounds].
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
