@@ -52,9 +52,10 @@ int omr_dist_create_rccl(const void* id, int rank, int world, omr_dist** out);
  * copies out of the sender's IPC-mapped buffer); ordering is carried on the device by IPC events, so calls return
  * without synchronising any stream, as with RCCL.  The transport caches IPC handles and peer mappings per allocation.
  * Plans allocate their device buffers through the transport, which keeps every buffer it exported alive until it is
- * destroyed itself and hands it to the next plan that asks for the same size (a freed allocation a peer still maps
- * may come back from hipMalloc at the same address, and ROCm then refuses to export it).  Buffers the caller hands
- * to a round must stay allocated while the transport lives.  Destroy is collective. */
+ * destroyed itself and hands it to the next plan whose request it fits (its size up to twice the request; a freed
+ * allocation a peer still maps may come back from hipMalloc at the same address, and ROCm then refuses to export it).
+ * So device memory only grows while the transport lives: re-planning at larger sizes adds to the pool.  Buffers the
+ * caller hands to a round must stay allocated while the transport lives.  Destroy is collective. */
 int omr_dist_ipc_unique_id(void* id /* OMR_UNIQUE_ID_BYTES */);
 int omr_dist_create_ipc(const void* id, int rank, int world, omr_dist** out);
 

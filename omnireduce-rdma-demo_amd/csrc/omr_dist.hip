@@ -616,15 +616,20 @@ struct IpcDist final : omr_dist {
   // a peer still maps can come back from hipMalloc at the same address, and hipIpcGetMemHandle then refuses it
   // ("invalid argument"; seen when a plan was destroyed and re-created on the transport).  A parked allocation keeps
   // its handle and id, so the peers' mappings of it stay right when the next plan reuses it.
+  // A parked allocation of at least the requested size (and at most twice it) is reused, so re-planning at another
+  // size (another bucket size, a regrown message log) reuses what it can instead of only adding device memory.  The
+  // pool still holds every exported allocation until the transport is destroyed (omr_dist.h).
   int alloc(void** ptr, size_t bytes) override {
-    auto it = parked.find(bytes);
-    if (it != parked.end()) {
+    auto it = parked.lower_bound(bytes);
+    size_t have = bytes;
+    if (it != parked.end() && it->first <= 2 * bytes) {
       *ptr = it->second;
+      have = it->first;
       parked.erase(it);
     } else {
       TRY(hip_check(hipMalloc(ptr, bytes), "hipMalloc"));
     }
-    sized[*ptr] = bytes;
+    sized[*ptr] = have;
     return 0;
   }
   void release(void* ptr) override {
