@@ -279,6 +279,19 @@ int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask
                         uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
                         uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
                         const struct omr_sum_list* list, omr_stream_t stream);
+/* omr_round_plan_list in row chunks (round 4): 256-thread workgroups, one per 256 rows of EVERY array (one wave per
+ * SIMD, so they fit on a CU beside a running scan workgroup), each publishing its chunk's per-array totals and adding
+ * its predecessors'.  Same outputs, bit for bit.  `workspace`: device uint32[omr_round_plan_workspace_words()],
+ * zeroed once by the caller and left zeroed by every launch (one launch at a time per workspace); it also replaces
+ * `arrive` (the completion notice's counter).  Plans of more than 64 * 256 rows run omr_round_plan_list's form, with
+ * workspace[0] as its arrival counter. */
+uint64_t omr_round_plan_workspace_words(void);
+int omr_round_plan_ws(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                      uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                      uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
+                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* workspace,
+                      uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                      const struct omr_sum_list* list, omr_stream_t stream);
 
 /* Block movement addressed by a row mask and its prefix (no block list): the k-th set bit of `row_masks` over
  * rows [0, rows) minus [skip_begin, skip_end) is block k of the packed stream.

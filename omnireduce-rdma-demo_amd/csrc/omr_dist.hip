@@ -970,7 +970,8 @@ struct omr_ar_plan {
   uint32_t* unext_ws = nullptr;
   void* scan_ws = nullptr;   // omr_worker_scan_f32 segment workspace (zeroed once, self-resetting)
   size_t scan_ws_bytes = 0;
-  uint32_t* arrive = nullptr;     // device arrival counter of the plan kernel's completion notice
+  uint32_t* arrive = nullptr;     // the plan kernel's workspace (omr_round_plan_ws; word 0: its arrival counter)
+  bool plan_v1 = false;           // OMR_PLAN_V1=1 (study knob): omr_round_plan_list's form
   uint32_t* flag_host = nullptr;  // [kSets] pinned, per set: the plan kernel stores the round's sequence number here
   uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
@@ -1378,7 +1379,9 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   if (rc == 0)
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->counts_map), p->counts_host, 0),
                 "hipHostGetDevicePointer"));
-  A(dev_alloc(p->d, &p->arrive, 1));
+  const uint64_t plan_ws_words = omr_round_plan_workspace_words();
+  A(dev_alloc(p->d, &p->arrive, plan_ws_words));
+  if (const char* pv = getenv("OMR_PLAN_V1")) p->plan_v1 = atoi(pv) != 0;
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), NSETS * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0) {
@@ -1386,7 +1389,7 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->flag_map), p->flag_host, 0),
                 "hipHostGetDevicePointer"));
   }
-  if (rc == 0) A(hip_check(hipMemset(p->arrive, 0, sizeof(uint32_t)), "hipMemset arrive"));
+  if (rc == 0) A(hip_check(hipMemset(p->arrive, 0, plan_ws_words * sizeof(uint32_t)), "hipMemset plan workspace"));
   for (auto& st : p->set)
     if (rc == 0) A(hip_check(hipMemset(st.own, 0, p->mstride * sizeof(uint64_t)), "hipMemset own masks"));
   for (auto& st : p->set)
@@ -1695,12 +1698,14 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
   //    ... and, by extra workgroups of the same launch, the aggregator chain (server.cc:86-96 min_next) over the union
   //    ... and the shard sum's pair list, by more workgroups (sum_list)
   const omr_sum_list sl = p->sum_list ? list_desc(p, S) : omr_sum_list{};
-  TRY(omr_check(omr_round_plan_list(S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes,
-                                    p->bounds_dev, NS, S.wset, S.umask, S.prefix,
-                                    p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, S.pack_cnt,
-                                    S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->arrive, p->flag_map + si, seq,
-                                    j.un, p->B, p->sum_list ? &sl : nullptr, qstream),
-                "omr_round_plan_list"));
+  //    (omr_round_plan_ws: 256-thread workgroups over row chunks, which fit beside a running scan workgroup;
+  //    OMR_PLAN_V1=1, a study knob, runs round 3's one-1024-thread-workgroup-per-array form instead)
+  TRY(omr_check((p->plan_v1 ? omr_round_plan_list : omr_round_plan_ws)(
+                    S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes, p->bounds_dev, NS,
+                    S.wset, S.umask, S.prefix, p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own,
+                    S.pack_cnt, S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->arrive, p->flag_map + si, seq, j.un,
+                    p->B, p->sum_list ? &sl : nullptr, qstream),
+                "omr_round_plan_ws"));
   ht.lap("1:plan");
   // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407): addressed by
   //     device-side data only, so it is queued before the host learns the counts and runs while it waits.  (Every

@@ -1236,6 +1236,161 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- the round plan in row chunks (round 4)
+// k_round_plan above gives each mask array ONE 1024-thread workgroup: 16 waves that cannot share a CU with a running
+// scan workgroup (VGPRs), so the plan waits for the scan's workgroups to drain, and its write-set workgroup alone reads
+// every worker's every row.  Here 256-thread workgroups (one wave per SIMD) each take a chunk of 256 rows of EVERY
+// array: one round trip loads the chunk's rows of the count workers' masks; the union, the write set, every array's
+// popcounts and their exclusive scans over the chunk come from registers; the chunk's per-array totals are published
+// (a flag per chunk) and each workgroup sums its predecessors' totals, which they all publish at about the same time
+// (no chain of look-backs).  A workgroup's chunk is a ticket taken when it starts, so every lower chunk belongs to a
+// workgroup that is already running (the look-back never waits on one that is not resident).  Workspace (uint32):
+// [0] the arrival counter, [1] the ticket counter, [2, 2 + kPlanChunksMax) the chunk flags, then the totals
+// [chunk][array]; the launch's last arrival leaves the counters and the flags zeroed again.
+constexpr uint32_t kPlan2Threads = kWGThreads;
+constexpr uint32_t kPlanChunksMax = 64;  // rows <= 64 * 256 (larger plans keep k_round_plan)
+constexpr uint32_t kPlanArrays = OMR_MAX_WORKERS + 1;
+constexpr uint64_t kPlan2WorkspaceWords = 2 + kPlanChunksMax + static_cast<uint64_t>(kPlanChunksMax) * kPlanArrays;
+
+template <bool LIST>
+__global__ __launch_bounds__(kPlan2Threads) void k_round_plan2(PlanArgs a, uint32_t nchunks, uint32_t* ws) {
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  constexpr uint32_t kW = kPlan2Threads / 64;
+  if constexpr (LIST) {
+    if (blockIdx.x >= nchunks + a.chain_wgs) {  // the shard sum's pair list, one unit per wave
+      const uint32_t w = __builtin_amdgcn_readfirstlane(wave);
+      build_sum_list(a.list, static_cast<uint64_t>(blockIdx.x - nchunks - a.chain_wgs) * kW + w,
+                     static_cast<uint64_t>(a.list_wgs) * kW);
+      return;
+    }
+  }
+  if (blockIdx.x >= nchunks) {  // the aggregator chain (server.cc:86-96 min_next) over the union, one segment each
+    const uint64_t* m = a.masks;
+    const uint32_t cnt = a.count;
+    const uint64_t ms = a.mstride;
+    next_segment<kW>(a.chain, blockIdx.x - nchunks, [&](uint64_t r) {
+      uint64_t u = 0;
+      for (uint32_t c = 0; c < cnt; ++c) u |= m[static_cast<uint64_t>(c) * ms + r];
+      return u;
+    }, a.chain.next);
+    return;
+  }
+  __shared__ uint32_t s_wtot[kW][kPlanArrays];
+  __shared__ uint32_t s_base[kPlanArrays];
+  __shared__ uint32_t s_ticket;
+  if (t == 0) s_ticket = __hip_atomic_fetch_add(&ws[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint32_t c = s_ticket;
+  const uint32_t NA = a.count + 1;  // the workers' arrays, then the write set
+  const uint64_t all_lanes = a.lanes >= 64 ? ~0ull : ((1ull << a.lanes) - 1ull);
+  uint32_t* const flags = ws + 2;
+  uint32_t* const totals = ws + 2 + kPlanChunksMax;
+  if (c == 0 && a.zero_cnt != nullptr && t < a.zero_cnt_n) a.zero_cnt[t] = 0;
+  // ---- one round trip: row r = c * 256 + t of every worker's masks; union, write set, every array's popcount
+  const uint64_t r = static_cast<uint64_t>(c) * kPlan2Threads + t;
+  const bool in = r < a.rows;
+  uint64_t mk[OMR_MAX_WORKERS];
+#pragma unroll
+  for (uint32_t w = 0; w < OMR_MAX_WORKERS; ++w)
+    mk[w] = (w < a.count && in) ? a.masks[static_cast<uint64_t>(w) * a.mstride + r] : 0ull;
+  uint64_t u = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < OMR_MAX_WORKERS; ++w) u |= mk[w];
+  const uint64_t wsr = in ? ((r % a.rpp == 0) ? (u | all_lanes) : u) : 0ull;  // union + lane heads (client.cc:201-205)
+  if (in) {
+    a.write_set[r] = wsr;
+    a.union_masks[r] = u;
+    if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
+  }
+  // ---- per array: the chunk's exclusive prefix at this row (wave scan, then the earlier waves' totals), the total
+  uint32_t pfx[kPlanArrays];
+#pragma unroll
+  for (uint32_t arr = 0; arr < kPlanArrays; ++arr) {  // (the row's popcounts first: the masks are dead after this)
+    const uint64_t bits = arr < OMR_MAX_WORKERS ? mk[arr] : 0ull;
+    pfx[arr] = arr < NA ? static_cast<uint32_t>(__builtin_popcountll(arr == a.count ? wsr : bits)) : 0u;
+  }
+#pragma unroll
+  for (uint32_t arr = 0; arr < kPlanArrays; ++arr) {
+    const uint32_t v = pfx[arr];
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d, 64);
+      if (lane >= static_cast<uint32_t>(d)) inc += o;
+    }
+    pfx[arr] = inc - v;
+    if (lane == 63) s_wtot[wave][arr] = inc;
+  }
+  __syncthreads();
+  uint32_t ctot[kPlanArrays];
+#pragma unroll
+  for (uint32_t arr = 0; arr < kPlanArrays; ++arr) {
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kW; ++w) {
+      const uint32_t x = s_wtot[w][arr];
+      before += w < wave ? x : 0u;
+      all += x;
+    }
+    pfx[arr] += before;
+    ctot[arr] = all;
+  }
+  // ---- publish the chunk's totals, then add the predecessors' (every chunk publishes before it looks back)
+  if (t == 0) {
+#pragma unroll
+    for (uint32_t arr = 0; arr < kPlanArrays; ++arr)
+      if (arr < NA) __hip_atomic_store(&totals[c * kPlanArrays + arr], ctot[arr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&flags[c], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // thread i < c waits for chunk i, whose workgroup took its ticket first: it is running or done
+  if (t < c)
+    while (__hip_atomic_load(&flags[t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) __builtin_amdgcn_s_sleep(1);
+  __syncthreads();
+  if (t < NA) {
+    uint32_t b = 0;
+    for (uint32_t i = 0; i < c; ++i)
+      b += __hip_atomic_load(&totals[i * kPlanArrays + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_base[t] = b;
+  }
+  __syncthreads();
+  // ---- prefixes, the counts at the shard bounds (system-scope stores: the host reads them), the totals
+  if (in) {
+#pragma unroll
+    for (uint32_t arr = 0; arr < kPlanArrays; ++arr) {
+      if (arr >= NA) continue;
+      const uint32_t pv = s_base[arr] + pfx[arr];
+      a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + r] = pv;
+      for (uint32_t s = 0; s < a.nbounds; ++s)
+        if (a.bounds[s] == r)
+          __hip_atomic_store(&a.counts[arr * a.nbounds + s], pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  if (c + 1 == nchunks && t == 0) {
+#pragma unroll
+    for (uint32_t arr = 0; arr < kPlanArrays; ++arr) {
+      if (arr >= NA) continue;
+      const uint32_t total = s_base[arr] + ctot[arr];
+      a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + a.rows] = total;
+      for (uint32_t s = 0; s < a.nbounds; ++s)
+        if (a.bounds[s] >= a.rows)
+          __hip_atomic_store(&a.counts[arr * a.nbounds + s], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  // ---- completion: every chunk's counts acknowledged (write-through, system scope), then the last arrival re-arms
+  // the workspace and posts the round's sequence number
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == nchunks) {  // every chunk is past its look-back: nothing reads the flags any more
+      for (uint32_t i = 0; i < nchunks; ++i) __hip_atomic_store(&flags[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ws[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ws[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.done_flag != nullptr) __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // Dense <-> packed block movement over the set bits of one mask array (dir 0: pack, the worker's gather of
 // common.cc:405-407; dir 1: unpack, the worker's in-place result copy of client.cc:89).  Rows [skip_b, skip_e)
 // are skipped and do not occupy the packed stream.
@@ -2387,12 +2542,17 @@ int omr_round_plan_ex(const uint64_t* row_masks, uint32_t count, uint64_t mask_s
                              arrive, done_flag, seq, union_next, block_size, nullptr, stream);
 }
 
-int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
-                        uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
-                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
-                        uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                        const omr_sum_list* list, omr_stream_t stream) {
+}  // extern "C"
+
+namespace {
+// omr_round_plan_list (v2 false: k_round_plan, `arrive` one word) and omr_round_plan_ws (v2 true: k_round_plan2 on
+// plans of up to kPlanChunksMax * 256 rows, `arrive` its workspace; larger plans use k_round_plan with word 0)
+int round_plan_launch(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                      uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                      uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
+                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
+                      uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                      const omr_sum_list* list, bool v2, hipStream_t st) {
   if (mask_stride < rows) return fail("round_plan: mask_stride %llu < rows", static_cast<unsigned long long>(mask_stride));
   if (num_zero_counters > kPlanThreads || (num_zero_counters > 0 && zero_counters == nullptr))
     return fail("round_plan: zero_counters");
@@ -2420,7 +2580,8 @@ int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask
   a.prefix = prefix;
   a.counts = counts;
   a.zero_masks = zero_masks;
-  if ((arrive == nullptr) != (done_flag == nullptr)) return fail("round_plan: arrive and done_flag go together");
+  if (!v2 && (arrive == nullptr) != (done_flag == nullptr)) return fail("round_plan: arrive and done_flag go together");
+  if (v2 && arrive == nullptr) return fail("round_plan_ws: NULL workspace");
   a.arrive = arrive;
   a.done_flag = done_flag;
   a.seq = seq;
@@ -2455,9 +2616,51 @@ int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask
     const uint64_t wgs = (units + kPlanThreads / 64 - 1) / (kPlanThreads / 64);
     a.list_wgs = static_cast<uint32_t>(wgs < 512 ? wgs : 512);
   }
+  const uint64_t nchunks = (rows + kPlan2Threads - 1) / kPlan2Threads;
+  if (v2 && nchunks <= kPlanChunksMax) {
+    if (arrive == nullptr) return fail("round_plan_ws: NULL workspace");
+    if (num_zero_counters > kPlan2Threads) return fail("round_plan_ws: zero_counters > %u", kPlan2Threads);
+    if (list != nullptr) {  // (k_round_plan's list workgroups had 16 waves each: the same units, 4 waves per workgroup)
+      const uint64_t units = list_units_host(a.list);
+      const uint64_t wgs = (units + kPlan2Threads / 64 - 1) / (kPlan2Threads / 64);
+      a.list_wgs = static_cast<uint32_t>(wgs < 2048 ? wgs : 2048);
+    }
+    a.arrive = nullptr;  // (k_round_plan2 counts its arrivals in the workspace)
+    const unsigned grid = static_cast<unsigned>(nchunks + chain_wgs + a.list_wgs);
+    if (list != nullptr) k_round_plan2<true><<<grid, kPlan2Threads, 0, st>>>(a, static_cast<uint32_t>(nchunks), arrive);
+    else k_round_plan2<false><<<grid, kPlan2Threads, 0, st>>>(a, static_cast<uint32_t>(nchunks), arrive);
+    return launch_status("k_round_plan2");
+  }
   const size_t lds = rows <= kPlanLdsRows ? rows * sizeof(uint64_t) : 0;
-  k_round_plan<<<count + 1 + chain_wgs + a.list_wgs, kPlanThreads, lds, S(stream)>>>(a);
+  k_round_plan<<<count + 1 + chain_wgs + a.list_wgs, kPlanThreads, lds, st>>>(a);
   return launch_status("k_round_plan");
+}
+}  // namespace
+
+extern "C" {
+
+int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                        uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
+                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
+                        uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                        const omr_sum_list* list, omr_stream_t stream) {
+  return round_plan_launch(row_masks, count, mask_stride, rows, rows_per_part, num_lanes, bounds, num_bounds,
+                           write_set, union_masks, prefix, counts, zero_masks, zero_counters, num_zero_counters, arrive,
+                           done_flag, seq, union_next, block_size, list, false, S(stream));
+}
+
+uint64_t omr_round_plan_workspace_words(void) { return kPlan2WorkspaceWords; }
+
+int omr_round_plan_ws(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                      uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                      uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
+                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* workspace,
+                      uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                      const omr_sum_list* list, omr_stream_t stream) {
+  return round_plan_launch(row_masks, count, mask_stride, rows, rows_per_part, num_lanes, bounds, num_bounds,
+                           write_set, union_masks, prefix, counts, zero_masks, zero_counters, num_zero_counters,
+                           workspace, done_flag, seq, union_next, block_size, list, true, S(stream));
 }
 
 int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,

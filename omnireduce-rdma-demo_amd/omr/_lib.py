@@ -69,6 +69,9 @@ SIGNATURES = {
                                        c_u32, c_u32, c_u64, c_u64, c_int, c_vp, c_vp]),
     "omr_round_plan_list": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
                                     c_vp, c_vp, c_u32, c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_vp]),
+    "omr_round_plan_ws": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
+                                    c_vp, c_vp, c_u32, c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_vp]),
+    "omr_round_plan_workspace_words": (c_u64, []),
     "omr_sum_list_geometry": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u64, c_u64, c_u32, c_vp, c_vp]),
     "omr_sum_list_build": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp]),
     "omr_shard_sum_list_f32": (c_int, [c_vp, c_vp, c_vp, c_u32, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_int, c_vp,

@@ -120,6 +120,67 @@ def test_round_plan(gpu, count, rows, rpp, lanes):
     assert int(zero.count_nonzero()) == 0
 
 
+@pytest.mark.parametrize("count,rows,rpp,lanes,stride_pad", [
+    (1, 64, 8, 64, 0), (3, 512, 64, 64, 5), (8, 4096, 512, 64, 1024), (5, 1280, 256, 16, 0), (16, 100, 25, 32, 3),
+    (2, 8192, 1024, 64, 0), (7, 16384, 2048, 16, 0),   # 64 chunks: the row-chunk form's largest plan
+    (3, 20480, 2560, 16, 0),                           # more rows: the one-workgroup-per-array form, workspace[0]
+    (8, 300, 30, 64, 7),                               # a partial last chunk
+])
+def test_round_plan_ws(gpu, count, rows, rpp, lanes, stride_pad):
+    """omr_round_plan_ws (round 4: 256-thread workgroups over row chunks of every array, chunk totals published and
+    summed by their successors) against numpy: union, write set, every array's prefix, the counts at the shard
+    bounds, the zeroed own masks and pack counters, the aggregator chain, and the completion notice three times in a
+    row with the workspace left zeroed after each."""
+    rng = np.random.default_rng(count * 31 + rows)
+    stride = rows + stride_pad
+    dens = rng.random(count) * 0.5
+    masks = np.zeros((count, stride), dtype=np.uint64)
+    lane_mask = np.uint64((1 << lanes) - 1 if lanes < 64 else (1 << 64) - 1)
+    for c in range(count):
+        bits = rng.random((rows, lanes)) < dens[c]
+        masks[c, :rows] = (bits.astype(np.uint64) << np.arange(lanes, dtype=np.uint64)).sum(axis=1).astype(np.uint64)
+        masks[c, :rows] &= lane_mask
+        masks[c, rows:] = np.uint64(0xDEADBEEF)  # whatever follows the rows (a position table) is not read as masks
+    N = max(1, min(count, 8))
+    bounds = np.array([s * rows // N for s in range(N + 1)], dtype=np.uint64)
+    lib = _lib.load()
+    words = lib.omr_round_plan_workspace_words()
+    md = torch.from_numpy(masks.reshape(-1).view(np.int64)).to(gpu)
+    bd = torch.from_numpy(bounds.view(np.int64)).to(gpu)
+    wset = torch.zeros(rows, dtype=torch.int64, device=gpu)
+    umask = torch.zeros(rows, dtype=torch.int64, device=gpu)
+    prefix = torch.zeros((count + 1) * (rows + 1), dtype=torch.int32, device=gpu)
+    counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int32, device=gpu)
+    zero = torch.full((rows,), -1, dtype=torch.int64, device=gpu)
+    zc = torch.full((8,), -1, dtype=torch.int32, device=gpu)
+    ws = torch.zeros(words, dtype=torch.int32, device=gpu)
+    done = torch.zeros(1, dtype=torch.int32, device=gpu)
+    B = 16384 // lanes
+    unext = torch.full((rows * lanes,), -1, dtype=torch.int32, device=gpu)
+    for seq in (7, 8, 9):
+        prefix.zero_()
+        assert lib.omr_round_plan_ws(P(md), count, stride, rows, rpp, lanes, P(bd), N + 1, P(wset), P(umask),
+                                     P(prefix), P(counts), P(zero), P(zc), 8, P(ws), P(done), seq, P(unext), B, None,
+                                     stream()) == 0, lib.omr_last_error()
+        torch.cuda.synchronize()
+        assert int(done.item()) == seq
+        assert int(ws.count_nonzero()) == 0 or rows > 64 * 256 and int(ws[0].item()) == 0, "workspace not re-armed"
+    mr = masks[:, :rows]
+    u, w = np_write_set(mr, rpp, lanes)
+    assert (umask.cpu().numpy().view(np.uint64) == u).all()
+    assert (wset.cpu().numpy().view(np.uint64) == w).all()
+    pre = prefix.cpu().numpy().view(np.uint32).reshape(count + 1, rows + 1)
+    cn = counts.cpu().numpy().view(np.uint32).reshape(count + 1, N + 1)
+    for a in range(count + 1):
+        exp = np_prefix(mr[a] if a < count else w)
+        assert (pre[a] == exp).all(), a
+        assert (cn[a] == exp[bounds.astype(np.int64)]).all(), a
+    assert int(zero.count_nonzero()) == 0 and int(zc.count_nonzero()) == 0
+    flags = ((u[:, None] >> np.arange(lanes, dtype=np.uint64)) & np.uint64(1)).astype(np.int32).ravel()
+    exp = oracle.next_offsets(flags, rows * lanes * B, B, lanes, rows // rpp)
+    assert (unext.cpu().numpy().view(np.uint32) == exp).all()
+
+
 @pytest.mark.parametrize("count,rows,rpp,lanes", [(1, 64, 8, 64), (3, 512, 64, 64), (8, 4096, 512, 64),
                                                    (5, 1280, 256, 16), (16, 100, 25, 32), (3, 20480, 2560, 16)])
 def test_round_plan_chain(gpu, count, rows, rpp, lanes):
