@@ -367,6 +367,8 @@ def round_world1_child(args):
                               rf.get("algorithmic_bytes_per_launch"), "frac": rf.get("frac"),
                               "traffic": rf.get("traffic"), "traffic_source": rf.get("traffic_source")},
             "stages_ms": ex.get("stages_ms"), "host_ms_per_call": ex.get("host_ms_per_call"),
+            "host_wait_ms_per_call": ex.get("host_wait_ms_per_call"),
+            "host_issue_ms_per_call": ex.get("host_issue_ms_per_call"),
             "note": ("the N=1 anchor of the per-GPU scaling fraction: the N>=2 lines' measurement at world 1 (a child "
                      "process, run after the headline's timed region)")}
 
@@ -576,6 +578,8 @@ def main():
     every = max(1, args.event_every)
     one_kernel = (not dist_mode) and m == 1 and args.kernel == "fused"
     span = (timing.Event(), timing.Event())  # single-kernel step: the kernel's mean duration over the timed region
+    if dist_mode:
+        engine.host_stats(reset=True)
     t0 = time.perf_counter()
     if one_kernel:
         span[0].record(stream)
@@ -583,6 +587,7 @@ def main():
         step(args.warmup + i, None if one_kernel else (kev[i] if i % every == 0 else None), timed_region=True)
     if one_kernel:
         span[1].record(stream)
+    host_wait_us = engine.host_stats(reset=True)[0] if dist_mode else 0.0  # (the timed calls' blocked time only)
     join()
     torch.cuda.synchronize()
     if dist_mode:
@@ -623,7 +628,11 @@ def main():
                     # where a round's time goes (rank 0): each stage's mean from events on its own stream, and the
                     # host time of one engine.run call (a round is host-bound when that exceeds ms_per_step)
                     "stages_ms": {k: round(v, 5) for k, v in stages.items()},
-                    "host_ms_per_call": round(host_s[0] / max(1, host_s[1]) * 1e3, 5)}
+                    "host_ms_per_call": round(host_s[0] / max(1, host_s[1]) * 1e3, 5),
+                    # of which blocked on the GPU (the count wait, set reuse, the progress thread): the rest is the
+                    # host's own issue time, the figure that says whether a round is host-bound
+                    "host_wait_ms_per_call": round(host_wait_us / max(1, host_s[1]) * 1e-3, 5),
+                    "host_issue_ms_per_call": round((host_s[0] * 1e6 - host_wait_us) / max(1, host_s[1]) * 1e-3, 5)}
     if not dist_mode:
         kev = kev[::every]
     if one_kernel:  # every step is exactly one k_scan1f launch: events around all K steps, divided by K

@@ -229,6 +229,10 @@ int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
 int omr_ar_plan_wait(omr_ar_plan* plan, omr_stream_t stream);
 /* The plan's first failure (0: none); see failure containment above. */
 int omr_ar_plan_failed(omr_ar_plan* plan);
+/* The calling thread's time blocked inside this plan's calls since the last reset, in microseconds (the wait for a
+ * round's block counts, the set-reuse and drain waits on the progress thread), and how many waits: a round's host
+ * ISSUE time is its call time minus this.  reset != 0 zeroes them after reading. */
+int omr_ar_plan_host_stats(omr_ar_plan* plan, double* wait_us, uint64_t* waits, int reset);
 
 /* ---------------------------------------------------------------- the round as wire messages between processes
  *

@@ -1055,6 +1055,10 @@ struct omr_ar_plan {
   int failed = 0;
   std::string failed_why;
   hipEvent_t wait_done = nullptr;  // omr_ar_plan_wait's event
+  // omr_ar_plan_host_stats: the calling thread's time blocked on the GPU or on the progress thread inside rounds (the
+  // count wait, the set-reuse waits, the drain), so a caller can tell issue time from waiting
+  std::atomic<uint64_t> host_wait_ns{0};
+  std::atomic<uint64_t> host_waits{0};
 };
 
 namespace {
@@ -1064,6 +1068,15 @@ int thread_drain(omr_ar_plan* p);
 void thread_stop(omr_ar_plan* p);
 thread_local bool t_progress = false;  // this thread is a plan's progress thread (OMR_ROUND_THREAD)
 HostTrace& ht_of(omr_ar_plan* p) { return t_progress ? p->ht_thread : p->ht; }
+
+// Accumulates the calling thread's blocked time into the plan's host statistics (the progress thread's waits are
+// off the caller's path and are not counted).
+struct HostWait {
+  omr_ar_plan* p;
+  std::chrono::steady_clock::time_point t0;
+  explicit HostWait(omr_ar_plan* pp);
+  ~HostWait();
+};
 
 // A round that had started failed: record it (first error wins) and abort the transport, so that no peer waits for
 // this rank's part of the round (the reference exits on a failed post, common.cc:450-451).  Returns rc.
@@ -1080,6 +1093,15 @@ int plan_fail(omr_ar_plan* p, int rc) {
   (void)p->d->abort_with(rc, why.c_str());
   snprintf(g_derr, sizeof(g_derr), "%s", why.c_str());  // (the caller's message, whatever abort_with did)
   return rc;
+}
+
+HostWait::HostWait(omr_ar_plan* pp) : p(t_progress ? nullptr : pp), t0(std::chrono::steady_clock::now()) {}
+HostWait::~HostWait() {
+  if (p == nullptr) return;
+  const auto dt = std::chrono::steady_clock::now() - t0;
+  p->host_wait_ns.fetch_add(static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(dt).count()),
+                            std::memory_order_relaxed);
+  p->host_waits.fetch_add(1, std::memory_order_relaxed);
 }
 
 // OMR_EABORTED if an earlier round of the plan failed
@@ -1517,12 +1539,18 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       std::lock_guard<std::mutex> g(p->mu);
       S.scan_wait = true;
     }
-    if (sent_blocks != nullptr || union_blocks != nullptr) TRY(wait_flag(p->d, flag, seq, st));
+    if (sent_blocks != nullptr || union_blocks != nullptr) {
+      HostWait hw(p);
+      TRY(wait_flag(p->d, flag, seq, st));
+    }
     if (sent_blocks) *sent_blocks = (r1 - r0) * p->lanes * static_cast<uint64_t>(N - 1);
     if (union_blocks) *union_blocks = per(M, me);
     return 0;
   }
-  TRY(wait_flag(p->d, flag, seq, st));
+  {
+    HostWait hw(p);
+    TRY(wait_flag(p->d, flag, seq, st));
+  }
   ht_of(p).lap("2:wait counts");
   const bool wk = p->worker();
   // a co-located rank keeps its own shard's blocks out of its packed stream (and reads them in place)
@@ -1796,6 +1824,7 @@ int thread_start(omr_ar_plan* p) {
 // every queued round issued; returns (and keeps) the progress thread's error, if any
 int thread_drain(omr_ar_plan* p) {
   if (!p->progress.joinable()) return 0;
+  HostWait hw(p);
   std::unique_lock<std::mutex> lk(p->mu);
   p->cv_done.wait(lk, [&] { return p->jobs.empty() && !p->busy; });
   if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
@@ -1870,6 +1899,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
   int tslot = -1;
   if (timed) TRY(timed_slot(p, &tslot));
   if (threaded) {  // that plan has been issued (and this set's `scanned` waited for) by the progress thread
+    HostWait hw(p);
     std::unique_lock<std::mutex> lk(p->mu);
     const uint64_t need = p->rounds_begun >= omr_ar_plan::kSets - 1 ? p->rounds_begun - (omr_ar_plan::kSets - 1) : 0;
     p->cv_done.wait(lk, [&] { return p->first_halves >= need || p->thread_rc != 0; });
@@ -1886,7 +1916,10 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
   if (pack_scan) {
     std::unique_lock<std::mutex> lk(p->mu);
     const uint64_t need = p->rounds_begun >= omr_ar_plan::kSets ? p->rounds_begun - (omr_ar_plan::kSets - 1) : 0;
-    if (threaded) p->cv_done.wait(lk, [&] { return p->second_halves >= need || p->thread_rc != 0; });
+    if (threaded) {
+      HostWait hw(p);
+      p->cv_done.wait(lk, [&] { return p->second_halves >= need || p->thread_rc != 0; });
+    }
     if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
     const bool w = S.scan_wait;
     S.scan_wait = false;
@@ -2189,6 +2222,17 @@ int omr_ar_plan_wait(omr_ar_plan* p, omr_stream_t stream) {
     TRY(hip_check(hipEventCreateWithFlags(&p->wait_done, hipEventDisableTiming), "hipEventCreate"));
   TRY(plan_fail(p, hip_check(hipEventRecord(p->wait_done, reinterpret_cast<hipStream_t>(stream)), "hipEventRecord")));
   return plan_fail(p, wait_event_bounded(p->d, p->wait_done, "ar_plan_wait"));
+}
+
+int omr_ar_plan_host_stats(omr_ar_plan* p, double* wait_us, uint64_t* waits, int reset) {
+  if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_host_stats: NULL");
+  if (wait_us) *wait_us = static_cast<double>(p->host_wait_ns.load()) * 1e-3;
+  if (waits) *waits = p->host_waits.load();
+  if (reset) {
+    p->host_wait_ns.store(0);
+    p->host_waits.store(0);
+  }
+  return 0;
 }
 
 int omr_ar_plan_failed(omr_ar_plan* p) {

@@ -54,6 +54,7 @@ def load():
         "omr_dist_poll": (i, [vp]),
         "omr_ar_plan_wait": (i, [vp, vp]),
         "omr_ar_plan_failed": (i, [vp]),
+        "omr_ar_plan_host_stats": (i, [vp, vp, vp, i]),
         "omr_ar_plan_create": (i, [vp, u64, u32, u32, u32, vp]),
         "omr_ar_plan_destroy": (i, [vp]),
         "omr_ar_plan_create_roles": (i, [vp, u32, u64, u32, u32, u32, vp]),
@@ -264,6 +265,14 @@ class CppSparseAllreduce:
     @property
     def aborted(self) -> bool:
         return bool(self._d) and bool(load().omr_dist_aborted(self._d))
+
+    def host_stats(self, reset: bool = True):
+        """(microseconds the calling thread spent blocked inside the plan's calls, number of waits) since the last
+        reset (omr_ar_plan_host_stats): a round's host issue time is its call time minus the blocked time."""
+        us, n = ctypes.c_double(), ctypes.c_uint64()
+        _check(load().omr_ar_plan_host_stats(self._p, ctypes.byref(us), ctypes.byref(n), int(reset)),
+               "omr_ar_plan_host_stats")
+        return us.value, n.value
 
     @property
     def failed(self) -> int:
