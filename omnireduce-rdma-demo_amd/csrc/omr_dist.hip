@@ -971,7 +971,7 @@ struct omr_ar_plan {
   void* scan_ws = nullptr;   // omr_worker_scan_f32 segment workspace (zeroed once, self-resetting)
   size_t scan_ws_bytes = 0;
   uint32_t* arrive = nullptr;     // the plan kernel's workspace (omr_round_plan_ws; word 0: its arrival counter)
-  bool plan_v1 = false;           // OMR_PLAN_V1=1 (study knob): omr_round_plan_list's form
+  bool plan_v1 = false;           // round 3's plan form (omr_round_plan_list) instead of omr_round_plan_ws
   uint32_t* flag_host = nullptr;  // [kSets] pinned, per set: the plan kernel stores the round's sequence number here
   uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
@@ -1403,6 +1403,13 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
                 "hipHostGetDevicePointer"));
   const uint64_t plan_ws_words = omr_round_plan_workspace_words();
   A(dev_alloc(p->d, &p->arrive, plan_ws_words));
+  // Which plan form.  Beside the world-1 round's scan (92 VGPRs, one 16-wave workgroup per CU) the row-chunk
+  // workgroups fit and run starved next to it: the world-1 round measured 64.8-67.9 us with them against 58.8-60.2 us
+  // with round 3's form, which waits for the scan's workgroups to drain (profiles/r04/plan_ab/).  The fused-pack scan of
+  // N > 1 (128 VGPRs, two 8-wave workgroups per CU) leaves no room for either, and a 256-thread workgroup needs only
+  // one of its workgroups to leave a CU, so rounds with the fused pack take the row-chunk form.  OMR_PLAN_V1=0 / 1
+  // forces one (study knob).
+  p->plan_v1 = !p->fused_pack;
   if (const char* pv = getenv("OMR_PLAN_V1")) p->plan_v1 = atoi(pv) != 0;
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), NSETS * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));

@@ -1529,6 +1529,9 @@ struct SumArgs {
   uint64_t rows, r0, r1;
   uint32_t count, me, lanes, block, packed_out;
   uint32_t S, gps;         // column streams: segment rows (shards are whole segments), 64-row groups per segment
+  // set by the launch, so a unit's coordinates are 32-bit shifts and two 32-bit divisions (round 3's 64-bit divisions
+  // by runtime values were ~1,000 scalar instructions before a wave's first load)
+  uint32_t units, lane_shift, seg0;
 };
 
 
@@ -1543,23 +1546,20 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool cols = a.pos_off != kRowStreams;
-  const uint64_t srows = a.r1 - a.r0;
-  const uint64_t units = cols ? (srows / a.S) * a.gps * 2 * a.lanes
-                              : ((srows + kSumUnitRows - 1) / kSumUnitRows) * a.lanes;
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
+  const uint32_t nw = gridDim.x * kWavesPerWG;
   const uint32_t* const pws = a.prefix + static_cast<uint64_t>(a.count) * (a.rows + 1);
   const uint32_t wpre0 = a.packed_out ? pws[a.r0] : 0u;
   const uint32_t bbytes = a.block * 4;
-  for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + wave; u < units; u += nw) {
-    const uint32_t l = static_cast<uint32_t>(u % a.lanes);
+  for (uint32_t u = blockIdx.x * kWavesPerWG + wave; u < a.units; u += nw) {
+    const uint32_t l = u & (a.lanes - 1);
     uint64_t g0, gidx = 0;  // first row the lanes load (lane i: row g0 + i); column streams: the group's table index
     uint32_t nload, h0, h1;  // rows loaded; the unit's rows are lanes [h0, h1)
     if (cols) {
-      uint64_t t = u / a.lanes;
-      const uint32_t h = static_cast<uint32_t>(t & 1u);
+      uint32_t t = u >> a.lane_shift;
+      const uint32_t h = t & 1u;
       t >>= 1;
-      const uint32_t j = static_cast<uint32_t>(t % a.gps);
-      const uint64_t seg = a.r0 / a.S + t / a.gps;
+      const uint32_t j = t % a.gps;
+      const uint64_t seg = a.seg0 + t / a.gps;
       g0 = seg * a.S + static_cast<uint64_t>(j) * kPackGroupRows;
       nload = a.S - j * kPackGroupRows < kPackGroupRows ? a.S - j * kPackGroupRows : kPackGroupRows;
       h0 = h * kSumUnitRows;
@@ -1567,7 +1567,7 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
       gidx = seg * a.gps + j;
       if (h0 >= h1) continue;
     } else {
-      g0 = a.r0 + (u / a.lanes) * kSumUnitRows;
+      g0 = a.r0 + static_cast<uint64_t>(u >> a.lane_shift) * kSumUnitRows;
       nload = a.r1 - g0 < kSumUnitRows ? static_cast<uint32_t>(a.r1 - g0) : kSumUnitRows;
       h0 = 0;
       h1 = nload;
@@ -2740,6 +2740,10 @@ int launch_shard_sum(const SumArgs& a0, const uint64_t* recv_offsets, hipStream_
   const uint64_t srows = a.r1 - a.r0;
   const uint64_t units = a.pos_off != kRowStreams ? (srows / a.S) * a.gps * 2 * a.lanes
                                                  : ((srows + kSumUnitRows - 1) / kSumUnitRows) * a.lanes;
+  if (units > 0xFFFFFFFFull) return fail("shard_sum: %llu units", static_cast<unsigned long long>(units));
+  a.units = static_cast<uint32_t>(units);
+  a.lane_shift = static_cast<uint32_t>(__builtin_ctz(a.lanes));
+  a.seg0 = a.pos_off != kRowStreams ? static_cast<uint32_t>(a.r0 / a.S) : 0u;
   const unsigned g = grid_for(units);
   if (a.count <= 2) launch_shard_sum_w<2>(a, g, st);
   else if (a.count <= 4) launch_shard_sum_w<4>(a, g, st);
