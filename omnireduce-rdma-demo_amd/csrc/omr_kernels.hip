@@ -1469,53 +1469,9 @@ __global__ __launch_bounds__(kWGThreads) void k_move(MoveArgs a) {
 // stream prefix or position).  Ballots over the lanes give each worker's column bits, so every (block, contributor)
 // pair's stream position is computed in registers; a wave-wide exclusive scan lays the pairs out in LDS in
 // (block, rank) order.  The pairs are then streamed P at a time: all P loads in flight (P * VEC dwordx4 per lane),
-// then a segmented sum in rank order whose last pair of each block stores it.  So a unit costs one index round trip
-// plus one per P pairs, whatever the number of contributors (the round-2 kernel paid a round trip per contributor
-// per batch of blocks behind a prefix round trip: 2.9 TB/s at an 8-worker shard).
-// One window of the shard sum: P (block, contributor) pairs, records `rec` lanes [cb, cb + P) (nv of them real).
-// Every window issues exactly P loads and then exactly P stores, whatever nv and whichever pairs end a block: an
-// unused slot loads through a zero-size descriptor, a store that does not end a block is pointed past its
-// descriptor's range and dropped.  On gfx9 `vmcnt` counts loads and stores together, so a data-dependent store
-// between two uses of loaded blocks made the compiler wait for every outstanding operation (s_waitcnt vmcnt(0)) before
-// each use -- one store's write latency per summed block.  With the static schedule each wait counts exactly the
-// younger operations and the window's loads stay in flight together.  Used by the pair-list sum (17.2 -> 15.4 us at
-// config 4's 8-worker shard); k_shard_sum keeps its branchy window, which measured faster for it (15.5-16.1 against
-// 17.8-18.0 us with this one: profiles/r03/round/static_s2h/tune_round_r03.log).
-template <int VEC, int P>
-__device__ __forceinline__ void sum_window(uint64_t rec, uint32_t cb, uint32_t nv, uint64_t pdst, bool packed,
-                                           const float* own, const float* recv, float* out, uint32_t block,
-                                           uint32_t bbytes, int lane, v4f (&acc)[VEC]) {
-  v4f v[P][VEC];
-#pragma unroll
-  for (int j = 0; j < P; ++j) {
-    const uint64_t rc = readlane64(rec, cb + j);
-    const bool load = static_cast<uint32_t>(j) < nv && !(rc & kRecZero);
-    const float* const sb = (rc & kRecOwn) ? own : recv;
-    const __amdgpu_buffer_rsrc_t src =
-        chunk_rsrc(load ? sb + static_cast<uint64_t>(static_cast<uint32_t>(rc)) * block : recv, load ? bbytes : 0u);
-#pragma unroll
-    for (int q = 0; q < VEC; ++q)
-      v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (q * 64 + lane) * 16, 0, kLoadAux));
-  }
-#pragma unroll
-  for (int j = 0; j < P; ++j) {
-    const uint64_t rc = readlane64(rec, cb + j);
-    const bool use = static_cast<uint32_t>(j) < nv;
-    const bool first = use && (rc & kRecFirst), last = use && (rc & kRecLast);
-#pragma unroll
-    for (int q = 0; q < VEC; ++q) {  // (0.0f + x_first) + ...: a block's first pair restarts from +0.0f
-      const v4f sum = add4(first ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
-      acc[q] = use ? sum : acc[q];
-    }
-    const uint64_t dst = packed ? readlane64(pdst, cb + j) : ((rc >> 32) & 0x0FFFFFFFull);
-    const __amdgpu_buffer_rsrc_t d = chunk_rsrc(out + (last ? dst * block : 0ull), bbytes);
-    const uint32_t drop = last ? 0u : kDropStore;
-#pragma unroll
-    for (int q = 0; q < VEC; ++q)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, acc[q]), d, ((q * 64 + lane) * 16) | drop, 0, 0);
-  }
-}
-
+// then the segmented sum in rank order, then the stores of the blocks the window completed (a block's last pair).  So
+// a unit costs one index round trip plus one per P pairs, whatever the number of contributors (the round-2 kernel
+// paid a round trip per contributor per batch of blocks behind a prefix round trip: 2.9 TB/s at an 8-worker shard).
 struct SumArgs {
   const float* own;
   const float* recv;
@@ -1715,21 +1671,25 @@ struct ListSumArgs {
   const uint64_t* write_set;  // packed output: the write set's rows and row prefix (omr_round_plan's prefix[count])
   const uint32_t* wprefix;
   float* out;
-  uint64_t units, r0;
+  uint32_t units;
+  uint64_t r0;
   uint32_t cap, lanes, block, packed_out;
 };
 
 template <int VEC>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
-  constexpr int P = 32 / VEC;  // pair slots per window
+  // pair slots per window: 64 at B = 256, so a unit at config 4's density (26 pairs on average, 32 rows x 8 workers at
+  // most 256) nearly always fits one window; each window is loads, then every add, then the stores (as k_shard_sum)
+  constexpr int P = 64 / VEC;
+  constexpr int kSlotGroup = 8;
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
+  const uint32_t nw = gridDim.x * kWavesPerWG;
   const uint32_t bbytes = a.block * 4;
   const uint32_t wpre0 = a.packed_out ? a.wprefix[a.r0] : 0u;
-  for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + wave; u < a.units; u += nw) {
+  for (uint32_t u = blockIdx.x * kWavesPerWG + wave; u < a.units; u += nw) {
     // ONE load: the unit's first 64 words; its length is the first terminator's lane (more chunks only past 63)
-    const uint64_t* const rec = a.records + u * a.cap;
+    const uint64_t* const rec = a.records + static_cast<uint64_t>(u) * a.cap;
     uint64_t chunk = static_cast<uint32_t>(lane) < a.cap ? rec[lane] : kRecEnd;
     uint32_t total = 0;
     for (uint64_t e = __ballot(chunk == kRecEnd);; ) {
@@ -1747,7 +1707,7 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
 #pragma unroll
     for (int q = 0; q < VEC; ++q) acc[q] = v4f{0.f, 0.f, 0.f, 0.f};
     for (uint32_t wbase = 0; wbase < total; wbase += P) {
-      const uint32_t cb = wbase & 63u;  // the window's first record in the chunk
+      const uint32_t cb = wbase & 63u;  // the window's first record in the chunk (P divides 64)
       if (cb == 0) {
         if (wbase != 0) chunk = wbase + lane < a.cap ? rec[wbase + lane] : 0ull;
         if (a.packed_out && wbase + lane < total) {
@@ -1759,7 +1719,54 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
         }
       }
       const uint32_t nv = total - wbase < static_cast<uint32_t>(P) ? total - wbase : static_cast<uint32_t>(P);
-      sum_window<VEC, P>(chunk, cb, nv, pdst, a.packed_out != 0, a.own, a.recv, a.out, a.block, bbytes, lane, acc);
+      v4f v[P][VEC];
+#pragma unroll
+      for (int g = 0; g < P; g += kSlotGroup) {
+        if (static_cast<uint32_t>(g) < nv) {  // (wave-uniform: a sparse unit issues only what it needs)
+#pragma unroll
+          for (int j = g; j < g + kSlotGroup; ++j) {
+            const uint64_t rc = readlane64(chunk, cb + j);
+            const bool load = static_cast<uint32_t>(j) < nv && !(rc & kRecZero);
+            const float* const sb = (rc & kRecOwn) ? a.own : a.recv;
+            const __amdgpu_buffer_rsrc_t src =
+                chunk_rsrc(sb + static_cast<uint64_t>(static_cast<uint32_t>(rc)) * a.block, load ? bbytes : 0u);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q)
+              v[j][q] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(src, (q * 64 + lane) * 16, 0,
+                                                                                     kLoadAux));
+          }
+        }
+      }
+      // the segmented rank-order sums (a block's first pair restarts from +0.0f), every slot's running sum kept in
+      // its registers; slots past the window's last pair are consumed and discarded, so no slot's load can still be
+      // pending at the stores below (the compiler would wait for it there, and so for the stores before it)
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const uint64_t rc = readlane64(chunk, cb + j);
+        const bool use = static_cast<uint32_t>(j) < nv;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) {
+          const v4f sum = add4((rc & kRecFirst) ? v4f{0.f, 0.f, 0.f, 0.f} : acc[q], v[j][q]);
+          acc[q] = use ? sum : acc[q];
+          v[j][q] = acc[q];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < P; ++j)
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) asm volatile("" : "+v"(v[j][q]));  // (every add above every store)
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        if (static_cast<uint32_t>(j) < nv) {
+          const uint64_t rc = readlane64(chunk, cb + j);
+          if (rc & kRecLast) {
+            const uint64_t dst = a.packed_out ? readlane64(pdst, cb + j) : ((rc >> 32) & 0x0FFFFFFFull);
+            v4f* const d = reinterpret_cast<v4f*>(a.out + dst * a.block);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = v[j][q];
+          }
+        }
+      }
     }
   }
 }
@@ -2867,7 +2874,8 @@ int omr_shard_sum_list_f32(const float* own, const float* recv, const omr_sum_li
   a.write_set = write_set;
   a.wprefix = write_prefix;
   a.out = out;
-  a.units = units;
+  if (units > 0xFFFFFFFFull) return fail("shard_sum_list: %llu units", static_cast<unsigned long long>(units));
+  a.units = static_cast<uint32_t>(units);
   a.r0 = list->row_begin;
   a.cap = cap;
   a.lanes = num_lanes;

@@ -19,6 +19,48 @@ import tune_shard_r03 as s03  # noqa: E402
 from omr import _lib  # noqa: E402
 
 
+SRC4 = os.path.join(ROOT, "tools", "tune", "shard_r04.hip")
+LIB4 = os.path.join(ROOT, "build", "libtune_shard_r04.so")
+
+
+def load4():
+    """The stamped copy of the product kernel (tools/make_shard_r04.py writes its source)."""
+    if not os.path.exists(LIB4) or os.path.getmtime(LIB4) < os.path.getmtime(SRC4):
+        os.makedirs(os.path.dirname(LIB4), exist_ok=True)
+        import subprocess
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                        "-I" + os.path.join(ROOT, "include"), "-o", LIB4, SRC4], check=True)
+    lib = ctypes.CDLL(LIB4)
+    vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
+    lib.tune_shard4.argtypes = [vp, u32, vp, vp, vp, u32, u64, u64, vp, vp, u64, u64, u64, u32, u32, u32, vp, vp, vp]
+    lib.tune_shard4_list.argtypes = [vp, vp, vp, vp, u64, u32, u64, u32, vp, vp, vp]
+    return lib
+
+
+def timeline(tl, units, what, detail=False):
+    t = tl.view(-1, 8)[:units].cpu().numpy().astype(np.int64)
+    t = t[t[:, 0] > 0]
+    base = t[:, 0].min()
+    if detail:  # the end time by XCD and by the unit's pair count
+        end = (t[:, 4] - base) / 100.0
+        for x in sorted(set(t[:, 6].tolist())):
+            sel = t[:, 6] == x
+            print(f"  XCC {x}: {sel.sum():4d} waves, end p50 {np.median(end[sel]):6.2f} max {end[sel].max():6.2f}",
+                  flush=True)
+        for lo, hi in ((0, 16), (16, 24), (24, 32), (32, 48), (48, 64), (64, 999)):
+            sel = (t[:, 7] >= lo) & (t[:, 7] < hi)
+            if sel.any():
+                print(f"  pairs [{lo:3d},{hi:3d}): {sel.sum():4d} waves, end p50 {np.median(end[sel]):6.2f} "
+                      f"max {end[sel].max():6.2f}", flush=True)
+    print(f"## timeline ({what}, {len(t)} waves; us from the first wave's entry)", flush=True)
+    for col, name in ((0, "entry"), (1, "index consumed"), (2, "pairs written"), (3, "first window summed"),
+                      (4, "end, stores acked")):
+        vals = (t[t[:, col] > 0, col] - base) / 100.0
+        if vals.size:
+            print(f"  {name:22s} p10 {np.percentile(vals, 10):7.2f}  p50 {np.percentile(vals, 50):7.2f}  "
+                  f"p90 {np.percentile(vals, 90):7.2f}  max {vals.max():7.2f}", flush=True)
+
+
 def main():
     ap = r03.parser()
     ap.add_argument("--rotate", type=int, default=3)
@@ -51,7 +93,28 @@ def main():
                                           D["mstride"], 2 * rows, D["prefix"].data_ptr(), D["wset"].data_ptr(), L.n, B,
                                           NB, L.num_threads, r0, r1, 0, out.data_ptr(), st)
 
-    cases = {"round-3 kernel (copy)": r03k, "product (round 4)": prod}
+    # the pair list of shard 0, built once (the round builds it in its plan launch: omr_round_plan_ws / _list)
+    units_l, cap = ctypes.c_uint64(), ctypes.c_uint32()
+    _lib.check(lib.omr_sum_list_geometry(L.n, B, NB, L.num_threads, r0, r1, m, ctypes.byref(units_l),
+                                         ctypes.byref(cap)), "geometry")
+    lrec = torch.empty(units_l.value * cap.value, dtype=torch.int64, device=D["dev"])
+    lcnt = torch.empty(units_l.value, dtype=torch.int32, device=D["dev"])
+    sls = []
+    for k in range(len(sets)):  # (one list per input set: the same pairs, different receive buffers)
+        sl = _lib.SumList(lrec.data_ptr(), lcnt.data_ptr(), r0, r1, 2 * rows, 0)
+        for w in range(m):
+            sl.recv_offsets[w] = int(D["roff"][w])
+        sls.append(sl)
+    _lib.check(lib.omr_sum_list_build(D["masks_all"].data_ptr(), m, D["mstride"], L.n, B, NB, L.num_threads,
+                                      ctypes.byref(sls[0]), st), "omr_sum_list_build")
+
+    def plist(k, out):
+        x, rc = sets[k % len(sets)]
+        return lib.omr_shard_sum_list_f32(x.data_ptr(), rc.data_ptr(), ctypes.byref(sls[k % len(sets)]), m, L.n, B,
+                                          NB, L.num_threads, D["wset"].data_ptr(),
+                                          D["prefix"][m * (rows + 1):].data_ptr(), 0, out.data_ptr(), st)
+
+    cases = {"round-3 kernel (copy)": r03k, "product (round 4)": prod, "product, pair list (round 4)": plist}
     ref = D["xs"][0].clone()
     assert r03k(0, ref) == 0
     for name, f in cases.items():
@@ -71,12 +134,36 @@ def main():
             torch.cuda.synchronize()
             if r:
                 times[name].append(e0.elapsed_time(e1) / a.reps)
+    # the stamped copy: bit-exact too, then one stamped launch after the timed ones (inputs of a fresh set)
+    t4 = load4()
+    o = D["xs"][0].clone()
+    x, rc = sets[-1]
+    assert t4.tune_shard4(x.data_ptr(), 0, rc.data_ptr(), roff, D["masks_all"].data_ptr(), m, D["mstride"], 2 * rows,
+                          D["prefix"].data_ptr(), D["wset"].data_ptr(), rows, r0, r1, NB, D["S"], D["gps"],
+                          o.data_ptr(), tlb.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(o.view(torch.int32), ref.view(torch.int32)), "stamped copy"
     sbytes = 45898752
     print(f"## shard 0 of {m}, {units} units, {len(sets)} input sets: {sbytes} algorithmic bytes", flush=True)
     for name in sorted(cases, key=lambda c: np.median(times[c])):
         t = np.median(times[name]) * 1e-3
         print(f"{name:26s} median {t * 1e6:7.2f} us  {sbytes / t / 1e9:7.1f} GB/s  "
               f"(min {min(times[name]) * 1e3:.2f} max {max(times[name]) * 1e3:.2f} us)", flush=True)
+    for k in range(2):  # the product kernel's phases (stamped copy), a cold and a warm launch
+        tlb.zero_()
+        x, rc = sets[k % len(sets)]
+        t4.tune_shard4(x.data_ptr(), 0, rc.data_ptr(), roff, D["masks_all"].data_ptr(), m, D["mstride"], 2 * rows,
+                       D["prefix"].data_ptr(), D["wset"].data_ptr(), rows, r0, r1, NB, D["S"], D["gps"],
+                       outs[0].data_ptr(), tlb.data_ptr(), st)
+        torch.cuda.synchronize()
+        timeline(tlb, units, f"product kernel, stamped copy, launch {k}", detail=k == 1)
+    for k in range(2):  # the pair-list kernel's phases (index consumed = its records loaded)
+        tlb.zero_()
+        x, rc = sets[k % len(sets)]
+        t4.tune_shard4_list(x.data_ptr(), rc.data_ptr(), lrec.data_ptr(), lcnt.data_ptr(), units_l.value, cap.value,
+                            r0, NB, outs[0].data_ptr(), tlb.data_ptr(), st)
+        torch.cuda.synchronize()
+        timeline(tlb, units, f"pair-list kernel, stamped copy, launch {k}")
 
 
 if __name__ == "__main__":
