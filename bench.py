@@ -232,16 +232,18 @@ def read_pmc(path: str, workload: str, dist_mode: bool):
 
 def read_pmc_round(world: int, L: Layout):
     """(HBM bytes per launch, source) of the N>1 round's worker scan with the fused pack, from tools/pmc_round.py's
-    summary: measured at config 4's shapes as rank 0 of 8, so it describes only a world-8 line over 256 MiB, B=256."""
-    path = os.path.join(ROOT, "profiles", "pmc_round_r03.json")
+    newest summary (profiles/pmc_round_r*.json): measured at config 4's shapes as rank 0 of 8, so it describes only a
+    world-8 line over 256 MiB, B=256."""
     if world != 8 or L.nbytes != 256 << 20 or L.block_size != 256:
         return None, None
-    try:
-        with open(path) as f:
-            k = json.load(f)["kernels"]
-        return k["scan + fused pack (product)"]["hbm_bytes_per_launch"], path
-    except (OSError, ValueError, KeyError):
-        return None, None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_round_r*.json")), reverse=True):  # newest round
+        try:
+            with open(path) as f:
+                k = json.load(f)["kernels"]
+            return k["scan + fused pack (product)"]["hbm_bytes_per_launch"], path
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
 
 
 def cpu_baseline(L: Layout, bm: np.ndarray, args):

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 4 final check on one MI355X: the whole -m gpu suite, smoke, then every bench line with its profiles.  The bench
+# runs only if the suite ended normally (passed, or tests failed: rc 0 / 1).  Each GPU step under its own limit.
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-r04final}
+mkdir -p $O
+cd $R
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+  > $O/tests.log 2>&1
+rc=$?
+echo "suite rc=$rc" >> $O/tests.log
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+bash tools/gpu_bench_r04.sh ${1:-r04final}/bench

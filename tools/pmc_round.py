@@ -19,6 +19,7 @@ CASES = [  # (tune_round_r03 case filter, kernel name in the trace)
     ("scan (omr_worker_scan_f32)", "::k_scan1f<"),
     ("pack pass", "::k_move<"),
     ("round plan + chain (k_round_plan)", "::k_round_plan("),
+    ("round plan + chain, row chunks", "::k_round_plan2<"),
     ("round plan + chain + pair list", "::k_round_plan("),
 ]
 TIMED = 10  # the case's own launches (--rounds 2 --reps 5): the last ones of its kernel in the trace

@@ -208,6 +208,14 @@ def main():
                                        counts.data_ptr(), None, None, 0, None, None, 0, unext.data_ptr(), B,
                                        ctypes.byref(sl), st)
 
+    pws = torch.zeros(lib.omr_round_plan_workspace_words(), dtype=torch.int32, device=dev)
+
+    def plan_ws():  # round 4's row-chunk form (omr_round_plan_ws), the round's plan with the fused pack
+        return lib.omr_round_plan_ws(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                     naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                     counts.data_ptr(), None, None, 0, pws.data_ptr(), None, 0, unext.data_ptr(), B,
+                                     None, st)
+
     def list_only():  # the pair list in a launch of its own
         return lib.omr_sum_list_build(masks_all.data_ptr(), m, mstride, L.n, B, NB, L.num_threads, ctypes.byref(sl),
                                       st)
@@ -222,6 +230,7 @@ def main():
     workers = {"scan (omr_worker_scan_f32)": scan, "scan + fused pack (product)": scan_pack,
                "scan + fused pack (16-wave workgroups)": scan_pack16,
                "pack pass (k_move, round 2)": pack, "round plan + chain (k_round_plan)": plan,
+               "round plan + chain, row chunks (k_round_plan2)": plan_ws,
                "round plan + chain + pair list": plan_list, "pair list alone (k_sum_list)": list_only}
     cases = {**sums, **workers}
     if a.only:
@@ -262,6 +271,7 @@ def main():
     nrec = int(lcnt.sum().item())
     lbytes = m * (r1 - r0) * 8 + m * (ent // naggs) * 4 + nrec * 8 + units.value * 4
     wbytes["round plan + chain + pair list"] = wbytes["round plan + chain (k_round_plan)"] + lbytes
+    wbytes["round plan + chain, row chunks (k_round_plan2)"] = wbytes["round plan + chain (k_round_plan)"]
     wbytes["pair list alone (k_sum_list)"] = lbytes
     report = {}
     print(f"## config 4 shapes, {m} workers, -r {a.density}: shard 0 write set {ub} blocks, received {nc}, own {own_blocks}: "
