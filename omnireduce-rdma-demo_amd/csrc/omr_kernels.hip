@@ -1244,15 +1244,16 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
 // popcounts and their exclusive scans over the chunk come from registers; the chunk's per-array totals are published
 // (a flag per chunk) and each workgroup sums its predecessors' totals, which they all publish at about the same time
 // (no chain of look-backs).  A workgroup's chunk is a ticket taken when it starts, so every lower chunk belongs to a
-// workgroup that is already running (the look-back never waits on one that is not resident).  Workspace (uint32):
-// [0] the arrival counter, [1] the ticket counter, [2, 2 + kPlanChunksMax) the chunk flags, then the totals
-// [chunk][array]; the launch's last arrival leaves the counters and the flags zeroed again.
+// workgroup that is already running (the look-back never waits on one that is not resident).  A total is published as
+// total + 1, so its word doubles as its flag.  Workspace (uint32): [0] the arrival counter, [1] the ticket counter,
+// [2, 2 + kPlanChunksMax) reserved, then the totals [chunk][array]; the launch's last arrival zeroes them again.
 constexpr uint32_t kPlan2Threads = kWGThreads;
 constexpr uint32_t kPlanChunksMax = 64;  // rows <= 64 * 256 (larger plans keep k_round_plan)
 constexpr uint32_t kPlanArrays = OMR_MAX_WORKERS + 1;
 constexpr uint64_t kPlan2WorkspaceWords = 2 + kPlanChunksMax + static_cast<uint64_t>(kPlanChunksMax) * kPlanArrays;
 
-template <bool LIST>
+// W >= count: the per-array loops are unrolled over W workers + the write set (the launch picks 2, 4, 8 or 16)
+template <bool LIST, int W>
 __global__ __launch_bounds__(kPlan2Threads) void k_round_plan2(PlanArgs a, uint32_t nchunks, uint32_t* ws) {
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
   constexpr uint32_t kW = kPlan2Threads / 64;
@@ -1275,42 +1276,39 @@ __global__ __launch_bounds__(kPlan2Threads) void k_round_plan2(PlanArgs a, uint3
     }, a.chain.next);
     return;
   }
-  __shared__ uint32_t s_wtot[kW][kPlanArrays];
-  __shared__ uint32_t s_base[kPlanArrays];
+  constexpr uint32_t NW = W + 1;  // arrays unrolled: W workers, then the write set
+  __shared__ uint32_t s_wtot[kW][NW];
+  __shared__ uint32_t s_base[NW];
   __shared__ uint32_t s_ticket;
+  __shared__ uint64_t s_bounds[OMR_MAX_WORKERS + 2];
   if (t == 0) s_ticket = __hip_atomic_fetch_add(&ws[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t < a.nbounds) s_bounds[t] = a.bounds[t];
   __syncthreads();
   const uint32_t c = s_ticket;
   const uint32_t NA = a.count + 1;  // the workers' arrays, then the write set
   const uint64_t all_lanes = a.lanes >= 64 ? ~0ull : ((1ull << a.lanes) - 1ull);
-  uint32_t* const flags = ws + 2;
-  uint32_t* const totals = ws + 2 + kPlanChunksMax;
+  uint32_t* const totals = ws + 2 + kPlanChunksMax;  // (words [2, 2 + kPlanChunksMax): reserved)
   if (c == 0 && a.zero_cnt != nullptr && t < a.zero_cnt_n) a.zero_cnt[t] = 0;
   // ---- one round trip: row r = c * 256 + t of every worker's masks; union, write set, every array's popcount
   const uint64_t r = static_cast<uint64_t>(c) * kPlan2Threads + t;
   const bool in = r < a.rows;
-  uint64_t mk[OMR_MAX_WORKERS];
+  uint64_t mk[W];
 #pragma unroll
-  for (uint32_t w = 0; w < OMR_MAX_WORKERS; ++w)
+  for (uint32_t w = 0; w < W; ++w)
     mk[w] = (w < a.count && in) ? a.masks[static_cast<uint64_t>(w) * a.mstride + r] : 0ull;
   uint64_t u = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < OMR_MAX_WORKERS; ++w) u |= mk[w];
+  for (uint32_t w = 0; w < W; ++w) u |= mk[w];
   const uint64_t wsr = in ? ((r % a.rpp == 0) ? (u | all_lanes) : u) : 0ull;  // union + lane heads (client.cc:201-205)
-  if (in) {
-    a.write_set[r] = wsr;
-    a.union_masks[r] = u;
-    if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
-  }
   // ---- per array: the chunk's exclusive prefix at this row (wave scan, then the earlier waves' totals), the total
-  uint32_t pfx[kPlanArrays];
+  uint32_t pfx[NW];
 #pragma unroll
-  for (uint32_t arr = 0; arr < kPlanArrays; ++arr) {  // (the row's popcounts first: the masks are dead after this)
-    const uint64_t bits = arr < OMR_MAX_WORKERS ? mk[arr] : 0ull;
+  for (uint32_t arr = 0; arr < NW; ++arr) {  // (the row's popcounts first: the masks are dead after this)
+    const uint64_t bits = arr < W ? mk[arr] : 0ull;
     pfx[arr] = arr < NA ? static_cast<uint32_t>(__builtin_popcountll(arr == a.count ? wsr : bits)) : 0u;
   }
 #pragma unroll
-  for (uint32_t arr = 0; arr < kPlanArrays; ++arr) {
+  for (uint32_t arr = 0; arr < NW; ++arr) {
     const uint32_t v = pfx[arr];
     uint32_t inc = v;
 #pragma unroll
@@ -1321,10 +1319,11 @@ __global__ __launch_bounds__(kPlan2Threads) void k_round_plan2(PlanArgs a, uint3
     pfx[arr] = inc - v;
     if (lane == 63) s_wtot[wave][arr] = inc;
   }
+  if (t < NW) s_base[t] = 0;
   __syncthreads();
-  uint32_t ctot[kPlanArrays];
+  uint32_t ctot[NW];
 #pragma unroll
-  for (uint32_t arr = 0; arr < kPlanArrays; ++arr) {
+  for (uint32_t arr = 0; arr < NW; ++arr) {
     uint32_t before = 0, all = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kW; ++w) {
@@ -1335,55 +1334,68 @@ __global__ __launch_bounds__(kPlan2Threads) void k_round_plan2(PlanArgs a, uint3
     pfx[arr] += before;
     ctot[arr] = all;
   }
-  // ---- publish the chunk's totals, then add the predecessors' (every chunk publishes before it looks back)
-  if (t == 0) {
-#pragma unroll
-    for (uint32_t arr = 0; arr < kPlanArrays; ++arr)
-      if (arr < NA) __hip_atomic_store(&totals[c * kPlanArrays + arr], ctot[arr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&flags[c], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // thread i < c waits for chunk i, whose workgroup took its ticket first: it is running or done
-  if (t < c)
-    while (__hip_atomic_load(&flags[t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) __builtin_amdgcn_s_sleep(1);
-  __syncthreads();
+  // ---- publish the chunk's totals (stored + 1: a zero word is "not yet"), then add the predecessors': thread
+  // (i, arr) waits for chunk i's total of array arr, whose workgroup took its ticket first (it is running or done)
   if (t < NA) {
-    uint32_t b = 0;
-    for (uint32_t i = 0; i < c; ++i)
-      b += __hip_atomic_load(&totals[i * kPlanArrays + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_base[t] = b;
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t arr = 0; arr < NW; ++arr) v = arr == t ? ctot[arr] : v;
+    __hip_atomic_store(&totals[c * kPlanArrays + t], v + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (uint32_t idx = t; idx < c * NA; idx += kPlan2Threads) {
+    const uint32_t i = idx / NA, arr = idx - i * NA;
+    uint32_t v;
+    while ((v = __hip_atomic_load(&totals[i * kPlanArrays + arr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+      __builtin_amdgcn_s_sleep(1);
+    atomicAdd(&s_base[arr], v - 1u);
   }
   __syncthreads();
-  // ---- prefixes, the counts at the shard bounds (system-scope stores: the host reads them), the totals
+  // ---- this chunk's rows: write set, union, own masks cleared, prefixes, the counts at the shard bounds
+  //      (system-scope stores: the host reads them), the totals
+  if (in) {
+    a.write_set[r] = wsr;
+    a.union_masks[r] = u;
+    if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
+  }
+  uint32_t bnd = kNone;  // the shard bound this row starts, if any (bounds are distinct except empty shards)
+  for (uint32_t s = 0; s < a.nbounds; ++s)
+    if (s_bounds[s] == r && in) bnd = s;
   if (in) {
 #pragma unroll
-    for (uint32_t arr = 0; arr < kPlanArrays; ++arr) {
+    for (uint32_t arr = 0; arr < NW; ++arr) {
       if (arr >= NA) continue;
       const uint32_t pv = s_base[arr] + pfx[arr];
       a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + r] = pv;
-      for (uint32_t s = 0; s < a.nbounds; ++s)
-        if (a.bounds[s] == r)
-          __hip_atomic_store(&a.counts[arr * a.nbounds + s], pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (bnd != kNone)  // (every bound equal to this row: empty shards repeat a bound)
+        for (uint32_t s = 0; s < a.nbounds; ++s)
+          if (s_bounds[s] == r)
+            __hip_atomic_store(&a.counts[arr * a.nbounds + s], pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   if (c + 1 == nchunks && t == 0) {
 #pragma unroll
-    for (uint32_t arr = 0; arr < kPlanArrays; ++arr) {
+    for (uint32_t arr = 0; arr < NW; ++arr) {
       if (arr >= NA) continue;
       const uint32_t total = s_base[arr] + ctot[arr];
       a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + a.rows] = total;
       for (uint32_t s = 0; s < a.nbounds; ++s)
-        if (a.bounds[s] >= a.rows)
+        if (s_bounds[s] >= a.rows)
           __hip_atomic_store(&a.counts[arr * a.nbounds + s], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   // ---- completion: every chunk's counts acknowledged (write-through, system scope), then the last arrival re-arms
-  // the workspace and posts the round's sequence number
+  // the workspace (every chunk is past its look-back: nothing reads the totals any more) and posts the sequence number
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __shared__ uint32_t s_last;
   __syncthreads();
-  if (t == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == nchunks) {  // every chunk is past its look-back: nothing reads the flags any more
-      for (uint32_t i = 0; i < nchunks; ++i) __hip_atomic_store(&flags[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) s_last = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == nchunks;
+  __syncthreads();
+  if (s_last) {
+    for (uint32_t idx = t; idx < nchunks * kPlanArrays; idx += kPlan2Threads)
+      __hip_atomic_store(&totals[idx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
       __hip_atomic_store(&ws[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&ws[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.done_flag != nullptr) __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2634,8 +2646,19 @@ int round_plan_launch(const uint64_t* row_masks, uint32_t count, uint64_t mask_s
     }
     a.arrive = nullptr;  // (k_round_plan2 counts its arrivals in the workspace)
     const unsigned grid = static_cast<unsigned>(nchunks + chain_wgs + a.list_wgs);
-    if (list != nullptr) k_round_plan2<true><<<grid, kPlan2Threads, 0, st>>>(a, static_cast<uint32_t>(nchunks), arrive);
-    else k_round_plan2<false><<<grid, kPlan2Threads, 0, st>>>(a, static_cast<uint32_t>(nchunks), arrive);
+    const uint32_t nc = static_cast<uint32_t>(nchunks);
+    if (list != nullptr) {
+      if (count <= 8) k_round_plan2<true, 8><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
+      else k_round_plan2<true, OMR_MAX_WORKERS><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
+    } else if (count <= 2) {
+      k_round_plan2<false, 2><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
+    } else if (count <= 4) {
+      k_round_plan2<false, 4><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
+    } else if (count <= 8) {
+      k_round_plan2<false, 8><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
+    } else {
+      k_round_plan2<false, OMR_MAX_WORKERS><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
+    }
     return launch_status("k_round_plan2");
   }
   const size_t lds = rows <= kPlanLdsRows ? rows * sizeof(uint64_t) : 0;

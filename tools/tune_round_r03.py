@@ -216,6 +216,16 @@ def main():
                                      counts.data_ptr(), None, None, 0, pws.data_ptr(), None, 0, unext.data_ptr(), B,
                                      None, st)
 
+    def plan_nochain():  # the plan without the aggregator chain (round 3's form)
+        return lib.omr_round_plan_ex(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                     naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                     counts.data_ptr(), None, None, 0, None, None, 0, None, B, st)
+
+    def plan_ws_nochain():  # the row-chunk form without the chain
+        return lib.omr_round_plan_ws(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                     naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                     counts.data_ptr(), None, None, 0, pws.data_ptr(), None, 0, None, B, None, st)
+
     def list_only():  # the pair list in a launch of its own
         return lib.omr_sum_list_build(masks_all.data_ptr(), m, mstride, L.n, B, NB, L.num_threads, ctypes.byref(sl),
                                       st)
@@ -231,6 +241,8 @@ def main():
                "scan + fused pack (16-wave workgroups)": scan_pack16,
                "pack pass (k_move, round 2)": pack, "round plan + chain (k_round_plan)": plan,
                "round plan + chain, row chunks (k_round_plan2)": plan_ws,
+               "round plan, no chain (k_round_plan)": plan_nochain,
+               "round plan, no chain, row chunks (k_round_plan2)": plan_ws_nochain,
                "round plan + chain + pair list": plan_list, "pair list alone (k_sum_list)": list_only}
     cases = {**sums, **workers}
     if a.only:
@@ -272,6 +284,8 @@ def main():
     lbytes = m * (r1 - r0) * 8 + m * (ent // naggs) * 4 + nrec * 8 + units.value * 4
     wbytes["round plan + chain + pair list"] = wbytes["round plan + chain (k_round_plan)"] + lbytes
     wbytes["round plan + chain, row chunks (k_round_plan2)"] = wbytes["round plan + chain (k_round_plan)"]
+    wbytes["round plan, no chain (k_round_plan)"] = wbytes["round plan + chain (k_round_plan)"] - L.nb * 4
+    wbytes["round plan, no chain, row chunks (k_round_plan2)"] = wbytes["round plan, no chain (k_round_plan)"]
     wbytes["pair list alone (k_sum_list)"] = lbytes
     report = {}
     print(f"## config 4 shapes, {m} workers, -r {a.density}: shard 0 write set {ub} blocks, received {nc}, own {own_blocks}: "
