@@ -20,6 +20,7 @@ from omr import _lib  # noqa: E402
 
 
 SRC4 = os.path.join(ROOT, "tools", "tune", "shard_r04.hip")
+POLICIES = ("plain", "nt", "sc0 sc1")
 LIB4 = os.path.join(ROOT, "build", "libtune_shard_r04.so")
 
 
@@ -32,7 +33,8 @@ def load4():
                         "-I" + os.path.join(ROOT, "include"), "-o", LIB4, SRC4], check=True)
     lib = ctypes.CDLL(LIB4)
     vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
-    lib.tune_shard4.argtypes = [vp, u32, vp, vp, vp, u32, u64, u64, vp, vp, u64, u64, u64, u32, u32, u32, vp, vp, vp]
+    lib.tune_shard4.argtypes = [vp, u32, vp, vp, vp, u32, u64, u64, vp, vp, u64, u64, u64, u32, u32, u32, vp, vp, vp,
+                                ctypes.c_int]
     lib.tune_shard4_list.argtypes = [vp, vp, vp, vp, u64, u32, u64, u32, vp, vp, vp]
     return lib
 
@@ -114,7 +116,19 @@ def main():
                                           NB, L.num_threads, D["wset"].data_ptr(),
                                           D["prefix"][m * (rows + 1):].data_ptr(), 0, out.data_ptr(), st)
 
+    t4 = load4()
+
+    def stamped(policy):
+        def f(k, out):
+            x, rc = sets[k % len(sets)]
+            return t4.tune_shard4(x.data_ptr(), 0, rc.data_ptr(), roff, D["masks_all"].data_ptr(), m, D["mstride"],
+                                  2 * rows, D["prefix"].data_ptr(), D["wset"].data_ptr(), rows, r0, r1, NB, D["S"],
+                                  D["gps"], out.data_ptr(), tlb.data_ptr(), st, policy)
+        return f
+
     cases = {"round-3 kernel (copy)": r03k, "product (round 4)": prod, "product, pair list (round 4)": plist}
+    for pol, pname in enumerate(POLICIES):
+        cases[f"stamped copy, {pname} stores"] = stamped(pol)
     ref = D["xs"][0].clone()
     assert r03k(0, ref) == 0
     for name, f in cases.items():
@@ -134,29 +148,18 @@ def main():
             torch.cuda.synchronize()
             if r:
                 times[name].append(e0.elapsed_time(e1) / a.reps)
-    # the stamped copy: bit-exact too, then one stamped launch after the timed ones (inputs of a fresh set)
-    t4 = load4()
-    o = D["xs"][0].clone()
-    x, rc = sets[-1]
-    assert t4.tune_shard4(x.data_ptr(), 0, rc.data_ptr(), roff, D["masks_all"].data_ptr(), m, D["mstride"], 2 * rows,
-                          D["prefix"].data_ptr(), D["wset"].data_ptr(), rows, r0, r1, NB, D["S"], D["gps"],
-                          o.data_ptr(), tlb.data_ptr(), st) == 0
-    torch.cuda.synchronize()
-    assert torch.equal(o.view(torch.int32), ref.view(torch.int32)), "stamped copy"
     sbytes = 45898752
     print(f"## shard 0 of {m}, {units} units, {len(sets)} input sets: {sbytes} algorithmic bytes", flush=True)
     for name in sorted(cases, key=lambda c: np.median(times[c])):
         t = np.median(times[name]) * 1e-3
         print(f"{name:26s} median {t * 1e6:7.2f} us  {sbytes / t / 1e9:7.1f} GB/s  "
               f"(min {min(times[name]) * 1e3:.2f} max {max(times[name]) * 1e3:.2f} us)", flush=True)
-    for k in range(2):  # the product kernel's phases (stamped copy), a cold and a warm launch
-        tlb.zero_()
-        x, rc = sets[k % len(sets)]
-        t4.tune_shard4(x.data_ptr(), 0, rc.data_ptr(), roff, D["masks_all"].data_ptr(), m, D["mstride"], 2 * rows,
-                       D["prefix"].data_ptr(), D["wset"].data_ptr(), rows, r0, r1, NB, D["S"], D["gps"],
-                       outs[0].data_ptr(), tlb.data_ptr(), st)
-        torch.cuda.synchronize()
-        timeline(tlb, units, f"product kernel, stamped copy, launch {k}", detail=k == 1)
+    for pol, pname in enumerate(POLICIES):  # the product kernel's phases (stamped copy), a cold and a warm launch
+        for k in range(2):
+            tlb.zero_()
+            stamped(pol)(k, outs[0])
+            torch.cuda.synchronize()
+            timeline(tlb, units, f"product kernel, stamped copy, {pname} stores, launch {k}", detail=k == 1 and pol == 0)
     for k in range(2):  # the pair-list kernel's phases (index consumed = its records loaded)
         tlb.zero_()
         x, rc = sets[k % len(sets)]
