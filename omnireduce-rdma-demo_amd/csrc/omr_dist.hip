@@ -180,10 +180,16 @@ struct RcclDist final : omr_dist {
     }
     return 0;
   }
+  // A one-rank group's collectives are copies: RCCL queues the same copy kernel for them, after 5-10 us of host-side
+  // group set-up per call (the world-1 round's host trace, profiles/r04/round_w1_trace/host_laps.txt), so they are
+  // issued as the copy directly.
   int do_allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
+    if (world == 1)
+      return in == out ? 0 : hip_check(hipMemcpyAsync(out, in, bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
     return nccl_check(ncclAllGather(in, out, bytes, ncclUint8, comm, st), "ncclAllGather");
   }
   int do_exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
+    if (world == 1) return fault(0);  // no peers: nothing to send or receive
     TRY(nccl_check(ncclGroupStart(), "ncclGroupStart"));
     // The group is closed on every path: a group left open would capture every later RCCL call of this thread (the
     // next round's all-gather and exchange would be queued into it and never launched).  After a failed piece the
@@ -205,6 +211,10 @@ struct RcclDist final : omr_dist {
     return rc ? rc : rc_end;
   }
   int do_reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
+    if (world == 1)
+      return in == out ? 0
+                       : hip_check(hipMemcpyAsync(out, in, count * sizeof(float), hipMemcpyDeviceToDevice, st),
+                                   "hipMemcpyAsync");
     return nccl_check(ncclReduceScatter(in, out, count, ncclFloat32, ncclSum, xcomm, st), "ncclReduceScatter");
   }
 };
@@ -928,7 +938,11 @@ struct omr_ar_plan {
   uint64_t mstride = 0;           // uint64 words per rank in masks_all (rows without the fused pack)
   // per-round state, kSets sets used in turn: an asynchronous round's bookkeeping and exchange still read their
   // set while the next rounds' scans fill the others
-  static constexpr int kSets = 3;
+  // Four sets by default: one more round between a set's plan and the scan that refills it.  With three the world-1
+  // round took 58.1-64.1 us, with four 56.9-57.3 (defer, 3 runs each; profiles/r04/round_sets/).  OMR_ROUND_SETS=3:
+  // three.
+  static constexpr int kSets = 4;
+  int nsets = kSets;
   struct Set {
     uint64_t* own = nullptr;        // [mstride] this rank's masks (the scan ORs into them; the plan kernel re-zeroes
                                     // them), then (fused pack) its position table
@@ -1354,7 +1368,9 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   // its stream 1.2 us instead of 2.8, tools/event_cost.hip); what the host reads goes out as system-scope stores
   const char* sf = getenv("OMR_EVENT_SYSFENCE");
   const unsigned evflags = hipEventDisableTiming | ((sf != nullptr && atoi(sf) != 0) ? 0u : hipEventDisableSystemFence);
-  for (auto& st : p->set) {
+  if (const char* ns = getenv("OMR_ROUND_SETS")) p->nsets = atoi(ns) == 3 ? 3 : omr_ar_plan::kSets;
+  for (int i = 0; i < p->nsets; ++i) {
+    omr_ar_plan::Set& st = p->set[i];
     A(dev_alloc(p->d, &st.own, p->mstride));
     A(dev_alloc(p->d, &st.masks_all, static_cast<size_t>(N) * p->mstride));
     if (p->fused_pack) A(dev_alloc(p->d, &st.pack_cnt, NA));
@@ -1388,7 +1404,8 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, evflags), "hipEventCreate"));
   A(dev_alloc(p->d, &p->bounds_dev, NA + 1));
   if (N > 1 && p->shard >= 0)
-    for (auto& st : p->set) A(dev_alloc(p->d, &st.recv, static_cast<size_t>(M) * p->shard_nb * block_size));
+    for (int i = 0; i < p->nsets; ++i)
+      A(dev_alloc(p->d, &p->set[i].recv, static_cast<size_t>(M) * p->shard_nb * block_size));
   A(dev_alloc(p->d, &p->results, n));
   A(dev_alloc(p->d, &p->flags_ws, p->nb));
   A(dev_alloc(p->d, &p->next_ws, p->nb));
@@ -1403,13 +1420,12 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
                 "hipHostGetDevicePointer"));
   const uint64_t plan_ws_words = omr_round_plan_workspace_words();
   A(dev_alloc(p->d, &p->arrive, plan_ws_words));
-  // Which plan form.  Beside the world-1 round's scan (92 VGPRs, one 16-wave workgroup per CU) the row-chunk
-  // workgroups fit and run starved next to it: the world-1 round measured 64.8-67.9 us with them against 58.8-60.2 us
-  // with round 3's form, which waits for the scan's workgroups to drain (profiles/r04/plan_ab/).  The fused-pack scan of
-  // N > 1 (128 VGPRs, two 8-wave workgroups per CU) leaves no room for either, and a 256-thread workgroup needs only
-  // one of its workgroups to leave a CU, so rounds with the fused pack take the row-chunk form.  OMR_PLAN_V1=0 / 1
-  // forces one (study knob).
-  p->plan_v1 = !p->fused_pack;
+  // Which plan form.  Round 3's (one 1024-thread workgroup per mask array) by default: standalone it takes 11.95 us at
+  // config 4's shapes against 13.4 for the row-chunk form (profiles/r04/round_kernels/), and beside the world-1
+  // round's scan the row-chunk workgroups fit and run starved next to it (the world-1 round: 64.8-67.9 us with them,
+  // 58.8-60.2 with round 3's form; profiles/r04/plan_ab/).  Rehearsed as 2 and 4 IPC ranks on one GPU, with the fused
+  // pack, the two forms were within the runs' spread.  OMR_PLAN_V1=0 selects the row-chunk form (omr_round_plan_ws).
+  p->plan_v1 = true;
   if (const char* pv = getenv("OMR_PLAN_V1")) p->plan_v1 = atoi(pv) != 0;
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), NSETS * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
@@ -1419,10 +1435,11 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
                 "hipHostGetDevicePointer"));
   }
   if (rc == 0) A(hip_check(hipMemset(p->arrive, 0, plan_ws_words * sizeof(uint32_t)), "hipMemset plan workspace"));
-  for (auto& st : p->set)
-    if (rc == 0) A(hip_check(hipMemset(st.own, 0, p->mstride * sizeof(uint64_t)), "hipMemset own masks"));
-  for (auto& st : p->set)
+  for (int i = 0; i < p->nsets && rc == 0; ++i) {
+    omr_ar_plan::Set& st = p->set[i];
+    A(hip_check(hipMemset(st.own, 0, p->mstride * sizeof(uint64_t)), "hipMemset own masks"));
     if (rc == 0 && st.pack_cnt) A(hip_check(hipMemset(st.pack_cnt, 0, NA * sizeof(uint32_t)), "hipMemset pack counters"));
+  }
   if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset scan ws"));
   if (rc == 0)
     A(hip_check(hipMemcpy(p->bounds_dev, p->bounds.data(), (NA + 1) * sizeof(uint64_t), hipMemcpyHostToDevice),
@@ -1892,7 +1909,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
   }
   const int si = p->cur;
   omr_ar_plan::Set& S = p->set[si];
-  p->cur = (p->cur + 1) % omr_ar_plan::kSets;
+  p->cur = (p->cur + 1) % p->nsets;
   // A one-rank group's aggregator sums one worker's blocks: its shard sum is 0.0f + x over the write set (the worker's
   // non-zero blocks and the lane heads), exactly what the worker scan writes when it is given `out` (k_scan1f, as
   // the single-GPU step).  So the scan writes the sums, and the second half skips the shard sum and the unpack.  (Not
@@ -1908,7 +1925,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
   if (threaded) {  // that plan has been issued (and this set's `scanned` waited for) by the progress thread
     HostWait hw(p);
     std::unique_lock<std::mutex> lk(p->mu);
-    const uint64_t need = p->rounds_begun >= omr_ar_plan::kSets - 1 ? p->rounds_begun - (omr_ar_plan::kSets - 1) : 0;
+    const uint64_t need = p->rounds_begun >= static_cast<uint64_t>(p->nsets - 1) ? p->rounds_begun - (p->nsets - 1) : 0;
     p->cv_done.wait(lk, [&] { return p->first_halves >= need || p->thread_rc != 0; });
     if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
   }
@@ -1922,7 +1939,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
   const bool pack_scan = p->fused_pack && p->worker() && mode != OMR_ROUND_DENSE_REDUCE_SCATTER;
   if (pack_scan) {
     std::unique_lock<std::mutex> lk(p->mu);
-    const uint64_t need = p->rounds_begun >= omr_ar_plan::kSets ? p->rounds_begun - (omr_ar_plan::kSets - 1) : 0;
+    const uint64_t need = p->rounds_begun >= static_cast<uint64_t>(p->nsets) ? p->rounds_begun - (p->nsets - 1) : 0;
     if (threaded) {
       HostWait hw(p);
       p->cv_done.wait(lk, [&] { return p->second_halves >= need || p->thread_rc != 0; });

@@ -122,6 +122,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float* base, 
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, static_cast<int>(bytes), 0x00020000);
 }
 
+// A wave's store of one block (VEC dwordx4 per lane) at a wave-uniform address, with kStoreAux (write-through): the
+// packed and summed blocks of the round's kernels leave no dirty lines in the XCD L2s either.  Plain stores did, and
+// the kernel-end write-back of them ran after the last wave: the shard sum took 15.3 us with these stores against
+// 16.8 with plain ones (stamped copies, profiles/r04/shard/shard_store_policy.log).
+template <int VEC>
+__device__ __forceinline__ void store_block_wt(float* dst, const v4f* v, int lane) {
+  const uint64_t a = reinterpret_cast<uint64_t>(dst);
+  const uint64_t u = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32))) << 32) |
+                     static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a)));
+  const __amdgpu_buffer_rsrc_t r = chunk_rsrc(reinterpret_cast<float*>(u), VEC * 1024u);
+#pragma unroll
+  for (int q = 0; q < VEC; ++q)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v[q]), r, (q * 64 + lane) * 16, 0, kStoreAux);
+}
+
 template <int VEC>
 __global__ __launch_bounds__(64 * kScanWaves) void k_scan1(ScanArgs a) {
   constexpr int B4 = 64 * VEC;  // 16-byte vectors per block
@@ -407,9 +422,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
         const uint64_t wb = static_cast<uint64_t>(base) + s_wpre[wave];
         for (uint32_t j = 0; j < taken; ++j) {  // stashed: the j-th from the top has rank cnt_w - 1 - j
           const v4f* const slot = stash + (static_cast<uint64_t>(wave) * a.wcap + j) * B4;
-          v4f* const d = reinterpret_cast<v4f*>(sbase + (wb + cnt_w - 1 - j) * a.block);
+          v4f t[VEC];
 #pragma unroll
-          for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = slot[q * 64 + lane];
+          for (int q = 0; q < VEC; ++q) t[q] = slot[q * 64 + lane];
+          store_block_wt<VEC>(sbase + (wb + cnt_w - 1 - j) * a.block, t, lane);
         }
         // the rest (the wave's lowest cnt_w - taken non-zero rows, in order): re-read, from `out` when the scan wrote
         // 0.0f + x there (the same bits), else from x
@@ -425,9 +441,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
             const uint32_t r = b0 + static_cast<uint32_t>(__builtin_ctz(m));
             m &= m - 1;
             const v4f* const sp = reinterpret_cast<const v4f*>(rsrc + ((row0 + r) * a.lanes + l) * a.block);
-            v4f* const d = reinterpret_cast<v4f*>(sbase + (wb + idx) * a.block);
+            v4f t[VEC];
 #pragma unroll
-            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = sp[q * 64 + lane];
+            for (int q = 0; q < VEC; ++q) t[q] = sp[q * 64 + lane];
+            store_block_wt<VEC>(sbase + (wb + idx) * a.block, t, lane);
             ++idx;
           }
         }
@@ -995,7 +1012,11 @@ __device__ __forceinline__ uint64_t plan_row(const uint64_t* masks, uint32_t a, 
 }
 
 constexpr uint64_t kRowStreams = ~0ull;
-constexpr uint32_t kSumUnitRows = 32;
+constexpr uint32_t kSumUnitRows = 32;    // the pair list's unit: 32 rows x one lane (half a 64-row group)
+// k_shard_sum's unit rows (a divisor of the 64-row group).  16: 2048 waves at config 4's 8-worker shard, two per
+// SIMD, nearly all of them one window (<= 32 pairs); with 32-row units 11 % of the waves needed a second window, a
+// round trip after everyone else's (14.16 against 15.35 us, stamped copies, profiles/r04/shard/)
+constexpr uint32_t kShardUnitRows = 16;
 // a pair record: source block (bits 0-31: in `own` or in `recv`), destination block (32-59), flags
 constexpr uint64_t kRecOwn = 1ull << 60, kRecZero = 1ull << 61, kRecFirst = 1ull << 62, kRecLast = 1ull << 63;
 // a pair list's unit ends with this word (no real record has every bit set: destinations are < 2^28 blocks), so the
@@ -1461,7 +1482,7 @@ __global__ __launch_bounds__(kWGThreads) void k_move(MoveArgs a) {
 #pragma unroll
         for (int q = 0; q < VEC; ++q)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v[j][q]), rt,
-                                                 (off + (q * 64 + lane) * 16) | drop, 0, 0);
+                                                 (off + (q * 64 + lane) * 16) | drop, 0, kStoreAux);
       }
       k += nv;
     }
@@ -1504,12 +1525,13 @@ struct SumArgs {
 
 
 // W >= count: the contributor loops are unrolled W times (the launch picks 2, 4, 8 or 16), so an 8-worker shard does
-// half the per-row work of a 16-way unroll.
-template <int VEC, int W>
+// half the per-row work of a 16-way unroll.  UR: rows per unit.
+template <int VEC, int W, uint32_t UR = kShardUnitRows>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
   constexpr int P = 32 / VEC;  // pair slots per window
   constexpr int kSlotGroup = P < 8 ? P : 8;
-  constexpr uint32_t kRecCap = kSumUnitRows * W;
+  constexpr uint32_t kRecCap = UR * W;
+  constexpr uint32_t QU = kPackGroupRows / UR;  // units per 64-row group (column streams)
   __shared__ uint64_t s_rec[kWavesPerWG][kRecCap];
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1524,19 +1546,19 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
     uint32_t nload, h0, h1;  // rows loaded; the unit's rows are lanes [h0, h1)
     if (cols) {
       uint32_t t = u >> a.lane_shift;
-      const uint32_t h = t & 1u;
-      t >>= 1;
+      const uint32_t h = t % QU;
+      t /= QU;
       const uint32_t j = t % a.gps;
       const uint64_t seg = a.seg0 + t / a.gps;
       g0 = seg * a.S + static_cast<uint64_t>(j) * kPackGroupRows;
       nload = a.S - j * kPackGroupRows < kPackGroupRows ? a.S - j * kPackGroupRows : kPackGroupRows;
-      h0 = h * kSumUnitRows;
-      h1 = nload < h0 + kSumUnitRows ? nload : h0 + kSumUnitRows;
+      h0 = h * UR;
+      h1 = nload < h0 + UR ? nload : h0 + UR;
       gidx = seg * a.gps + j;
       if (h0 >= h1) continue;
     } else {
-      g0 = a.r0 + static_cast<uint64_t>(u >> a.lane_shift) * kSumUnitRows;
-      nload = a.r1 - g0 < kSumUnitRows ? static_cast<uint32_t>(a.r1 - g0) : kSumUnitRows;
+      g0 = a.r0 + static_cast<uint64_t>(u >> a.lane_shift) * UR;
+      nload = a.r1 - g0 < UR ? static_cast<uint32_t>(a.r1 - g0) : UR;
       h0 = 0;
       h1 = nload;
     }
@@ -1661,9 +1683,7 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
         if (static_cast<uint32_t>(j) < nv) {
           const uint64_t rc = readlane64(myrec, j);
           if (rc & kRecLast) {
-            v4f* const d = reinterpret_cast<v4f*>(a.out + ((rc >> 32) & 0x0FFFFFFFull) * a.block);
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = v[j][q];
+            store_block_wt<VEC>(a.out + ((rc >> 32) & 0x0FFFFFFFull) * a.block, v[j], lane);
           }
         }
       }
@@ -1773,9 +1793,7 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
           const uint64_t rc = readlane64(chunk, cb + j);
           if (rc & kRecLast) {
             const uint64_t dst = a.packed_out ? readlane64(pdst, cb + j) : ((rc >> 32) & 0x0FFFFFFFull);
-            v4f* const d = reinterpret_cast<v4f*>(a.out + dst * a.block);
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) d[q * 64 + lane] = v[j][q];
+            store_block_wt<VEC>(a.out + dst * a.block, v[j], lane);
           }
         }
       }
@@ -2768,8 +2786,8 @@ int launch_shard_sum(const SumArgs& a0, const uint64_t* recv_offsets, hipStream_
     if (c < a.count && c != a.me && a.recv_off[c] > 0xFFFFFFFFull) return fail("shard_sum: recv offset beyond 2^32 blocks");
   }
   const uint64_t srows = a.r1 - a.r0;
-  const uint64_t units = a.pos_off != kRowStreams ? (srows / a.S) * a.gps * 2 * a.lanes
-                                                 : ((srows + kSumUnitRows - 1) / kSumUnitRows) * a.lanes;
+  const uint64_t units = a.pos_off != kRowStreams ? (srows / a.S) * a.gps * (kPackGroupRows / kShardUnitRows) * a.lanes
+                                                 : ((srows + kShardUnitRows - 1) / kShardUnitRows) * a.lanes;
   if (units > 0xFFFFFFFFull) return fail("shard_sum: %llu units", static_cast<unsigned long long>(units));
   a.units = static_cast<uint32_t>(units);
   a.lane_shift = static_cast<uint32_t>(__builtin_ctz(a.lanes));

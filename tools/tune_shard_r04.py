@@ -118,17 +118,18 @@ def main():
 
     t4 = load4()
 
-    def stamped(policy):
+    def stamped(policy, ur=32):
         def f(k, out):
             x, rc = sets[k % len(sets)]
             return t4.tune_shard4(x.data_ptr(), 0, rc.data_ptr(), roff, D["masks_all"].data_ptr(), m, D["mstride"],
                                   2 * rows, D["prefix"].data_ptr(), D["wset"].data_ptr(), rows, r0, r1, NB, D["S"],
-                                  D["gps"], out.data_ptr(), tlb.data_ptr(), st, policy)
+                                  D["gps"], out.data_ptr(), tlb.data_ptr(), st, policy, ur)
         return f
 
     cases = {"round-3 kernel (copy)": r03k, "product (round 4)": prod, "product, pair list (round 4)": plist}
     for pol, pname in enumerate(POLICIES):
         cases[f"stamped copy, {pname} stores"] = stamped(pol)
+    cases["stamped copy, sc0 sc1 stores, 16-row units"] = stamped(2, 16)
     ref = D["xs"][0].clone()
     assert r03k(0, ref) == 0
     for name, f in cases.items():
@@ -154,12 +155,13 @@ def main():
         t = np.median(times[name]) * 1e-3
         print(f"{name:26s} median {t * 1e6:7.2f} us  {sbytes / t / 1e9:7.1f} GB/s  "
               f"(min {min(times[name]) * 1e3:.2f} max {max(times[name]) * 1e3:.2f} us)", flush=True)
-    for pol, pname in enumerate(POLICIES):  # the product kernel's phases (stamped copy), a cold and a warm launch
+    for pol, ur in ((0, 32), (2, 32), (2, 16)):  # the product kernel's phases (stamped copy), a cold and a warm launch
         for k in range(2):
             tlb.zero_()
-            stamped(pol)(k, outs[0])
+            stamped(pol, ur)(k, outs[0])
             torch.cuda.synchronize()
-            timeline(tlb, units, f"product kernel, stamped copy, {pname} stores, launch {k}", detail=k == 1 and pol == 0)
+            timeline(tlb, units * 32 // ur, f"product kernel, stamped copy, {POLICIES[pol]} stores, {ur}-row units, "
+                     f"launch {k}", detail=k == 1)
     for k in range(2):  # the pair-list kernel's phases (index consumed = its records loaded)
         tlb.zero_()
         x, rc = sets[k % len(sets)]
