@@ -932,7 +932,8 @@ struct omr_ar_plan {
   // power-of-two layout); otherwise (ragged shards, or OMR_PACK_MOVE=1) the round packs with omr_move_blocks_f32.
   // Each rank's all-gathered array is then its masks followed by its position table: mstride words per rank.
   bool fused_pack = false;
-  bool sum_list = false;            // the shard sum's pairs built by the plan launch (fused pack, N > 1, an aggregator)
+  bool sum_list = false;            // the shard sum's pairs built by the plan launch (fused pack, N > 1, an aggregator;
+                                    // the default since round 4)
   uint64_t list_units = 0;
   uint32_t list_cap = 0;
   uint64_t mstride = 0;           // uint64 words per rank in masks_all (rows without the fused pack)
@@ -1349,11 +1350,12 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
                   "omr_pack_geometry"));
     p->fused_pack = true;
     p->mstride = p->rows + (entries + 1) / 2;
-    // OMR_SUM_LIST=1 (study knob): the plan launch builds the shard sum's pairs and omr_shard_sum_list_f32 sums them.
-    // At config 4's 8-worker shard that sum took 16.6-17.2 us against 15.5-16.1 for omr_shard_sum_cols_f32, which
-    // builds its pairs itself (profiles/r03/round/list_s2g/), so the round keeps the latter by default.
+    // The plan launch builds the shard sum's pairs (16-row units, beside the plan's own workgroups: 11.68 against
+    // 11.76 us without them) and omr_shard_sum_list_f32 sums them with its first load: 9.32 us at config 4's 8-worker
+    // shard against 11.83 for omr_shard_sum_cols_f32, which builds its pairs itself (round 4,
+    // profiles/r04/round_kernels/tune_round_list16.log).  OMR_SUM_LIST=0 (study knob): the latter.
     const char* le = getenv("OMR_SUM_LIST");
-    if (p->shard >= 0 && le != nullptr && atoi(le) != 0) {
+    if (p->shard >= 0 && (le == nullptr || atoi(le) != 0)) {
       TRY(omr_check(omr_sum_list_geometry(n, block_size, num_lanes, num_parts, p->bounds[p->shard],
                                           p->bounds[p->shard + 1], static_cast<uint32_t>(p->M), &p->list_units,
                                           &p->list_cap), "omr_sum_list_geometry"));

@@ -1012,7 +1012,9 @@ __device__ __forceinline__ uint64_t plan_row(const uint64_t* masks, uint32_t a, 
 }
 
 constexpr uint64_t kRowStreams = ~0ull;
-constexpr uint32_t kSumUnitRows = 32;    // the pair list's unit: 32 rows x one lane (half a 64-row group)
+// the pair list's unit: 16 rows x one lane (a quarter of a 64-row group), as k_shard_sum's
+constexpr uint32_t kSumUnitRows = 16;
+constexpr uint32_t kSumUnitsPerGroup = 64 / kSumUnitRows;
 // k_shard_sum's unit rows (a divisor of the 64-row group).  16: 2048 waves at config 4's 8-worker shard, two per
 // SIMD, nearly all of them one window (<= 32 pairs); with 32-row units 11 % of the waves needed a second window, a
 // round trip after everyone else's (14.16 against 15.35 us, stamped copies, profiles/r04/shard/)
@@ -1042,11 +1044,11 @@ struct ListArgs {
 };
 
 __device__ __forceinline__ uint64_t list_units(const ListArgs& a) {
-  return ((a.r1 - a.r0) / a.S) * a.gps * 2 * a.lanes;
+  return ((a.r1 - a.r0) / a.S) * a.gps * kSumUnitsPerGroup * a.lanes;
 }
 
-// Units [u0, units) step ustride, one wave each: unit = 32 rows x one lane (one half of a segment's 64-row group), as
-// k_shard_sum's column-stream units.  Lane i holds row i of the group: ONE round trip fetches every worker's mask row
+// Units [u0, units) step ustride, one wave each: unit = kSumUnitRows rows x one lane (a part of a segment's 64-row
+// group), as k_shard_sum's column-stream units.  Lane i holds row i of the group: ONE round trip fetches every worker's mask row
 // and position-table entry; ballots give each worker's column bits; a wave-wide exclusive scan places each lane's
 // pairs; records go straight to global memory.
 __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, uint64_t ustride) {
@@ -1055,8 +1057,8 @@ __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, u
   for (uint64_t u = u0; u < units; u += ustride) {
     const uint32_t l = static_cast<uint32_t>(u % a.lanes);
     uint64_t t = u / a.lanes;
-    const uint32_t h = static_cast<uint32_t>(t & 1u);
-    t >>= 1;
+    const uint32_t h = static_cast<uint32_t>(t % kSumUnitsPerGroup);
+    t /= kSumUnitsPerGroup;
     const uint32_t j = static_cast<uint32_t>(t % a.gps);
     const uint64_t seg = a.r0 / a.S + t / a.gps;
     const uint64_t g0 = seg * a.S + static_cast<uint64_t>(j) * kPackGroupRows;
@@ -1497,7 +1499,7 @@ __global__ __launch_bounds__(kWGThreads) void k_move(MoveArgs a) {
 //   column-ordered (k_scan1f's fused pack): segment by segment, position from its position table.
 // Output dense (block position, in place) or packed (write-set order of the shard, for the sums' return trip).
 //
-// Work unit = 32 rows x one lane column (column streams: one half of a segment's 64-row group).  Lane i holds row i
+// Work unit = UR rows x one lane column (column streams: a part of a segment's 64-row group).  Lane i holds row i
 // of the rows it loads: ONE round trip fetches the unit's index data (write-set row, every worker's mask row and
 // stream prefix or position).  Ballots over the lanes give each worker's column bits, so every (block, contributor)
 // pair's stream position is computed in registers; a wave-wide exclusive scan lays the pairs out in LDS in
@@ -1710,9 +1712,10 @@ struct ListSumArgs {
 
 template <int VEC>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
-  // pair slots per window: 64 at B = 256, so a unit at config 4's density (26 pairs on average, 32 rows x 8 workers at
-  // most 256) nearly always fits one window; each window is loads, then every add, then the stores (as k_shard_sum)
-  constexpr int P = 64 / VEC;
+  // pair slots per window: 32 at B = 256, so a unit at config 4's density (13 pairs on average, 16 rows x 8 workers at
+  // most 128) nearly always fits one window; each window is loads, then every add, then the stores (as k_shard_sum)
+  constexpr int P = 2 * kSumUnitRows / VEC;
+  static_assert(64 % P == 0, "a window lies inside one 64-record chunk");
   constexpr int kSlotGroup = 8;
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2122,7 +2125,7 @@ int make_list_args(const Layout& L, const uint64_t* masks, uint32_t count, uint6
   return 0;
 }
 
-uint64_t list_units_host(const ListArgs& a) { return ((a.r1 - a.r0) / a.S) * a.gps * 2 * a.lanes; }
+uint64_t list_units_host(const ListArgs& a) { return ((a.r1 - a.r0) / a.S) * a.gps * kSumUnitsPerGroup * a.lanes; }
 
 __global__ __launch_bounds__(kWGThreads) void k_sum_list(ListArgs a) {
   build_sum_list(a, static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
@@ -2873,7 +2876,7 @@ int omr_sum_list_geometry(uint64_t n, uint32_t block_size, uint32_t num_lanes, u
   if (row_begin > row_end || row_end > L.rows || row_begin % f.S != 0 || row_end % f.S != 0)
     return fail("sum_list: rows [%llu, %llu) are not whole %u-row column segments",
                 static_cast<unsigned long long>(row_begin), static_cast<unsigned long long>(row_end), f.S);
-  if (units) *units = ((row_end - row_begin) / f.S) * pack_groups(f) * 2 * L.lanes;
+  if (units) *units = ((row_end - row_begin) / f.S) * pack_groups(f) * kSumUnitsPerGroup * L.lanes;
   if (capacity) *capacity = kSumUnitRows * count + 1;  // + the terminator
   return 0;
 }

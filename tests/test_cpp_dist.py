@@ -217,10 +217,11 @@ def test_cpp_async_rounds_loopback(gpu, world, mode, round_flags):
 
 @pytest.mark.parametrize("world,mode,round_flags", [
     (8, 1, (D_,) * 7), (4, 0, (A, D_, D_, A, D_, D_, D_)), (4, 0, (T | D_,) * 7), (8, 1, (0,) * 4)])
-def test_cpp_rounds_sum_list_loopback(gpu, monkeypatch, world, mode, round_flags):
-    """The same rounds with OMR_SUM_LIST=1: the plan launch builds each shard's pair list (omr_round_plan_list) and
-    the aggregator sums over it (omr_shard_sum_list_f32), every worker's stream received at its fixed region."""
-    monkeypatch.setenv("OMR_SUM_LIST", "1")
+def test_cpp_rounds_cols_sum_loopback(gpu, monkeypatch, world, mode, round_flags):
+    """The same rounds with OMR_SUM_LIST=0: the aggregator's shard sum builds its pairs itself
+    (omr_shard_sum_cols_f32) instead of summing the pair list the plan launch built (omr_round_plan_list +
+    omr_shard_sum_list_f32, the round's default since round 4)."""
+    monkeypatch.setenv("OMR_SUM_LIST", "0")
     test_cpp_async_rounds_loopback(gpu, world, mode, round_flags)
 
 

@@ -6,18 +6,19 @@
 #include "../../omnireduce-rdma-demo_amd/csrc/omr_kernels.hip"
 
 namespace {
+constexpr uint32_t kR03UnitRows = 32;  // round 3's unit (the product's kSumUnitRows has changed since)
 template <int VEC, int PP, int STAMP>
 __global__ __launch_bounds__(kWGThreads) void k_shard_sum_s(SumArgs a, uint64_t* tl) {
   constexpr int P = PP / VEC;  // pair slots per window
   constexpr int kSlotGroup = P < 8 ? P : 8;
-  constexpr uint32_t kRecCap = kSumUnitRows * OMR_MAX_WORKERS;
+  constexpr uint32_t kRecCap = kR03UnitRows * OMR_MAX_WORKERS;
   __shared__ uint64_t s_rec[kWavesPerWG][kRecCap];
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool cols = a.pos_off != kRowStreams;
   const uint64_t srows = a.r1 - a.r0;
   const uint64_t units = cols ? (srows / a.S) * a.gps * 2 * a.lanes
-                              : ((srows + kSumUnitRows - 1) / kSumUnitRows) * a.lanes;
+                              : ((srows + kR03UnitRows - 1) / kR03UnitRows) * a.lanes;
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWavesPerWG;
   const uint32_t* const pws = a.prefix + static_cast<uint64_t>(a.count) * (a.rows + 1);
   const uint32_t wpre0 = a.packed_out ? pws[a.r0] : 0u;
@@ -37,13 +38,13 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum_s(SumArgs a, uint64_t*
       const uint64_t seg = a.r0 / a.S + t / a.gps;
       g0 = seg * a.S + static_cast<uint64_t>(j) * kPackGroupRows;
       nload = a.S - j * kPackGroupRows < kPackGroupRows ? a.S - j * kPackGroupRows : kPackGroupRows;
-      h0 = h * kSumUnitRows;
-      h1 = nload < h0 + kSumUnitRows ? nload : h0 + kSumUnitRows;
+      h0 = h * kR03UnitRows;
+      h1 = nload < h0 + kR03UnitRows ? nload : h0 + kR03UnitRows;
       gidx = seg * a.gps + j;
       if (h0 >= h1) continue;
     } else {
-      g0 = a.r0 + (u / a.lanes) * kSumUnitRows;
-      nload = a.r1 - g0 < kSumUnitRows ? static_cast<uint32_t>(a.r1 - g0) : kSumUnitRows;
+      g0 = a.r0 + (u / a.lanes) * kR03UnitRows;
+      nload = a.r1 - g0 < kR03UnitRows ? static_cast<uint32_t>(a.r1 - g0) : kR03UnitRows;
       h0 = 0;
       h1 = nload;
     }

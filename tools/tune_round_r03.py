@@ -115,7 +115,9 @@ def main():
     torch.cuda.init()
     tl = r02.load()
     lib = _lib.load()
+    print("# setting up config 4's shapes", flush=True)
     D = setup(a)
+    print("# set up", flush=True)
     L, m, naggs, rows, B, NB, ent, mstride = (D[k] for k in ("L", "m", "naggs", "rows", "B", "NB", "ent", "mstride"))
     bounds, bptr, xs, wsb, ws, flags, nxt = (D[k] for k in ("bounds", "bptr", "xs", "wsb", "ws", "flags", "nxt"))
     masks_all, wset, umask, prefix, counts, bdev = (D[k] for k in ("masks_all", "wset", "umask", "prefix", "counts",
@@ -150,6 +152,8 @@ def main():
         sl.recv_offsets[w] = int(roff[w])
     _lib.check(lib.omr_sum_list_build(masks_all.data_ptr(), m, mstride, L.n, B, NB, L.num_threads, ctypes.byref(sl),
                                       st), "omr_sum_list_build")
+    torch.cuda.synchronize()
+    print("# pair list built", flush=True)
 
     def sum_list(out):
         return lib.omr_shard_sum_list_f32(xs[0].data_ptr(), recv_c.data_ptr(), ctypes.byref(sl), m, L.n, B, NB,
@@ -170,8 +174,10 @@ def main():
     ref = None
     for name, fn in sums.items():
         o = xs[0].clone()
+        print(f"# checking {name}", flush=True)
         assert fn(o) == 0, name
         torch.cuda.synchronize()
+        print(f"# {name} ran", flush=True)
         if ref is None:
             ref = o
         assert torch.equal(o.view(torch.int32), ref.view(torch.int32)), f"{name} differs"
@@ -250,7 +256,9 @@ def main():
     outs = [xs[0].clone() for _ in range(2)]
     times = {k: [] for k in cases}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    print("# checked; timing", flush=True)
     for r in range(a.rounds):
+        print(f"# round {r}", flush=True)
         for name, fn in cases.items():
             cntbig.zero_()
             e0.record()
