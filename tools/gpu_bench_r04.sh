@@ -22,3 +22,11 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o c2 --output-
   python3 $R/bench.py --no-cpu --no-round > $O/c2_prof.json 2> $O/c2_prof.err
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o c3 --output-format csv -- \
   python3 $R/bench.py --size-mib 1024 --block-size 1024 --density 0.0099 --no-cpu --no-round > $O/c3_prof.json 2> $O/c3_prof.err
+# the world-1 round's kernel trace beside its host laps (OMR_HOST_TRACE=2: CLOCK_MONOTONIC, rocprofv3's clock), and
+# the round's kernels at config 4's shapes (their PMC traffic: tools/gpu_r04_pmc_round.sh, a call of its own)
+cd $R
+( export MASTER_ADDR=127.0.0.1 MASTER_PORT=29641 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 OMR_HOST_TRACE=2 \
+         OMR_HOST_TRACE_FILE=$O/w1_host_laps.txt
+  cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/w1_trace -o w1 -- \
+    python3 $R/bench.py --force-dist --no-cpu --steps 100 --dist-pipe defer > $O/w1_trace.json 2> $O/w1_trace.err )
+timeout -k 10 300 python3 -u tools/tune_round_r03.py > $O/tune_round.log 2>&1

@@ -10,6 +10,8 @@ back to back on one stream, adding one ingredient of the round at a time, each c
   D  C + an event record after every scan (the round's `scanned`: DisableTiming | DisableSystemFence)
   E  D + a side stream that waits for each record and copies 32 KiB (the world-1 all-gather)
   F  E + a device-to-host-mapped 4-byte write on the side stream (hipMemsetAsync of a pinned word: the count notice)
+  G  C + a stream write of a sequence number after every scan (hipStreamWriteValue32 to signal memory), no event
+  H  G + a side stream that waits for it (hipStreamWaitValue32 >=) and copies 32 KiB
 usage: python tools/round_gap_r04.py [--rounds 8] [--reps 20]"""
 import argparse
 import ctypes
@@ -40,6 +42,12 @@ def main():
     hip.hipStreamWaitEvent.argtypes = [vp, vp, ctypes.c_uint]
     hip.hipMemcpyAsync.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
     hip.hipMemsetAsync.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, vp]
+    hip.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_uint]
+    hip.hipStreamWriteValue32.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint]
+    hip.hipStreamWaitValue32.argtypes = [vp, vp, ctypes.c_uint32, ctypes.c_uint, ctypes.c_uint32]
+    sig = vp()
+    assert hip.hipExtMallocWithFlags(ctypes.byref(sig), 8, 0x2) == 0  # hipMallocSignalMemory
+    seq = [0]
     evs = []
     for _ in range(3):
         e = vp()
@@ -91,9 +99,20 @@ def main():
         rc = E(i)
         return rc or hip.hipMemsetAsync(pinned.data_ptr(), 0, 4, ss)
 
+    def G(i):
+        rc = scan(i, False)
+        seq[0] += 1
+        return rc or hip.hipStreamWriteValue32(st, sig, seq[0], 0)
+
+    def H(i):
+        rc = G(i)
+        rc = rc or hip.hipStreamWaitValue32(ss, sig, seq[0], 0x0, 0xFFFFFFFF)  # hipStreamWaitValueGte
+        return rc or hip.hipMemcpyAsync(gathered.data_ptr(), masks.data_ptr(), 32 << 10, 3, ss)
+
     cases = {"A headline, in place": A, "B round scan (+ masks), in place": B, "C round scan, out of place": C,
              "D C + event record per scan": D, "E D + side stream: wait + 32 KiB copy": E,
-             "F E + side-stream pinned 4-byte memset": F}
+             "F E + side-stream pinned 4-byte memset": F, "G C + stream write value per scan": G,
+             "H G + side stream: wait value + 32 KiB copy": H}
     for fn in cases.values():
         assert fn(0) == 0, lib.omr_last_error().decode()
     torch.cuda.synchronize()
