@@ -1723,11 +1723,18 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum_list(ListSumArgs a) {
   const uint32_t bbytes = a.block * 4;
   const uint32_t wpre0 = a.packed_out ? a.wprefix[a.r0] : 0u;
   for (uint32_t u = blockIdx.x * kWavesPerWG + wave; u < a.units; u += nw) {
-    // ONE load: the unit's first 64 words; its length is the first terminator's lane (more chunks only past 63)
+    // ONE load: the unit's first 32 words (2 of the 4 lines of a 64-word chunk: a 16-row unit nearly always has fewer
+    // records); its length is the first terminator's lane.  Past 31 records the whole first 64 are loaded, past 63
+    // the next chunks (lanes >= 32 of the first load hold terminators, so the ballot's low half decides)
     const uint64_t* const rec = a.records + static_cast<uint64_t>(u) * a.cap;
-    uint64_t chunk = static_cast<uint32_t>(lane) < a.cap ? rec[lane] : kRecEnd;
+    uint64_t chunk = static_cast<uint32_t>(lane) < (a.cap < 32u ? a.cap : 32u) ? rec[lane] : kRecEnd;
+    uint64_t e0 = __ballot(chunk == kRecEnd);
+    if ((e0 & 0xFFFFFFFFull) == 0) {
+      chunk = static_cast<uint32_t>(lane) < a.cap ? rec[lane] : kRecEnd;
+      e0 = __ballot(chunk == kRecEnd);
+    }
     uint32_t total = 0;
-    for (uint64_t e = __ballot(chunk == kRecEnd);; ) {
+    for (uint64_t e = e0;; ) {
       if (e != 0) {
         total += static_cast<uint32_t>(__builtin_ctzll(e));
         break;
