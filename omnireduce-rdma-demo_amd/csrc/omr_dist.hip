@@ -982,7 +982,6 @@ struct omr_ar_plan {
   uint64_t last_sums_blocks = 0;  // a dedicated aggregator: blocks of its last round's shard sums in `results`
   int32_t* flags_ws = nullptr;
   uint32_t* next_ws = nullptr;
-  uint32_t* unext_ws = nullptr;
   void* scan_ws = nullptr;   // omr_worker_scan_f32 segment workspace (zeroed once, self-resetting)
   size_t scan_ws_bytes = 0;
   uint32_t* arrive = nullptr;     // the plan kernel's workspace (omr_round_plan_ws; word 0: its arrival counter)
@@ -1272,7 +1271,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   p->npend = 0;
   (void)hipDeviceSynchronize();  // (an aborted RCCL communicator has cancelled its queued operations)
   // back to the transport, which keeps the exported ones alive for the next plan (omr_dist::alloc)
-  void* devs[] = {p->bounds_dev, p->results, p->flags_ws, p->next_ws, p->unext_ws, p->scan_ws, p->arrive};
+  void* devs[] = {p->bounds_dev, p->results, p->flags_ws, p->next_ws, p->scan_ws, p->arrive};
   for (void* v : devs) p->d->release(v);
   for (auto& st : p->set) {
     void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed, st.pack_cnt, st.list_rec, st.list_cnt,
@@ -1411,7 +1410,6 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   A(dev_alloc(p->d, &p->results, n));
   A(dev_alloc(p->d, &p->flags_ws, p->nb));
   A(dev_alloc(p->d, &p->next_ws, p->nb));
-  A(dev_alloc(p->d, &p->unext_ws, p->nb));
   p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
   A(dev_alloc(p->d, reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
   constexpr int NSETS = omr_ar_plan::kSets;
@@ -1889,7 +1887,9 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
   p->ht.start();
   int32_t* fl = flags ? flags : p->flags_ws;
   uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
-  uint32_t* un = union_next ? union_next : p->unext_ws;
+  // (no union_next: the plan launch skips the aggregator chain, whose only output it is -- at world 1 that is 64
+  // 1024-thread workgroups fewer beside the next scan)
+  uint32_t* un = union_next;
   // a stream other than the previous round's starts behind it (plan-wide state is shared by every round)
   if (p->last_st != nullptr && p->last_st != st) {
     TRY(hip_check(hipEventRecord(p->st_ev, p->last_st), "hipEventRecord"));
