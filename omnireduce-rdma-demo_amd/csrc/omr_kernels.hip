@@ -2039,6 +2039,25 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
       default: return launch_fused_pack<4, 1>(a, L, f, grid, st);
     }
   }
+  // The multi-rank round's worker scan (it writes row masks) runs 8-wave workgroups, two per CU, as the fused pack's
+  // does: beside the round's plan and copy kernels on the other streams a plan workgroup then displaces half a CU's
+  // scan instead of all of it.  The world-1 round took 55.8-57.0 us so against 57.6-58.4 with one 16-wave workgroup
+  // per CU (54.4-55.7 in a second set of runs), its scan 0.68-0.71 of spec against 0.66; the single-GPU step keeps 16
+  // waves (47.8 against 49.6 us alone; profiles/r04/scan_waves/).  OMR_SCAN_WAVES=8 / 16 forces one shape for both
+  // (study knob).
+  static const int waves_env = [] {
+    const char* e = getenv("OMR_SCAN_WAVES");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  const bool waves8 = waves_env == 8 || (waves_env != 16 && masks != nullptr);
+  if (waves8) {
+    switch (L.vec) {
+      case 1: k_scan1f<1, 8, kFusedLoads><<<grid, 512, 0, st>>>(a); break;
+      case 2: k_scan1f<2, 8, kFusedLoads><<<grid, 512, 0, st>>>(a); break;
+      default: k_scan1f<4, 8, kFusedLoads, 1><<<grid, 512, 0, st>>>(a); break;
+    }
+    return launch_status("k_scan1f (8 waves)");
+  }
   switch (L.vec) {
     case 1: k_scan1f<1, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
     case 2: k_scan1f<2, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
