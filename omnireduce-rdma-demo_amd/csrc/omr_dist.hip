@@ -985,7 +985,7 @@ struct omr_ar_plan {
   void* scan_ws = nullptr;   // omr_worker_scan_f32 segment workspace (zeroed once, self-resetting)
   size_t scan_ws_bytes = 0;
   uint32_t* arrive = nullptr;     // the plan kernel's workspace (omr_round_plan_ws; word 0: its arrival counter)
-  bool plan_v1 = false;           // round 3's plan form (omr_round_plan_list) instead of omr_round_plan_ws
+  bool plan_v1 = true;            // round 3's plan form (omr_round_plan_list, the default) or omr_round_plan_ws
   uint32_t* flag_host = nullptr;  // [kSets] pinned, per set: the plan kernel stores the round's sequence number here
   uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
@@ -1750,14 +1750,14 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
   //    ... and, by extra workgroups of the same launch, the aggregator chain (server.cc:86-96 min_next) over the union
   //    ... and the shard sum's pair list, by more workgroups (sum_list)
   const omr_sum_list sl = p->sum_list ? list_desc(p, S) : omr_sum_list{};
-  //    (omr_round_plan_ws: 256-thread workgroups over row chunks, which fit beside a running scan workgroup;
-  //    OMR_PLAN_V1=1, a study knob, runs round 3's one-1024-thread-workgroup-per-array form instead)
+  //    (round 3's one-1024-thread-workgroup-per-array form, omr_round_plan_list; OMR_PLAN_V1=0, a study knob, runs
+  //    the row-chunk form, omr_round_plan_ws: 256-thread workgroups that fit beside a running scan workgroup)
   TRY(omr_check((p->plan_v1 ? omr_round_plan_list : omr_round_plan_ws)(
                     S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes, p->bounds_dev, NS,
                     S.wset, S.umask, S.prefix, p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own,
                     S.pack_cnt, S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->arrive, p->flag_map + si, seq, j.un,
                     p->B, p->sum_list ? &sl : nullptr, qstream),
-                "omr_round_plan_ws"));
+                p->plan_v1 ? "omr_round_plan_list" : "omr_round_plan_ws"));
   ht.lap("1:plan");
   // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407): addressed by
   //     device-side data only, so it is queued before the host learns the counts and runs while it waits.  (Every
