@@ -126,6 +126,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float* base, 
 // packed and summed blocks of the round's kernels leave no dirty lines in the XCD L2s either.  Plain stores did, and
 // the kernel-end write-back of them ran after the last wave: the shard sum took 15.3 us with these stores against
 // 16.8 with plain ones (stamped copies, profiles/r04/shard/shard_store_policy.log).
+#ifndef OMR_BLOCK_STORE_AUX  // (tools: a study build may pick another policy, e.g. 2 = nt)
+#define OMR_BLOCK_STORE_AUX kStoreAux
+#endif
 template <int VEC>
 __device__ __forceinline__ void store_block_wt(float* dst, const v4f* v, int lane) {
   const uint64_t a = reinterpret_cast<uint64_t>(dst);
@@ -134,7 +137,8 @@ __device__ __forceinline__ void store_block_wt(float* dst, const v4f* v, int lan
   const __amdgpu_buffer_rsrc_t r = chunk_rsrc(reinterpret_cast<float*>(u), VEC * 1024u);
 #pragma unroll
   for (int q = 0; q < VEC; ++q)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v[q]), r, (q * 64 + lane) * 16, 0, kStoreAux);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v[q]), r, (q * 64 + lane) * 16, 0,
+                                           OMR_BLOCK_STORE_AUX);
 }
 
 template <int VEC>
