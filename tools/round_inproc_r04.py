@@ -19,10 +19,61 @@ import bench  # noqa: E402
 from omr import Layout, ops  # noqa: E402
 
 
+def round_loop(eng, sets, stream, steps):
+    """bench.round_world1's loop on a given engine: reduce-scatter, deferred, out of place; us per round."""
+    outs = []
+    for xs, out in sets:
+        out.copy_(xs[0])
+        outs.append(out)
+    for i in range(20):
+        eng.run(sets[i % len(sets)][0][0], out=outs[i % len(sets)], mode=1, async_=True, defer=True)
+    eng.join(stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        eng.run(sets[i % len(sets)][0][0], out=outs[i % len(sets)], mode=1, async_=True, defer=True)
+    eng.join(stream)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e6
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--comm-first", action="store_true",
+                    help="make the one-rank communicator and plan before any kernel runs, then the headline, then the "
+                         "round on that plan")
+    ap.add_argument("--torch-group", action="store_true", help="--comm-first after a one-rank torch nccl group")
     a = ap.parse_args()
+    if a.comm_first:
+        from omr import cdist
+        args = bench.parse(["--no-cpu"])
+        dev = torch.device("cuda:0")
+        if a.torch_group:  # a one-rank torch nccl group first, as bench.py's N>1 path makes (env: MASTER_*, RANK, ...)
+            before = dict(os.environ)
+            torch.cuda.set_device(0)
+            torch.distributed.init_process_group("nccl", device_id=dev)
+            changed = {k: v for k, v in os.environ.items() if before.get(k) != v}
+            print(f"torch group made; environment it changed: {changed}", flush=True)
+        L = Layout.from_bytes(args.size_mib << 20, args.block_size)
+        eng = cdist.CppSparseAllreduce(L, dev, transport="rccl1")  # (first GPU work of the process)
+        bm = ops.gen_bitmap(0, args.density, L.nb)
+        sets = [([ops.fill_blocks(torch.from_numpy(bm).to(dev), L, mode=0)], torch.zeros(L.n, device=dev))
+                for _ in range(4)]
+        stream = torch.cuda.current_stream(dev)
+        print(f"comm first, round before the headline: {round_loop(eng, sets, stream, a.steps):.1f} us", flush=True)
+        side = torch.cuda.Stream(dev)  # the same rounds issued on a created (non-null) stream
+        with torch.cuda.stream(side):
+            print(f"comm first, round on a created stream: {round_loop(eng, sets, side, a.steps):.1f} us "
+                  f"(stream {side.cuda_stream:#x}; null stream {stream.cuda_stream:#x})", flush=True)
+        plan = ops.ScanSumPlan(L, 1, device=dev, fused=True)
+        launches = [plan.bind(xs[0], xs[0], stream) for xs, _ in sets]
+        for i in range(a.steps):
+            launches[i % 4]()
+        torch.cuda.synchronize()
+        print(f"comm first, round after the headline: {round_loop(eng, sets, stream, a.steps):.1f} us", flush=True)
+        eng.close()
+        return
     args = bench.parse(["--no-cpu", "--steps", str(a.steps), "--warmup", "20"])
     dev = torch.device("cuda:0")
     L = Layout.from_bytes(args.size_mib << 20, args.block_size)
