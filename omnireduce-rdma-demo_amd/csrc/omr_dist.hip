@@ -1281,7 +1281,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
       if (e) (void)hipEventDestroy(e);
   }
   if (p->ps) (void)hipStreamDestroy(p->ps);
-  if (p->cs) (void)hipStreamDestroy(p->cs);
+  if (p->cs && p->cs != p->ps) (void)hipStreamDestroy(p->cs);
   if (p->as) (void)hipStreamDestroy(p->as);
   for (int r = 0; r < omr_ar_plan::kStage; ++r) {
     p->d->release(p->stage[r]);
@@ -1394,7 +1394,15 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     A(hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange"));
     const int prio = (pe != nullptr && atoi(pe) != 0) ? greatest : least;
     A(hip_check(hipStreamCreateWithPriority(&p->ps, hipStreamNonBlocking, prio), "hipStreamCreate"));
-    A(hip_check(hipStreamCreateWithPriority(&p->cs, hipStreamNonBlocking, prio), "hipStreamCreate"));
+    // A one-rank group has no exchange: its communication stream would carry only event waits and records, so it is
+    // the plan stream itself.  Fewer streams share the process's hardware queues less: the in-process world-1 round
+    // ran 52.4-53.2 us instead of 101-108 in 5 of the 6 stream / group orders that were slow with two side streams,
+    // the bench child unchanged (profiles/r04/inproc/one_side/).  At N > 1 the exchange keeps a stream of its own, so
+    // it runs beside the next round's all-gather and plan.  OMR_ONE_SIDE_STREAM=0 / 1 forces two / one (study knob).
+    const char* os1 = getenv("OMR_ONE_SIDE_STREAM");
+    const bool one_side = os1 != nullptr ? atoi(os1) != 0 : N == 1;
+    if (one_side) p->cs = p->ps;
+    else A(hip_check(hipStreamCreateWithPriority(&p->cs, hipStreamNonBlocking, prio), "hipStreamCreate"));
     // OMR_AGG_STREAM=1 (opt-in): the aggregation stream.  Off by default: a fourth side stream exceeds the process's
     // four hardware queues (GPU_MAX_HW_QUEUES), and its wait for the exchange can then block whatever shares its queue.
     // As 4 IPC ranks on one GPU it took 27.5 ms per round against 1.47 ms without (profiles/r03/agg_stream/).
