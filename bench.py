@@ -272,7 +272,7 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
         "cores": args.cpu_threads,
         "pinned_cores": cores,
         "kind": "port",
-        "sample": (f"config 2 tensor ({L.nbytes >> 20} MiB, B={L.block_size}, -r {args.density}), data-derived "
+        "sample": (f"the workload's tensor ({L.nbytes >> 20} MiB, B={L.block_size}, -r {args.density}), data-derived "
                    f"fp32 scan + next offsets + block aggregate, {args.cpu_warmups} warm-up + {args.cpu_rounds} "
                    f"rounds, {args.cpu_threads} pthreads one per partition (client.cc:384-392)"),
         "ms_per_round": round(t * 1e3, 3),
@@ -357,7 +357,9 @@ def round_world1_child(args):
         return {"error": "the world-1 round's child run timed out (240 s)"}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
-        return {"error": f"child exit {r.returncode}: " + (r.stderr or r.stdout)[-300:]}
+        err = r.stderr or r.stdout
+        k = err.find("Traceback")
+        return {"error": f"child exit {r.returncode}: " + (err[k:k + 2000] if k >= 0 else err[-600:])}
     d = json.loads(lines[-1])
     ex = d.get("exchange", {})
     rf = d.get("roofline", {})

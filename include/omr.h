@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define OMR_ABI_VERSION 1
+#define OMR_ABI_VERSION 2
 #define OMR_EINVAL (-1)
 #define OMR_MAX_WORKERS 16 /* reference caps peers at 10: common.h:59 peer_names[10] */
 
@@ -213,20 +213,40 @@ int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint3
  * omr_worker_scan_f32, and every non-zero block of a row of shard s != own_shard is also written to `send`, so no
  * separate pass re-reads the blocks to pack them.  Shards: rows [shard_bounds[s], shard_bounds[s+1]) (HOST uint64,
  * num_shards + 1 entries, 0 .. rows), each made of whole column segments of the scan (omr_pack_supported says
- * whether a set of bounds is; a ragged shard packs with omr_move_blocks_f32 instead).  Shard s's stream starts at
- * send + shard_bounds[s] * num_lanes * block_size floats (send: n floats, device) and holds its non-zero blocks
- * segment by segment (column segments of omr_pack_geometry's seg_rows rows), each segment's in row order; segments
+ * whether a set of bounds is; a ragged shard packs with omr_move_blocks_f32 instead).  The streams follow one another
+ * in shard order without own_shard's: shard s's starts at send + (shard_bounds[s] - (s > own_shard ? own_shard's rows :
+ * 0)) * num_lanes * block_size floats (send: device, n floats less own_shard's rows; omr_pack_send_offset gives the
+ * offset), and holds its non-zero blocks segment by segment (column segments of omr_pack_geometry's seg_rows rows),
+ * each segment's in row order; segments
  * take their places in completion order through shard_counters (device uint32[num_shards], zero on entry: after the
  * call counter s = the stream's block count).  pos_table (device uint32[table_entries]) receives for each
  * (segment, 64-row group g, lane l) the stream position of the first block of lane l at or after row 64 g of the
  * segment: the aggregator's address of block (row r, lane l) is pos + the lane's set bits in the group below r
- * (omr_shard_sum_cols_f32).  Entries of segments with no non-zero block, and of own_shard's, are not written.
+ * (the pair list of omr_sum_list_build / omr_round_plan_list).  Entries of segments with no non-zero block, and of
+ * own_shard's, are not written.
  * own_shard: -1 packs every shard (a worker that aggregates none). */
 int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
                              int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out,
                              const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard, float* send,
                              uint32_t* shard_counters, uint32_t* pos_table, void* workspace, size_t workspace_bytes,
                              omr_stream_t stream);
+/* The one-rank round's worker scan (a world-1 group: one worker, one aggregator; server.cc:83-96 with one worker:
+ * the union is the worker's own blocks and min_next its own chain, so the aggregator's bookkeeping is two counts).
+ * As omr_scan_sum_fused_f32 (flags, next offsets, out = 0.0f + x over the write set if non-NULL), plus
+ *   tally (device uint64[omr_tally_slots()]): workgroup b stores {non-zero blocks, zero lane-head blocks} of its part
+ *   as (heads << 32) | non-zero (one slot per workgroup, overwritten by every launch);
+ *   publish_src / publish_dst (both or neither): workgroup 0 of the same launch sums an EARLIER launch's slots (same
+ *   layout) and stores {publish_seq, non-zero blocks, write-set blocks = non-zero + zero lane heads (client.cc:201-205),
+ *   publish_seq} (one 16-byte system-scope store) into publish_dst (host-mapped, 16-byte aligned).  A host that reads
+ *   publish_seq in both halves has the counts.
+ * So a pipelined one-rank round is ONE launch on the caller's stream (no event, no side stream). */
+uint32_t omr_tally_slots(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts);
+int omr_worker_scan_tally_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                              int32_t* flags, uint32_t* next_offsets, float* out, uint64_t* tally,
+                              const uint64_t* publish_src, uint32_t* publish_dst, uint32_t publish_seq, void* workspace,
+                              size_t workspace_bytes, omr_stream_t stream);
+/* The same publication as a launch of its own (one wave): for a round no later scan follows. */
+int omr_tally_publish(const uint64_t* tally, uint32_t slots, uint32_t* dst, uint32_t seq, omr_stream_t stream);
 /* The fused pack's geometry on this layout: rows per column segment, 64-row groups per segment, position-table
  * entries (num_parts * segments per partition * groups * num_lanes); and whether shard bounds (HOST) are whole
  * segments (0, else OMR_EINVAL with the reason). */
@@ -234,6 +254,10 @@ int omr_pack_geometry(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint3
                       uint32_t* groups_per_seg, uint64_t* table_entries);
 int omr_pack_supported(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
                        const uint64_t* shard_bounds, uint32_t num_shards);
+/* Where shard s's stream starts in omr_worker_scan_pack_f32's `send` (floats), and the floats `send` needs (*total;
+ * NULL: not asked), for shard bounds in rows (HOST, num_shards + 1 entries) and own_shard (-1: none). */
+uint64_t omr_pack_send_offset(const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard, uint32_t s,
+                              uint32_t num_lanes, uint32_t block_size, uint64_t* total);
 
 /* The aggregator bookkeeping of a round in ONE launch (server.cc:83-96, for the whole tensor at once), from
  * `count` workers' row masks (device, stride rows):
@@ -243,14 +267,15 @@ int omr_pack_supported(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint
  *   prefix[a*(rows+1) + r] = set bits of array a in rows [0, r), for a < count (workers) and a == count (the
  *                    write set); r = rows gives the total;
  *   counts[a*num_bounds + s] = prefix[a][bounds[s]] (bounds: device uint64[num_bounds], each <= rows);
- *   zero_masks (device uint64[rows] or NULL) is cleared (the next round's omr_worker_scan_f32 target).
- * Completion notice (both NULL, or both set): once every count is visible system-wide, *done_flag = seq.  `arrive`
- * is a device uint32 zeroed once by the caller and left zeroed; done_flag may be pinned host memory (mapped), so
- * a host can poll it instead of synchronising the stream (the multi-rank round does). */
+ *   zero_masks (device uint64[rows] or NULL) is cleared (the next round's omr_worker_scan_f32 target);
+ *   union_masks may be NULL (not stored).
+ * Completion notice (done_flag non-NULL): once every count is visible system-wide, *done_flag = seq.  done_flag may
+ * be pinned host memory (mapped), so a host can poll it instead of synchronising the stream (the multi-rank round
+ * does).  One 1024-thread workgroup does all of it, every mask read once (ABI 2; ABI 1 took an arrival counter). */
 int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                    uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
                    uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                   uint32_t* arrive, uint32_t* done_flag, uint32_t seq, omr_stream_t stream);
+                   uint32_t* done_flag, uint32_t seq, omr_stream_t stream);
 /* omr_round_plan plus, in the same launch, the aggregator chain (server.cc:86-96: min_next over the workers =
  * next offsets over the union) into union_next (device uint32[rows * num_lanes], the omr_next_offsets layout of
  * the union masks), computed by extra workgroups from the workers' masks directly.  union_next NULL: exactly
@@ -258,17 +283,16 @@ int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uin
 int omr_round_plan_chain(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                          uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
                          uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                         uint32_t* arrive, uint32_t* done_flag, uint32_t seq, uint32_t* union_next,
-                         uint32_t block_size, omr_stream_t stream);
+                         uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                         omr_stream_t stream);
 /* omr_round_plan_chain with worker c's masks at row_masks + c * mask_stride (mask_stride >= rows: the all-gathered
  * arrays of the fused pack carry each worker's position table after its masks), and zero_counters (device
  * uint32[num_zero_counters <= 1024], or NULL) cleared: the next round's pack counters. */
 int omr_round_plan_ex(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
                       uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
                       uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
-                      uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                      omr_stream_t stream);
+                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* done_flag,
+                      uint32_t seq, uint32_t* union_next, uint32_t block_size, omr_stream_t stream);
 struct omr_sum_list;
 /* omr_round_plan_ex plus, by further workgroups of the same launch, an aggregator's shard-sum pair list
  * (omr_sum_list below; NULL: none), over column streams of the layout (rows * num_lanes * block_size floats,
@@ -276,22 +300,9 @@ struct omr_sum_list;
 int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
                         uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
                         uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
-                        uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                        const struct omr_sum_list* list, omr_stream_t stream);
-/* omr_round_plan_list in row chunks (round 4): 256-thread workgroups, one per 256 rows of EVERY array (one wave per
- * SIMD, so they fit on a CU beside a running scan workgroup), each publishing its chunk's per-array totals and adding
- * its predecessors'.  Same outputs, bit for bit.  `workspace`: device uint32[omr_round_plan_workspace_words()],
- * zeroed once by the caller and left zeroed by every launch (one launch at a time per workspace); it also replaces
- * `arrive` (the completion notice's counter).  Plans of more than 64 * 256 rows run omr_round_plan_list's form, with
- * workspace[0] as its arrival counter. */
-uint64_t omr_round_plan_workspace_words(void);
-int omr_round_plan_ws(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
-                      uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
-                      uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* workspace,
-                      uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                      const struct omr_sum_list* list, omr_stream_t stream);
+                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* done_flag,
+                        uint32_t seq, uint32_t* union_next, uint32_t block_size, const struct omr_sum_list* list,
+                        omr_stream_t stream);
 
 /* Block movement addressed by a row mask and its prefix (no block list): the k-th set bit of `row_masks` over
  * rows [0, rows) minus [skip_begin, skip_end) is block k of the packed stream.
@@ -311,21 +322,12 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
                       const uint64_t* row_masks, uint32_t count, const uint32_t* prefix, const uint64_t* write_set,
                       uint64_t rows, uint64_t row_begin, uint64_t row_end, uint32_t num_lanes, uint32_t block_size,
                       int packed_out, float* out, omr_stream_t stream);
-/* The same over the fused pack's column-ordered streams (omr_worker_scan_pack_f32): worker a's stream of these rows
- * at recv + recv_offsets[a] blocks, a block's place from worker a's position table, which sits at word pos_offset
- * (uint32 words) of its array row_masks + a * mask_stride (after its masks: pos_offset >= 2 * rows).  Rows
- * [row_begin, row_end) must be whole column segments of the layout (n, block_size, num_lanes, num_parts); `prefix`
- * is used for the write set's entry (packed_out) only. */
-int omr_shard_sum_cols_f32(const float* own, uint32_t me, const float* recv, const uint64_t* recv_offsets,
-                           const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t pos_offset,
-                           const uint32_t* prefix, const uint64_t* write_set, uint64_t n, uint32_t block_size,
-                           uint32_t num_lanes, uint32_t num_parts, uint64_t row_begin, uint64_t row_end,
-                           int packed_out, float* out, omr_stream_t stream);
 
-/* The same shard sum in two steps (the multi-rank round's form since round 3): its (block, contributor) pair list,
- * which depends only on the all-gathered masks and position tables and on where each worker's stream will land in
- * `recv`, is built before the exchange (by the plan launch: omr_round_plan_list); the sum then streams the pairs'
- * blocks (server.cc:97-98, rank order from +0.0f, bit-exact with omr_shard_sum_cols_f32).
+/* The shard sum over the fused pack's column-ordered streams (omr_worker_scan_pack_f32; the multi-rank round's form),
+ * in two steps: its (block, contributor) pair list, which depends only on the all-gathered masks and position tables
+ * and on where each worker's stream will land in `recv`, is built before the exchange (by the plan launch:
+ * omr_round_plan_list); the sum then streams the pairs' blocks (server.cc:97-98, rank order from +0.0f: the same sums,
+ * bit for bit, as omr_shard_sum_f32 over row-ordered streams).
  *   records  device uint64[units * capacity] (omr_sum_list_geometry: a unit's records end with a terminator word),
  *   counts   device uint32[units] (each unit's record count);
  *   rows [row_begin, row_end): the shard, whole column segments of the layout;

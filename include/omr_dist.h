@@ -104,6 +104,11 @@ int omr_dist_poll(omr_dist* d);
  * half). */
 int omr_dist_inject_fault(omr_dist* d, int64_t after_pieces);
 int omr_dist_inject_allgather_fault(omr_dist* d);
+/* Test hook (on: 1): a one-rank group runs the multi-rank round's code path -- worker scan, mask all-gather, plan and
+ * exchange on the side stream -- instead of the one-launch round, and an RCCL transport issues its all-gather, exchange
+ * and reduce-scatter as RCCL calls instead of as copies.  So the fault tests reach RCCL's group and ncclCommAbort paths,
+ * and the N > 1 round's stream layout can be timed, on a one-GPU box. */
+int omr_dist_test_world1_round(omr_dist* d, int on);
 
 /* Workspaces for tensors of n floats on the layout (block_size, num_lanes, num_parts); allocated on the current
  * HIP device, which must be the device the rank's tensors live on. */
@@ -221,6 +226,12 @@ int omr_ar_plan_stage_timings(omr_ar_plan* plan, float* stage_ms, uint64_t* byte
  * whole column segments of the scan, world > 1, OMR_PACK_MOVE unset), 0 if a separate pack pass does
  * (omr_move_blocks_f32). */
 int omr_ar_plan_fused_pack(const omr_ar_plan* plan);
+/* Device memory the plan holds (bytes), through its transport: per round set the masks, write set, prefixes and pair
+ * list; three send buffers of the tensor less this rank's own shard (the exchange's streams, then an all-reduce's
+ * returned sums); one receive buffer for this shard's blocks from the other workers; this shard's sums; the scan's
+ * flags / next offsets when the caller passes none; and, once omr_sparse_buckets_f32 has staged a host gradient, its
+ * four staging buckets.  A 256 MiB plan at world 8 holds about 3.6 x the tensor (round 5; 9 x before). */
+uint64_t omr_ar_plan_device_bytes(const omr_ar_plan* plan);
 /* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
 int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
 /* Join, then wait on the host until `stream` has run every round issued so far: the bounded counterpart of a stream

@@ -119,6 +119,9 @@ struct omr_dist {
   }
   // the operations the round uses (every rank of the group calls them in the same order); an error aborts
   bool fault_allgather = false;  // omr_dist_inject_allgather_fault (test hook)
+  // omr_dist_test_world1_round (test hook): a one-rank group runs the multi-rank round's code path (all-gather, plan,
+  // exchange on the side stream) instead of the one-launch round, and RCCL issues its collectives as RCCL calls
+  bool world1_general = false;
   int allgather(const void* in, void* out, size_t bytes, hipStream_t st) {
     TRY(check_open("allgather"));
     if (fault_allgather) {
@@ -160,6 +163,12 @@ namespace {
 // the same order on every rank.
 struct RcclDist final : omr_dist {
   ncclComm_t comm = nullptr, xcomm = nullptr;
+  // Cross-thread abort (omr_dist_abort may run on another thread while this rank waits): ncclCommAbort
+  // frees a communicator, so every use of comm / xcomm holds `cm`, and the aborting thread takes it before aborting.
+  // The owner's calls that can block inside RCCL (a group end waiting on a peer) are not held back by it: the aborter
+  // waits for them at most the deadline, then aborts anyway (which is what ends such a wait).
+  std::mutex cm;
+  std::atomic<int> in_rccl{0};  // owner-thread RCCL calls in progress (outside `cm`)
   ~RcclDist() override {
     if (xcomm) (void)ncclCommDestroy(xcomm);
     if (comm) (void)ncclCommDestroy(comm);
@@ -167,11 +176,17 @@ struct RcclDist final : omr_dist {
   // ncclCommAbort on both communicators (the split one first): the operations queued on them are cancelled on the
   // device, so this rank's streams drain; the peers' matching operations are left to their own deadlines
   void abort_group() override {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (in_rccl.load(std::memory_order_acquire) != 0 &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(timeout_ms))
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    std::lock_guard<std::mutex> g(cm);
     if (xcomm) (void)ncclCommAbort(xcomm);
     if (comm) (void)ncclCommAbort(comm);
     xcomm = comm = nullptr;
   }
   int do_poll() override {
+    std::lock_guard<std::mutex> g(cm);
     for (ncclComm_t c : {comm, xcomm}) {
       if (c == nullptr) continue;
       ncclResult_t a = ncclSuccess;
@@ -180,16 +195,31 @@ struct RcclDist final : omr_dist {
     }
     return 0;
   }
+  // an owner-thread RCCL call: counted (an aborter waits for it up to the deadline), and refused once aborted
+  struct InRccl {
+    RcclDist* d;
+    explicit InRccl(RcclDist* dd) : d(dd) { d->in_rccl.fetch_add(1, std::memory_order_acq_rel); }
+    ~InRccl() { d->in_rccl.fetch_sub(1, std::memory_order_acq_rel); }
+  };
+  int live(const char* what) {
+    if (comm == nullptr || xcomm == nullptr || aborted.load(std::memory_order_acquire))
+      return derr(OMR_EABORTED, "%s: rank %d's communicators were aborted", what, rank);
+    return 0;
+  }
   // A one-rank group's collectives are copies: RCCL queues the same copy kernel for them, after 5-10 us of host-side
   // group set-up per call (the world-1 round's host trace, profiles/r04/round_w1_trace/host_laps.txt), so they are
-  // issued as the copy directly.
+  // issued as the copy directly (world1_general: as RCCL calls, so the fault tests reach RCCL's group and abort paths).
   int do_allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
-    if (world == 1)
+    if (world == 1 && !world1_general)
       return in == out ? 0 : hip_check(hipMemcpyAsync(out, in, bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+    InRccl g(this);
+    TRY(live("allgather"));
     return nccl_check(ncclAllGather(in, out, bytes, ncclUint8, comm, st), "ncclAllGather");
   }
   int do_exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
-    if (world == 1) return fault(0);  // no peers: nothing to send or receive
+    if (world == 1 && !world1_general) return fault(0);  // no peers: nothing to send or receive
+    InRccl g(this);
+    TRY(live("exchange"));
     TRY(nccl_check(ncclGroupStart(), "ncclGroupStart"));
     // The group is closed on every path: a group left open would capture every later RCCL call of this thread (the
     // next round's all-gather and exchange would be queued into it and never launched).  After a failed piece the
@@ -211,10 +241,12 @@ struct RcclDist final : omr_dist {
     return rc ? rc : rc_end;
   }
   int do_reduce_scatter(const float* in, float* out, size_t count, hipStream_t st) override {
-    if (world == 1)
+    if (world == 1 && !world1_general)
       return in == out ? 0
                        : hip_check(hipMemcpyAsync(out, in, count * sizeof(float), hipMemcpyDeviceToDevice, st),
                                    "hipMemcpyAsync");
+    InRccl g(this);
+    TRY(live("reduce_scatter"));
     return nccl_check(ncclReduceScatter(in, out, count, ncclFloat32, ncclSum, xcomm, st), "ncclReduceScatter");
   }
 };
@@ -904,10 +936,13 @@ struct HostTrace {
   }
 };
 
-// a plan's device buffer, through its transport (omr_dist::alloc)
+// a plan's device buffer, through its transport (omr_dist::alloc); *total (if given) counts its bytes
 template <typename T>
-int dev_alloc(omr_dist* d, T** p, size_t count) {
-  return d->alloc(reinterpret_cast<void**>(p), std::max<size_t>(count, 1) * sizeof(T));
+int dev_alloc(omr_dist* d, T** p, size_t count, uint64_t* total = nullptr) {
+  const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+  TRY(d->alloc(reinterpret_cast<void**>(p), bytes));
+  if (total) *total += bytes;
+  return 0;
 }
 
 }  // namespace
@@ -928,8 +963,8 @@ struct omr_ar_plan {
   std::vector<uint64_t> bounds;   // shard s = rows [bounds[s], bounds[s+1])
   uint64_t shard_nb = 0;          // blocks of the largest shard
   // Fused pack (omr_worker_scan_pack_f32): the worker scan writes its blocks of the other shards into their send
-  // streams itself (no pack pass).  Needs every shard to be whole column segments of the scan (world 1, 2, 4, 8 of a
-  // power-of-two layout); otherwise (ragged shards, or OMR_PACK_MOVE=1) the round packs with omr_move_blocks_f32.
+  // streams itself (no pack pass).  Needs every shard to be whole column segments of the scan (world 2, 4, 8 of a
+  // power-of-two layout); otherwise (ragged shards) the round packs with omr_move_blocks_f32.
   // Each rank's all-gathered array is then its masks followed by its position table: mstride words per rank.
   bool fused_pack = false;
   bool sum_list = false;            // the shard sum's pairs built by the plan launch (fused pack, N > 1, an aggregator;
@@ -938,57 +973,71 @@ struct omr_ar_plan {
   uint32_t list_cap = 0;
   uint64_t mstride = 0;           // uint64 words per rank in masks_all (rows without the fused pack)
   // per-round state, kSets sets used in turn: an asynchronous round's bookkeeping and exchange still read their
-  // set while the next rounds' scans fill the others
-  // Four sets by default: one more round between a set's plan and the scan that refills it.  With three the world-1
-  // round took 58.1-64.1 us, with four 56.9-57.3 (defer, 3 runs each; profiles/r04/round_sets/).  OMR_ROUND_SETS=3:
-  // three.
+  // set while the next rounds' scans fill the others.  Four: one more round between a set's plan and the scan that
+  // refills it (with three the world-1 round took 58.1-64.1 us, with four 56.9-57.3; profiles/r04/round_sets/).
   static constexpr int kSets = 4;
-  int nsets = kSets;
+  static constexpr int nsets = kSets;
   struct Set {
     uint64_t* own = nullptr;        // [mstride] this rank's masks (the scan ORs into them; the plan kernel re-zeroes
                                     // them), then (fused pack) its position table
     uint64_t* masks_all = nullptr;  // [N][mstride] every rank's `own` (all-gather)
     uint32_t* pack_cnt = nullptr;   // fused pack: [A] the scan's per-shard stream counters (the plan re-zeroes them)
     uint64_t* wset = nullptr;       // [rows] write set: union + lane heads
-    uint64_t* umask = nullptr;      // [rows] union of the workers' masks
     uint32_t* prefix = nullptr;     // [N+1][rows+1] popcount prefixes: workers, then the write set
-    float* packed = nullptr;        // own non-zero blocks of the other shards, block order
-    float* recv = nullptr;          // this shard's blocks from each peer, worker w's at w * shard_nb blocks
-    hipEvent_t xdone = nullptr;     // aggregation stream: recorded on the communication stream after the exchange
     uint64_t* list_rec = nullptr;   // sum list: the shard sum's pair records, built by the plan launch
     uint32_t* list_cnt = nullptr;   //   and their count per unit
     hipEvent_t scanned = nullptr;   // async: recorded on the caller's stream after the worker scan
-    hipEvent_t ready = nullptr;     // recorded once the set is filled (the plan stream for async rounds)
-    hipEvent_t done = nullptr;      // recorded on the communication stream once the round is through with it
+    hipEvent_t ready = nullptr;     // recorded once the set is filled (the side stream for async rounds)
+    hipEvent_t done = nullptr;      // recorded on the side stream once the round is through with it
     bool pending = false;           // `done` recorded and not yet waited for by a refill
     bool plan_pending = false;      // `ready` recorded (the plan has consumed and re-zeroed `own`) and not yet waited
                                     // for by a scan
-    bool scan_wait = false;         // fused pack: `done` recorded and not yet waited for by the scan that refills
-                                    // `packed` (guarded by mu: the progress thread sets it)
   } set[kSets];
+  // Send buffers (a worker's other-shard blocks for the exchange; an all-reduce's returned sums land in the same
+  // buffer afterwards), kPackBufs used in turn by the rounds: round k's is read by its exchange, issued kDeferDepth calls
+  // later, so round k + kPackBufs's scan (the fused pack writes it) waits for that round's `done` (round 5: three
+  // instead of one per set, so a 256 MiB plan at world 8 holds 3.6x the tensor instead of 9x).
+  static constexpr int kPackBufs = 3;
+  struct PackBuf {
+    float* buf = nullptr;   // n floats less this rank's own shard (pack_send_floats)
+    int done_set = -1;      // the set whose `done` frees it, once its round's second half is issued
+    bool scan_wait = false; // fused pack: that `done` not yet waited for by the scan that refills it (guarded by mu)
+  } pk[kPackBufs];
+  uint64_t pack_floats = 0;
+  uint64_t rounds_total = 0;        // rounds issued so far (round k uses pk[k % kPackBufs])
+  float* recv = nullptr;            // this shard's blocks from each peer (recv_slot): one buffer, every round's exchange
+                                    // and shard sum run in order on the side stream
   int cur = 0;                      // the set the next round fills
   int last_async = -1;              // set of the last asynchronous round (for join)
-  hipStream_t ps = nullptr;         // plan stream of asynchronous rounds: mask all-gather, plan, pack, union chain
-  hipStream_t cs = nullptr;         // communication stream of asynchronous rounds: exchange, shard sums [, sums back]
-  hipStream_t as = nullptr;         // aggregation stream: an asynchronous co-located reduce-scatter round's shard sums,
-                                    // so round k+1's exchange on `cs` runs while round k's sums do (OMR_AGG_STREAM=1:
-                                    // on; off by default)
-  int as_last = -1;                 // set of the last round whose sums went on `as` (for join)
+  // Asynchronous rounds run their steps after the worker scan on ONE side stream, in the order they are issued:
+  // round k-2's exchange and sums, then round k's all-gather and plan (round 5; two side streams before).  The caller's
+  // stream runs only the scans.
+  hipStream_t ps = nullptr;         // the side stream (cs == ps)
+  hipStream_t cs = nullptr;
   hipStream_t tail = nullptr;       // the stream of the last asynchronous round's last work (the bucket write-back)
   uint64_t* bounds_dev = nullptr;
   uint32_t* counts_host = nullptr;  // [kSets][M+1][A+1] per set: prefix[a][bounds[s]], pinned memory the plan kernel writes
   uint32_t* counts_map = nullptr;   // its device-side address
-  float* results = nullptr;  // all-reduce: every shard's sums, write-set order (a dedicated aggregator: its own)
+  float* results = nullptr;  // an aggregator's own shard sums, write-set order (all-reduce, dedicated aggregators)
   uint64_t last_sums_blocks = 0;  // a dedicated aggregator: blocks of its last round's shard sums in `results`
   int32_t* flags_ws = nullptr;
   uint32_t* next_ws = nullptr;
   void* scan_ws = nullptr;   // omr_worker_scan_f32 segment workspace (zeroed once, self-resetting)
   size_t scan_ws_bytes = 0;
-  uint32_t* arrive = nullptr;     // the plan kernel's workspace (omr_round_plan_ws; word 0: its arrival counter)
-  bool plan_v1 = true;            // round 3's plan form (omr_round_plan_list, the default) or omr_round_plan_ws
   uint32_t* flag_host = nullptr;  // [kSets] pinned, per set: the plan kernel stores the round's sequence number here
   uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
+  // The one-rank round (world 1, one worker = its own aggregator; omr_worker_scan_tally_f32): the bookkeeping is two
+  // counts, tallied by the scan's workgroups and published by the NEXT round's scan (one extra workgroup), so a
+  // pipelined world-1 round is one launch on the caller's stream.
+  uint64_t* tally = nullptr;        // device [kSets][tally_slots]: a slot per scan workgroup
+  uint32_t tally_slots = 0;
+  uint32_t* pub_host = nullptr;     // pinned [kSets][4]: {seq, non-zero blocks, write-set blocks, seq}
+  uint32_t* pub_map = nullptr;
+  int pub_set = -1;                 // the set whose tally no launch has published yet
+  uint32_t pub_seq = 0;
+  hipStream_t pub_st = nullptr;     // the stream its scan went on
+  uint64_t dev_bytes = 0;           // device memory of the plan (omr_ar_plan_device_bytes)
   // OMR_ROUND_TIME_EXCHANGE: events around the last timed round's worker -> aggregator exchange, and its bytes
   hipEvent_t xt0 = nullptr, xt1 = nullptr;  // the last timed exchange's events (owned by its ring record)
   bool xt_recorded = false;
@@ -1009,11 +1058,11 @@ struct omr_ar_plan {
   // OMR_ROUND_DEFER: the rounds whose exchange and aggregation later calls (or join) issue, oldest first.  Call k
   // issues round k - kDeferDepth's: its block counts have been in host memory since about the middle of round k-1's
   // scan, so the host never waits for them, and the caller's stream always has the next scan queued.
-  static constexpr int kDeferDepth = 2;  // <= kSets - 1 (a set is refilled kSets calls later)
-  int defer_depth = kDeferDepth;         // OMR_DEFER_DEPTH=1 (diagnostic): issue the previous round's instead
+  static constexpr int kDeferDepth = 2;  // <= kSets - 1 (a set is refilled kSets calls later), < kPackBufs
+  static constexpr int defer_depth = kDeferDepth;
   struct Pending {
     bool active = false;
-    int si = 0, mode = 0;
+    int si = 0, mode = 0, pki = 0;
     bool timed = false;
     const float* x = nullptr;
     float* out = nullptr;
@@ -1031,7 +1080,8 @@ struct omr_ar_plan {
   // calling thread queues the scan, then a job; it runs at most kSets - 1 rounds ahead of the thread's first halves
   // (a set's `ready` / `scanned` events must have been recorded / waited for before the set is reused).
   struct Job {
-    int si = 0, mode = 0, tslot = -1;
+    int si = 0, mode = 0, tslot = -1, pki = 0;
+    uint32_t seq = 0;  // a one-rank round's sequence number (taken when its scan was issued)
     bool async = false, defer = false, timed = false, flush_first = false;
     const float* x = nullptr;
     float* out = nullptr;
@@ -1232,6 +1282,12 @@ int omr_dist_inject_fault(omr_dist* d, int64_t after_pieces) {
   return 0;
 }
 
+int omr_dist_test_world1_round(omr_dist* d, int on) {
+  if (d == nullptr) return derr(OMR_EINVAL, "test_world1_round: NULL");
+  d->world1_general = on != 0;
+  return 0;
+}
+
 int omr_dist_inject_allgather_fault(omr_dist* d) {
   if (d == nullptr) return derr(OMR_EINVAL, "inject_allgather_fault: NULL");
   d->fault_allgather = true;
@@ -1269,20 +1325,42 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   // transport is aborted, and their second halves would only fail)
   if (p->npend > 0 && p->failed == 0 && !p->d->aborted.load()) (void)flush_pending(p, p->cs, nullptr, nullptr);
   p->npend = 0;
-  (void)hipDeviceSynchronize();  // (an aborted RCCL communicator has cancelled its queued operations)
+  if (p->failed == 0 && !p->d->aborted.load()) {
+    (void)hipDeviceSynchronize();
+  } else {
+    // After a failure the plan's streams may hold waits on a peer that will never come (an IPC peer's event; an aborted
+    // RCCL communicator has cancelled its queued operations, the IPC and loopback transports cannot): wait for them
+    // within the deadline only, and if they are still busy leave the plan's device memory allocated rather than free
+    // it under queued work (destroy must not block on a dead peer).
+    const auto t0 = std::chrono::steady_clock::now();
+    bool idle = false;
+    while (!idle) {
+      idle = true;
+      for (hipStream_t s : {p->ps, p->s_in, p->s_out})
+        if (s != nullptr && hipStreamQuery(s) == hipErrorNotReady) idle = false;
+      if (idle || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(p->d->timeout_ms)) break;
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    (void)hipGetLastError();
+    if (!idle) {
+      const int rc = derr(OMR_ETIMEDOUT, "ar_plan_destroy: the plan's streams were still busy %lld ms after its failure; "
+                          "its device memory is left allocated", static_cast<long long>(p->d->timeout_ms));
+      if (p->ht.on) p->ht.print(p->me);
+      delete p;  // (host state only: streams, events and buffers may still be in use on the device)
+      return rc;
+    }
+  }
   // back to the transport, which keeps the exported ones alive for the next plan (omr_dist::alloc)
-  void* devs[] = {p->bounds_dev, p->results, p->flags_ws, p->next_ws, p->scan_ws, p->arrive};
+  void* devs[] = {p->bounds_dev, p->results, p->flags_ws, p->next_ws, p->scan_ws, p->recv, p->tally};
   for (void* v : devs) p->d->release(v);
+  for (auto& b : p->pk) p->d->release(b.buf);
   for (auto& st : p->set) {
-    void* sv[] = {st.own, st.masks_all, st.wset, st.umask, st.prefix, st.packed, st.pack_cnt, st.list_rec, st.list_cnt,
-                  st.recv};
+    void* sv[] = {st.own, st.masks_all, st.wset, st.prefix, st.pack_cnt, st.list_rec, st.list_cnt};
     for (void* v : sv) p->d->release(v);
-    for (hipEvent_t e : {st.scanned, st.ready, st.done, st.xdone})
+    for (hipEvent_t e : {st.scanned, st.ready, st.done})
       if (e) (void)hipEventDestroy(e);
   }
   if (p->ps) (void)hipStreamDestroy(p->ps);
-  if (p->cs && p->cs != p->ps) (void)hipStreamDestroy(p->cs);
-  if (p->as) (void)hipStreamDestroy(p->as);
   for (int r = 0; r < omr_ar_plan::kStage; ++r) {
     p->d->release(p->stage[r]);
     for (hipEvent_t e : {p->ev_in[r], p->ev_round[r], p->ev_out[r]})
@@ -1297,6 +1375,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
       if (e) (void)hipEventDestroy(e);
   (void)hipHostFree(p->counts_host);
   (void)hipHostFree(p->flag_host);
+  (void)hipHostFree(p->pub_host);
   delete p;
   return 0;
 }
@@ -1321,7 +1400,6 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   const char* trace = getenv("OMR_HOST_TRACE");
   p->ht.on = trace != nullptr && (trace[0] == '1' || trace[0] == '2');
   p->ht.log = trace != nullptr && trace[0] == '2';
-  if (const char* dd = getenv("OMR_DEFER_DEPTH")) p->defer_depth = std::min(std::max(atoi(dd), 1), omr_ar_plan::kDeferDepth);
   p->M = static_cast<int>(num_workers);
   p->A = naggs;
   p->colocated = num_workers == static_cast<uint32_t>(d->world);
@@ -1342,19 +1420,16 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   for (int s = 0; s < NA; ++s) max_rows = std::max(max_rows, p->bounds[s + 1] - p->bounds[s]);
   p->shard_nb = max_rows * num_lanes;
   p->mstride = p->rows;
-  if (N > 1 && getenv("OMR_PACK_MOVE") == nullptr &&
-      omr_pack_supported(n, block_size, num_lanes, num_parts, p->bounds.data(), static_cast<uint32_t>(NA)) == 0) {
+  if (N > 1 && omr_pack_supported(n, block_size, num_lanes, num_parts, p->bounds.data(), static_cast<uint32_t>(NA)) == 0) {
     uint64_t entries = 0;
     TRY(omr_check(omr_pack_geometry(n, block_size, num_lanes, num_parts, nullptr, nullptr, &entries),
                   "omr_pack_geometry"));
     p->fused_pack = true;
     p->mstride = p->rows + (entries + 1) / 2;
-    // The plan launch builds the shard sum's pairs (16-row units, beside the plan's own workgroups: 11.68 against
-    // 11.76 us without them) and omr_shard_sum_list_f32 sums them with its first load: 9.32 us at config 4's 8-worker
-    // shard against 11.83 for omr_shard_sum_cols_f32, which builds its pairs itself (round 4,
-    // profiles/r04/round_kernels/tune_round_list16.log).  OMR_SUM_LIST=0 (study knob): the latter.
-    const char* le = getenv("OMR_SUM_LIST");
-    if (p->shard >= 0 && (le == nullptr || atoi(le) != 0)) {
+    // The plan launch builds the shard sum's pairs (16-row units) and omr_shard_sum_list_f32 sums them with its first
+    // load: 9.32 us at config 4's 8-worker shard against 11.83 for round 3's form that built its pairs itself (round 4,
+    // profiles/r04/round_kernels/tune_round_list16.log; that form is tools/tune/plan_r04.hip's k_shard_sum_r04 now).
+    if (p->shard >= 0) {
       TRY(omr_check(omr_sum_list_geometry(n, block_size, num_lanes, num_parts, p->bounds[p->shard],
                                           p->bounds[p->shard + 1], static_cast<uint32_t>(p->M), &p->list_units,
                                           &p->list_cap), "omr_sum_list_geometry"));
@@ -1365,76 +1440,54 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   auto A = [&](int r) {
     if (rc == 0) rc = r;
   };
+  uint64_t* const DB = &p->dev_bytes;
   // the round's events order work between streams of this device only: no system-scope fence (a record costs
   // its stream 1.2 us instead of 2.8, tools/event_cost.hip); what the host reads goes out as system-scope stores
-  const char* sf = getenv("OMR_EVENT_SYSFENCE");
-  const unsigned evflags = hipEventDisableTiming | ((sf != nullptr && atoi(sf) != 0) ? 0u : hipEventDisableSystemFence);
-  if (const char* ns = getenv("OMR_ROUND_SETS")) p->nsets = atoi(ns) == 3 ? 3 : omr_ar_plan::kSets;
+  const unsigned evflags = hipEventDisableTiming | hipEventDisableSystemFence;
   for (int i = 0; i < p->nsets; ++i) {
     omr_ar_plan::Set& st = p->set[i];
-    A(dev_alloc(p->d, &st.own, p->mstride));
-    A(dev_alloc(p->d, &st.masks_all, static_cast<size_t>(N) * p->mstride));
-    if (p->fused_pack) A(dev_alloc(p->d, &st.pack_cnt, NA));
-    A(dev_alloc(p->d, &st.wset, p->rows));
-    A(dev_alloc(p->d, &st.umask, p->rows));
-    A(dev_alloc(p->d, &st.prefix, static_cast<size_t>(M + 1) * (p->rows + 1)));
-    if (N > 1 && p->worker()) A(dev_alloc(p->d, &st.packed, n));
+    A(dev_alloc(p->d, &st.own, p->mstride, DB));
+    A(dev_alloc(p->d, &st.masks_all, static_cast<size_t>(N) * p->mstride, DB));
+    if (p->fused_pack) A(dev_alloc(p->d, &st.pack_cnt, NA, DB));
+    A(dev_alloc(p->d, &st.wset, p->rows, DB));
+    A(dev_alloc(p->d, &st.prefix, static_cast<size_t>(M + 1) * (p->rows + 1), DB));
     if (p->sum_list) {
-      A(dev_alloc(p->d, &st.list_rec, p->list_units * p->list_cap));
-      A(dev_alloc(p->d, &st.list_cnt, p->list_units));
+      A(dev_alloc(p->d, &st.list_rec, p->list_units * p->list_cap, DB));
+      A(dev_alloc(p->d, &st.list_cnt, p->list_units, DB));
     }
-    for (hipEvent_t* e : {&st.scanned, &st.ready, &st.done, &st.xdone})
+    for (hipEvent_t* e : {&st.scanned, &st.ready, &st.done})
       A(hip_check(hipEventCreateWithFlags(e, evflags), "hipEventCreate"));
   }
-  {
-    // OMR_SIDE_PRIORITY (study knob): 1 = the plan and communication streams at the device's greatest priority, so
-    // their short kernels are dispatched ahead of the caller's scan workgroups; 0 = normal priority
-    const char* pe = getenv("OMR_SIDE_PRIORITY");
-    int least = 0, greatest = 0;
-    A(hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange"));
-    const int prio = (pe != nullptr && atoi(pe) != 0) ? greatest : least;
-    A(hip_check(hipStreamCreateWithPriority(&p->ps, hipStreamNonBlocking, prio), "hipStreamCreate"));
-    // A one-rank group has no exchange: its communication stream would carry only event waits and records, so it is
-    // the plan stream itself.  Fewer streams share the process's hardware queues less: the in-process world-1 round
-    // ran 52.4-53.2 us instead of 101-108 in 5 of the 6 stream / group orders that were slow with two side streams,
-    // the bench child unchanged (profiles/r04/inproc/one_side/).  At N > 1 the exchange keeps a stream of its own, so
-    // it runs beside the next round's all-gather and plan.  OMR_ONE_SIDE_STREAM=0 / 1 forces two / one (study knob).
-    const char* os1 = getenv("OMR_ONE_SIDE_STREAM");
-    const bool one_side = os1 != nullptr ? atoi(os1) != 0 : N == 1;
-    if (one_side) p->cs = p->ps;
-    else A(hip_check(hipStreamCreateWithPriority(&p->cs, hipStreamNonBlocking, prio), "hipStreamCreate"));
-    // OMR_AGG_STREAM=1 (opt-in): the aggregation stream.  Off by default: a fourth side stream exceeds the process's
-    // four hardware queues (GPU_MAX_HW_QUEUES), and its wait for the exchange can then block whatever shares its queue.
-    // As 4 IPC ranks on one GPU it took 27.5 ms per round against 1.47 ms without (profiles/r03/agg_stream/).
-    const char* ae = getenv("OMR_AGG_STREAM");
-    if (N > 1 && p->shard >= 0 && ae != nullptr && atoi(ae) != 0)
-      A(hip_check(hipStreamCreateWithPriority(&p->as, hipStreamNonBlocking, prio), "hipStreamCreate"));
-  }
+  // The side stream: every asynchronous round's steps after its scan, in issue order (round 5).  Each stream the
+  // process makes takes one of its hardware queues (GPU_MAX_HW_QUEUES, 4 on the box) round robin, and streams that
+  // share a queue run one after the other: with two side streams the world-1 round ran 2x slower in the stream orders
+  // whose side stream shared the caller's queue (profiles/r04/inproc/).  One side stream halves that exposure, and the
+  // one-rank round (solo) uses none.
+  A(hip_check(hipStreamCreateWithFlags(&p->ps, hipStreamNonBlocking), "hipStreamCreate"));
+  p->cs = p->ps;
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, evflags), "hipEventCreate"));
-  A(dev_alloc(p->d, &p->bounds_dev, NA + 1));
-  if (N > 1 && p->shard >= 0)
-    for (int i = 0; i < p->nsets; ++i)
-      A(dev_alloc(p->d, &p->set[i].recv, static_cast<size_t>(M) * p->shard_nb * block_size));
-  A(dev_alloc(p->d, &p->results, n));
-  A(dev_alloc(p->d, &p->flags_ws, p->nb));
-  A(dev_alloc(p->d, &p->next_ws, p->nb));
+  A(dev_alloc(p->d, &p->bounds_dev, NA + 1, DB));
+  if (N > 1 && p->worker()) {
+    // (N - 1) / N of the tensor on a co-located rank: the own shard is never sent, and the sums of the other shards
+    // that an all-reduce returns fit the same space
+    p->pack_floats = p->colocated ? n - (p->bounds[p->me + 1] - p->bounds[p->me]) * num_lanes * block_size : n;
+    for (auto& b : p->pk) A(dev_alloc(p->d, &b.buf, p->pack_floats, DB));
+  }
+  if (N > 1 && p->shard >= 0)  // every other worker's stream of this shard, worker w's at recv_slot(w)
+    A(dev_alloc(p->d, &p->recv, static_cast<size_t>(p->colocated ? M - 1 : M) * p->shard_nb * block_size, DB));
+  if (p->shard >= 0) A(dev_alloc(p->d, &p->results, p->shard_nb * block_size, DB));
+  A(dev_alloc(p->d, &p->flags_ws, p->nb, DB));
+  A(dev_alloc(p->d, &p->next_ws, p->nb, DB));
   p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
-  A(dev_alloc(p->d, reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes));
+  A(dev_alloc(p->d, reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes, DB));
+  p->tally_slots = omr_tally_slots(n, block_size, num_lanes, num_parts);
+  A(dev_alloc(p->d, &p->tally, static_cast<size_t>(p->tally_slots) * omr_ar_plan::kSets, DB));
   constexpr int NSETS = omr_ar_plan::kSets;
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), NSETS * (M + 1) * (NA + 1) * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0)
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->counts_map), p->counts_host, 0),
                 "hipHostGetDevicePointer"));
-  const uint64_t plan_ws_words = omr_round_plan_workspace_words();
-  A(dev_alloc(p->d, &p->arrive, plan_ws_words));
-  // Which plan form.  Round 3's (one 1024-thread workgroup per mask array) by default: standalone it takes 11.95 us at
-  // config 4's shapes against 13.4 for the row-chunk form (profiles/r04/round_kernels/), and beside the world-1
-  // round's scan the row-chunk workgroups fit and run starved next to it (the world-1 round: 64.8-67.9 us with them,
-  // 58.8-60.2 with round 3's form; profiles/r04/plan_ab/).  Rehearsed as 2 and 4 IPC ranks on one GPU, with the fused
-  // pack, the two forms were within the runs' spread.  OMR_PLAN_V1=0 selects the row-chunk form (omr_round_plan_ws).
-  p->plan_v1 = true;
-  if (const char* pv = getenv("OMR_PLAN_V1")) p->plan_v1 = atoi(pv) != 0;
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), NSETS * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0) {
@@ -1442,7 +1495,13 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->flag_map), p->flag_host, 0),
                 "hipHostGetDevicePointer"));
   }
-  if (rc == 0) A(hip_check(hipMemset(p->arrive, 0, plan_ws_words * sizeof(uint32_t)), "hipMemset plan workspace"));
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->pub_host), NSETS * 4 * sizeof(uint32_t),
+                            hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
+  if (rc == 0) {
+    memset(p->pub_host, 0, NSETS * 4 * sizeof(uint32_t));
+    A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->pub_map), p->pub_host, 0),
+                "hipHostGetDevicePointer"));
+  }
   for (int i = 0; i < p->nsets && rc == 0; ++i) {
     omr_ar_plan::Set& st = p->set[i];
     A(hip_check(hipMemset(st.own, 0, p->mstride * sizeof(uint64_t)), "hipMemset own masks"));
@@ -1492,9 +1551,12 @@ int timed_exchange(omr_ar_plan* p, int slot) {
   return 0;
 }
 
-// Worker w's stream of this rank's shard lands at a fixed region of `recv` (w * shard_nb blocks), so the shard sum's
-// pairs can be addressed before the exchange (the plan launch builds them: omr_round_plan_list).
-uint64_t recv_slot(const omr_ar_plan* p, int w) { return static_cast<uint64_t>(w) * p->shard_nb; }
+// Worker w's stream of this rank's shard lands at a fixed region of `recv`, so the shard sum's pairs can be addressed
+// before the exchange (the plan launch builds them: omr_round_plan_list).  A co-located aggregator reads its own blocks
+// in place: its slot is left out.
+uint64_t recv_slot(const omr_ar_plan* p, int w) {
+  return static_cast<uint64_t>(p->colocated && w > p->me ? w - 1 : w) * p->shard_nb;
+}
 
 omr_sum_list list_desc(const omr_ar_plan* p, const omr_ar_plan::Set& S) {
   omr_sum_list l{};
@@ -1508,15 +1570,55 @@ omr_sum_list list_desc(const omr_ar_plan* p, const omr_ar_plan::Set& S) {
   return l;
 }
 
-// (internal bit in a round's mode: a one-rank round whose worker scan wrote the sums itself, see omr_sparse_round_f32)
+// (internal bits in a round's mode, see sparse_round_issue: a one-rank round whose worker scan wrote the sums itself,
+// and one whose worker scan also tallied its bookkeeping, the one-launch round)
 constexpr int kModeSolo = 0x10000;
+constexpr int kModeTally = 0x20000;
 
 int wait_ev(hipStream_t on, hipEvent_t ev);
 
-int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, bool async, bool timed, uint32_t seq,
-                 hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks, int tslot) {
-  const bool solo = (mode & kModeSolo) != 0;
-  mode &= ~kModeSolo;
+// The one-rank round's counts: {seq, non-zero blocks, write-set blocks, seq} from omr_worker_scan_tally_f32's publishing
+// workgroup (or omr_tally_publish).  Bounded as wait_flag; `st` is the stream the publication went on.
+int wait_pub(omr_dist* d, const uint32_t* rec, uint32_t seq, hipStream_t st, uint32_t* nz, uint32_t* ws) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 1;; ++spin) {
+    if (__atomic_load_n(&rec[0], __ATOMIC_ACQUIRE) == seq && __atomic_load_n(&rec[3], __ATOMIC_ACQUIRE) == seq) {
+      *nz = __atomic_load_n(&rec[1], __ATOMIC_ACQUIRE);
+      *ws = __atomic_load_n(&rec[2], __ATOMIC_ACQUIRE);
+      return 0;
+    }
+    if ((spin & 4095) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q != hipSuccess && q != hipErrorNotReady) return d->contain(hip_check(q, "one-rank round"));
+      if (q == hipSuccess && !(__atomic_load_n(&rec[0], __ATOMIC_ACQUIRE) == seq &&
+                               __atomic_load_n(&rec[3], __ATOMIC_ACQUIRE) == seq))
+        return d->contain(derr(OMR_EINVAL, "one-rank round: stream idle but no counts (seq %u)", seq));
+      TRY(d->poll());
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(d->timeout_ms))
+        return d->contain(derr(OMR_ETIMEDOUT, "one-rank round: no counts after %lld ms (seq %u)",
+                               static_cast<long long>(d->timeout_ms), seq));
+    }
+    __builtin_ia32_pause();
+  }
+}
+
+// The oldest round whose tally no launch has published: publish it now, by a launch of its own (no later scan of the
+// plan will, or its second half is wanted before the next scan).
+int publish_pending(omr_ar_plan* p) {
+  if (p->pub_set < 0) return 0;
+  const int si = p->pub_set;
+  p->pub_set = -1;
+  return omr_check(omr_tally_publish(p->tally + static_cast<size_t>(p->tally_slots) * si, p->tally_slots,
+                                     p->pub_map + 4 * si, p->pub_seq, reinterpret_cast<omr_stream_t>(p->pub_st)),
+                   "omr_tally_publish");
+}
+
+// The second half of a round (steps 4b-7): wait for the plan's counts, exchange, shard sums [, sums back, unpack].
+// `async`: on the side stream, behind the round's first half (issued on it earlier: no event needed).
+int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, int mode, bool async, bool timed,
+                 uint32_t seq, hipStream_t st, uint64_t* sent_blocks, uint64_t* union_blocks, int tslot) {
+  const bool solo = (mode & kModeSolo) != 0, tally = (mode & kModeTally) != 0;
+  mode &= ~(kModeSolo | kModeTally);
   struct CloseRecord {  // the timing record is complete (or abandoned) once this second half returns
     omr_ar_plan* p;
     int slot;
@@ -1524,7 +1626,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       if (slot >= 0) p->timed[slot].open = false;
     }
   } close_record{p, timed ? tslot : -1};
-  struct CountHalf {  // (a fused-pack scan that refills this set waits until this second half is issued)
+  struct CountHalf {  // (a fused-pack scan that refills this round's send buffer waits until this second half is issued)
     omr_ar_plan* p;
     ~CountHalf() {
       {
@@ -1537,20 +1639,41 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
   omr_ar_plan::Set& S = p->set[si];
   const int N = p->N, M = p->M, NA = p->A, me = p->me, sh = p->shard;
   const uint64_t rows = p->rows, B = p->B;
+  ht_of(p).start();
+  if (tally) {
+    // the one-launch round: its worker scan wrote the sums and tallied the counts; they reach the host through the next
+    // round's scan or, if none has been issued, a publication of their own
+    if (p->pub_set == si && p->pub_seq == seq) TRY(publish_pending(p));
+    uint32_t nz = 0, ws = 0;
+    {
+      HostWait hw(p);
+      TRY(wait_pub(p->d, p->pub_host + 4 * si, seq, st, &nz, &ws));
+    }
+    ht_of(p).lap("2:wait counts");
+    if (sent_blocks) *sent_blocks = 0;
+    if (union_blocks) *union_blocks = ws;
+    return 0;
+  }
   const uint32_t NS = static_cast<uint32_t>(NA + 1);  // count columns per array (shard bounds)
   const uint32_t* counts = p->counts_host + static_cast<size_t>(si) * (M + 1) * NS;
   const uint32_t* flag = p->flag_host + si;
-  hipStream_t xs = st;
-  ht_of(p).start();
-  if (async) {
-    // (a deferred round's `ready` fired long ago, as a rule: then no wait is queued at all)
-    TRY(wait_ev(p->cs, S.ready));
-    xs = p->cs;
-  }
+  const hipStream_t xs = async ? p->cs : st;
   ht_of(p).lap("2:cs wait ready");
   const omr_stream_t xstream = reinterpret_cast<omr_stream_t>(xs);
   auto cnt = [&](int a, int s) -> uint64_t { return counts[a * NS + s]; };
   auto per = [&](int a, int s) -> uint64_t { return cnt(a, s + 1) - cnt(a, s); };
+  auto finish_async = [&](bool used_pack) {
+    TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
+    S.pending = true;
+    p->last_async = si;
+    p->tail = xs;  // the stream this round's last work is on
+    if (used_pack) {
+      std::lock_guard<std::mutex> g(p->mu);
+      p->pk[pki].done_set = si;
+      p->pk[pki].scan_wait = true;
+    }
+    return 0;
+  };
   if (mode == OMR_ROUND_DENSE_REDUCE_SCATTER) {  // co-located only (checked by the caller)
     // the dense stand-in: every element of this rank's shard, reduced over all ranks by the transport
     const uint64_t r0 = p->bounds[me], r1 = p->bounds[me + 1];
@@ -1564,13 +1687,7 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       p->xt_recorded = true;
       TRY(timed_exchange(p, tslot));
     }
-    if (async) {
-      TRY(hip_check(hipEventRecord(S.done, xs), "hipEventRecord"));
-      S.pending = true;
-      p->last_async = si;
-      std::lock_guard<std::mutex> g(p->mu);
-      S.scan_wait = true;
-    }
+    if (async) TRY(finish_async(false));
     if (sent_blocks != nullptr || union_blocks != nullptr) {
       HostWait hw(p);
       TRY(wait_flag(p->d, flag, seq, st));
@@ -1585,7 +1702,8 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
   }
   ht_of(p).lap("2:wait counts");
   const bool wk = p->worker();
-  // a co-located rank keeps its own shard's blocks out of its packed stream (and reads them in place)
+  float* const send = (wk && N > 1) ? p->pk[pki].buf : nullptr;
+  // a co-located rank keeps its own shard's blocks out of its send streams (and reads them in place)
   const uint64_t own_shard = (wk && p->colocated) ? per(me, me) : 0;
   const uint64_t total_send = wk ? cnt(me, NA) - own_shard : 0;
   // 4b. workers send each shard's slice to its aggregator (common.cc:449); an aggregator receives its shard's blocks
@@ -1599,17 +1717,19 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       for (int s = 0; s < NA; ++s) {
         const int ar = p->agg_rank(s);
         if (ar == me) continue;
-        // the fused pack's stream of shard s starts at the shard's first block; the pack pass's streams follow one
-        // another in block order without this rank's own shard
-        const uint64_t k0 = p->fused_pack ? p->bounds[s] * p->lanes
+        // the fused pack's stream of shard s starts at the shard's place in the send buffer (the shards in order, the
+        // own one left out); the pack pass's streams follow one another in block order without the own shard
+        const uint64_t k0 = p->fused_pack ? omr_pack_send_offset(p->bounds.data(), static_cast<uint32_t>(NA),
+                                                                 p->colocated ? me : -1, static_cast<uint32_t>(s),
+                                                                 p->lanes, p->B, nullptr) / B
                                           : cnt(me, s) - (p->colocated && s > me ? own_shard : 0);
-        sends[ar] = {Slice{S.packed + k0 * B, per(me, s) * B * sizeof(float)}};
+        sends[ar] = {Slice{send + k0 * B, per(me, s) * B * sizeof(float)}};
       }
     if (sh >= 0)
       for (int w = 0; w < M; ++w) {
         if (w == me) continue;
         roff[w] = recv_slot(p, w);
-        recvs[w] = {Slice{S.recv + roff[w] * B, per(w, sh) * B * sizeof(float)}};
+        recvs[w] = {Slice{p->recv + roff[w] * B, per(w, sh) * B * sizeof(float)}};
         in_blocks += per(w, sh);
       }
     TRY(p->d->exchange(sends, recvs, xs));
@@ -1623,46 +1743,37 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
     TRY(timed_exchange(p, tslot));
   }
   const bool rs_mode = mode == OMR_ROUND_REDUCE_SCATTER;
-  // An asynchronous reduce-scatter round sums on the aggregation stream, behind this exchange only, so the next
-  // round's exchange on the communication stream need not wait for these sums (its blocks land in another set's
-  // `recv`).  The set's `done` then follows the sums, and with them the exchange.
-  hipStream_t ss = xs;
-  if (async && rs_mode && p->colocated && p->as != nullptr && sh >= 0 && !solo) {
-    TRY(hip_check(hipEventRecord(S.xdone, xs), "hipEventRecord"));
-    TRY(hip_check(hipStreamWaitEvent(p->as, S.xdone, 0), "hipStreamWaitEvent"));
-    ss = p->as;
-  }
-  const omr_stream_t sstream = reinterpret_cast<omr_stream_t>(ss);
   // 5. aggregator: rank-order shard sums (server.cc:97-98); a co-located rank reads its own blocks in place.
-  //    Co-located reduce-scatter writes them in place (dense); otherwise packed in write-set order
+  //    Co-located reduce-scatter writes them in place (dense); otherwise packed in write-set order into `results`
   float* sums = nullptr;
-  if (sh >= 0 && !solo) {
-    const uint64_t r0 = p->bounds[sh], r1 = p->bounds[sh + 1];
+  const uint32_t* const wprefix = S.prefix + static_cast<uint64_t>(M) * (rows + 1);
+  uint64_t r0 = 0, r1 = 0;
+  if (sh >= 0 && !solo) {  // (a one-rank round's worker scan wrote its sums: 0.0f + x over the write set)
+    r0 = p->bounds[sh];
+    r1 = p->bounds[sh + 1];
     const bool dense_out = rs_mode && p->colocated;
-    // (a dedicated aggregator keeps only its own shard's sums: at the start of `results`)
-    sums = dense_out ? out : p->results + (wk ? cnt(M, sh) * B : 0);
+    sums = dense_out ? out : p->results;
     const float* own = p->colocated ? x : nullptr;
     const uint32_t own_idx = p->colocated ? static_cast<uint32_t>(me) : static_cast<uint32_t>(M);
     if (p->sum_list) {  // the pairs were built by this round's plan launch
       const omr_sum_list l = list_desc(p, S);
-      TRY(omr_check(omr_shard_sum_list_f32(own, S.recv, &l, static_cast<uint32_t>(M), p->n, p->B, p->lanes, p->parts,
-                                           S.wset, S.prefix + static_cast<uint64_t>(M) * (rows + 1), dense_out ? 0 : 1,
-                                           sums, sstream),
+      TRY(omr_check(omr_shard_sum_list_f32(own, p->recv, &l, static_cast<uint32_t>(M), p->n, p->B, p->lanes, p->parts,
+                                           S.wset, wprefix, dense_out ? 0 : 1, sums, xstream),
                     "omr_shard_sum_list_f32"));
-    } else if (p->fused_pack)  // the workers' streams are column-ordered: positions from their all-gathered tables
-      TRY(omr_check(omr_shard_sum_cols_f32(own, own_idx, S.recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
-                                           p->mstride, 2 * rows, S.prefix, S.wset, p->n, p->B, p->lanes, p->parts,
-                                           r0, r1, dense_out ? 0 : 1, sums, sstream),
-                    "omr_shard_sum_cols_f32"));
-    else
-      TRY(omr_check(omr_shard_sum_f32(own, own_idx, S.recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
-                                      S.prefix, S.wset, rows, r0, r1, p->lanes, p->B, dense_out ? 0 : 1, sums, sstream),
+    } else {  // row-ordered streams (the pack pass of ragged shards)
+      TRY(omr_check(omr_shard_sum_f32(own, own_idx, p->recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
+                                      S.prefix, S.wset, rows, r0, r1, p->lanes, p->B, dense_out ? 0 : 1, sums, xstream),
                     "omr_shard_sum_f32"));
+    }
     if (!p->colocated) p->last_sums_blocks = per(M, sh);
   }
   ht_of(p).lap("2:shard sum");
   if (!rs_mode) {
-    // 6. sums back to every worker (server.cc:162), scattered in place (client.cc:89)
+    // 6. sums back to every worker (server.cc:162), into the round's send buffer (its exchange above is through with
+    //    it), then scattered in place (client.cc:89).  A co-located rank's own shard comes from `results`.
+    auto back_off = [&](int s) -> uint64_t {  // shard s's returned sums in the send buffer (blocks)
+      return cnt(M, s) - (p->colocated && s > me ? per(M, me) : 0);
+    };
     if (N > 1) {
       std::vector<Slices> ss(N), sr(N);
       if (sh >= 0)
@@ -1671,27 +1782,28 @@ int round_finish(omr_ar_plan* p, int si, const float* x, float* out, int mode, b
       if (wk)
         for (int s = 0; s < NA; ++s) {
           const int ar = p->agg_rank(s);
-          if (ar != me) sr[ar] = {Slice{p->results + cnt(M, s) * B, per(M, s) * B * sizeof(float)}};
+          if (ar != me) sr[ar] = {Slice{send + back_off(s) * B, per(M, s) * B * sizeof(float)}};
         }
       TRY(p->d->exchange(ss, sr, xs));
     }
-    if (wk && out != nullptr && !solo)
-      TRY(omr_check(omr_move_blocks_f32(p->results, out, 1, S.wset, S.prefix + static_cast<uint64_t>(M) * (rows + 1),
-                                        rows, p->lanes, p->B, 0, 0, xstream), "omr_move_blocks_f32 unpack"));
+    if (wk && out != nullptr && !solo) {
+      const bool own_part = p->colocated && sh >= 0;
+      if (N > 1 && (!own_part || r1 - r0 < rows))  // the other shards' sums (a co-located rank's own rows skipped)
+        TRY(omr_check(omr_move_blocks_f32(send, out, 1, S.wset, wprefix, rows, p->lanes, p->B, own_part ? r0 : 0,
+                                          own_part ? r1 : 0, xstream), "omr_move_blocks_f32 unpack"));
+      if (own_part && r1 > r0) {  // its own shard's, from `results` (write-set order from row r0)
+        const float* rbase = reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(p->results) -
+                                                            cnt(M, sh) * B * sizeof(float));
+        TRY(omr_check(omr_move_blocks_f32(rbase, out + r0 * p->lanes * B, 1, S.wset + r0, wprefix + r0, r1 - r0,
+                                          p->lanes, p->B, 0, 0, xstream), "omr_move_blocks_f32 unpack own"));
+      }
+    }
   }
   if (timed && p->timed[tslot].xchg) {
-    TRY(hip_check(hipEventRecord(p->timed[tslot].a1, ss), "hipEventRecord"));
+    TRY(hip_check(hipEventRecord(p->timed[tslot].a1, xs), "hipEventRecord"));
     p->timed[tslot].agg = true;
   }
-  if (async) {
-    TRY(hip_check(hipEventRecord(S.done, ss), "hipEventRecord"));
-    S.pending = true;
-    p->last_async = si;
-    p->tail = ss;  // the stream this round's last work is on
-    if (ss == p->as) p->as_last = si;
-    std::lock_guard<std::mutex> g(p->mu);
-    S.scan_wait = true;
-  }
+  if (async) TRY(finish_async(send != nullptr));
   ht_of(p).lap("2:rest");
   if (sent_blocks) *sent_blocks = total_send;
   if (union_blocks) *union_blocks = (rs_mode || !wk) ? (sh >= 0 ? per(M, sh) : 0) : cnt(M, NA);
@@ -1703,7 +1815,8 @@ int issue_oldest(omr_ar_plan* p, uint64_t* sent_blocks, uint64_t* union_blocks) 
   const omr_ar_plan::Pending q = p->pend[0];
   for (int i = 1; i < p->npend; ++i) p->pend[i - 1] = p->pend[i];
   --p->npend;
-  return round_finish(p, q.si, q.x, q.out, q.mode, true, q.timed, q.seq, q.st, sent_blocks, union_blocks, q.tslot);
+  return round_finish(p, q.si, q.pki, q.x, q.out, q.mode, true, q.timed, q.seq, q.st, sent_blocks, union_blocks,
+                      q.tslot);
 }
 
 // Issue every deferred round's second half, oldest first (outputs: the last one's counts; 0 if none).
@@ -1730,63 +1843,76 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
   if (t_progress) ht.start();
   const int si = j.si, mode = j.mode, tslot = j.tslot, M = p->M, me = p->me, N = p->N;
   const bool async = j.async, timed = j.timed;
+  const bool tally = (mode & kModeTally) != 0;
   const uint64_t rows = p->rows;
   const uint32_t NS = static_cast<uint32_t>(p->A + 1);
   const float* x = j.x;
   omr_ar_plan::Set& S = p->set[si];
   // a threaded round that is not deferred finishes the deferred ones first (rounds complete in call order)
   if (j.flush_first) TRY(flush_pending(p, j.st, nullptr, nullptr));
-  // the round's bookkeeping stream: an asynchronous round runs it on the plan stream, so the caller's stream is
-  // left with the worker scans alone (round k+1's scan overlaps round k's all-gather, plan and pack, and round
-  // k-1's exchange)
+  // Deferred: the second half of the round kDeferDepth calls back goes first, on the side stream, so its exchange
+  // runs beside this round's scan instead of queueing behind this round's wait for it (round 5: one side stream).
+  // Its counts have long been in host memory, so the host does not wait either.
+  if (j.defer && p->npend >= p->defer_depth) TRY(issue_oldest(p, sent_blocks, union_blocks));
+  else if (j.defer) {
+    if (sent_blocks) *sent_blocks = 0;
+    if (union_blocks) *union_blocks = 0;
+  }
+  // the round's bookkeeping stream: an asynchronous round runs it on the side stream, so the caller's stream is left
+  // with the worker scans alone (round k+1's scan overlaps round k's all-gather and plan, and round k-1's exchange)
   hipStream_t qs = async ? p->ps : j.st;
   const omr_stream_t qstream = reinterpret_cast<omr_stream_t>(qs);
-  if (async) TRY(hip_check(hipStreamWaitEvent(qs, S.scanned, 0), "hipStreamWaitEvent"));
-  // the rest of the set is refilled from here on: the asynchronous round kSets calls back must be through with it
-  if (S.pending) {
-    TRY(wait_ev(qs, S.done));
-    S.pending = false;
-  }
-  // 2. every worker's row masks
-  ht.lap("1:refill wait");
-  if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].q0, qs), "hipEventRecord"));
-  TRY(p->d->allgather(S.own, S.masks_all, p->mstride * sizeof(uint64_t), qs));
-  ht.lap("1:allgather");
-  // 3. write set, union, prefixes, per-shard counts; own mask buffer cleared for its next round
-  //    (the counts are stored straight into pinned host memory: no copy-engine hop before the host sees them)
-  const uint32_t seq = ++p->seq;
-  //    ... and, by extra workgroups of the same launch, the aggregator chain (server.cc:86-96 min_next) over the union
-  //    ... and the shard sum's pair list, by more workgroups (sum_list)
-  const omr_sum_list sl = p->sum_list ? list_desc(p, S) : omr_sum_list{};
-  //    (round 3's one-1024-thread-workgroup-per-array form, omr_round_plan_list; OMR_PLAN_V1=0, a study knob, runs
-  //    the row-chunk form, omr_round_plan_ws: 256-thread workgroups that fit beside a running scan workgroup)
-  TRY(omr_check((p->plan_v1 ? omr_round_plan_list : omr_round_plan_ws)(
-                    S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes, p->bounds_dev, NS,
-                    S.wset, S.umask, S.prefix, p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own,
-                    S.pack_cnt, S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->arrive, p->flag_map + si, seq, j.un,
-                    p->B, p->sum_list ? &sl : nullptr, qstream),
-                p->plan_v1 ? "omr_round_plan_list" : "omr_round_plan_ws"));
-  ht.lap("1:plan");
-  // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407): addressed by
-  //     device-side data only, so it is queued before the host learns the counts and runs while it waits.  (Every
-  //     host API call costs microseconds; a round that spends them on side streams and events is host-bound.)
-  if (N > 1 && mode != OMR_ROUND_DENSE_REDUCE_SCATTER && p->worker() && !p->fused_pack) {
-    const uint64_t r0 = p->colocated ? p->bounds[me] : 0, r1 = p->colocated ? p->bounds[me + 1] : 0;
-    TRY(omr_check(omr_move_blocks_f32(x, S.packed, 0, S.masks_all + static_cast<uint64_t>(me) * p->mstride,
-                                      S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
-                                      r1, qstream), "omr_move_blocks_f32 pack"));
-  }
-  if (timed) {
-    TRY(hip_check(hipEventRecord(p->timed[tslot].q1, qs), "hipEventRecord"));
-    p->timed[tslot].prep = true;
-  }
-  ht.lap("1:pack");
-  // the rest goes on the communication stream for an asynchronous round, behind everything queued so far.  The same
-  // event tells the scan that refills this set's own masks that the plan has consumed and re-zeroed them (one record
-  // per round instead of two: every host API call costs the round microseconds)
-  if (async) {
-    TRY(hip_check(hipEventRecord(S.ready, qs), "hipEventRecord"));
-    S.plan_pending = true;
+  uint32_t seq = 0;
+  if (tally) {
+    // the one-launch round: the scan tallied the bookkeeping (omr_worker_scan_tally_f32); nothing runs after it
+    seq = j.seq;
+  } else {
+    if (async) TRY(hip_check(hipStreamWaitEvent(qs, S.scanned, 0), "hipStreamWaitEvent"));
+    // the rest of the set is refilled from here on: the round kSets calls back must be through with it (on the side
+    // stream, in stream order already)
+    if (S.pending) {
+      if (qs != p->cs) TRY(wait_ev(qs, S.done));
+      S.pending = false;
+    }
+    // 2. every worker's row masks
+    ht.lap("1:refill wait");
+    if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].q0, qs), "hipEventRecord"));
+    TRY(p->d->allgather(S.own, S.masks_all, p->mstride * sizeof(uint64_t), qs));
+    ht.lap("1:allgather");
+    // 3. write set, prefixes, per-shard counts; own mask buffer cleared for its next round (the counts are stored
+    //    straight into pinned host memory: no copy-engine hop before the host sees them)
+    //    ... and, by extra workgroups of the same launch, the aggregator chain (server.cc:86-96 min_next) over the
+    //    union, when asked for, and the shard sum's pair list (sum_list)
+    seq = ++p->seq;
+    const omr_sum_list sl = p->sum_list ? list_desc(p, S) : omr_sum_list{};
+    TRY(omr_check(omr_round_plan_list(S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes,
+                                      p->bounds_dev, NS, S.wset, nullptr, S.prefix,
+                                      p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, S.pack_cnt,
+                                      S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->flag_map + si, seq, j.un, p->B,
+                                      p->sum_list ? &sl : nullptr, qstream),
+                  "omr_round_plan_list"));
+    ht.lap("1:plan");
+    // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407) where the scan
+    //     could not (ragged shards): addressed by device-side data only, so it is queued before the host learns the
+    //     counts.  (Every host API call costs microseconds; a round that spends them on streams and events is
+    //     host-bound.)
+    if (N > 1 && (mode & ~(kModeSolo | kModeTally)) != OMR_ROUND_DENSE_REDUCE_SCATTER && p->worker() &&
+        !p->fused_pack) {
+      const uint64_t r0 = p->colocated ? p->bounds[me] : 0, r1 = p->colocated ? p->bounds[me + 1] : 0;
+      TRY(omr_check(omr_move_blocks_f32(x, p->pk[j.pki].buf, 0, S.masks_all + static_cast<uint64_t>(me) * p->mstride,
+                                        S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
+                                        r1, qstream), "omr_move_blocks_f32 pack"));
+    }
+    if (timed) {
+      TRY(hip_check(hipEventRecord(p->timed[tslot].q1, qs), "hipEventRecord"));
+      p->timed[tslot].prep = true;
+    }
+    ht.lap("1:pack");
+    // the same event tells the scan that refills this set's own masks that the plan has consumed and re-zeroed them
+    if (async) {
+      TRY(hip_check(hipEventRecord(S.ready, qs), "hipEventRecord"));
+      S.plan_pending = true;
+    }
   }
   {  // the set's `ready` is recorded and its `scanned` waited for: the caller may reuse it
     std::lock_guard<std::mutex> g(p->mu);
@@ -1794,22 +1920,23 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
   }
   p->cv_done.notify_all();
   ht.lap("1:next+ready");
-  if (!j.defer) return round_finish(p, si, x, j.out, mode, async, timed, seq, qs, sent_blocks, union_blocks, tslot);
-  // deferred: this round's first half is queued; now issue the exchange of the round kDeferDepth calls back, whose
-  // counts have long been in host memory, so the host neither waits nor leaves the caller's stream idle
+  (void)NS;
+  // (a one-rank round's counts come on the caller's stream: the wait for them watches that stream)
+  if (!j.defer)
+    return round_finish(p, si, j.pki, x, j.out, mode, async, timed, seq, tally ? j.st : qs, sent_blocks, union_blocks,
+                        tslot);
+  // deferred: this round's second half waits in the queue (issued kDeferDepth calls later, or by join)
   omr_ar_plan::Pending& q = p->pend[p->npend++];
   q.active = true;
   q.si = si;
+  q.pki = j.pki;
   q.mode = mode;
   q.timed = timed;
   q.x = x;
   q.out = j.out;
   q.seq = seq;
   q.tslot = tslot;
-  q.st = qs;
-  if (sent_blocks) *sent_blocks = 0;
-  if (union_blocks) *union_blocks = 0;
-  if (p->npend > p->defer_depth) TRY(issue_oldest(p, sent_blocks, union_blocks));
+  q.st = tally ? j.st : qs;
   return 0;
 }
 
@@ -1889,14 +2016,25 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
                        uint32_t* union_next, int mode, bool threaded, bool defer, bool async, bool timed,
                        uint64_t* sent_blocks, uint64_t* union_blocks, omr_stream_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // A one-rank group's aggregator sums one worker's blocks: its shard sum is 0.0f + x over the write set (the worker's
+  // non-zero blocks and the lane heads), exactly what the worker scan writes when it is given `out` (k_scan1f, as the
+  // single-GPU step): so the scan writes the sums (solo).  Its bookkeeping is two counts (the union is the worker's own
+  // blocks, min_next its own chain), which the scan tallies too (tally): the round is ONE launch
+  // (omr_worker_scan_tally_f32) on the caller's stream, no side stream, no event, and no progress thread (nothing to
+  // issue after the scan).  (Not in the bucket pipeline, whose `out` may be a pinned host buffer's mapping: there the
+  // write-back stays beside the next bucket's scan instead of inside it.  omr_dist_test_world1_round keeps the
+  // bookkeeping on the multi-rank round's path: all-gather and plan on the side stream.)
+  const bool solo = p->N == 1 && p->worker() && p->colocated && p->scan_from == nullptr && !p->in_buckets &&
+                    mode != OMR_ROUND_DENSE_REDUCE_SCATTER;
+  const bool tally = solo && !p->d->world1_general;
+  if (tally) threaded = false;
   // a threaded round hands its steps after the scan to the progress thread; any other call first lets the thread
   // issue everything queued (the plan's state is then this thread's alone)
   TRY(threaded ? thread_start(p) : thread_drain(p));
   p->ht.start();
   int32_t* fl = flags ? flags : p->flags_ws;
   uint32_t* nx = next_offsets ? next_offsets : p->next_ws;
-  // (no union_next: the plan launch skips the aggregator chain, whose only output it is -- at world 1 that is 64
-  // 1024-thread workgroups fewer beside the next scan)
+  // (no union_next: the plan launch skips the aggregator chain, whose only output it is)
   uint32_t* un = union_next;
   // a stream other than the previous round's starts behind it (plan-wide state is shared by every round)
   if (p->last_st != nullptr && p->last_st != st) {
@@ -1907,85 +2045,110 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
   // a round that is not deferred finishes a deferred one first (rounds complete in call order; a threaded round's
   // progress thread does this, it owns the deferred rounds)
   if (!defer && !threaded) TRY(flush_pending(p, st, nullptr, nullptr));
-  // a synchronous round after asynchronous ones: its all-gather and exchange go on `stream`, so the plan and
-  // communication streams must be idle first (one communicator is never driven from two streams at once; the
-  // last asynchronous round's `done` follows all of its plan-stream work)
+  // a synchronous round after asynchronous ones: its all-gather and exchange go on `stream`, so the side stream must
+  // be idle first (one communicator is never driven from two streams at once; the last asynchronous round's `done`
+  // follows all of its side-stream work)
   if (!async && p->last_async >= 0) {
     TRY(hip_check(hipStreamWaitEvent(st, p->set[p->last_async].done, 0), "hipStreamWaitEvent"));
-    if (p->as_last >= 0 && p->as_last != p->last_async)
-      TRY(hip_check(hipStreamWaitEvent(st, p->set[p->as_last].done, 0), "hipStreamWaitEvent"));
     p->last_async = -1;
-    p->as_last = -1;
   }
   const int si = p->cur;
   omr_ar_plan::Set& S = p->set[si];
   p->cur = (p->cur + 1) % p->nsets;
-  // A one-rank group's aggregator sums one worker's blocks: its shard sum is 0.0f + x over the write set (the worker's
-  // non-zero blocks and the lane heads), exactly what the worker scan writes when it is given `out` (k_scan1f, as
-  // the single-GPU step).  So the scan writes the sums, and the second half skips the shard sum and the unpack.  (Not
-  // in the bucket pipeline, whose `out` may be a pinned host buffer's mapping: there the write-back stays beside the
-  // next bucket's scan instead of inside it.)
-  const bool solo = p->N == 1 && p->worker() && p->colocated && p->scan_from == nullptr && !p->in_buckets &&
-                    mode != OMR_ROUND_DENSE_REDUCE_SCATTER;
+  const int pki = static_cast<int>(p->rounds_total++ % omr_ar_plan::kPackBufs);
   // 1. worker scan (client.cc:19-31): flags, own next chain, own row masks, in one pass (a dedicated aggregator
   //    offers its all-zero mask buffer to the all-gather).  The set's own masks must have been consumed and
   //    re-zeroed by the plan of the round kSets calls back.
   int tslot = -1;
   if (timed) TRY(timed_slot(p, &tslot));
-  if (threaded) {  // that plan has been issued (and this set's `scanned` waited for) by the progress thread
-    HostWait hw(p);
-    std::unique_lock<std::mutex> lk(p->mu);
-    const uint64_t need = p->rounds_begun >= static_cast<uint64_t>(p->nsets - 1) ? p->rounds_begun - (p->nsets - 1) : 0;
-    p->cv_done.wait(lk, [&] { return p->first_halves >= need || p->thread_rc != 0; });
-    if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
-  }
-  if (S.plan_pending) {
-    TRY(wait_ev(st, S.ready));
-    S.plan_pending = false;
-  }
-  // A fused-pack scan refills the set's send streams: the exchange of the round kSets calls back, which reads them
-  // (issued up to kDeferDepth calls later, on the communication stream), must be through first.  The progress thread
-  // may not have issued it yet: wait until it has (at most one call behind then), then for it on the device.
-  const bool pack_scan = p->fused_pack && p->worker() && mode != OMR_ROUND_DENSE_REDUCE_SCATTER;
-  if (pack_scan) {
-    std::unique_lock<std::mutex> lk(p->mu);
-    const uint64_t need = p->rounds_begun >= static_cast<uint64_t>(p->nsets) ? p->rounds_begun - (p->nsets - 1) : 0;
-    if (threaded) {
-      HostWait hw(p);
-      p->cv_done.wait(lk, [&] { return p->second_halves >= need || p->thread_rc != 0; });
-    }
-    if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
-    const bool w = S.scan_wait;
-    S.scan_wait = false;
-    lk.unlock();
-    if (w) TRY(wait_ev(st, S.done));
-  }
-  if (p->worker()) {
+  uint32_t solo_seq = 0;
+  if (tally) {
     if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
-    const float* src = p->scan_from ? p->scan_from : x;
-    float* sout = p->scan_from ? const_cast<float*>(x) : (solo ? out : nullptr);
-    const bool pack = p->fused_pack && (mode & 0xFF) != OMR_ROUND_DENSE_REDUCE_SCATTER;
-    if (pack)  // the scan also writes this worker's blocks of the other shards into their send streams
-      TRY(omr_check(omr_worker_scan_pack_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout, p->bounds.data(),
-                                             static_cast<uint32_t>(p->A), p->colocated ? me_shard(p) : -1, S.packed,
-                                             S.pack_cnt, reinterpret_cast<uint32_t*>(S.own + p->rows), p->scan_ws,
-                                             p->scan_ws_bytes, stream),
-                    "omr_worker_scan_pack_f32"));
-    else
-      TRY(omr_check(omr_worker_scan_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout, p->scan_ws,
-                                        p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+    // the previous one-rank round's counts go out with this scan's extra workgroup (on its own stream if it was
+    // another one: then by a launch of its own, before this scan)
+    if (p->pub_set >= 0 && p->pub_st != st) TRY(publish_pending(p));
+    const int ps_i = p->pub_set;
+    p->pub_set = -1;
+    solo_seq = ++p->seq;
+    const size_t TS = p->tally_slots;
+    TRY(omr_check(omr_worker_scan_tally_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, out, p->tally + TS * si,
+                                            ps_i >= 0 ? p->tally + TS * ps_i : nullptr,
+                                            ps_i >= 0 ? p->pub_map + 4 * ps_i : nullptr, p->pub_seq, p->scan_ws,
+                                            p->scan_ws_bytes, stream),
+                  "omr_worker_scan_tally_f32"));
+    p->pub_set = si;
+    p->pub_seq = solo_seq;
+    p->pub_st = st;
+    // min_next over one worker is the worker's own chain
+    if (un != nullptr)
+      TRY(hip_check(hipMemcpyAsync(un, nx, p->nb * sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "hipMemcpyAsync"));
     if (timed) {
       TRY(hip_check(hipEventRecord(p->timed[tslot].s1, st), "hipEventRecord"));
       p->timed[tslot].scan = true;
     }
     p->ht.lap("1:scan");
+  } else {
+    if (threaded) {  // that plan has been issued (and this set's `scanned` waited for) by the progress thread
+      HostWait hw(p);
+      std::unique_lock<std::mutex> lk(p->mu);
+      const uint64_t need = p->rounds_begun >= static_cast<uint64_t>(p->nsets - 1) ? p->rounds_begun - (p->nsets - 1) : 0;
+      p->cv_done.wait(lk, [&] { return p->first_halves >= need || p->thread_rc != 0; });
+      if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
+    }
+    if (S.plan_pending) {
+      TRY(wait_ev(st, S.ready));
+      S.plan_pending = false;
+    }
+    // A fused-pack scan refills the round's send buffer: the round kPackBufs calls back, which read it (its exchange
+    // issued up to kDeferDepth calls later, on the side stream), must be through first.  The progress thread may not
+    // have issued it yet: wait until it has (at most one call behind then), then for it on the device.
+    const bool pack_scan = p->fused_pack && p->worker() && mode != OMR_ROUND_DENSE_REDUCE_SCATTER;
+    if (pack_scan) {
+      std::unique_lock<std::mutex> lk(p->mu);
+      constexpr uint64_t KP = omr_ar_plan::kPackBufs;
+      const uint64_t need = p->rounds_begun >= KP ? p->rounds_begun - (KP - 1) : 0;
+      if (threaded) {
+        HostWait hw(p);
+        p->cv_done.wait(lk, [&] { return p->second_halves >= need || p->thread_rc != 0; });
+      }
+      if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
+      const bool w = p->pk[pki].scan_wait;
+      const int ds = p->pk[pki].done_set;
+      p->pk[pki].scan_wait = false;
+      lk.unlock();
+      if (w) TRY(wait_ev(st, p->set[ds].done));
+    }
+    if (p->worker()) {
+      if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
+      const float* src = p->scan_from ? p->scan_from : x;
+      // (a one-rank round's scan writes the sums; a bucket's writes the staging buffer's blocks when it reads the
+      // pinned host buffer, and the sums come from the round's own shard sum)
+      float* sout = p->scan_from ? const_cast<float*>(x) : (solo ? out : nullptr);
+      if (pack_scan)  // the scan also writes this worker's blocks of the other shards into their send streams
+        TRY(omr_check(omr_worker_scan_pack_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout,
+                                               p->bounds.data(), static_cast<uint32_t>(p->A),
+                                               p->colocated ? me_shard(p) : -1, p->pk[pki].buf, S.pack_cnt,
+                                               reinterpret_cast<uint32_t*>(S.own + p->rows), p->scan_ws,
+                                               p->scan_ws_bytes, stream),
+                      "omr_worker_scan_pack_f32"));
+      else
+        TRY(omr_check(omr_worker_scan_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout, p->scan_ws,
+                                          p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+      if (timed) {
+        TRY(hip_check(hipEventRecord(p->timed[tslot].s1, st), "hipEventRecord"));
+        p->timed[tslot].scan = true;
+      }
+      p->ht.lap("1:scan");
+    }
+    // (a dedicated aggregator has nothing to scan: the side stream starts behind whatever the caller queued)
+    if (async) TRY(hip_check(hipEventRecord(S.scanned, st), "hipEventRecord"));
   }
-  // (a dedicated aggregator has nothing to scan: the plan stream starts behind whatever the caller queued)
-  if (async) TRY(hip_check(hipEventRecord(S.scanned, st), "hipEventRecord"));
   p->ht.lap("1:scan events");
   omr_ar_plan::Job j;
   j.si = si;
-  j.mode = mode | (solo ? kModeSolo : 0);
+  j.pki = pki;
+  j.seq = solo_seq;
+  j.mode = mode | (solo ? kModeSolo : 0) | (tally ? kModeTally : 0);
   j.tslot = tslot;
   j.async = async;
   j.defer = defer;
@@ -2111,7 +2274,7 @@ int sparse_buckets_issue(omr_ar_plan* p, float* buf, uint64_t total_n, int mode,
   constexpr int R = omr_ar_plan::kStage;
   if (p->s_in == nullptr) {
     for (int r = 0; r < R; ++r) {
-      TRY(dev_alloc(p->d, &p->stage[r], p->n));
+      TRY(dev_alloc(p->d, &p->stage[r], p->n, &p->dev_bytes));
       TRY(hip_check(hipEventCreateWithFlags(&p->ev_in[r], hipEventDisableTiming), "hipEventCreate"));
       TRY(hip_check(hipEventCreateWithFlags(&p->ev_round[r], hipEventDisableTiming), "hipEventCreate"));
       TRY(hip_check(hipEventCreateWithFlags(&p->ev_out[r], hipEventDisableTiming), "hipEventCreate"));
@@ -2233,19 +2396,17 @@ int omr_ar_plan_shard(omr_ar_plan* p, int* shard, uint64_t* row_begin, uint64_t*
 
 int omr_ar_plan_fused_pack(const omr_ar_plan* p) { return p != nullptr && p->fused_pack ? 1 : 0; }
 
+uint64_t omr_ar_plan_device_bytes(const omr_ar_plan* p) { return p != nullptr ? p->dev_bytes : 0; }
+
 int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_join: NULL");
   TRY(plan_check(p, "ar_plan_join"));
   TRY(plan_fail(p, thread_drain(p)));
   TRY(plan_fail(p, flush_pending(p, reinterpret_cast<hipStream_t>(stream), nullptr, nullptr)));
   if (p->last_async < 0) return 0;
-  // the communication and aggregation streams each run rounds in issue order: waiting for the last one on each
-  // covers every earlier one
+  // the side stream runs rounds in issue order: waiting for the last one covers every earlier one
   TRY(hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), p->set[p->last_async].done, 0),
                 "hipStreamWaitEvent"));
-  if (p->as_last >= 0 && p->as_last != p->last_async)
-    TRY(hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), p->set[p->as_last].done, 0),
-                  "hipStreamWaitEvent"));
   return 0;
 }
 

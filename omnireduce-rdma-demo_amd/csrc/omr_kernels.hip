@@ -48,6 +48,7 @@ int launch_status(const char* what) {
 // Native 16-byte vectors: one dwordx4 per lane, a wave-wide load moves 1 KiB = one 256-float block.
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
 struct WorkerPtrs {
   const float* p[OMR_MAX_WORKERS];
@@ -245,20 +246,57 @@ struct FusedArgs {
   uint32_t lanes, rpp, K, S, block, sentinel;
   uint32_t part0;      // first partition of the launch (a per-partition call scans partitions [part0, part0 + grid))
   // PACK
-  float* send;         // shard s's stream starts at float bounds[s] * lanes * block (a buffer of n floats)
+  float* send;         // shard s's stream starts at float send_row[s] * lanes * block (the streams in shard order,
+                       // own_shard's left out: n floats less its rows)
   uint32_t* shard_cnt; // [nshards] blocks taken so far in each shard's stream (zero on entry)
   uint32_t* pos;       // [parts * K * gps * lanes] stream position of (segment, group, lane)'s first block
   uint32_t bounds[OMR_MAX_WORKERS + 1];  // shard s = rows [bounds[s], bounds[s + 1]), whole segments
+  uint32_t send_row[OMR_MAX_WORKERS];
   uint32_t nshards, gps, wcap;
   int32_t own_shard;   // this rank's own shard (read in place by its aggregator, not packed); -1: none
+  // TALLY (the one-rank round): workgroup b stores tally[b] = {non-zero blocks, zero lane-head blocks} of its segment
+  // (one slot per workgroup: no atomic, so no queue of 512 of them on one address at the launch's end); workgroup 0's
+  // first wave also publishes an earlier launch's slots, pub_src (pub_slots of them), to pub_dst (publish_tally)
+  uint64_t* tally;
+  const uint64_t* pub_src;
+  uint32_t* pub_dst;
+  uint32_t pub_seq, pub_slots;
 };
+
+// The one-rank round's counts, from an earlier launch's slots, one wave: lane i sums slots i, i + 64, ... (loaded by
+// tally_load, a launch's first instructions), then a DPP reduction.
+__device__ __forceinline__ void tally_load(const uint64_t* src, uint32_t slots, uint32_t* nz, uint32_t* heads) {
+  const int lane = threadIdx.x & 63;
+  uint32_t z = 0, h = 0;
+  for (uint32_t i = lane; i < slots; i += 64) {
+    const uint64_t v = src[i];
+    z += static_cast<uint32_t>(v);
+    h += static_cast<uint32_t>(v >> 32);
+  }
+  *nz = z;
+  *heads = h;
+}
+
+// ... reduced over the wave and stored as the completion notice {seq, non-zero blocks, write-set blocks, seq} in ONE
+// 16-byte write-through store to host-mapped memory (a host that sees seq in both halves has the counts: each aligned
+// 8-byte half lands whole).
+__device__ __forceinline__ void publish_tally(uint32_t* dst, uint32_t seq, uint32_t nz, uint32_t heads) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    nz += static_cast<uint32_t>(__shfl_xor(static_cast<int>(nz), d, 64));
+    heads += static_cast<uint32_t>(__shfl_xor(static_cast<int>(heads), d, 64));
+  }
+  if ((threadIdx.x & 63) != 0) return;
+  const v4u rec = v4u{seq, nz, nz + heads, seq};
+  __builtin_amdgcn_raw_buffer_store_b128(rec, chunk_rsrc(reinterpret_cast<float*>(dst), 16u), 0, 0, kStoreAux);
+}
 
 constexpr uint32_t kPackLdsBytes = 128u << 10;  // the waves' stash slots: 8 blocks per wave at B = 256 (16 waves)
 constexpr uint32_t kPackGroupRows = 64;         // the position table's row granularity (one wave of row masks)
 
 constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
 
-template <int VEC, int WAVES, int LOADS = 16, int SKIP = 0, bool PACK = false>
+template <int VEC, int WAVES, int LOADS = 16, int SKIP = 0, bool PACK = false, bool TALLY = false>
 __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
   constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
   static_assert(RB >= 1 && RB <= 32 && 32 % RB == 0, "a batch's bits lie inside one 32-bit word");
@@ -269,11 +307,18 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
   __shared__ uint32_t s_seg_last[64];
   // PACK: dynamic LDS = the segment's non-zero-row bits [ceil(S / 32) words, 16-byte aligned] + the stash slots
   extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
-  __shared__ uint32_t s_wcnt[PACK ? WAVES : 1], s_wpre[PACK ? WAVES : 1];
+  __shared__ uint32_t s_wcnt[(PACK || TALLY) ? WAVES : 1], s_wpre[PACK ? WAVES : 1];
   __shared__ uint32_t s_base, s_total;
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t T = gridDim.x, bid = blockIdx.x;
+  // TALLY: workgroup 0 publishes the previous round's counts.  Their loads go out now, ahead of the scan's own (their
+  // latency hides behind the first batch), and the store at the end of this workgroup's work, which is in the launch's
+  // first wave of workgroups: no part of it waits at the end of the launch.
+  [[maybe_unused]] uint32_t pub_nz = 0, pub_heads = 0;
+  if constexpr (TALLY) {
+    if (bid == 0 && a.pub_src != nullptr && wave == 0) tally_load(a.pub_src, a.pub_slots, &pub_nz, &pub_heads);
+  }
   const uint32_t lin = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
   const uint32_t k = lin % a.K, col = lin / a.K + a.part0 * a.lanes;  // col: global (partition, lane) index
   const uint32_t l = col % a.lanes, p = col / a.lanes;
@@ -296,6 +341,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
   [[maybe_unused]] const uint32_t bits_words = ((a.S + 31) / 32 + 3) & ~3u;
   [[maybe_unused]] v4f* const stash = reinterpret_cast<v4f*>(s_dyn + bits_words);
   [[maybe_unused]] uint32_t cnt_w = 0, taken = 0;  // the wave's non-zero rows, and how many of them (the highest) it stashed
+  [[maybe_unused]] uint32_t head0 = 0;             // TALLY: the column's lane-head block is zero (it is still returned)
   if constexpr (PACK) {
     while (shard + 1 < a.nshards && row0 >= a.bounds[shard + 1]) ++shard;
     pack = static_cast<int32_t>(shard) != a.own_shard;
@@ -377,6 +423,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
         }
       }
     }
+    if constexpr (TALLY) {
+      cnt_w += static_cast<uint32_t>(__builtin_popcount(bits));
+      if (r0 + rr == 0 && !(bits & 1u)) head0 = 1;
+    }
     if (bits != 0) {
       if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
       carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
@@ -385,8 +435,20 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
   if (lane == 0) {
     s_wfirst[wave] = carry;  // first non-zero row of the wave's range (kNone: all zero)
     s_wlast[wave] = wlast;   // last one
+    if constexpr (TALLY) s_wcnt[wave] = cnt_w | (head0 << 31);
   }
   __syncthreads();
+  if constexpr (TALLY) {  // the one-rank round's bookkeeping: one pair of device atomics per workgroup, no return
+    if (threadIdx.x == 0) {
+      uint32_t nz = 0, heads = 0;
+      for (uint32_t w2 = 0; w2 < WAVES; ++w2) {
+        nz += s_wcnt[w2] & 0x7fffffffu;
+        heads += s_wcnt[w2] >> 31;
+      }
+      a.tally[bid] = (static_cast<uint64_t>(heads) << 32) | nz;
+    }
+    if (bid == 0 && a.pub_src != nullptr && wave == 0) publish_tally(a.pub_dst, a.pub_seq, pub_nz, pub_heads);
+  }
   // tail rows [wlast or lo, hi): successor = first non-zero row of a later wave, else of a later segment
   uint32_t succ = kNone;
   for (uint32_t w2 = wave + 1; w2 < WAVES; ++w2)
@@ -422,7 +484,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
           a.pos[(seg * a.gps + j) * a.lanes + l] = base + c;
         }
         // the wave's blocks: its range's non-zero rows take stream places base + s_wpre[wave] + (rank among them)
-        float* const sbase = a.send + static_cast<uint64_t>(a.bounds[shard]) * row_stride;
+        float* const sbase = a.send + static_cast<uint64_t>(a.send_row[shard]) * row_stride;
         const uint64_t wb = static_cast<uint64_t>(base) + s_wpre[wave];
         for (uint32_t j = 0; j < taken; ++j) {  // stashed: the j-th from the top has rank cnt_w - 1 - j
           const v4f* const slot = stash + (static_cast<uint64_t>(wave) * a.wcap + j) * B4;
@@ -996,26 +1058,6 @@ __device__ __forceinline__ uint32_t take_bits(uint64_t& rem, uint32_t (&lj)[SL],
   return nv;
 }
 
-// One workgroup per mask array (count worker arrays + the write set), 1024 threads.  Pass 1 reads the array's
-// rows coalesced (row r by thread r mod 1024, four rows in flight per thread) and keeps them in LDS; the
-// write-set workgroup also forms union = OR of the workers (the aggregator's min_next domain, server.cc:86-96)
-// and write set = union | lane heads (every lane head is sent and returned: client.cc:201-205), and clears the
-// next round's own-mask buffer.  Pass 2 gives each thread a contiguous run of rows: popcounts -> block-wide
-// exclusive scan -> prefix[a][r]; counts[a][s] = prefix[a][bounds[s]].  (Arrays of more than kPlanLdsRows rows
-// are re-read in pass 2 instead of kept in LDS.)
-constexpr int kPlanThreads = 1024;
-constexpr uint64_t kPlanLdsRows = 8192;  // 64 KiB of dynamic LDS
-
-__device__ __forceinline__ uint64_t plan_row(const uint64_t* masks, uint32_t a, uint32_t count, uint64_t mstride,
-                                             uint64_t r, uint32_t rpp, uint64_t all_lanes, uint64_t* uni) {
-  if (a < count) return masks[static_cast<uint64_t>(a) * mstride + r];
-  uint64_t u = 0;
-  for (uint32_t c = 0; c < count; ++c) u |= masks[static_cast<uint64_t>(c) * mstride + r];
-  *uni = u;
-  return (r % rpp == 0) ? (u | all_lanes) : u;
-}
-
-constexpr uint64_t kRowStreams = ~0ull;
 // the pair list's unit: 16 rows x one lane (a quarter of a 64-row group), as k_shard_sum's
 constexpr uint32_t kSumUnitRows = 16;
 constexpr uint32_t kSumUnitsPerGroup = 64 / kSumUnitRows;
@@ -1079,9 +1121,12 @@ __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, u
     }
     const bool rl = static_cast<uint32_t>(lane) < nload;
     const uint64_t r = g0 + (rl ? static_cast<uint32_t>(lane) : 0u);
-    uint64_t mk[OMR_MAX_WORKERS];
+    uint64_t mk[OMR_MAX_WORKERS];  // (unconditional loads from clamped addresses: one round trip, see plan_rows)
 #pragma unroll
-    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) mk[c] = (c < a.count && rl) ? a.masks[c * a.mstride + r] : 0ull;
+    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) {
+      const uint64_t v = a.masks[(c < a.count ? c : 0u) * a.mstride + r];
+      mk[c] = (c < a.count && rl) ? v : 0ull;
+    }
     const bool cl = static_cast<uint32_t>(lane) < a.count;
     const uint32_t base_c =
         cl ? reinterpret_cast<const uint32_t*>(a.masks + lane * a.mstride)[a.pos_off + gidx * a.lanes + l] : 0u;
@@ -1142,292 +1187,175 @@ struct PlanArgs {
   const uint64_t* masks;  // worker c's row masks at masks + c * mstride
   uint32_t count, rpp, lanes, nbounds;
   uint64_t rows, mstride;
-  uint32_t* zero_cnt;     // [zero_cnt_n] cleared by the write-set workgroup (the next round's pack counters), or null
+  uint32_t* zero_cnt;     // [zero_cnt_n] cleared (the next round's pack counters), or null
   uint32_t zero_cnt_n;
   const uint64_t* bounds;
   uint64_t* write_set;
-  uint64_t* union_masks;
+  uint64_t* union_masks;  // or null
   uint32_t* prefix;
   uint32_t* counts;     // device or host-mapped memory: stored at system scope
-  uint64_t* zero_masks;
-  uint32_t* arrive;     // device arrival counter (zero between launches) or null
-  uint32_t* done_flag;  // receives `seq` once every workgroup's counts are visible system-wide, or null
+  uint64_t* zero_masks;  // or null
+  uint32_t* done_flag;  // receives `seq` once the counts are visible system-wide, or null
   uint32_t seq;
-  NextArgs chain;       // union_next: the aggregator chain over the union, by workgroups count+1.. (chain.next null: none)
+  NextArgs chain;       // union_next: the aggregator chain over the union, by workgroups 1.. (chain.next null: none)
   uint32_t chain_wgs;
   uint32_t list_wgs;    // the shard sum's pair list, by the workgroups after the chain's (0: none)
   ListArgs list;
 };
 
-__global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
-  if (blockIdx.x > a.count + a.chain_wgs) {  // the shard sum's pair list, one unit per wave
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr uint32_t kW = kPlanThreads / 64;
-    build_sum_list(a.list, static_cast<uint64_t>(blockIdx.x - a.count - 1 - a.chain_wgs) * kW + w,
-                   static_cast<uint64_t>(a.list_wgs) * kW);
-    return;
-  }
-  if (blockIdx.x > a.count) {  // the aggregator chain (server.cc:86-96 min_next) over the union, one segment each
-    const uint64_t* m = a.masks;
-    const uint32_t cnt = a.count;
-    const uint64_t ms = a.mstride;
-    next_segment<kPlanThreads / 64>(a.chain, blockIdx.x - a.count - 1, [&](uint64_t r) {
-      uint64_t u = 0;
-      for (uint32_t c = 0; c < cnt; ++c) u |= m[static_cast<uint64_t>(c) * ms + r];
-      return u;
-    }, a.chain.next);
-    return;
-  }
-  extern __shared__ uint64_t s_val[];  // [rows] when rows <= kPlanLdsRows
-  __shared__ uint32_t s_wave[kPlanThreads / 64];
-  __shared__ uint64_t s_bounds[OMR_MAX_WORKERS + 2];
-  const uint32_t arr = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const uint64_t all_lanes = a.lanes >= 64 ? ~0ull : ((1ull << a.lanes) - 1ull);
-  const bool ws = arr == a.count;
-  const bool keep = a.rows <= kPlanLdsRows;
-  if (t < a.nbounds) s_bounds[t] = a.bounds[t];
-  if (ws && a.zero_cnt != nullptr && t < a.zero_cnt_n) a.zero_cnt[t] = 0;
-  // pass 1: coalesced row reads, 4 rows per thread per step
-  for (uint64_t r0 = t; r0 < a.rows; r0 += 4 * kPlanThreads) {
-    uint64_t v[4], u[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint64_t r = r0 + static_cast<uint64_t>(i) * kPlanThreads;
-      v[i] = r < a.rows ? plan_row(a.masks, arr, a.count, a.mstride, r, a.rpp, all_lanes, &u[i]) : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint64_t r = r0 + static_cast<uint64_t>(i) * kPlanThreads;
-      if (r >= a.rows) break;
-      if (keep) s_val[r] = v[i];
-      if (ws) {
-        a.write_set[r] = v[i];
-        a.union_masks[r] = u[i];
-        if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
-      }
-    }
-  }
-  __syncthreads();  // LDS rows (and, when re-read, this workgroup's write-set stores) visible to every thread
-  const uint64_t per = (a.rows + kPlanThreads - 1) / kPlanThreads;
-  const uint64_t rb = t * per < a.rows ? t * per : a.rows;
-  const uint64_t re = rb + per < a.rows ? rb + per : a.rows;
-  auto row = [&](uint64_t r) -> uint64_t {
-    if (keep) return s_val[r];
-    if (ws) return a.write_set[r];
-    return a.masks[static_cast<uint64_t>(arr) * a.mstride + r];
-  };
-  uint32_t sum = 0;
-  for (uint64_t r = rb; r < re; ++r) sum += static_cast<uint32_t>(__builtin_popcountll(row(r)));
-  // block-wide exclusive scan of the per-thread sums (wave shuffles, then the 16 wave totals)
-  uint32_t inc = sum;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(inc, d, 64);
-    if (lane >= static_cast<uint32_t>(d)) inc += o;
-  }
-  if (lane == 63) s_wave[wave] = inc;
-  __syncthreads();
-  uint32_t wbase = 0, total = 0;
-  for (uint32_t w = 0; w < kPlanThreads / 64; ++w) {
-    if (w < wave) wbase += s_wave[w];
-    total += s_wave[w];
-  }
-  uint32_t run = wbase + inc - sum;  // exclusive prefix at row rb
-  uint32_t* pre = a.prefix + static_cast<uint64_t>(arr) * (a.rows + 1);
-  for (uint64_t r = rb; r < re; ++r) {
-    for (uint32_t s = 0; s < a.nbounds; ++s)
-      if (s_bounds[s] == r)
-        __hip_atomic_store(&a.counts[arr * a.nbounds + s], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    pre[r] = run;
-    run += static_cast<uint32_t>(__builtin_popcountll(row(r)));
-  }
-  if (t == 0) {
-    pre[a.rows] = total;
-    for (uint32_t s = 0; s < a.nbounds; ++s)
-      if (s_bounds[s] >= a.rows)
-        __hip_atomic_store(&a.counts[arr * a.nbounds + s], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if (a.arrive == nullptr) return;
-  // completion notice for a host that polls instead of waiting on an event.  The counts went out as system-scope
-  // (write-through) stores; once every thread has seen them acknowledged (vmcnt(0)) and passed the barrier, the
-  // workgroup arrives, and the last arrival stores the round's sequence number and re-arms the counter.  No L2
-  // write-back is needed: nothing the host reads sits in an L2.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == a.count) {
-      __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+// Inclusive prefix sum over the 64 lanes of a wave in six DPP steps (no LDS): row_shr 1, 2, 4, 8 inside each 16-lane
+// row, then row_bcast:15 (rows 1 and 3 add the last lane of the row before) and row_bcast:31 (rows 2 and 3 add lane 31).
+// Lanes whose source is out of the row keep `old` = 0.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false));
+  return v;
 }
 
-// ---------------------------------------------------------------- the round plan in row chunks (round 4)
-// k_round_plan above gives each mask array ONE 1024-thread workgroup: 16 waves that cannot share a CU with a running
-// scan workgroup (VGPRs), so the plan waits for the scan's workgroups to drain, and its write-set workgroup alone reads
-// every worker's every row.  Here 256-thread workgroups (one wave per SIMD) each take a chunk of 256 rows of EVERY
-// array: one round trip loads the chunk's rows of the count workers' masks; the union, the write set, every array's
-// popcounts and their exclusive scans over the chunk come from registers; the chunk's per-array totals are published
-// (a flag per chunk) and each workgroup sums its predecessors' totals, which they all publish at about the same time
-// (no chain of look-backs).  A workgroup's chunk is a ticket taken when it starts, so every lower chunk belongs to a
-// workgroup that is already running (the look-back never waits on one that is not resident).  A total is published as
-// total + 1, so its word doubles as its flag.  Workspace (uint32): [0] the arrival counter, [1] the ticket counter,
-// [2, 2 + kPlanChunksMax) reserved, then the totals [chunk][array]; the launch's last arrival zeroes them again.
-constexpr uint32_t kPlan2Threads = kWGThreads;
-constexpr uint32_t kPlanChunksMax = 64;  // rows <= 64 * 256 (larger plans keep k_round_plan)
-constexpr uint32_t kPlanArrays = OMR_MAX_WORKERS + 1;
-constexpr uint64_t kPlan2WorkspaceWords = 2 + kPlanChunksMax + static_cast<uint64_t>(kPlanChunksMax) * kPlanArrays;
+// The round's bookkeeping (server.cc:83-96) in ONE workgroup of 1024 threads, every mask read once (round 5; rounds 3-4
+// gave each array a workgroup of its own, and the write-set workgroup re-read every worker's masks: 1.95-1.99 x the
+// algorithmic HBM bytes and 12 us at config 4's shapes, profiles/pmc_round_r04.json).  Rows go in tiles of 1024 * R:
+// thread t owns rows tile + i * 1024 + t (i < R), so every load instruction is lane-contiguous, and all W * R loads of a
+// tile are in flight together (one round trip).  From registers: union = OR of the workers (the aggregator's min_next
+// domain), write set = union | lane heads (every lane head is sent and returned, client.cc:201-205), each array's
+// popcounts; the prefixes are DPP wave scans, then one wave scans the tile's 16 R wave totals per array (two barriers
+// per tile, no atomics, no look-back).  prefix[a][r] = set bits of array a before row r; counts[a][s] = prefix[a] at
+// bounds[s], stored at system scope into host-mapped memory; once they are acknowledged (vmcnt) the workgroup posts
+// `seq` to done_flag (one workgroup: no arrival counter).  The next round's own masks and pack counters are cleared.
+constexpr int kPlanThreads = 1024;
+constexpr uint32_t kPlanWaves = kPlanThreads / 64;
 
-// W >= count: the per-array loops are unrolled over W workers + the write set (the launch picks 2, 4, 8 or 16)
-template <bool LIST, int W>
-__global__ __launch_bounds__(kPlan2Threads) void k_round_plan2(PlanArgs a, uint32_t nchunks, uint32_t* ws) {
+template <int W, int R>
+__device__ __forceinline__ void plan_rows(const PlanArgs& a) {
+  constexpr uint32_t NA = W + 1;  // arrays unrolled: W workers, then the write set
+  constexpr uint32_t ENT = kPlanWaves * R;  // wave totals per array and tile (<= 64: one scanning wave's lanes)
+  static_assert(ENT <= 64, "a tile's wave totals fit one wave");
+  __shared__ uint32_t s_wtot[ENT][NA];
+  __shared__ uint32_t s_base[ENT][NA];
+  __shared__ uint64_t s_bounds[OMR_MAX_WORKERS + 2];
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  constexpr uint32_t kW = kPlan2Threads / 64;
-  if constexpr (LIST) {
-    if (blockIdx.x >= nchunks + a.chain_wgs) {  // the shard sum's pair list, one unit per wave
-      const uint32_t w = __builtin_amdgcn_readfirstlane(wave);
-      build_sum_list(a.list, static_cast<uint64_t>(blockIdx.x - nchunks - a.chain_wgs) * kW + w,
-                     static_cast<uint64_t>(a.list_wgs) * kW);
-      return;
+  const uint32_t cnt = a.count;
+  const uint64_t all_lanes = a.lanes >= 64 ? ~0ull : ((1ull << a.lanes) - 1ull);
+  if (t < a.nbounds) s_bounds[t] = a.bounds[t];
+  if (a.zero_cnt != nullptr && t < a.zero_cnt_n) a.zero_cnt[t] = 0;
+  uint32_t carry = 0;  // wave 0, lane a < NA: array a's set bits before the tile
+  __syncthreads();
+  for (uint64_t tile = 0; tile < a.rows; tile += static_cast<uint64_t>(kPlanThreads) * R) {
+    // Buffer loads over each worker's rows: a row past the end, or a worker past `count` (a zero-size descriptor),
+    // reads 0 without a branch.  (Plain loads under `c < count && r < rows` were branched around one by one, each
+    // followed by a vmcnt(0) wait: W * R round trips in a row instead of one, 33 us at config 4's shapes.)
+    uint64_t mk[R][W];
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+      const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint64_t*>(a.masks + static_cast<uint64_t>(static_cast<uint32_t>(c) < cnt ? c : 0) * a.mstride),
+          0, static_cast<uint32_t>(c) < cnt ? static_cast<int>(a.rows * 8) : 0, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const uint32_t r = static_cast<uint32_t>(tile) + static_cast<uint32_t>(i) * kPlanThreads + t;
+        const v2u v = __builtin_bit_cast(v2u, __builtin_amdgcn_raw_buffer_load_b64(src, r * 8u, 0, 0));
+        mk[i][c] = static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32);
+      }
     }
-  }
-  if (blockIdx.x >= nchunks) {  // the aggregator chain (server.cc:86-96 min_next) over the union, one segment each
-    const uint64_t* m = a.masks;
-    const uint32_t cnt = a.count;
-    const uint64_t ms = a.mstride;
-    next_segment<kW>(a.chain, blockIdx.x - nchunks, [&](uint64_t r) {
+    uint32_t ex[R][NA];  // exclusive prefix inside the wave, per row and array
+    uint64_t ws[R], un[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const uint64_t r = tile + static_cast<uint64_t>(i) * kPlanThreads + t;
       uint64_t u = 0;
-      for (uint32_t c = 0; c < cnt; ++c) u |= m[static_cast<uint64_t>(c) * ms + r];
-      return u;
-    }, a.chain.next);
+#pragma unroll
+      for (int c = 0; c < W; ++c) u |= mk[i][c];
+      un[i] = u;
+      ws[i] = (r < a.rows && r % a.rpp == 0) ? (u | all_lanes) : u;
+#pragma unroll
+      for (uint32_t k = 0; k < NA; ++k) {
+        const uint32_t v = static_cast<uint32_t>(__builtin_popcountll(k < W ? mk[i][k] : ws[i]));
+        const uint32_t inc = wave_incl_scan(v);
+        ex[i][k] = inc - v;
+        if (lane == 63) s_wtot[i * kPlanWaves + wave][k] = inc;
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {  // every (row group, wave) total of the tile, in row order: lane e = i * 16 + w
+#pragma unroll
+      for (uint32_t k = 0; k < NA; ++k) {
+        const uint32_t v = lane < ENT ? s_wtot[lane][k] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        const uint32_t base = __builtin_amdgcn_readlane(static_cast<int>(carry), static_cast<int>(k));
+        if (lane < ENT) s_base[lane][k] = base + inc - v;
+        const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
+        if (lane == k) carry += tot;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const uint64_t r = tile + static_cast<uint64_t>(i) * kPlanThreads + t;
+      if (r >= a.rows) continue;
+      a.write_set[r] = ws[i];
+      if (a.union_masks != nullptr) a.union_masks[r] = un[i];
+      if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
+      uint32_t bnd = kNone;  // the last shard bound equal to this row (empty shards repeat a bound)
+      for (uint32_t s = 0; s < a.nbounds; ++s)
+        if (s_bounds[s] == r) bnd = s;
+#pragma unroll
+      for (uint32_t k = 0; k < NA; ++k) {
+        if (k < W && k >= cnt) continue;
+        const uint32_t arr = k < W ? k : cnt;
+        const uint32_t pv = s_base[i * kPlanWaves + wave][k] + ex[i][k];
+        a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + r] = pv;
+        if (bnd != kNone)
+          for (uint32_t s = 0; s < a.nbounds; ++s)
+            if (s_bounds[s] == r)
+              __hip_atomic_store(&a.counts[arr * a.nbounds + s], pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    __syncthreads();  // (s_wtot / s_base are refilled by the next tile)
+  }
+  // the totals: prefix[a][rows], and the counts of every bound at or past the end
+  if (wave == 0 && lane < NA && (lane == W || lane < cnt)) {
+    const uint32_t arr = lane < W ? lane : cnt;
+    a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + a.rows] = carry;
+    for (uint32_t s = 0; s < a.nbounds; ++s)
+      if (s_bounds[s] >= a.rows)
+        __hip_atomic_store(&a.counts[arr * a.nbounds + s], carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (a.done_flag == nullptr) return;
+  // completion notice for a host that polls instead of waiting on an event: the counts went out as system-scope
+  // (write-through) stores; once every thread has seen its own acknowledged and passed the barrier, one store posts the
+  // round's sequence number.  No L2 write-back: nothing the host reads sits in an L2.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One launch: workgroup 0 the bookkeeping (plan_rows), then the aggregator chain (server.cc:86-96 min_next over the
+// union, one k_next segment each), then the shard sum's pair list (one unit per wave).  W >= count (2, 4, 8, 16), R rows
+// per thread and tile (W * R <= 32 masks in registers).
+template <int W, int R>
+__global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
+  if (blockIdx.x == 0) {
+    plan_rows<W, R>(a);
     return;
   }
-  constexpr uint32_t NW = W + 1;  // arrays unrolled: W workers, then the write set
-  __shared__ uint32_t s_wtot[kW][NW];
-  __shared__ uint32_t s_base[NW];
-  __shared__ uint32_t s_ticket;
-  __shared__ uint64_t s_bounds[OMR_MAX_WORKERS + 2];
-  if (t == 0) s_ticket = __hip_atomic_fetch_add(&ws[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t < a.nbounds) s_bounds[t] = a.bounds[t];
-  __syncthreads();
-  const uint32_t c = s_ticket;
-  const uint32_t NA = a.count + 1;  // the workers' arrays, then the write set
-  const uint64_t all_lanes = a.lanes >= 64 ? ~0ull : ((1ull << a.lanes) - 1ull);
-  uint32_t* const totals = ws + 2 + kPlanChunksMax;  // (words [2, 2 + kPlanChunksMax): reserved)
-  if (c == 0 && a.zero_cnt != nullptr && t < a.zero_cnt_n) a.zero_cnt[t] = 0;
-  // ---- one round trip: row r = c * 256 + t of every worker's masks; union, write set, every array's popcount
-  const uint64_t r = static_cast<uint64_t>(c) * kPlan2Threads + t;
-  const bool in = r < a.rows;
-  uint64_t mk[W];
-#pragma unroll
-  for (uint32_t w = 0; w < W; ++w)
-    mk[w] = (w < a.count && in) ? a.masks[static_cast<uint64_t>(w) * a.mstride + r] : 0ull;
-  uint64_t u = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < W; ++w) u |= mk[w];
-  const uint64_t wsr = in ? ((r % a.rpp == 0) ? (u | all_lanes) : u) : 0ull;  // union + lane heads (client.cc:201-205)
-  // ---- per array: the chunk's exclusive prefix at this row (wave scan, then the earlier waves' totals), the total
-  uint32_t pfx[NW];
-#pragma unroll
-  for (uint32_t arr = 0; arr < NW; ++arr) {  // (the row's popcounts first: the masks are dead after this)
-    const uint64_t bits = arr < W ? mk[arr] : 0ull;
-    pfx[arr] = arr < NA ? static_cast<uint32_t>(__builtin_popcountll(arr == a.count ? wsr : bits)) : 0u;
+  if (blockIdx.x > a.chain_wgs) {  // the shard sum's pair list, one unit per wave
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    build_sum_list(a.list, static_cast<uint64_t>(blockIdx.x - 1 - a.chain_wgs) * kPlanWaves + w,
+                   static_cast<uint64_t>(a.list_wgs) * kPlanWaves);
+    return;
   }
-#pragma unroll
-  for (uint32_t arr = 0; arr < NW; ++arr) {
-    const uint32_t v = pfx[arr];
-    uint32_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = __shfl_up(inc, d, 64);
-      if (lane >= static_cast<uint32_t>(d)) inc += o;
-    }
-    pfx[arr] = inc - v;
-    if (lane == 63) s_wtot[wave][arr] = inc;
-  }
-  if (t < NW) s_base[t] = 0;
-  __syncthreads();
-  uint32_t ctot[NW];
-#pragma unroll
-  for (uint32_t arr = 0; arr < NW; ++arr) {
-    uint32_t before = 0, all = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < kW; ++w) {
-      const uint32_t x = s_wtot[w][arr];
-      before += w < wave ? x : 0u;
-      all += x;
-    }
-    pfx[arr] += before;
-    ctot[arr] = all;
-  }
-  // ---- publish the chunk's totals (stored + 1: a zero word is "not yet"), then add the predecessors': thread
-  // (i, arr) waits for chunk i's total of array arr, whose workgroup took its ticket first (it is running or done)
-  if (t < NA) {
-    uint32_t v = 0;
-#pragma unroll
-    for (uint32_t arr = 0; arr < NW; ++arr) v = arr == t ? ctot[arr] : v;
-    __hip_atomic_store(&totals[c * kPlanArrays + t], v + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  for (uint32_t idx = t; idx < c * NA; idx += kPlan2Threads) {
-    const uint32_t i = idx / NA, arr = idx - i * NA;
-    uint32_t v;
-    while ((v = __hip_atomic_load(&totals[i * kPlanArrays + arr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
-      __builtin_amdgcn_s_sleep(1);
-    atomicAdd(&s_base[arr], v - 1u);
-  }
-  __syncthreads();
-  // ---- this chunk's rows: write set, union, own masks cleared, prefixes, the counts at the shard bounds
-  //      (system-scope stores: the host reads them), the totals
-  if (in) {
-    a.write_set[r] = wsr;
-    a.union_masks[r] = u;
-    if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
-  }
-  uint32_t bnd = kNone;  // the shard bound this row starts, if any (bounds are distinct except empty shards)
-  for (uint32_t s = 0; s < a.nbounds; ++s)
-    if (s_bounds[s] == r && in) bnd = s;
-  if (in) {
-#pragma unroll
-    for (uint32_t arr = 0; arr < NW; ++arr) {
-      if (arr >= NA) continue;
-      const uint32_t pv = s_base[arr] + pfx[arr];
-      a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + r] = pv;
-      if (bnd != kNone)  // (every bound equal to this row: empty shards repeat a bound)
-        for (uint32_t s = 0; s < a.nbounds; ++s)
-          if (s_bounds[s] == r)
-            __hip_atomic_store(&a.counts[arr * a.nbounds + s], pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  if (c + 1 == nchunks && t == 0) {
-#pragma unroll
-    for (uint32_t arr = 0; arr < NW; ++arr) {
-      if (arr >= NA) continue;
-      const uint32_t total = s_base[arr] + ctot[arr];
-      a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + a.rows] = total;
-      for (uint32_t s = 0; s < a.nbounds; ++s)
-        if (s_bounds[s] >= a.rows)
-          __hip_atomic_store(&a.counts[arr * a.nbounds + s], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  // ---- completion: every chunk's counts acknowledged (write-through, system scope), then the last arrival re-arms
-  // the workspace (every chunk is past its look-back: nothing reads the totals any more) and posts the sequence number
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __shared__ uint32_t s_last;
-  __syncthreads();
-  if (t == 0) s_last = __hip_atomic_fetch_add(&ws[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == nchunks;
-  __syncthreads();
-  if (s_last) {
-    for (uint32_t idx = t; idx < nchunks * kPlanArrays; idx += kPlan2Threads)
-      __hip_atomic_store(&totals[idx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-      __hip_atomic_store(&ws[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ws[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (a.done_flag != nullptr) __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  const uint64_t* m = a.masks;  // the aggregator chain over the union, one segment each
+  const uint32_t cnt = a.count;
+  const uint64_t ms = a.mstride;
+  next_segment<kPlanWaves>(a.chain, blockIdx.x - 1, [&](uint64_t r) {
+    uint64_t u = 0;
+    for (uint32_t c = 0; c < cnt; ++c) u |= m[static_cast<uint64_t>(c) * ms + r];
+    return u;
+  }, a.chain.next);
 }
 
 // Dense <-> packed block movement over the set bits of one mask array (dir 0: pack, the worker's gather of
@@ -1518,15 +1446,11 @@ struct SumArgs {
   const uint64_t* masks;   // worker c's row masks at masks + c * mstride
   uint64_t mstride;
   const uint32_t* prefix;  // [count + 1][rows + 1]: the workers' row-stream prefixes, then the write set's
-  uint64_t pos_off;        // column streams: worker c's position table at (const uint32_t*)(masks + c * mstride) + pos_off
   const uint64_t* write_set;
   float* out;
   uint64_t rows, r0, r1;
   uint32_t count, me, lanes, block, packed_out;
-  uint32_t S, gps;         // column streams: segment rows (shards are whole segments), 64-row groups per segment
-  // set by the launch, so a unit's coordinates are 32-bit shifts and two 32-bit divisions (round 3's 64-bit divisions
-  // by runtime values were ~1,000 scalar instructions before a wave's first load)
-  uint32_t units, lane_shift, seg0;
+  uint32_t units, lane_shift;  // set by the launch (a unit's coordinates are 32-bit shifts)
 };
 
 
@@ -1537,37 +1461,18 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
   constexpr int P = 32 / VEC;  // pair slots per window
   constexpr int kSlotGroup = P < 8 ? P : 8;
   constexpr uint32_t kRecCap = UR * W;
-  constexpr uint32_t QU = kPackGroupRows / UR;  // units per 64-row group (column streams)
   __shared__ uint64_t s_rec[kWavesPerWG][kRecCap];
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool cols = a.pos_off != kRowStreams;
   const uint32_t nw = gridDim.x * kWavesPerWG;
   const uint32_t* const pws = a.prefix + static_cast<uint64_t>(a.count) * (a.rows + 1);
   const uint32_t wpre0 = a.packed_out ? pws[a.r0] : 0u;
   const uint32_t bbytes = a.block * 4;
   for (uint32_t u = blockIdx.x * kWavesPerWG + wave; u < a.units; u += nw) {
     const uint32_t l = u & (a.lanes - 1);
-    uint64_t g0, gidx = 0;  // first row the lanes load (lane i: row g0 + i); column streams: the group's table index
-    uint32_t nload, h0, h1;  // rows loaded; the unit's rows are lanes [h0, h1)
-    if (cols) {
-      uint32_t t = u >> a.lane_shift;
-      const uint32_t h = t % QU;
-      t /= QU;
-      const uint32_t j = t % a.gps;
-      const uint64_t seg = a.seg0 + t / a.gps;
-      g0 = seg * a.S + static_cast<uint64_t>(j) * kPackGroupRows;
-      nload = a.S - j * kPackGroupRows < kPackGroupRows ? a.S - j * kPackGroupRows : kPackGroupRows;
-      h0 = h * UR;
-      h1 = nload < h0 + UR ? nload : h0 + UR;
-      gidx = seg * a.gps + j;
-      if (h0 >= h1) continue;
-    } else {
-      g0 = a.r0 + static_cast<uint64_t>(u >> a.lane_shift) * UR;
-      nload = a.r1 - g0 < UR ? static_cast<uint32_t>(a.r1 - g0) : UR;
-      h0 = 0;
-      h1 = nload;
-    }
+    // the unit: rows [g0, g0 + nload) of lane l (lane i of the wave: row g0 + i)
+    const uint64_t g0 = a.r0 + static_cast<uint64_t>(u >> a.lane_shift) * UR;
+    const uint32_t nload = a.r1 - g0 < UR ? static_cast<uint32_t>(a.r1 - g0) : UR;
     // ---- index loads, all issued together (one round trip)
     const bool rl = static_cast<uint32_t>(lane) < nload;
     const uint64_t r = g0 + (rl ? static_cast<uint32_t>(lane) : 0u);
@@ -1578,17 +1483,13 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
 #pragma unroll
     for (uint32_t c = 0; c < W; ++c) {
       mk[c] = (c < a.count && rl) ? a.masks[c * a.mstride + r] : 0ull;
-      pre[c] = (!cols && c < a.count && rl) ? a.prefix[c * (a.rows + 1) + r] : 0u;
+      pre[c] = (c < a.count && rl) ? a.prefix[c * (a.rows + 1) + r] : 0u;
     }
-    // lane c < count: worker c's group position (column streams) or its stream prefix at r0 (row streams)
-    const bool cl = static_cast<uint32_t>(lane) < a.count;
+    // lane c < count: worker c's stream prefix at r0 (its stream of this shard starts there)
     const uint32_t base_c =
-        !cl ? 0u
-            : cols ? reinterpret_cast<const uint32_t*>(a.masks + lane * a.mstride)[a.pos_off + gidx * a.lanes + l]
-                   : a.prefix[static_cast<uint64_t>(lane) * (a.rows + 1) + a.r0];
+        static_cast<uint32_t>(lane) < a.count ? a.prefix[static_cast<uint64_t>(lane) * (a.rows + 1) + a.r0] : 0u;
     // ---- (block, contributor) pairs of the unit's write-set blocks, rank order within a block
-    const bool mine = static_cast<uint32_t>(lane) >= h0 && static_cast<uint32_t>(lane) < h1;
-    const bool wb = mine && ((w >> l) & 1ull);
+    const bool wb = rl && ((w >> l) & 1ull);
     uint32_t cb = 0;
 #pragma unroll
     for (uint32_t c = 0; c < W; ++c) cb |= static_cast<uint32_t>((mk[c] >> l) & 1ull) << c;
@@ -1601,9 +1502,6 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
     }
     const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
     if (total == 0) continue;
-    uint64_t ccol[W];  // column streams: worker c's bits of column l over the loaded rows
-#pragma unroll
-    for (uint32_t c = 0; c < W; ++c) ccol[c] = (cols && c < a.count) ? __ballot((mk[c] >> l) & 1ull) : 0ull;
     if (np != 0) {
       uint32_t k = inc - np;
       const uint32_t first = k, last = inc - 1;
@@ -1622,10 +1520,8 @@ __global__ __launch_bounds__(kWGThreads) void k_shard_sum(SumArgs a) {
             rec = (r * a.lanes + l) | kRecOwn;
           } else {
             const uint32_t bc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_c), c));
-            const uint64_t pos = cols ? static_cast<uint64_t>(bc) + static_cast<uint64_t>(__builtin_popcountll(
-                                                                        ccol[c] & below(static_cast<uint32_t>(lane))))
-                                      : static_cast<uint64_t>(pre[c] - bc) +
-                                            static_cast<uint64_t>(__builtin_popcountll(mk[c] & below(l)));
+            const uint64_t pos = static_cast<uint64_t>(pre[c] - bc) +
+                                 static_cast<uint64_t>(__builtin_popcountll(mk[c] & below(l)));
             rec = (a.recv_off[c] + pos) & 0xFFFFFFFFull;
           }
           rec |= hdr | (k == first ? kRecFirst : 0ull) | (k == last ? kRecLast : 0ull);
@@ -1970,7 +1866,18 @@ int pack_check(const Layout& L, const FusedShape& f, const uint64_t* bounds, uin
   return 0;
 }
 
-template <int VEC, int SKIP, int WAVES = kFusedWaves>
+constexpr int kPackWaves = 8;  // the fused pack's workgroups (two per CU)
+
+// First row of shard s's stream in the send buffer, and the buffer's rows (*total_rows): the streams in shard order,
+// own_shard's left out (the pack never writes it, so a co-located rank's send buffer is (N - 1) / N of the tensor).
+uint64_t pack_send_row(const uint64_t* bounds, uint32_t nshards, int32_t own_shard, uint32_t s, uint64_t* total_rows) {
+  const uint64_t own_rows = (own_shard >= 0 && static_cast<uint32_t>(own_shard) < nshards)
+                                ? bounds[own_shard + 1] - bounds[own_shard] : 0;
+  if (total_rows) *total_rows = bounds[nshards] - own_rows;
+  return bounds[s] - ((own_shard >= 0 && s > static_cast<uint32_t>(own_shard)) ? own_rows : 0);
+}
+
+template <int VEC, int SKIP, int WAVES = kPackWaves>
 int launch_fused_pack(const FusedArgs& a, const Layout& L, const FusedShape& f, unsigned grid, hipStream_t st) {
   const uint32_t bits_words = ((f.S + 31) / 32 + 3) & ~3u;
   const size_t lds = bits_words * sizeof(uint32_t) + static_cast<size_t>(WAVES) * a.wcap * L.block * 4;
@@ -1992,9 +1899,17 @@ int launch_fused_pack(const FusedArgs& a, const Layout& L, const FusedShape& f, 
   return launch_status("k_scan1f (pack)");
 }
 
+// The one-rank round's tally (omr_worker_scan_tally_f32).
+struct TallySpec {
+  uint64_t* tally;
+  const uint64_t* pub_src;  // or null: nothing to publish
+  uint32_t* pub_dst;
+  uint32_t pub_seq;
+};
+
 int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* out, int32_t* flags, uint32_t* next,
                  void* ws, hipStream_t st, uint64_t* masks = nullptr, uint32_t part_begin = 0,
-                 uint32_t part_count = 0, const PackSpec* pk = nullptr) {
+                 uint32_t part_count = 0, const PackSpec* pk = nullptr, const TallySpec* tl = nullptr) {
   if (part_count == 0) part_count = L.parts - part_begin;
   FusedArgs a{};
   a.part0 = part_begin;
@@ -2015,28 +1930,35 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
   a.masks = masks;
   const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(part_count) * L.lanes * f.K);
   constexpr int T = 64 * kFusedWaves;
+  if (tl != nullptr) {
+    // the one-rank round: the single-GPU step's shape (one 16-wave workgroup per column segment) with its tally
+    a.tally = tl->tally;
+    a.pub_src = tl->pub_src;
+    a.pub_dst = tl->pub_dst;
+    a.pub_seq = tl->pub_seq;
+    a.pub_slots = grid;  // (the earlier launch had the same shape)
+    const unsigned g = grid;
+    switch (L.vec) {
+      case 1: k_scan1f<1, kFusedWaves, kFusedLoads, 0, false, true><<<g, T, 0, st>>>(a); break;
+      case 2: k_scan1f<2, kFusedWaves, kFusedLoads, 0, false, true><<<g, T, 0, st>>>(a); break;
+      default: k_scan1f<4, kFusedWaves, kFusedLoads, 1, false, true><<<g, T, 0, st>>>(a); break;
+    }
+    return launch_status("k_scan1f (tally)");
+  }
   if (pk != nullptr) {
     a.send = pk->send;
     a.shard_cnt = pk->shard_cnt;
     a.pos = pk->pos;
     for (uint32_t s = 0; s <= pk->nshards; ++s) a.bounds[s] = static_cast<uint32_t>(pk->bounds[s]);
+    for (uint32_t s = 0; s < pk->nshards; ++s)
+      a.send_row[s] = static_cast<uint32_t>(pack_send_row(pk->bounds, pk->nshards, pk->own_shard, s, nullptr));
     a.nshards = pk->nshards;
     a.own_shard = pk->own_shard;
     a.gps = pack_groups(f);
     // 8-wave workgroups with half the stash (64 KiB each), so two share a CU: one streams while the other takes its
     // stream place and writes its blocks out.  At config 4's shapes 50.3 us against 52.8 us for one 16-wave workgroup
-    // per CU (tools/tune_round_r03.py, profiles/r03/round/tune_round_r03_list.log).  OMR_PACK_WAVES=16: the latter.
-    const char* pw = getenv("OMR_PACK_WAVES");
-    const int pack_waves = (pw != nullptr && atoi(pw) == 16) ? kFusedWaves : 8;
-    if (pack_waves == 8) {
-      a.wcap = (kPackLdsBytes / 2) / (8 * L.block * 4);
-      switch (L.vec) {
-        case 1: return launch_fused_pack<1, 0, 8>(a, L, f, grid, st);
-        case 2: return launch_fused_pack<2, 0, 8>(a, L, f, grid, st);
-        default: return launch_fused_pack<4, 1, 8>(a, L, f, grid, st);
-      }
-    }
-    a.wcap = kPackLdsBytes / (kFusedWaves * L.block * 4);
+    // per CU (tools/tune_round_r03.py, profiles/r03/round/tune_round_r03_list.log).
+    a.wcap = (kPackLdsBytes / 2) / (kPackWaves * L.block * 4);
     switch (L.vec) {
       case 1: return launch_fused_pack<1, 0>(a, L, f, grid, st);
       case 2: return launch_fused_pack<2, 0>(a, L, f, grid, st);
@@ -2047,14 +1969,8 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
   // does: beside the round's plan and copy kernels on the other streams a plan workgroup then displaces half a CU's
   // scan instead of all of it.  The world-1 round took 55.8-57.0 us so against 57.6-58.4 with one 16-wave workgroup
   // per CU (54.4-55.7 in a second set of runs), its scan 0.68-0.71 of spec against 0.66; the single-GPU step keeps 16
-  // waves (47.8 against 49.6 us alone; profiles/r04/scan_waves/).  OMR_SCAN_WAVES=8 / 16 forces one shape for both
-  // (study knob).
-  static const int waves_env = [] {
-    const char* e = getenv("OMR_SCAN_WAVES");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  const bool waves8 = waves_env == 8 || (waves_env != 16 && masks != nullptr);
-  if (waves8) {
+  // waves (47.8 against 49.6 us alone; profiles/r04/scan_waves/).
+  if (masks != nullptr) {
     switch (L.vec) {
       case 1: k_scan1f<1, 8, kFusedLoads><<<grid, 512, 0, st>>>(a); break;
       case 2: k_scan1f<2, 8, kFusedLoads><<<grid, 512, 0, st>>>(a); break;
@@ -2153,6 +2069,12 @@ int make_list_args(const Layout& L, const uint64_t* masks, uint32_t count, uint6
   g.records = sl->records;
   g.counts = sl->counts;
   return 0;
+}
+
+__global__ __launch_bounds__(64) void k_publish_tally(const uint64_t* tally, uint32_t slots, uint32_t* dst, uint32_t seq) {
+  uint32_t nz = 0, heads = 0;
+  tally_load(tally, slots, &nz, &heads);
+  publish_tally(dst, seq, nz, heads);
 }
 
 uint64_t list_units_host(const ListArgs& a) { return ((a.r1 - a.r0) / a.S) * a.gps * kSumUnitsPerGroup * a.lanes; }
@@ -2573,6 +2495,40 @@ int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, 
   return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks, 0, 0, &pk);
 }
 
+uint32_t omr_tally_slots(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts) {
+  Layout L;
+  if (make_layout(n, block_size, num_lanes, num_parts, &L)) return 0;
+  return static_cast<uint32_t>(static_cast<uint64_t>(L.parts) * L.lanes * fused_shape(L).K);
+}
+
+int omr_worker_scan_tally_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                              int32_t* flags, uint32_t* next_offsets, float* out, uint64_t* tally,
+                              const uint64_t* publish_src, uint32_t* publish_dst, uint32_t publish_seq, void* workspace,
+                              size_t workspace_bytes, omr_stream_t stream) {
+  Layout L;
+  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
+  if (buf == nullptr || next_offsets == nullptr || tally == nullptr)
+    return fail("worker_scan_tally: buf, next_offsets and tally are required");
+  if ((publish_src == nullptr) != (publish_dst == nullptr)) return fail("worker_scan_tally: publish_src and _dst go together");
+  if (reinterpret_cast<uintptr_t>(buf) % 16 != 0 || reinterpret_cast<uintptr_t>(out) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(publish_dst) % 16 != 0)
+    return fail("worker_scan_tally: buffers must be 16-byte aligned");
+  const FusedShape f = fused_shape(L);
+  const size_t need = fused_workspace_bytes(L, f);
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need))
+    return fail("worker_scan_tally: needs a zero-initialised workspace of %zu bytes", need);
+  const TallySpec tl{tally, publish_src, publish_dst, publish_seq};
+  return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), nullptr, 0, 0, nullptr,
+                      &tl);
+}
+
+int omr_tally_publish(const uint64_t* tally, uint32_t slots, uint32_t* dst, uint32_t seq, omr_stream_t stream) {
+  if (tally == nullptr || dst == nullptr || reinterpret_cast<uintptr_t>(dst) % 16 != 0)
+    return fail("tally_publish: NULL or unaligned pointer");
+  k_publish_tally<<<1, 64, 0, S(stream)>>>(tally, slots, dst, seq);
+  return launch_status("k_publish_tally");
+}
+
 int omr_pack_geometry(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, uint32_t* seg_rows,
                       uint32_t* groups_per_seg, uint64_t* table_entries) {
   Layout L;
@@ -2591,45 +2547,48 @@ int omr_pack_supported(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint
   return pack_check(L, fused_shape(L), shard_bounds, num_shards);
 }
 
+uint64_t omr_pack_send_offset(const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard, uint32_t s,
+                              uint32_t num_lanes, uint32_t block_size, uint64_t* total) {
+  uint64_t rows = 0;
+  const uint64_t r = pack_send_row(shard_bounds, num_shards, own_shard, s, &rows);
+  const uint64_t row_floats = static_cast<uint64_t>(num_lanes) * block_size;
+  if (total) *total = rows * row_floats;
+  return r * row_floats;
+}
+
 int omr_round_plan_chain(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                          uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
                          uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                         uint32_t* arrive, uint32_t* done_flag, uint32_t seq, uint32_t* union_next,
-                         uint32_t block_size, omr_stream_t stream) {
+                         uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                         omr_stream_t stream) {
   return omr_round_plan_ex(row_masks, count, rows, rows, rows_per_part, num_lanes, bounds, num_bounds, write_set,
-                           union_masks, prefix, counts, zero_masks, nullptr, 0, arrive, done_flag, seq, union_next,
-                           block_size, stream);
+                           union_masks, prefix, counts, zero_masks, nullptr, 0, done_flag, seq, union_next, block_size,
+                           stream);
 }
 
 int omr_round_plan_ex(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
                       uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
                       uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
-                      uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                      omr_stream_t stream) {
+                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* done_flag,
+                      uint32_t seq, uint32_t* union_next, uint32_t block_size, omr_stream_t stream) {
   return omr_round_plan_list(row_masks, count, mask_stride, rows, rows_per_part, num_lanes, bounds, num_bounds,
                              write_set, union_masks, prefix, counts, zero_masks, zero_counters, num_zero_counters,
-                             arrive, done_flag, seq, union_next, block_size, nullptr, stream);
+                             done_flag, seq, union_next, block_size, nullptr, stream);
 }
 
-}  // extern "C"
-
-namespace {
-// omr_round_plan_list (v2 false: k_round_plan, `arrive` one word) and omr_round_plan_ws (v2 true: k_round_plan2 on
-// plans of up to kPlanChunksMax * 256 rows, `arrive` its workspace; larger plans use k_round_plan with word 0)
-int round_plan_launch(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
-                      uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
-                      uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
-                      uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                      const omr_sum_list* list, bool v2, hipStream_t st) {
+int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                        uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
+                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* done_flag,
+                        uint32_t seq, uint32_t* union_next, uint32_t block_size, const omr_sum_list* list,
+                        omr_stream_t stream) {
   if (mask_stride < rows) return fail("round_plan: mask_stride %llu < rows", static_cast<unsigned long long>(mask_stride));
   if (num_zero_counters > kPlanThreads || (num_zero_counters > 0 && zero_counters == nullptr))
     return fail("round_plan: zero_counters");
   if (count == 0 || count > OMR_MAX_WORKERS) return fail("round_plan: count %u out of range", count);
   if (rows == 0 || rows_per_part == 0 || rows % rows_per_part != 0) return fail("round_plan: bad rows");
   if (num_lanes == 0 || num_lanes > 64) return fail("round_plan: num_lanes %u out of range", num_lanes);
-  if (row_masks == nullptr || write_set == nullptr || union_masks == nullptr || prefix == nullptr ||
+  if (row_masks == nullptr || write_set == nullptr || prefix == nullptr ||
       (num_bounds > 0 && (bounds == nullptr || counts == nullptr)))
     return fail("round_plan: NULL pointer");
   if (rows > 0xFFFFFFFFull / 64) return fail("round_plan: too many rows");
@@ -2650,9 +2609,6 @@ int round_plan_launch(const uint64_t* row_masks, uint32_t count, uint64_t mask_s
   a.prefix = prefix;
   a.counts = counts;
   a.zero_masks = zero_masks;
-  if (!v2 && (arrive == nullptr) != (done_flag == nullptr)) return fail("round_plan: arrive and done_flag go together");
-  if (v2 && arrive == nullptr) return fail("round_plan_ws: NULL workspace");
-  a.arrive = arrive;
   a.done_flag = done_flag;
   a.seq = seq;
   memset(&a.chain, 0, sizeof(a.chain));
@@ -2683,73 +2639,25 @@ int round_plan_launch(const uint64_t* row_masks, uint32_t count, uint64_t mask_s
       return rc;
     if (int rc = make_list_args(L, row_masks, count, mask_stride, list, &a.list)) return rc;
     const uint64_t units = list_units_host(a.list);
-    const uint64_t wgs = (units + kPlanThreads / 64 - 1) / (kPlanThreads / 64);
+    const uint64_t wgs = (units + kPlanWaves - 1) / kPlanWaves;
     a.list_wgs = static_cast<uint32_t>(wgs < 512 ? wgs : 512);
   }
-  const uint64_t nchunks = (rows + kPlan2Threads - 1) / kPlan2Threads;
-  if (v2 && nchunks <= kPlanChunksMax) {
-    if (arrive == nullptr) return fail("round_plan_ws: NULL workspace");
-    if (num_zero_counters > kPlan2Threads) return fail("round_plan_ws: zero_counters > %u", kPlan2Threads);
-    if (list != nullptr) {  // (k_round_plan's list workgroups had 16 waves each: the same units, 4 waves per workgroup)
-      const uint64_t units = list_units_host(a.list);
-      const uint64_t wgs = (units + kPlan2Threads / 64 - 1) / (kPlan2Threads / 64);
-      a.list_wgs = static_cast<uint32_t>(wgs < 2048 ? wgs : 2048);
-    }
-    a.arrive = nullptr;  // (k_round_plan2 counts its arrivals in the workspace)
-    const unsigned grid = static_cast<unsigned>(nchunks + chain_wgs + a.list_wgs);
-    const uint32_t nc = static_cast<uint32_t>(nchunks);
-    if (list != nullptr) {
-      if (count <= 8) k_round_plan2<true, 8><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
-      else k_round_plan2<true, OMR_MAX_WORKERS><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
-    } else if (count <= 2) {
-      k_round_plan2<false, 2><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
-    } else if (count <= 4) {
-      k_round_plan2<false, 4><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
-    } else if (count <= 8) {
-      k_round_plan2<false, 8><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
-    } else {
-      k_round_plan2<false, OMR_MAX_WORKERS><<<grid, kPlan2Threads, 0, st>>>(a, nc, arrive);
-    }
-    return launch_status("k_round_plan2");
-  }
-  const size_t lds = rows <= kPlanLdsRows ? rows * sizeof(uint64_t) : 0;
-  k_round_plan<<<count + 1 + chain_wgs + a.list_wgs, kPlanThreads, lds, st>>>(a);
+  const unsigned grid = 1 + chain_wgs + a.list_wgs;
+  hipStream_t st = S(stream);
+  // (the masks of W * R rows per thread and tile stay in registers: at most 16 of them)
+  if (count <= 2) k_round_plan<2, 4><<<grid, kPlanThreads, 0, st>>>(a);
+  else if (count <= 4) k_round_plan<4, 4><<<grid, kPlanThreads, 0, st>>>(a);
+  else if (count <= 8) k_round_plan<8, 2><<<grid, kPlanThreads, 0, st>>>(a);
+  else k_round_plan<OMR_MAX_WORKERS, 1><<<grid, kPlanThreads, 0, st>>>(a);
   return launch_status("k_round_plan");
-}
-}  // namespace
-
-extern "C" {
-
-int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
-                        uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
-                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* arrive,
-                        uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                        const omr_sum_list* list, omr_stream_t stream) {
-  return round_plan_launch(row_masks, count, mask_stride, rows, rows_per_part, num_lanes, bounds, num_bounds,
-                           write_set, union_masks, prefix, counts, zero_masks, zero_counters, num_zero_counters, arrive,
-                           done_flag, seq, union_next, block_size, list, false, S(stream));
-}
-
-uint64_t omr_round_plan_workspace_words(void) { return kPlan2WorkspaceWords; }
-
-int omr_round_plan_ws(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
-                      uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
-                      uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* workspace,
-                      uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                      const omr_sum_list* list, omr_stream_t stream) {
-  return round_plan_launch(row_masks, count, mask_stride, rows, rows_per_part, num_lanes, bounds, num_bounds,
-                           write_set, union_masks, prefix, counts, zero_masks, zero_counters, num_zero_counters,
-                           workspace, done_flag, seq, union_next, block_size, list, true, S(stream));
 }
 
 int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                    uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
                    uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                   uint32_t* arrive, uint32_t* done_flag, uint32_t seq, omr_stream_t stream) {
+                   uint32_t* done_flag, uint32_t seq, omr_stream_t stream) {
   return omr_round_plan_chain(row_masks, count, rows, rows_per_part, num_lanes, bounds, num_bounds, write_set,
-                              union_masks, prefix, counts, zero_masks, arrive, done_flag, seq, nullptr, 0, stream);
+                              union_masks, prefix, counts, zero_masks, done_flag, seq, nullptr, 0, stream);
 }
 
 int omr_move_blocks_f32(const float* src, float* dst, int dir, const uint64_t* row_masks, const uint32_t* prefix,
@@ -2819,12 +2727,10 @@ int launch_shard_sum(const SumArgs& a0, const uint64_t* recv_offsets, hipStream_
     if (c < a.count && c != a.me && a.recv_off[c] > 0xFFFFFFFFull) return fail("shard_sum: recv offset beyond 2^32 blocks");
   }
   const uint64_t srows = a.r1 - a.r0;
-  const uint64_t units = a.pos_off != kRowStreams ? (srows / a.S) * a.gps * (kPackGroupRows / kShardUnitRows) * a.lanes
-                                                 : ((srows + kShardUnitRows - 1) / kShardUnitRows) * a.lanes;
+  const uint64_t units = ((srows + kShardUnitRows - 1) / kShardUnitRows) * a.lanes;
   if (units > 0xFFFFFFFFull) return fail("shard_sum: %llu units", static_cast<unsigned long long>(units));
   a.units = static_cast<uint32_t>(units);
   a.lane_shift = static_cast<uint32_t>(__builtin_ctz(a.lanes));
-  a.seg0 = a.pos_off != kRowStreams ? static_cast<uint32_t>(a.r0 / a.S) : 0u;
   const unsigned g = grid_for(units);
   if (a.count <= 2) launch_shard_sum_w<2>(a, g, st);
   else if (a.count <= 4) launch_shard_sum_w<4>(a, g, st);
@@ -2846,7 +2752,6 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
   a.masks = row_masks;
   a.mstride = rows;
   a.prefix = prefix;
-  a.pos_off = kRowStreams;
   a.write_set = write_set;
   a.out = out;
   a.rows = rows;
@@ -2857,43 +2762,6 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
   a.lanes = num_lanes;
   a.block = block_size;
   a.packed_out = packed_out ? 1u : 0u;
-  return launch_shard_sum(a, recv_offsets, S(stream));
-}
-
-int omr_shard_sum_cols_f32(const float* own, uint32_t me, const float* recv, const uint64_t* recv_offsets,
-                           const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t pos_offset,
-                           const uint32_t* prefix, const uint64_t* write_set, uint64_t n, uint32_t block_size,
-                           uint32_t num_lanes, uint32_t num_parts, uint64_t row_begin, uint64_t row_end,
-                           int packed_out, float* out, omr_stream_t stream) {
-  Layout L;
-  if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
-  const FusedShape f = fused_shape(L);
-  if (row_begin % f.S != 0 || row_end % f.S != 0)
-    return fail("shard_sum_cols: rows [%llu, %llu) are not whole %u-row column segments",
-                static_cast<unsigned long long>(row_begin), static_cast<unsigned long long>(row_end), f.S);
-  const uint64_t words = mask_stride * 2;  // the position table must lie inside each worker's array
-  if (mask_stride < L.rows || pos_offset < L.rows * 2 || pos_offset + pack_table_entries(L, f) > words)
-    return fail("shard_sum_cols: position table outside the mask arrays (stride %llu, offset %llu)",
-                static_cast<unsigned long long>(mask_stride), static_cast<unsigned long long>(pos_offset));
-  SumArgs a{};
-  a.own = own;
-  a.recv = recv;
-  a.masks = row_masks;
-  a.mstride = mask_stride;
-  a.prefix = prefix;
-  a.pos_off = pos_offset;
-  a.write_set = write_set;
-  a.out = out;
-  a.rows = L.rows;
-  a.r0 = row_begin;
-  a.r1 = row_end;
-  a.count = count;
-  a.me = me;
-  a.lanes = L.lanes;
-  a.block = L.block;
-  a.packed_out = packed_out ? 1u : 0u;
-  a.S = f.S;
-  a.gps = pack_groups(f);
   return launch_shard_sum(a, recv_offsets, S(stream));
 }
 

@@ -53,9 +53,9 @@ SIGNATURES = {
     "omr_row_prefix": (c_int, [c_vp, c_u32, c_u64, c_vp, c_vp, c_size, c_vp]),
     "omr_worker_scan_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "omr_round_plan": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                               c_vp, c_u32, c_vp]),
+                               c_u32, c_vp]),
     "omr_round_plan_chain": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                     c_vp, c_vp, c_u32, c_vp, c_u32, c_vp]),
+                                     c_vp, c_u32, c_vp, c_u32, c_vp]),
     "omr_move_blocks_f32": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_u64, c_u32, c_u32, c_u64, c_u64, c_vp]),
     "omr_shard_sum_f32": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, c_vp, c_vp, c_u64, c_u64, c_u64, c_u32,
                                   c_u32, c_int, c_vp, c_vp]),
@@ -63,15 +63,15 @@ SIGNATURES = {
                                          ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "omr_pack_geometry": (c_int, [c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp]),
     "omr_pack_supported": (c_int, [c_u64, c_u32, c_u32, c_u32, c_vp, c_u32]),
+    "omr_pack_send_offset": (c_u64, [c_vp, c_u32, ctypes.c_int32, c_u32, c_u32, c_u32, c_vp]),
+    "omr_worker_scan_tally_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32,
+                                          c_vp, c_size, c_vp]),
+    "omr_tally_publish": (c_int, [c_vp, c_u32, c_vp, c_u32, c_vp]),
+    "omr_tally_slots": (c_u32, [c_u64, c_u32, c_u32, c_u32]),
     "omr_round_plan_ex": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
-                                  c_vp, c_vp, c_u32, c_vp, c_vp, c_u32, c_vp, c_u32, c_vp]),
-    "omr_shard_sum_cols_f32": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, c_u64, c_u64, c_vp, c_vp, c_u64, c_u32,
-                                       c_u32, c_u32, c_u64, c_u64, c_int, c_vp, c_vp]),
+                                  c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_u32, c_vp]),
     "omr_round_plan_list": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
-                                    c_vp, c_vp, c_u32, c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_vp]),
-    "omr_round_plan_ws": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
-                                    c_vp, c_vp, c_u32, c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_vp]),
-    "omr_round_plan_workspace_words": (c_u64, []),
+                                    c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_u32, c_vp, c_vp]),
     "omr_sum_list_geometry": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u64, c_u64, c_u32, c_vp, c_vp]),
     "omr_sum_list_build": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp]),
     "omr_shard_sum_list_f32": (c_int, [c_vp, c_vp, c_vp, c_u32, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_int, c_vp,
@@ -124,8 +124,8 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.omr_abi_version() != 1:
-        raise OmrError(f"libomr ABI {lib.omr_abi_version()} != 1")
+    if lib.omr_abi_version() != 2:
+        raise OmrError(f"libomr ABI {lib.omr_abi_version()} != 2 (rebuild: make -C omnireduce-rdma-demo_amd)")
     _lib = lib
     return lib
 

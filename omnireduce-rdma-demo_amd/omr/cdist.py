@@ -63,6 +63,8 @@ def load():
         "omr_sparse_round_f32": (i, [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]),
         "omr_ar_plan_join": (i, [vp, vp]),
         "omr_ar_plan_fused_pack": (i, [vp]),
+        "omr_ar_plan_device_bytes": (u64, [vp]),
+        "omr_dist_test_world1_round": (i, [vp, i]),
         "omr_sparse_buckets_f32": (i, [vp, vp, u64, i, vp, vp, vp]),
         "omr_msgd_plan_create": (i, [vp, u32, u64, u32, u32, u32, vp]),
         "omr_msgd_plan_destroy": (i, [vp]),
@@ -147,12 +149,24 @@ class CppSparseAllreduce:
         """The worker scan packs the exchange's blocks itself (omr_ar_plan_fused_pack)."""
         return bool(load().omr_ar_plan_fused_pack(self._p))
 
-    def replan(self):
-        """Destroy the plan and make a new one of the same shape on the same transport (collective: every rank calls
-        it).  The new plan's buffers may land at the old ones' addresses: the transport must not reuse what it cached
-        about the freed ones (the IPC transport's handles)."""
+    @property
+    def device_bytes(self) -> int:
+        """Device memory the plan holds (omr_ar_plan_device_bytes)."""
+        return int(load().omr_ar_plan_device_bytes(self._p))
+
+    def test_world1_round(self, on: bool = True):
+        """Test hook (omr_dist_test_world1_round): a one-rank group runs the multi-rank round's code path (all-gather,
+        plan, exchange on the side stream) and an RCCL transport issues its collectives as RCCL calls."""
+        _check(load().omr_dist_test_world1_round(self._d, int(on)), "omr_dist_test_world1_round")
+
+    def replan(self, L: Optional[Layout] = None):
+        """Destroy the plan and make a new one on the same transport, of the same shape or of layout L (collective: every
+        rank calls it).  The new plan's buffers may land at the old ones' addresses, or reuse the transport's parked
+        exported ones (IPC): the transport must not reuse what it cached about the freed ones (their handles)."""
         load().omr_ar_plan_destroy(self._p)
         self._p = ctypes.c_void_p()
+        if L is not None:
+            self.L = L
         self._plan()
 
     ALLREDUCE, REDUCE_SCATTER, DENSE_REDUCE_SCATTER, ASYNC, TIME_EXCHANGE, DEFER = 0, 1, 2, 0x100, 0x200, 0x400
@@ -163,9 +177,10 @@ class CppSparseAllreduce:
             defer: bool = False, thread: bool = False):
         """mode 0: all-reduce (every worker gets every shard's sums); 1: reduce-scatter (stop at the
         aggregators: `out` gets this rank's shard sums only); 2: the dense stand-in (the whole tensor reduce-scattered
-        by RCCL, every block).  async_: only the worker scan runs on the caller's stream; the bookkeeping runs on the
-        plan stream and the exchange and sums on the communication stream, overlapping the next calls' scans;
-        `out` (and union_next) are ready after join().  time_exchange: bracket the worker scan and the worker ->
+        by RCCL, every block).  async_: only the worker scan runs on the caller's stream; the bookkeeping, the
+        exchange and the sums run on the plan's side stream, overlapping the next calls' scans; `out` (and
+        union_next) are ready after join().  (A one-rank group's round is its worker scan alone, on the caller's
+        stream.)  time_exchange: bracket the worker scan and the worker ->
         aggregator exchange with timing events (read with timings() / exchange_time()).  defer: OMR_ROUND_DEFER,
         this round's exchange is issued two calls later (or by a call without the flag, or join()); the returned
         counts are those of the round whose exchange this call issued.  thread: OMR_ROUND_THREAD (implies async_),

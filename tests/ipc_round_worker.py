@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--replan", action="store_true",
                     help="run the rounds, destroy the plan, make a new one on the same transport and run them again "
                          "(the saved outputs are the second plan's)")
+    ap.add_argument("--replan-first-n", type=int, default=0,
+                    help="--replan: the first plan (and its rounds) at this larger n; the second plan, at --n, then "
+                         "reuses the first one's parked, larger exported buffers (ADVICE r04)")
     ap.add_argument("--timeout-ms", type=int, default=0, help="the transport's deadline (omr_dist_set_timeout)")
     ap.add_argument("--fault-rank", type=int, default=-1, help="this rank's first exchange fails (omr_dist_inject_fault)")
     ap.add_argument("--fault-after", type=int, default=0)
@@ -46,6 +49,7 @@ def main():
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     L = Layout(n=a.n, block_size=a.block)
+    L0 = Layout(n=a.replan_first_n, block_size=a.block) if a.replan and a.replan_first_n else L
     if a.transport == "rccl":
         a.rank, a.world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
         local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -53,13 +57,13 @@ def main():
         dev = torch.device("cuda", local)
         torch.distributed.init_process_group("nccl", device_id=dev)
         nw = a.workers or a.world
-        eng = cdist.CppSparseAllreduce(L, dev, num_workers=nw)
+        eng = cdist.CppSparseAllreduce(L0, dev, num_workers=nw)
         a.out = a.out.replace("RANK", str(a.rank))
     else:
         torch.cuda.set_device(0)
         dev = torch.device("cuda:0")
         nw = a.workers or a.world
-        eng = cdist.CppSparseAllreduce(L, dev, transport="ipc", uid=bytes.fromhex(a.uid), rank=a.rank, world=a.world,
+        eng = cdist.CppSparseAllreduce(L0, dev, transport="ipc", uid=bytes.fromhex(a.uid), rank=a.rank, world=a.world,
                                        num_workers=nw)
     worker = a.rank < nw
     if a.timeout_ms:
@@ -83,12 +87,22 @@ def main():
     unx = torch.empty(L.nb, dtype=torch.int32, device=dev)
     sums = {}
     if a.replan:
-        for r in range(a.rounds):
-            eng.run(xs[r % K], out=outs[r % K], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
-                    async_=a.pipe != "sync", defer=a.pipe in ("defer", "thread"), thread=a.pipe.startswith("thread"))
+        if L0 is not L:  # the first plan's rounds on inputs of its own, larger size
+            x0 = [torch.from_numpy(oracle.fill(oracle.gen_bitmap(a.rank + 50 + r, a.density, L0.nb), a.block, mode=1,
+                                               seed=a.rank + 3 * r)).to(dev) if worker else None for r in range(2)]
+            o0 = [x.clone() if x is not None else None for x in x0]
+            f0 = torch.zeros(L0.nb, dtype=torch.int32, device=dev)
+            n0 = torch.zeros(L0.nb, dtype=torch.int32, device=dev)
+            for r in range(a.rounds):
+                eng.run(x0[r % 2], out=o0[r % 2], flags=f0, next_offsets=n0, mode=a.mode, async_=a.pipe != "sync",
+                        defer=a.pipe in ("defer", "thread"), thread=a.pipe.startswith("thread"))
+        else:
+            for r in range(a.rounds):
+                eng.run(xs[r % K], out=outs[r % K], flags=flags, next_offsets=nxt, union_next=unx, mode=a.mode,
+                        async_=a.pipe != "sync", defer=a.pipe in ("defer", "thread"), thread=a.pipe.startswith("thread"))
         eng.join()
         torch.cuda.synchronize()
-        eng.replan()
+        eng.replan(L)
         for r in range(K):
             if outs[r] is not None:
                 outs[r].copy_(xs[r])

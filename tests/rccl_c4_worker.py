@@ -109,6 +109,8 @@ def main():
     if a.timeout_ms:
         eng.set_timeout(a.timeout_ms)
     if a.fault_rank == rank:
+        if world == 1:  # a one-rank group's round is its scan alone: run the multi-rank round's path to reach the op
+            eng.test_world1_round(True)
         eng.inject_fault(0) if a.fault_op == "exchange" else eng.inject_allgather_fault()
     out = a.out.replace("RANK", str(rank))
     t0 = time.monotonic()

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.omr_abi_version() == 1
+    assert lib.omr_abi_version() == 2
 
 
 @pytest.mark.parametrize("B,NB", [(256, 64), (512, 32), (1024, 16)])

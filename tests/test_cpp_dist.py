@@ -215,26 +215,6 @@ def test_cpp_async_rounds_loopback(gpu, world, mode, round_flags):
             assert (outs[r][k].view(np.uint32) == exp.view(np.uint32)).all(), f"round {k} rank {r}"
 
 
-@pytest.mark.parametrize("world,mode,round_flags", [
-    (8, 1, (D_,) * 7), (4, 0, (A, D_, D_, A, D_, D_, D_)), (4, 0, (T | D_,) * 7), (8, 1, (0,) * 4)])
-def test_cpp_rounds_cols_sum_loopback(gpu, monkeypatch, world, mode, round_flags):
-    """The same rounds with OMR_SUM_LIST=0: the aggregator's shard sum builds its pairs itself
-    (omr_shard_sum_cols_f32) instead of summing the pair list the plan launch built (omr_round_plan_list +
-    omr_shard_sum_list_f32, the round's default since round 4)."""
-    monkeypatch.setenv("OMR_SUM_LIST", "0")
-    test_cpp_async_rounds_loopback(gpu, world, mode, round_flags)
-
-
-@pytest.mark.parametrize("world,mode,round_flags", [
-    (8, 1, (D_,) * 7), (4, 1, (A, D_, 0, D_, A, D_, D_)), (4, 1, (T | D_,) * 7), (3, 0, (D_, D_, A, D_))])
-def test_cpp_rounds_agg_stream_loopback(gpu, monkeypatch, world, mode, round_flags):
-    """The same rounds with OMR_AGG_STREAM=1: asynchronous reduce-scatter rounds sum on the aggregation stream (each
-    set with its own receive buffer), mixed with synchronous rounds and all-reduce rounds that stay on the
-    communication stream."""
-    monkeypatch.setenv("OMR_AGG_STREAM", "1")
-    test_cpp_async_rounds_loopback(gpu, world, mode, round_flags)
-
-
 @pytest.mark.parametrize("world,flags", [(4, 0), (8, 0x100)])
 def test_cpp_dense_reduce_scatter_loopback(gpu, world, flags):
     """OMR_ROUND_DENSE_REDUCE_SCATTER (the dense stand-in): this rank's shard of the elementwise rank-order sum of

@@ -46,10 +46,22 @@ def _round_matches_oracle(eng, gpu, L, seed=5):
     assert (nxt.cpu().numpy().view(np.uint32) == oracle.next_offsets(f, L.n, 256, L.num_lanes, 8)).all()
 
 
-def test_rccl_failed_exchange_aborts(gpu):
+@pytest.mark.parametrize("rccl_calls", [False, True])
+def test_rccl_failed_exchange_aborts(gpu, rccl_calls):
+    """rccl_calls: the one-rank communicator issues its collectives as RCCL calls (omr_dist_test_world1_round), so the
+    failed exchange is inside ncclGroupStart / ncclGroupEnd and the abort runs ncclCommAbort after RCCL calls were made
+    on both communicators (world 1's copies bypass RCCL otherwise)."""
     L = Layout(n=1 << 20, block_size=256)
     eng = cdist.CppSparseAllreduce(L, gpu, transport="rccl1")
     try:
+        if rccl_calls:
+            eng.test_world1_round(True)
+            src = torch.arange(64, dtype=torch.int32, device=gpu)
+            dst = torch.zeros(64, dtype=torch.int32, device=gpu)
+            eng.allgather(src, dst)  # an RCCL all-gather on `comm`
+            assert eng.exchange([None], [None]) == 0  # an empty RCCL group on `xcomm`
+            torch.cuda.synchronize()
+            assert torch.equal(src, dst)
         _round_matches_oracle(eng, gpu, L)
         eng.inject_fault(0)
         t0 = time.monotonic()
@@ -67,6 +79,8 @@ def test_rccl_failed_exchange_aborts(gpu):
     # a group left open by the failed exchange would capture this communicator's all-gather (never launched)
     eng2 = cdist.CppSparseAllreduce(L, gpu, transport="rccl1")
     try:
+        if rccl_calls:
+            eng2.test_world1_round(True)
         src = torch.arange(64, dtype=torch.int32, device=gpu)
         dst = torch.zeros(64, dtype=torch.int32, device=gpu)
         eng2.allgather(src, dst)
@@ -87,6 +101,65 @@ def _sleep_cycles_for(seconds):
     torch.cuda.synchronize()
     per_s = cyc / (a.elapsed_time(b) * 1e-3)
     return int(per_s * seconds)
+
+
+def test_rccl_world1_calls_round(gpu):
+    """With RCCL calls kept at world 1 (omr_dist_test_world1_round), the rounds that use the transport at world 1 -- the
+    dense stand-in (ncclReduceScatter) and a bucket round (ncclAllGather of the masks, an empty grouped exchange) --
+    are bit-exact against the oracle."""
+    B = 256
+    L = Layout(n=1 << 20, block_size=B)
+    eng = cdist.CppSparseAllreduce(L, gpu, transport="rccl1")
+    try:
+        eng.test_world1_round(True)
+        x = oracle.fill(oracle.gen_bitmap(0, 0.3, L.nb), B, mode=1, seed=4)
+        f = oracle.flags_from_data(x, B)
+        exp = x.copy()
+        oracle.block_sum([x], L.n, B, L.num_lanes, 8, f, exp)
+        xd = torch.from_numpy(x).to(gpu)
+        for mode in (0, 1):  # the multi-rank round's path at world 1: all-gather, plan, empty exchange, shard sum
+            out = xd.clone()
+            eng.run(xd, out=out, mode=mode, async_=True, defer=True)
+            eng.join()
+            torch.cuda.synchronize()
+            assert (out.cpu().numpy().view(np.uint32) == exp.view(np.uint32)).all(), mode
+        out = torch.zeros_like(xd)
+        eng.run(xd, out=out, mode=2)  # dense reduce-scatter over one rank: the tensor itself
+        torch.cuda.synchronize()
+        assert (out.cpu().numpy().view(np.uint32) == x.view(np.uint32)).all()
+        buf = torch.from_numpy(np.concatenate([x, x])).to(gpu)
+        eng.run_buckets(buf, mode=0)
+        torch.cuda.synchronize()
+        got = buf.cpu().numpy()
+        for k in range(2):
+            assert (got[k * L.n:(k + 1) * L.n].view(np.uint32) == exp.view(np.uint32)).all(), k
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("transport", ["rccl1", "local1"])
+def test_abort_from_another_thread_during_wait(gpu, transport):
+    """omr_dist_abort from a second thread while the owner waits in omr_ar_plan_wait (the abort must not
+    free an RCCL communicator that the waiting thread's poll is using): the wait ends with an error well before its
+    deadline, the transport is aborted, and closing it returns."""
+    L = Layout(n=1 << 20, block_size=256)
+    eng = cdist.CppSparseAllreduce(L, gpu, transport=transport)
+    try:
+        _round_matches_oracle(eng, gpu, L)
+        eng.set_timeout(20000)
+        torch.cuda._sleep(_sleep_cycles_for(2.0))
+        t = threading.Thread(target=lambda: (time.sleep(0.3), eng.abort()), daemon=True)
+        t0 = time.monotonic()
+        t.start()
+        with pytest.raises(OmrError, match="abort"):
+            eng.wait()
+        t.join(timeout=30)
+        assert not t.is_alive()
+        assert eng.aborted
+        assert time.monotonic() - t0 < 10.0
+        torch.cuda.synchronize()  # the sleep ends by itself
+    finally:
+        eng.close()
 
 
 @pytest.mark.parametrize("transport", ["rccl1", "local1"])

@@ -76,6 +76,17 @@ def test_cpp_round_processes_replan(gpu, tmp_path, world, pipe, mode):
     check_rounds(res, L, world, 256, 0.2, mode, 3, 3)
 
 
+@pytest.mark.parametrize("world,pipe,mode", [(2, "defer", 0), (3, "sync", 1)])
+def test_cpp_round_processes_replan_smaller(gpu, tmp_path, world, pipe, mode):
+    """the second plan is SMALLER (2 MiB floats after 3 MiB: between 0.5 and 1 x), so the IPC transport hands
+    it parked exported allocations up to twice its sizes (the lower_bound reuse), which keep their handles and ids; the
+    peers must still address the right bytes of them.  Outputs bit-exact against the oracle."""
+    L = Layout(n=2 << 20, block_size=256)
+    res = run_ranks(tmp_path, world, L.n, 256, 0.2, mode, pipe, 3, cycle=3,
+                    extra=["--replan", "--replan-first-n", str(3 << 20)])
+    check_rounds(res, L, world, 256, 0.2, mode, 3, 3)
+
+
 def check_rounds(res, L, world, B, density, mode, rounds, K):
     """Every rank's outputs of rounds 0..K-1 (inputs seeded rank + 10 round, as the worker makes them) against the
     oracle: rank-order block sums, flags, next chains and the union chain of the last round."""

@@ -1,17 +1,17 @@
-"""The round's fused pack and the column-stream shard sum, through the C ABI, against the oracle.
+"""The round's fused pack and the shard sum over its column streams, through the C ABI, against the oracle.
 
 omr_worker_scan_pack_f32 (the worker scan with the pack of common.cc:399-407 fused in): besides flags, next offsets
 and row masks (client.cc:19-31), every non-zero block of a row of another shard is written to that shard's send
-stream; the stream's length is its counter, and the position table locates every block (segment, 64-row group,
-lane) -> stream place.  Checked: each stream is a permutation of exactly its shard's non-zero blocks, every block sits
+stream (the streams in shard order, the own shard's left out: omr_pack_send_offset); the stream's length is its
+counter, and the position table locates every block (segment, 64-row group, lane) -> stream place.  Checked: each stream is a permutation of exactly its shard's non-zero blocks, every block sits
 where the table says, nothing outside the streams is written, own-shard rows are not packed; including densities
 that overflow the waves' LDS slots (the re-read path), B = 512 / 1024 (two column segments per partition), and 1-8
 shards.
 
-omr_shard_sum_cols_f32 (server.cc:83-99 over those streams): M workers' scans on one device, their streams
+omr_shard_sum_list_f32 (server.cc:83-99 over those streams): M workers' scans on one device, their streams
 concatenated as the transport would deliver them to an aggregator, the bookkeeping from omr_round_plan_ex over the
-all-gathered masks + tables, then the shard sums — dense in place and packed in write-set order — bit-exact against
-the oracle's rank-order sum (0 ulp)."""
+all-gathered masks + tables, the pair list built by the plan launch and by a launch of its own, then the shard sums —
+dense in place and packed in write-set order — bit-exact against the oracle's rank-order sum (0 ulp)."""
 import ctypes
 
 import numpy as np
@@ -43,6 +43,20 @@ def geometry(L):
 
 def bounds_of(L, world):
     return np.array([s * L.rows // world for s in range(world + 1)], dtype=np.uint64)
+
+
+def send_offset(L, bounds, own, s):
+    """Where shard s's stream starts in the send buffer (floats): omr_pack_send_offset, checked against its rule."""
+    lib = _lib.load()
+    bh = bounds.astype(np.uint64)
+    tot = ctypes.c_uint64()
+    off = lib.omr_pack_send_offset(bh.ctypes.data_as(ctypes.c_void_p), len(bounds) - 1, own, s, L.num_lanes,
+                                   L.block_size, ctypes.byref(tot))
+    rowf = L.num_lanes * L.block_size
+    own_rows = int(bounds[own + 1] - bounds[own]) if own >= 0 else 0
+    assert off == (int(bounds[s]) - (own_rows if 0 <= own < s else 0)) * rowf
+    assert tot.value == L.n - own_rows * rowf
+    return off
 
 
 def scan_pack(xd, L, bounds, own, masks_out=None, table_out=None):
@@ -119,7 +133,7 @@ def test_worker_scan_pack(gpu, n, B, density, world, own):
             pos = stream_positions(f, L, S, gps, table, r0, r1)
             places = sorted(p for _, p in pos)
             assert places == list(range(nz)), f"shard {s}: stream places are not a permutation of 0..{nz}"
-            base = r0 * rowf
+            base = send_offset(L, bounds, own, s)
             for blk, p in pos:
                 got = send[base + p * B:base + (p + 1) * B]
                 assert (got.view(np.uint32) == x[blk * B:(blk + 1) * B].view(np.uint32)).all(), (s, blk, p)
@@ -144,7 +158,7 @@ def test_pack_rejects_ragged_shards(gpu):
     (2 << 20, 256, 0.5, 16, 8, False),  # the largest group (OMR_MAX_WORKERS workers)
 ])
 @pytest.mark.parametrize("packed_out", [0, 1])
-def test_shard_sum_cols(gpu, n, B, density, m, naggs, colocated, packed_out):
+def test_shard_sum_list(gpu, n, B, density, m, naggs, colocated, packed_out):
     L = Layout(n=n, block_size=B)
     lib = _lib.load()
     S, gps, ent = geometry(L)
@@ -173,8 +187,7 @@ def test_shard_sum_cols(gpu, n, B, density, m, naggs, colocated, packed_out):
     bdev = torch.from_numpy(bounds.astype(np.int64)).to(gpu)
     counts = torch.zeros((m + 1) * (naggs + 1), dtype=torch.int32, device=gpu)
     rc = lib.omr_round_plan_ex(P(masks_all), m, mstride, rows, L.rows_per_part, L.num_lanes, P(bdev), naggs + 1,
-                               P(wset), P(umask), P(prefix), P(counts), None, None, 0, None, None, 0, None, B,
-                               stream())
+                               P(wset), P(umask), P(prefix), P(counts), None, None, 0, None, 0, None, B, stream())
     assert rc == 0, lib.omr_last_error()
     torch.cuda.synchronize()
     ws_np = wset.cpu().numpy().view(np.uint64)
@@ -189,7 +202,8 @@ def test_shard_sum_cols(gpu, n, B, density, m, naggs, colocated, packed_out):
                 continue
             send, cnt = sends[w]
             offs[w] = k
-            parts.append(send[r0 * rowf:r0 * rowf + int(cnt[s]) * B])
+            base = send_offset(L, bounds, w if colocated else -1, s)
+            parts.append(send[base:base + int(cnt[s]) * B])
             k += int(cnt[s])
         recv = torch.from_numpy(np.concatenate(parts) if parts else np.zeros(B, np.float32)).to(gpu)
         if packed_out:
@@ -198,13 +212,10 @@ def test_shard_sum_cols(gpu, n, B, density, m, naggs, colocated, packed_out):
             out = xds[me].clone() if colocated else torch.zeros(L.n, device=gpu)
         own = xds[me] if colocated else None
         out0 = out.clone()
-        rc = lib.omr_shard_sum_cols_f32(P(own), me, P(recv), offs.ctypes.data_as(ctypes.c_void_p), P(masks_all), m,
-                                        mstride, 2 * rows, P(prefix), P(wset), L.n, B, L.num_lanes, L.num_threads, r0,
-                                        r1, packed_out, P(out), stream())
-        assert rc == 0, lib.omr_last_error()
-        # the same sums through the pair list: built by the plan launch (omr_round_plan_list) and in a launch of its
-        # own (omr_sum_list_build); each must equal the one-kernel form bit for bit
+        # the pair list, built by the plan launch (omr_round_plan_list) and in a launch of its own
+        # (omr_sum_list_build); the sums over each must equal the oracle's bit for bit, and each other
         units, cap = ctypes.c_uint64(), ctypes.c_uint32()
+        outs = []
         assert lib.omr_sum_list_geometry(L.n, B, L.num_lanes, L.num_threads, r0, r1, m, ctypes.byref(units),
                                          ctypes.byref(cap)) == 0, lib.omr_last_error()
         for how in ("plan", "build"):
@@ -216,7 +227,7 @@ def test_shard_sum_cols(gpu, n, B, density, m, naggs, colocated, packed_out):
             if how == "plan":
                 rc = lib.omr_round_plan_list(P(masks_all), m, mstride, rows, L.rows_per_part, L.num_lanes, P(bdev),
                                              naggs + 1, P(wset), P(umask), P(prefix), P(counts), None, None, 0, None,
-                                             None, 0, None, B, ctypes.byref(sl), stream())
+                                             0, None, B, ctypes.byref(sl), stream())
             else:
                 rc = lib.omr_sum_list_build(P(masks_all), m, mstride, L.n, B, L.num_lanes, L.num_threads,
                                             ctypes.byref(sl), stream())
@@ -226,9 +237,9 @@ def test_shard_sum_cols(gpu, n, B, density, m, naggs, colocated, packed_out):
                                             P(wset), P(prefix[m * (rows + 1):]), packed_out, P(out2), stream())
             assert rc == 0, lib.omr_last_error()
             torch.cuda.synchronize()
-            assert torch.equal(out2.view(torch.int32), out.view(torch.int32)), f"shard {s}: pair list ({how})"
-        torch.cuda.synchronize()
-        o = out.cpu().numpy()
+            outs.append(out2)
+        assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)), f"shard {s}: plan vs build list"
+        o = outs[0].cpu().numpy()
         if packed_out:
             blocks = [r * L.num_lanes + ln for r in range(r0, r1) for ln in range(L.num_lanes)
                       if (int(ws_np[r]) >> ln) & 1]

@@ -78,59 +78,19 @@ def test_worker_scan_masks(gpu, n, B, density):
     assert torch.equal(xd, torch.from_numpy(x).to(gpu))  # out = NULL: the tensor is not written
 
 
-@pytest.mark.parametrize("count,rows,rpp,lanes", [(1, 64, 8, 64), (3, 512, 64, 64), (8, 4096, 512, 64),
-                                                   (5, 1280, 256, 16), (16, 100, 25, 32),
-                                                   (2, 8192, 1024, 64), (3, 20480, 2560, 16)])
-def test_round_plan(gpu, count, rows, rpp, lanes):
-    """Rows <= 8192 stay in LDS between the two passes; more are re-read (the last case)."""
-    rng = np.random.default_rng(count * 1000 + rows)
-    lane_mask = (1 << lanes) - 1 if lanes < 64 else (1 << 64) - 1
-    dens = rng.random(count) * 0.5
-    masks = np.zeros((count, rows), dtype=np.uint64)
-    for c in range(count):
-        bits = rng.random((rows, lanes)) < dens[c]
-        masks[c] = (bits.astype(np.uint64) << np.arange(lanes, dtype=np.uint64)).sum(axis=1).astype(np.uint64)
-        masks[c] &= np.uint64(lane_mask)
-    N = max(1, min(count, 8))
-    bounds = np.array([s * rows // N for s in range(N + 1)], dtype=np.uint64)
-    lib = _lib.load()
-    md = torch.from_numpy(masks.view(np.int64)).to(gpu)
-    bd = torch.from_numpy(bounds.view(np.int64)).to(gpu)
-    wset = torch.zeros(rows, dtype=torch.int64, device=gpu)
-    umask = torch.zeros(rows, dtype=torch.int64, device=gpu)
-    prefix = torch.zeros((count + 1) * (rows + 1), dtype=torch.int32, device=gpu)
-    counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int32, device=gpu)
-    zero = torch.full((rows,), -1, dtype=torch.int64, device=gpu)
-    arrive = torch.zeros(1, dtype=torch.int32, device=gpu)
-    done = torch.zeros(1, dtype=torch.int32, device=gpu)
-    for seq in (7, 8):  # the completion notice, twice: the arrival counter re-arms itself
-        assert lib.omr_round_plan(P(md), count, rows, rpp, lanes, P(bd), N + 1, P(wset), P(umask), P(prefix),
-                                  P(counts), P(zero), P(arrive), P(done), seq, stream()) == 0, lib.omr_last_error()
-        torch.cuda.synchronize()
-        assert int(done.item()) == seq and int(arrive.item()) == 0
-    u, w = np_write_set(masks, rpp, lanes)
-    assert (umask.cpu().numpy().view(np.uint64) == u).all()
-    assert (wset.cpu().numpy().view(np.uint64) == w).all()
-    pre = prefix.cpu().numpy().view(np.uint32).reshape(count + 1, rows + 1)
-    cn = counts.cpu().numpy().view(np.uint32).reshape(count + 1, N + 1)
-    for a in range(count + 1):
-        exp = np_prefix(masks[a] if a < count else w)
-        assert (pre[a] == exp).all(), a
-        assert (cn[a] == exp[bounds.astype(np.int64)]).all(), a
-    assert int(zero.count_nonzero()) == 0
-
-
 @pytest.mark.parametrize("count,rows,rpp,lanes,stride_pad", [
     (1, 64, 8, 64, 0), (3, 512, 64, 64, 5), (8, 4096, 512, 64, 1024), (5, 1280, 256, 16, 0), (16, 100, 25, 32, 3),
-    (2, 8192, 1024, 64, 0), (7, 16384, 2048, 16, 0),   # 64 chunks: the row-chunk form's largest plan
-    (3, 20480, 2560, 16, 0),                           # more rows: the one-workgroup-per-array form, workspace[0]
-    (8, 300, 30, 64, 7),                               # a partial last chunk
+    (2, 8192, 1024, 64, 0),                           # two 4096-row tiles
+    (7, 16384, 2048, 16, 0),                          # eight 2048-row tiles (W = 8, R = 2)
+    (3, 20480, 2560, 16, 0),                          # five tiles
+    (8, 300, 30, 64, 7),                              # a partial tile
+    (16, 5000, 1000, 64, 0),                          # W = 16, R = 1: five 1024-row tiles, the last partial
 ])
-def test_round_plan_ws(gpu, count, rows, rpp, lanes, stride_pad):
-    """omr_round_plan_ws (round 4: 256-thread workgroups over row chunks of every array, chunk totals published and
-    summed by their successors) against numpy: union, write set, every array's prefix, the counts at the shard
-    bounds, the zeroed own masks and pack counters, the aggregator chain, and the completion notice three times in a
-    row with the workspace left zeroed after each."""
+def test_round_plan(gpu, count, rows, rpp, lanes, stride_pad):
+    """omr_round_plan_list (round 5: ONE 1024-thread workgroup, every mask read once, row tiles of 1024 * R, DPP wave
+    scans) against numpy: union, write set, every array's prefix, the counts at the shard bounds, the zeroed own masks
+    and pack counters, the aggregator chain, and the completion notice three times in a row; worker arrays at a stride
+    whose tail (a position table) is not read as masks."""
     rng = np.random.default_rng(count * 31 + rows)
     stride = rows + stride_pad
     dens = rng.random(count) * 0.5
@@ -140,11 +100,10 @@ def test_round_plan_ws(gpu, count, rows, rpp, lanes, stride_pad):
         bits = rng.random((rows, lanes)) < dens[c]
         masks[c, :rows] = (bits.astype(np.uint64) << np.arange(lanes, dtype=np.uint64)).sum(axis=1).astype(np.uint64)
         masks[c, :rows] &= lane_mask
-        masks[c, rows:] = np.uint64(0xDEADBEEF)  # whatever follows the rows (a position table) is not read as masks
+        masks[c, rows:] = np.uint64(0xDEADBEEF)
     N = max(1, min(count, 8))
     bounds = np.array([s * rows // N for s in range(N + 1)], dtype=np.uint64)
     lib = _lib.load()
-    words = lib.omr_round_plan_workspace_words()
     md = torch.from_numpy(masks.reshape(-1).view(np.int64)).to(gpu)
     bd = torch.from_numpy(bounds.view(np.int64)).to(gpu)
     wset = torch.zeros(rows, dtype=torch.int64, device=gpu)
@@ -153,19 +112,19 @@ def test_round_plan_ws(gpu, count, rows, rpp, lanes, stride_pad):
     counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int32, device=gpu)
     zero = torch.full((rows,), -1, dtype=torch.int64, device=gpu)
     zc = torch.full((8,), -1, dtype=torch.int32, device=gpu)
-    ws = torch.zeros(words, dtype=torch.int32, device=gpu)
     done = torch.zeros(1, dtype=torch.int32, device=gpu)
     B = 16384 // lanes
     unext = torch.full((rows * lanes,), -1, dtype=torch.int32, device=gpu)
     for seq in (7, 8, 9):
         prefix.zero_()
-        assert lib.omr_round_plan_ws(P(md), count, stride, rows, rpp, lanes, P(bd), N + 1, P(wset), P(umask),
-                                     P(prefix), P(counts), P(zero), P(zc), 8, P(ws), P(done), seq, P(unext), B, None,
-                                     stream()) == 0, lib.omr_last_error()
+        umask.zero_()
+        assert lib.omr_round_plan_list(P(md), count, stride, rows, rpp, lanes, P(bd), N + 1, P(wset),
+                                       P(umask) if seq != 8 else None, P(prefix), P(counts), P(zero), P(zc), 8,
+                                       P(done), seq, P(unext), B, None, stream()) == 0, lib.omr_last_error()
         torch.cuda.synchronize()
         assert int(done.item()) == seq
-        # the whole workspace is zero again (counters, and the totals, which double as their flags)
-        assert int(ws.count_nonzero()) == 0, "workspace not re-armed"
+        if seq == 8:
+            assert int(umask.count_nonzero()) == 0  # no union_masks asked for: not written
     mr = masks[:, :rows]
     u, w = np_write_set(mr, rpp, lanes)
     assert (umask.cpu().numpy().view(np.uint64) == u).all()
@@ -180,6 +139,28 @@ def test_round_plan_ws(gpu, count, rows, rpp, lanes, stride_pad):
     flags = ((u[:, None] >> np.arange(lanes, dtype=np.uint64)) & np.uint64(1)).astype(np.int32).ravel()
     exp = oracle.next_offsets(flags, rows * lanes * B, B, lanes, rows // rpp)
     assert (unext.cpu().numpy().view(np.uint32) == exp).all()
+
+
+def test_round_plan_counts_past_the_end(gpu):
+    """Shard bounds that repeat (empty shards) and bounds at the end: every count = the prefix at its bound."""
+    rows, lanes, rpp, count = 2048, 64, 256, 3
+    rng = np.random.default_rng(5)
+    masks = (rng.integers(0, 2 ** 63, size=(count, rows), dtype=np.int64)).view(np.uint64)
+    bounds = np.array([0, 512, 512, 1500, 2048, 2048], dtype=np.uint64)
+    lib = _lib.load()
+    md = torch.from_numpy(masks.reshape(-1).view(np.int64)).to(gpu)
+    bd = torch.from_numpy(bounds.view(np.int64)).to(gpu)
+    wset = torch.zeros(rows, dtype=torch.int64, device=gpu)
+    prefix = torch.zeros((count + 1) * (rows + 1), dtype=torch.int32, device=gpu)
+    counts = torch.full(((count + 1) * len(bounds),), -1, dtype=torch.int32, device=gpu)
+    assert lib.omr_round_plan_list(P(md), count, rows, rows, rpp, lanes, P(bd), len(bounds), P(wset), None, P(prefix),
+                                   P(counts), None, None, 0, None, 0, None, 64, None, stream()) == 0, lib.omr_last_error()
+    torch.cuda.synchronize()
+    _, w = np_write_set(masks, rpp, lanes)
+    cn = counts.cpu().numpy().view(np.uint32).reshape(count + 1, len(bounds))
+    for a in range(count + 1):
+        exp = np_prefix(masks[a] if a < count else w)
+        assert (cn[a] == exp[bounds.astype(np.int64)]).all(), a
 
 
 @pytest.mark.parametrize("count,rows,rpp,lanes", [(1, 64, 8, 64), (3, 512, 64, 64), (8, 4096, 512, 64),
@@ -207,7 +188,7 @@ def test_round_plan_chain(gpu, count, rows, rpp, lanes):
         counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int32, device=gpu)
         unext = torch.full((rows * lanes,), -1, dtype=torch.int32, device=gpu)
         assert lib.omr_round_plan_chain(P(md), count, rows, rpp, lanes, P(bd), N + 1, P(wset), P(umask), P(prefix),
-                                        P(counts), None, None, None, 0, P(unext) if chain else None, B,
+                                        P(counts), None, None, 0, P(unext) if chain else None, B,
                                         stream()) == 0, lib.omr_last_error()
         torch.cuda.synchronize()
         outs.append((wset.cpu(), umask.cpu(), prefix.cpu(), counts.cpu(), unext.cpu()))

@@ -20,7 +20,8 @@ def test_product_kernels_have_no_study_knobs():
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
-@pytest.mark.parametrize("name", ["fused_r02", "round_r02", "scanm_r02", "fused_variants"])
+@pytest.mark.parametrize("name", ["fused_r02", "round_r02", "scanm_r02", "fused_variants", "plan_r04", "shard_r04",
+                                  "shard_r03"])
 def test_tune_harness_builds(tmp_path, name):
     out = str(tmp_path / f"{name}.o")
     p = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O1", "-std=c++17", "-fPIC", "-c",

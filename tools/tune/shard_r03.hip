@@ -2,13 +2,12 @@
 // kernel with a window of PP/VEC pair slots (the product's PP is 32) and, with STAMP, per-wave s_memrealtime stamps
 // {start, index data consumed, pair list written, first window summed, end with stores acknowledged, units, XCC} so the
 // phases of a unit can be seen.  Built from the product source's kernel text (copied here when the study was made).
-#define OMR_NO_CAPI
-#include "../../omnireduce-rdma-demo_amd/csrc/omr_kernels.hip"
+#include "plan_r04.hip"  // (the product kernels + the round-4 SumArgsR04 with its column-stream fields)
 
 namespace {
 constexpr uint32_t kR03UnitRows = 32;  // round 3's unit (the product's kSumUnitRows has changed since)
 template <int VEC, int PP, int STAMP>
-__global__ __launch_bounds__(kWGThreads) void k_shard_sum_s(SumArgs a, uint64_t* tl) {
+__global__ __launch_bounds__(kWGThreads) void k_shard_sum_s(SumArgsR04 a, uint64_t* tl) {
   constexpr int P = PP / VEC;  // pair slots per window
   constexpr int kSlotGroup = P < 8 ? P : 8;
   constexpr uint32_t kRecCap = kR03UnitRows * OMR_MAX_WORKERS;
@@ -177,7 +176,7 @@ int tune_shard(int v, int stamp, const float* own, uint32_t me, const float* rec
                const uint64_t* masks, uint32_t count, uint64_t mstride, uint64_t pos_off, const uint32_t* prefix,
                const uint64_t* write_set, uint64_t rows, uint64_t r0, uint64_t r1, uint32_t lanes, uint32_t S,
                uint32_t gps, float* out, uint64_t* tl, unsigned grid, hipStream_t st) {
-  SumArgs a{};
+  SumArgsR04 a{};
   a.own = own; a.recv = recv; a.masks = masks; a.mstride = mstride; a.prefix = prefix; a.pos_off = pos_off;
   a.write_set = write_set; a.out = out; a.rows = rows; a.r0 = r0; a.r1 = r1; a.count = count; a.me = me;
   a.lanes = lanes; a.block = 256; a.packed_out = 0; a.S = S; a.gps = gps;

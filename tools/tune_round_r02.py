@@ -56,7 +56,7 @@ def setup(L, m, naggs, dev, stream):
     counts = torch.empty((m + 1, naggs + 1), dtype=torch.int32, device=dev)
     _lib.check(lib.omr_round_plan(masks.data_ptr(), m, L.rows, L.rows_per_part, L.num_lanes, bdev.data_ptr(),
                                   naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(), counts.data_ptr(),
-                                  None, None, None, 0, stream), "omr_round_plan")
+                                  None, None, 0, stream), "omr_round_plan")
     torch.cuda.synchronize()
     cnt = counts.cpu().numpy().astype(np.int64)
     r0, r1 = bounds[0], bounds[1]

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Round 3: the multi-rank round's worker and aggregator kernels at config-4 shapes on one MI355X (8 workers x 256 MiB,
--r 0.095, seeds 1..8; rank 0's view: worker 0 and aggregator of shard 0 of 8).
+"""Rounds 3-5: the multi-rank round's worker and aggregator kernels at config-4 shapes on one MI355X (8 workers x 256 MiB,
+-r 0.095, seeds 1..8; rank 0's view: worker 0 and aggregator of shard 0 of 8).  Forms that lost (round 4's row-chunk
+plan, round 3's column-stream shard sum, the round-3/4 plan) come from tools/tune/plan_r04.hip (built on first use).
 
 Worker side, per launch (algorithmic bytes in brackets):
   scan       omr_worker_scan_f32             [S + nb*8 + rows*8]
@@ -84,7 +85,7 @@ def setup(a):
     bdev = torch.from_numpy(bounds.astype(np.int64)).to(dev)
     _lib.check(lib.omr_round_plan_ex(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
                                      naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
-                                     counts.data_ptr(), None, None, 0, None, None, 0, None, B, st), "plan")
+                                     counts.data_ptr(), None, None, 0, None, 0, None, B, st), "plan")
     # the round-2 layout: masks [m][rows] contiguous, row-ordered streams packed by k_move
     masks = torch.stack([masks_all[w * mstride:w * mstride + rows] for w in range(m)]).contiguous()
     torch.cuda.synchronize()
@@ -110,10 +111,33 @@ def setup(a):
                 acc=acc, recv_c=recv_c, recv_r=recv_r, S=S_.value, gps=gps.value, dev=dev, st=st)
 
 
+TUNE_SRC = os.path.join(ROOT, "tools", "tune", "plan_r04.hip")
+TUNE_LIB = os.path.join(ROOT, "gpurun_out", "tune", "libplan_r04.so")
+
+
+def load_r04():
+    """tools/tune/plan_r04.hip (the losing forms, kept for A/B), compiled on first use."""
+    import subprocess
+    if not os.path.exists(TUNE_LIB) or os.path.getmtime(TUNE_LIB) < os.path.getmtime(TUNE_SRC):
+        os.makedirs(os.path.dirname(TUNE_LIB), exist_ok=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                        "-I" + os.path.join(ROOT, "include"), "-o", TUNE_LIB, TUNE_SRC], check=True)
+    t = ctypes.CDLL(TUNE_LIB)
+    vp, u64, u32, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    plan_args = [vp, u32, u64, u64, u32, u32, vp, u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, u32, vp, u32, vp, vp]
+    t.tune_round_plan_list_r04.argtypes = plan_args
+    t.tune_round_plan_ws_r04.argtypes = plan_args
+    t.tune_round_plan_workspace_words_r04.restype = u64
+    t.tune_shard_sum_cols_r04.argtypes = [vp, u32, vp, vp, vp, u32, u64, u64, vp, vp, u64, u32, u32, u32, u64, u64, i,
+                                          vp, vp]
+    return t
+
+
 def main():
     a = parser().parse_args()
     torch.cuda.init()
     tl = r02.load()
+    t4 = load_r04()
     lib = _lib.load()
     print("# setting up config 4's shapes", flush=True)
     D = setup(a)
@@ -136,8 +160,8 @@ def main():
         return lib.omr_shard_sum_f32(xs[0].data_ptr(), 0, recv_r.data_ptr(), roff_c, masks.data_ptr(), m,
                                      prefix.data_ptr(), wset.data_ptr(), rows, r0, r1, NB, B, 0, out.data_ptr(), st)
 
-    def sum_cols(out):
-        return lib.omr_shard_sum_cols_f32(xs[0].data_ptr(), 0, recv_c.data_ptr(), roff_c, masks_all.data_ptr(), m,
+    def sum_cols(out):  # round 3's column-stream sum (tools/tune/plan_r04.hip)
+        return t4.tune_shard_sum_cols_r04(xs[0].data_ptr(), 0, recv_c.data_ptr(), roff_c, masks_all.data_ptr(), m,
                                           mstride, 2 * rows, prefix.data_ptr(), wset.data_ptr(), L.n, B, NB,
                                           L.num_threads, r0, r1, 0, out.data_ptr(), st)
 
@@ -170,7 +194,7 @@ def main():
         return run
 
     sums = {"round-2 k_shard_sum (rows)": sum_r02, "product k_shard_sum (rows)": sum_rows,
-            "product k_shard_sum (cols)": sum_cols, "product k_shard_sum_list (pairs from the plan)": sum_list}
+            "round-3 k_shard_sum (cols)": sum_cols, "product k_shard_sum_list (pairs from the plan)": sum_list}
     ref = None
     for name, fn in sums.items():
         o = xs[0].clone()
@@ -203,53 +227,80 @@ def main():
 
     unext = torch.empty(L.nb, dtype=torch.int32, device=dev)
 
-    def plan():  # the round's bookkeeping launch: union, write set, prefixes, counts, aggregator chain
+    # the round's own setting: counts into pinned host memory (system-scope stores), the completion notice posted, the
+    # own masks and pack counters cleared (scratch copies here), the pair list, no chain (bench asks for no union_next)
+    pin = torch.zeros(4096, dtype=torch.int32).pin_memory()
+    pin_d = ctypes.c_void_p()
+    assert ctypes.CDLL("libamdhip64.so").hipHostGetDevicePointer(ctypes.byref(pin_d), ctypes.c_void_p(pin.data_ptr()),
+                                                                 0) == 0
+    cnt_d, flag_d = pin_d.value, pin_d.value + 4 * 2048
+    zmask = torch.empty(rows, dtype=torch.int64, device=dev)
+    zcnt = torch.empty(naggs, dtype=torch.int32, device=dev)
+    arrive = torch.zeros(1, dtype=torch.int32, device=dev)
+    seqs = [0]
+
+    def plan():  # the round's bookkeeping launch: write set, union, prefixes, counts, aggregator chain
         return lib.omr_round_plan_ex(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
                                      naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
-                                     counts.data_ptr(), None, None, 0, None, None, 0, unext.data_ptr(), B, st)
+                                     counts.data_ptr(), None, None, 0, None, 0, unext.data_ptr(), B, st)
 
     def plan_list():  # ... with shard 0's pair list built by the same launch (the round since round 3)
         return lib.omr_round_plan_list(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
                                        naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
-                                       counts.data_ptr(), None, None, 0, None, None, 0, unext.data_ptr(), B,
+                                       counts.data_ptr(), None, None, 0, None, 0, unext.data_ptr(), B,
                                        ctypes.byref(sl), st)
 
-    pws = torch.zeros(lib.omr_round_plan_workspace_words(), dtype=torch.int32, device=dev)
+    def plan_round():  # exactly the round's call (round 5's single-workgroup plan)
+        seqs[0] += 1
+        return lib.omr_round_plan_list(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                       naggs + 1, wset.data_ptr(), None, prefix.data_ptr(), cnt_d, zmask.data_ptr(),
+                                       zcnt.data_ptr(), naggs, flag_d, seqs[0], None, B, ctypes.byref(sl), st)
 
-    def plan_ws():  # round 4's row-chunk form (omr_round_plan_ws), the round's plan with the fused pack
-        return lib.omr_round_plan_ws(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
-                                     naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
-                                     counts.data_ptr(), None, None, 0, pws.data_ptr(), None, 0, unext.data_ptr(), B,
-                                     None, st)
+    def plan_round_r04():  # the same call to the round-3/4 plan (one workgroup per mask array, arrival counter)
+        seqs[0] += 1
+        return t4.tune_round_plan_list_r04(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB,
+                                           bdev.data_ptr(), naggs + 1, wset.data_ptr(), umask.data_ptr(),
+                                           prefix.data_ptr(), cnt_d, zmask.data_ptr(), zcnt.data_ptr(), naggs,
+                                           arrive.data_ptr(), flag_d, seqs[0], None, B, ctypes.byref(sl), st)
 
-    def plan_nochain():  # the plan without the aggregator chain (round 3's form)
+    pws = torch.zeros(t4.tune_round_plan_workspace_words_r04(), dtype=torch.int32, device=dev)
+
+    def plan_ws():  # round 4's row-chunk form, the round's plan with the fused pack (tools/tune/plan_r04.hip)
+        return t4.tune_round_plan_ws_r04(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                         naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                         counts.data_ptr(), None, None, 0, pws.data_ptr(), None, 0, unext.data_ptr(),
+                                         B, None, st)
+
+    def plan_nochain():  # the plan without the aggregator chain
         return lib.omr_round_plan_ex(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
                                      naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
-                                     counts.data_ptr(), None, None, 0, None, None, 0, None, B, st)
+                                     counts.data_ptr(), None, None, 0, None, 0, None, B, st)
+
+    def plan_nochain_r04():  # the round-3/4 plan without the chain
+        return t4.tune_round_plan_list_r04(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB,
+                                           bdev.data_ptr(), naggs + 1, wset.data_ptr(), umask.data_ptr(),
+                                           prefix.data_ptr(), counts.data_ptr(), None, None, 0, None, None, 0, None, B,
+                                           None, st)
 
     def plan_ws_nochain():  # the row-chunk form without the chain
-        return lib.omr_round_plan_ws(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
-                                     naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
-                                     counts.data_ptr(), None, None, 0, pws.data_ptr(), None, 0, None, B, None, st)
+        return t4.tune_round_plan_ws_r04(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                         naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                         counts.data_ptr(), None, None, 0, pws.data_ptr(), None, 0, None, B, None, st)
 
     def list_only():  # the pair list in a launch of its own
         return lib.omr_sum_list_build(masks_all.data_ptr(), m, mstride, L.n, B, NB, L.num_threads, ctypes.byref(sl),
                                       st)
 
-    def scan_pack16(i=0):  # OMR_PACK_WAVES=16: one 16-wave workgroup per CU (the product until round 3's 2nd session)
-        os.environ["OMR_PACK_WAVES"] = "16"
-        try:
-            return scan_pack(i)
-        finally:
-            del os.environ["OMR_PACK_WAVES"]
-
     workers = {"scan (omr_worker_scan_f32)": scan, "scan + fused pack (product)": scan_pack,
-               "scan + fused pack (16-wave workgroups)": scan_pack16,
                "pack pass (k_move, round 2)": pack, "round plan + chain (k_round_plan)": plan,
                "round plan + chain, row chunks (k_round_plan2)": plan_ws,
                "round plan, no chain (k_round_plan)": plan_nochain,
+               "round plan, no chain (round-3/4 k_round_plan_r04)": plan_nochain_r04,
                "round plan, no chain, row chunks (k_round_plan2)": plan_ws_nochain,
-               "round plan + chain + pair list": plan_list, "pair list alone (k_sum_list)": list_only}
+               "round plan + chain + pair list": plan_list,
+               "round plan as the round calls it (pair list, pinned counts, notice)": plan_round,
+               "round plan as the round calls it, round-3/4 form": plan_round_r04,
+               "pair list alone (k_sum_list)": list_only}
     cases = {**sums, **workers}
     if a.only:
         cases = {k: v for k, v in cases.items() if a.only in k}
@@ -265,7 +316,7 @@ def main():
             for i in range(a.reps):
                 if name in sums:
                     fn(outs[i % 2])
-                elif fn is scan_pack or fn is scan_pack16:
+                elif fn is scan_pack:
                     fn(i)
                 else:
                     fn()
@@ -282,7 +333,6 @@ def main():
     scan_b = L.nbytes + L.nb * 8 + rows * 8
     table_b = ent * 4 * (naggs - 1) // naggs
     wbytes = {"scan (omr_worker_scan_f32)": scan_b, "scan + fused pack (product)": scan_b + other * B * 4 + table_b,
-              "scan + fused pack (16-wave workgroups)": scan_b + other * B * 4 + table_b,
               "pack pass (k_move, round 2)": 2 * other * B * 4,
               # reads every worker's masks; writes write set, union, m + 1 prefix arrays, counts, the union chain
               "round plan + chain (k_round_plan)": m * rows * 8 + 2 * rows * 8 + (m + 1) * (rows + 1) * 4 +
@@ -294,6 +344,12 @@ def main():
     wbytes["round plan + chain, row chunks (k_round_plan2)"] = wbytes["round plan + chain (k_round_plan)"]
     wbytes["round plan, no chain (k_round_plan)"] = wbytes["round plan + chain (k_round_plan)"] - L.nb * 4
     wbytes["round plan, no chain, row chunks (k_round_plan2)"] = wbytes["round plan, no chain (k_round_plan)"]
+    wbytes["round plan, no chain (round-3/4 k_round_plan_r04)"] = wbytes["round plan, no chain (k_round_plan)"]
+    # the round's call: no union stored, no chain; its own masks cleared (rows words), the pair list
+    wbytes["round plan as the round calls it (pair list, pinned counts, notice)"] = (
+        m * rows * 8 + rows * 8 + (m + 1) * (rows + 1) * 4 + rows * 8 + lbytes)
+    wbytes["round plan as the round calls it, round-3/4 form"] = (
+        wbytes["round plan as the round calls it (pair list, pinned counts, notice)"] + rows * 8)  # (+ its union)
     wbytes["pair list alone (k_sum_list)"] = lbytes
     report = {}
     print(f"## config 4 shapes, {m} workers, -r {a.density}: shard 0 write set {ub} blocks, received {nc}, own {own_blocks}: "
