@@ -266,43 +266,36 @@ uint64_t omr_pack_send_offset(const uint64_t* shard_bounds, uint32_t num_shards,
  *                    the aggregators return (lane heads are always sent: client.cc:201-205);
  *   prefix[a*(rows+1) + r] = set bits of array a in rows [0, r), for a < count (workers) and a == count (the
  *                    write set); r = rows gives the total;
- *   counts[a*num_bounds + s] = prefix[a][bounds[s]] (bounds: device uint64[num_bounds], each <= rows);
+ *   counts[a*num_bounds + s] = (seq << 32) | prefix[a][bounds[s]] (bounds: device uint64[num_bounds], each <= rows),
+ *                    stored at system scope: counts may be pinned host memory (mapped), and a host that polls them
+ *                    until every one it needs carries `seq` has them without synchronising the stream (the
+ *                    multi-rank round does);
  *   zero_masks (device uint64[rows] or NULL) is cleared (the next round's omr_worker_scan_f32 target);
  *   union_masks may be NULL (not stored).
- * Completion notice (done_flag non-NULL): once every count is visible system-wide, *done_flag = seq.  done_flag may
- * be pinned host memory (mapped), so a host can poll it instead of synchronising the stream (the multi-rank round
- * does).  One 1024-thread workgroup does all of it, every mask read once (ABI 2; ABI 1 took an arrival counter). */
+ * workspace: device uint64[omr_round_plan_workspace_words()], zero-filled before its first launch and left to the
+ * plan between launches (the kernel re-arms it); launches sharing a workspace run in stream order.  seq != 0 and
+ * differs from the previous launch's on the same workspace and counts.  Row chunks of the launch run side by side
+ * and hand each other their popcount totals through the workspace (ABI 2; ABI 1 took an arrival counter). */
+uint64_t omr_round_plan_workspace_words(void);
 int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                    uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
-                   uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                   uint32_t* done_flag, uint32_t seq, omr_stream_t stream);
-/* omr_round_plan plus, in the same launch, the aggregator chain (server.cc:86-96: min_next over the workers =
- * next offsets over the union) into union_next (device uint32[rows * num_lanes], the omr_next_offsets layout of
- * the union masks), computed by extra workgroups from the workers' masks directly.  union_next NULL: exactly
- * omr_round_plan. */
-int omr_round_plan_chain(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
-                         uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
-                         uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                         uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                         omr_stream_t stream);
-/* omr_round_plan_chain with worker c's masks at row_masks + c * mask_stride (mask_stride >= rows: the all-gathered
- * arrays of the fused pack carry each worker's position table after its masks), and zero_counters (device
- * uint32[num_zero_counters <= 1024], or NULL) cleared: the next round's pack counters. */
-int omr_round_plan_ex(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
-                      uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
-                      uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* done_flag,
-                      uint32_t seq, uint32_t* union_next, uint32_t block_size, omr_stream_t stream);
+                   uint64_t* union_masks, uint32_t* prefix, uint64_t* counts, uint64_t* zero_masks,
+                   uint64_t* workspace, uint32_t seq, omr_stream_t stream);
 struct omr_sum_list;
-/* omr_round_plan_ex plus, by further workgroups of the same launch, an aggregator's shard-sum pair list
- * (omr_sum_list below; NULL: none), over column streams of the layout (rows * num_lanes * block_size floats,
- * rows / rows_per_part partitions). */
+/* omr_round_plan with worker c's masks at row_masks + c * mask_stride (mask_stride >= rows: the all-gathered arrays
+ * of the fused pack carry each worker's position table after its masks), plus, in the same launch:
+ *   zero_counters (device uint32[num_zero_counters <= 256], or NULL) cleared: the next round's pack counters;
+ *   union_next (device uint32[rows * num_lanes], or NULL): the aggregator chain (server.cc:86-96: min_next over
+ *     the workers = next offsets over the union, the omr_next_offsets layout of the union masks), computed by
+ *     extra workgroups from the workers' masks directly;
+ *   list (or NULL): an aggregator's shard-sum pair list (omr_sum_list below) over the layout (rows * num_lanes *
+ *     block_size floats, rows / rows_per_part partitions). */
 int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
                         uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
-                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* done_flag,
-                        uint32_t seq, uint32_t* union_next, uint32_t block_size, const struct omr_sum_list* list,
-                        omr_stream_t stream);
+                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint64_t* counts,
+                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters,
+                        uint64_t* workspace, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                        const struct omr_sum_list* list, omr_stream_t stream);
 
 /* Block movement addressed by a row mask and its prefix (no block list): the k-th set bit of `row_masks` over
  * rows [0, rows) minus [skip_begin, skip_end) is block k of the packed stream.

@@ -857,23 +857,30 @@ struct IpcDist final : omr_dist {
   }
 };
 
-// Spin until the plan kernel's completion notice (the round's sequence number) lands in pinned memory: the host
-// learns the block counts about a microsecond after the kernel ends, without an event or a stream sync.  Bails
-// out if the stream drains without the notice (a failed launch), on the transport's group-wide failure signals
-// (RCCL's asynchronous errors, a peer's abort) and after the transport's deadline (a stuck or dead peer: the mask
-// all-gather before the plan never completes); the transport is then aborted, so no peer waits on this rank.
-int wait_flag(omr_dist* d, const uint32_t* flag, uint32_t seq, hipStream_t st) {
+// Spin until every one of the plan kernel's `n` counts in pinned memory carries the round's sequence number (each is
+// one 64-bit store, (seq << 32) | count): the host learns the block counts about a microsecond after the kernel stores
+// them, without an event, a stream sync or a completion notice.  Bails out if the stream drains with a count still
+// stale (a failed launch), on the transport's group-wide failure signals (RCCL's asynchronous errors, a peer's abort)
+// and after the transport's deadline (a stuck or dead peer: the mask all-gather before the plan never completes); the
+// transport is then aborted, so no peer waits on this rank.  out[i] = the counts.
+int wait_counts(omr_dist* d, const uint64_t* counts, uint32_t n, uint32_t seq, hipStream_t st, uint32_t* out) {
   const auto t0 = std::chrono::steady_clock::now();
+  uint32_t i = 0;
   for (uint64_t spin = 1;; ++spin) {
-    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return 0;
+    for (; i < n; ++i) {
+      const uint64_t v = __atomic_load_n(counts + i, __ATOMIC_ACQUIRE);
+      if (static_cast<uint32_t>(v >> 32) != seq) break;
+      out[i] = static_cast<uint32_t>(v);
+    }
+    if (i == n) return 0;
     if ((spin & 4095) == 0) {
       const hipError_t q = hipStreamQuery(st);
       if (q != hipSuccess && q != hipErrorNotReady) return d->contain(hip_check(q, "round plan"));
-      if (q == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq)
-        return d->contain(derr(OMR_EINVAL, "round plan: stream idle but no completion notice (seq %u)", seq));
+      if (q == hipSuccess && static_cast<uint32_t>(__atomic_load_n(counts + i, __ATOMIC_ACQUIRE) >> 32) != seq)
+        return d->contain(derr(OMR_EINVAL, "round plan: stream idle but count %u stale (seq %u)", i, seq));
       TRY(d->poll());
       if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(d->timeout_ms))
-        return d->contain(derr(OMR_ETIMEDOUT, "round plan: rank %d had no completion notice after %lld ms (seq %u): "
+        return d->contain(derr(OMR_ETIMEDOUT, "round plan: rank %d had no counts after %lld ms (seq %u): "
                                               "a peer is stuck or gone", d->rank,
                                static_cast<long long>(d->timeout_ms), seq));
     }
@@ -984,6 +991,7 @@ struct omr_ar_plan {
     uint32_t* pack_cnt = nullptr;   // fused pack: [A] the scan's per-shard stream counters (the plan re-zeroes them)
     uint64_t* wset = nullptr;       // [rows] write set: union + lane heads
     uint32_t* prefix = nullptr;     // [N+1][rows+1] popcount prefixes: workers, then the write set
+    uint64_t* plan_ws = nullptr;    // the plan kernel's workspace (its row chunks' totals; zeroed once, self-resetting)
     uint64_t* list_rec = nullptr;   // sum list: the shard sum's pair records, built by the plan launch
     uint32_t* list_cnt = nullptr;   //   and their count per unit
     hipEvent_t scanned = nullptr;   // async: recorded on the caller's stream after the worker scan
@@ -1016,16 +1024,15 @@ struct omr_ar_plan {
   hipStream_t cs = nullptr;
   hipStream_t tail = nullptr;       // the stream of the last asynchronous round's last work (the bucket write-back)
   uint64_t* bounds_dev = nullptr;
-  uint32_t* counts_host = nullptr;  // [kSets][M+1][A+1] per set: prefix[a][bounds[s]], pinned memory the plan kernel writes
-  uint32_t* counts_map = nullptr;   // its device-side address
+  uint64_t* counts_host = nullptr;  // [kSets][M+1][A+1] per set: (seq << 32) | prefix[a][bounds[s]], pinned memory the
+                                    // plan kernel writes
+  uint64_t* counts_map = nullptr;   // its device-side address
   float* results = nullptr;  // an aggregator's own shard sums, write-set order (all-reduce, dedicated aggregators)
   uint64_t last_sums_blocks = 0;  // a dedicated aggregator: blocks of its last round's shard sums in `results`
   int32_t* flags_ws = nullptr;
   uint32_t* next_ws = nullptr;
   void* scan_ws = nullptr;   // omr_worker_scan_f32 segment workspace (zeroed once, self-resetting)
   size_t scan_ws_bytes = 0;
-  uint32_t* flag_host = nullptr;  // [kSets] pinned, per set: the plan kernel stores the round's sequence number here
-  uint32_t* flag_map = nullptr;   // its device-side address
   uint32_t seq = 0;
   // The one-rank round (world 1, one worker = its own aggregator; omr_worker_scan_tally_f32): the bookkeeping is two
   // counts, tallied by the scan's workgroups and published by the NEXT round's scan (one extra workgroup), so a
@@ -1355,7 +1362,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   for (void* v : devs) p->d->release(v);
   for (auto& b : p->pk) p->d->release(b.buf);
   for (auto& st : p->set) {
-    void* sv[] = {st.own, st.masks_all, st.wset, st.prefix, st.pack_cnt, st.list_rec, st.list_cnt};
+    void* sv[] = {st.own, st.masks_all, st.wset, st.prefix, st.plan_ws, st.pack_cnt, st.list_rec, st.list_cnt};
     for (void* v : sv) p->d->release(v);
     for (hipEvent_t e : {st.scanned, st.ready, st.done})
       if (e) (void)hipEventDestroy(e);
@@ -1374,7 +1381,6 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     for (hipEvent_t e : {t.s0, t.s1, t.x0, t.x1, t.q0, t.q1, t.a1})
       if (e) (void)hipEventDestroy(e);
   (void)hipHostFree(p->counts_host);
-  (void)hipHostFree(p->flag_host);
   (void)hipHostFree(p->pub_host);
   delete p;
   return 0;
@@ -1451,6 +1457,7 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     if (p->fused_pack) A(dev_alloc(p->d, &st.pack_cnt, NA, DB));
     A(dev_alloc(p->d, &st.wset, p->rows, DB));
     A(dev_alloc(p->d, &st.prefix, static_cast<size_t>(M + 1) * (p->rows + 1), DB));
+    A(dev_alloc(p->d, &st.plan_ws, omr_round_plan_workspace_words(), DB));
     if (p->sum_list) {
       A(dev_alloc(p->d, &st.list_rec, p->list_units * p->list_cap, DB));
       A(dev_alloc(p->d, &st.list_cnt, p->list_units, DB));
@@ -1483,16 +1490,12 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   p->tally_slots = omr_tally_slots(n, block_size, num_lanes, num_parts);
   A(dev_alloc(p->d, &p->tally, static_cast<size_t>(p->tally_slots) * omr_ar_plan::kSets, DB));
   constexpr int NSETS = omr_ar_plan::kSets;
-  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), NSETS * (M + 1) * (NA + 1) * sizeof(uint32_t),
-                            hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
-  if (rc == 0)
-    A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->counts_map), p->counts_host, 0),
-                "hipHostGetDevicePointer"));
-  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->flag_host), NSETS * sizeof(uint32_t),
+  const size_t ncounts = static_cast<size_t>(NSETS) * (M + 1) * (NA + 1);
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), ncounts * sizeof(uint64_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0) {
-    for (int i = 0; i < NSETS; ++i) p->flag_host[i] = 0;
-    A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->flag_map), p->flag_host, 0),
+    for (size_t i = 0; i < ncounts; ++i) p->counts_host[i] = 0;  // (tag 0: no round's)
+    A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->counts_map), p->counts_host, 0),
                 "hipHostGetDevicePointer"));
   }
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->pub_host), NSETS * 4 * sizeof(uint32_t),
@@ -1505,6 +1508,8 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   for (int i = 0; i < p->nsets && rc == 0; ++i) {
     omr_ar_plan::Set& st = p->set[i];
     A(hip_check(hipMemset(st.own, 0, p->mstride * sizeof(uint64_t)), "hipMemset own masks"));
+    if (rc == 0)
+      A(hip_check(hipMemset(st.plan_ws, 0, omr_round_plan_workspace_words() * sizeof(uint64_t)), "hipMemset plan ws"));
     if (rc == 0 && st.pack_cnt) A(hip_check(hipMemset(st.pack_cnt, 0, NA * sizeof(uint32_t)), "hipMemset pack counters"));
   }
   if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset scan ws"));
@@ -1655,8 +1660,8 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
     return 0;
   }
   const uint32_t NS = static_cast<uint32_t>(NA + 1);  // count columns per array (shard bounds)
-  const uint32_t* counts = p->counts_host + static_cast<size_t>(si) * (M + 1) * NS;
-  const uint32_t* flag = p->flag_host + si;
+  const uint64_t* const tagged = p->counts_host + static_cast<size_t>(si) * (M + 1) * NS;
+  uint32_t counts[(OMR_MAX_WORKERS + 1) * (OMR_MAX_WORKERS + 2)];
   const hipStream_t xs = async ? p->cs : st;
   ht_of(p).lap("2:cs wait ready");
   const omr_stream_t xstream = reinterpret_cast<omr_stream_t>(xs);
@@ -1690,7 +1695,7 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
     if (async) TRY(finish_async(false));
     if (sent_blocks != nullptr || union_blocks != nullptr) {
       HostWait hw(p);
-      TRY(wait_flag(p->d, flag, seq, st));
+      TRY(wait_counts(p->d, tagged, (M + 1) * NS, seq, st, counts));
     }
     if (sent_blocks) *sent_blocks = (r1 - r0) * p->lanes * static_cast<uint64_t>(N - 1);
     if (union_blocks) *union_blocks = per(M, me);
@@ -1698,7 +1703,7 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
   }
   {
     HostWait hw(p);
-    TRY(wait_flag(p->d, flag, seq, st));
+    TRY(wait_counts(p->d, tagged, (M + 1) * NS, seq, st, counts));
   }
   ht_of(p).lap("2:wait counts");
   const bool wk = p->worker();
@@ -1888,7 +1893,7 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
     TRY(omr_check(omr_round_plan_list(S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes,
                                       p->bounds_dev, NS, S.wset, nullptr, S.prefix,
                                       p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, S.pack_cnt,
-                                      S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, p->flag_map + si, seq, j.un, p->B,
+                                      S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, S.plan_ws, seq, j.un, p->B,
                                       p->sum_list ? &sl : nullptr, qstream),
                   "omr_round_plan_list"));
     ht.lap("1:plan");

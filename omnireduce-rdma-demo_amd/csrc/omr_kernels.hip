@@ -438,7 +438,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
     if constexpr (TALLY) s_wcnt[wave] = cnt_w | (head0 << 31);
   }
   __syncthreads();
-  if constexpr (TALLY) {  // the one-rank round's bookkeeping: one pair of device atomics per workgroup, no return
+  if constexpr (TALLY) {  // the one-rank round's bookkeeping: one slot store per workgroup, no atomic
     if (threadIdx.x == 0) {
       uint32_t nz = 0, heads = 0;
       for (uint32_t w2 = 0; w2 < WAVES; ++w2) {
@@ -1193,12 +1193,13 @@ struct PlanArgs {
   uint64_t* write_set;
   uint64_t* union_masks;  // or null
   uint32_t* prefix;
-  uint32_t* counts;     // device or host-mapped memory: stored at system scope
-  uint64_t* zero_masks;  // or null
-  uint32_t* done_flag;  // receives `seq` once the counts are visible system-wide, or null
-  uint32_t seq;
-  NextArgs chain;       // union_next: the aggregator chain over the union, by workgroups 1.. (chain.next null: none)
-  uint32_t chain_wgs;
+  uint64_t* counts;       // (seq << 32) | prefix at a bound; device or host-mapped memory (stored at system scope)
+  uint64_t* zero_masks;   // or null
+  uint64_t* ws;           // [0] ticket counter (zero between launches), [1 + chunk * kPlanArrays + a] chunk totals
+  uint32_t seq;           // this launch's tag (differs from the previous launch's on the workspace)
+  uint32_t nchunks, tiles;  // chunks of tiles * 256 rows
+  NextArgs chain;       // union_next: the aggregator chain over the union, by workgroups after the chunks' (chain.next
+  uint32_t chain_wgs;   //   null: none)
   uint32_t list_wgs;    // the shard sum's pair list, by the workgroups after the chain's (0: none)
   ListArgs list;
 };
@@ -1216,142 +1217,190 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// The round's bookkeeping (server.cc:83-96) in ONE workgroup of 1024 threads, every mask read once (round 5; rounds 3-4
-// gave each array a workgroup of its own, and the write-set workgroup re-read every worker's masks: 1.95-1.99 x the
-// algorithmic HBM bytes and 12 us at config 4's shapes, profiles/pmc_round_r04.json).  Rows go in tiles of 1024 * R:
-// thread t owns rows tile + i * 1024 + t (i < R), so every load instruction is lane-contiguous, and all W * R loads of a
-// tile are in flight together (one round trip).  From registers: union = OR of the workers (the aggregator's min_next
-// domain), write set = union | lane heads (every lane head is sent and returned, client.cc:201-205), each array's
-// popcounts; the prefixes are DPP wave scans, then one wave scans the tile's 16 R wave totals per array (two barriers
-// per tile, no atomics, no look-back).  prefix[a][r] = set bits of array a before row r; counts[a][s] = prefix[a] at
-// bounds[s], stored at system scope into host-mapped memory; once they are acknowledged (vmcnt) the workgroup posts
-// `seq` to done_flag (one workgroup: no arrival counter).  The next round's own masks and pack counters are cleared.
-constexpr int kPlanThreads = 1024;
+// The round's bookkeeping (server.cc:83-96) over row chunks (round 5).  Every mask is read once, by the chunk that owns
+// its row, and the chunks run side by side: a single workgroup doing everything measured 32.6 us at config 4's shapes,
+// 11 of it per 2048-row tile issuing its prefix stores from one CU (profiles/r05/plan_probe/), and round 3/4's
+// workgroup per mask array (the write-set one re-reading every worker's masks) 11.6 us at 1.95-1.99 x the algorithmic
+// HBM bytes.  A chunk workgroup (256 threads, one row per thread and tile):
+//   1. takes a ticket (its chunk: every lower chunk belongs to a workgroup that has started, so the wait in 3 ends);
+//   2. reads its rows of every worker's masks (range-checked buffer loads: a row past the end or a worker past `count`
+//      reads 0, no branch), forms union = OR of the workers (the aggregator's min_next domain) and write set = union |
+//      lane heads (every lane head is sent and returned, client.cc:201-205), and each array's popcount total;
+//   3. publishes its totals tagged with `seq` and adds the lower chunks' totals as they appear (no chain: every chunk
+//      publishes before it waits, so the waits overlap);
+//   4. lays out its rows' prefixes (DPP wave scans, one LDS exchange of the wave totals) and stores them with the write
+//      set, the union and the cleared own masks; a row at a shard bound stores counts[a][s] = (seq << 32) | prefix.
+// The host reads the counts when every one it needs carries `seq`: no completion notice, no arrival counter, no wait for
+// the stores' acknowledgements inside the kernel.  The last chunk re-arms the ticket and stores the totals.
+constexpr uint32_t kPlanThreads = 256;
 constexpr uint32_t kPlanWaves = kPlanThreads / 64;
+constexpr uint32_t kPlanChunksMax = 64;
+constexpr uint32_t kPlanArrays = OMR_MAX_WORKERS + 1;
+constexpr uint64_t kPlanWorkspaceWords = 1 + static_cast<uint64_t>(kPlanChunksMax) * kPlanArrays;
 
-template <int W, int R>
-__device__ __forceinline__ void plan_rows(const PlanArgs& a) {
+template <int W>
+__device__ __forceinline__ void plan_chunk(const PlanArgs& a) {
   constexpr uint32_t NA = W + 1;  // arrays unrolled: W workers, then the write set
-  constexpr uint32_t ENT = kPlanWaves * R;  // wave totals per array and tile (<= 64: one scanning wave's lanes)
-  static_assert(ENT <= 64, "a tile's wave totals fit one wave");
-  __shared__ uint32_t s_wtot[ENT][NA];
-  __shared__ uint32_t s_base[ENT][NA];
+  __shared__ uint32_t s_wtot[kPlanWaves][NA];
+  __shared__ uint32_t s_base[NA];
+  __shared__ uint32_t s_chunk;
   __shared__ uint64_t s_bounds[OMR_MAX_WORKERS + 2];
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint32_t cnt = a.count;
   const uint64_t all_lanes = a.lanes >= 64 ? ~0ull : ((1ull << a.lanes) - 1ull);
+  const uint64_t tag = static_cast<uint64_t>(a.seq) << 32;
+  if (t == 0) s_chunk = static_cast<uint32_t>(__hip_atomic_fetch_add(&a.ws[0], 1ull, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT));
   if (t < a.nbounds) s_bounds[t] = a.bounds[t];
-  if (a.zero_cnt != nullptr && t < a.zero_cnt_n) a.zero_cnt[t] = 0;
-  uint32_t carry = 0;  // wave 0, lane a < NA: array a's set bits before the tile
+  if (t < NA) s_base[t] = 0;
   __syncthreads();
-  for (uint64_t tile = 0; tile < a.rows; tile += static_cast<uint64_t>(kPlanThreads) * R) {
-    // Buffer loads over each worker's rows: a row past the end, or a worker past `count` (a zero-size descriptor),
-    // reads 0 without a branch.  (Plain loads under `c < count && r < rows` were branched around one by one, each
-    // followed by a vmcnt(0) wait: W * R round trips in a row instead of one, 33 us at config 4's shapes.)
-    uint64_t mk[R][W];
+  const uint32_t c = s_chunk;
+  if (c == 0 && a.zero_cnt != nullptr && t < a.zero_cnt_n) a.zero_cnt[t] = 0;
+  const uint64_t row0 = static_cast<uint64_t>(c) * a.tiles * kPlanThreads;
+  __amdgpu_buffer_rsrc_t src[W];
 #pragma unroll
-    for (int c = 0; c < W; ++c) {
-      const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<uint64_t*>(a.masks + static_cast<uint64_t>(static_cast<uint32_t>(c) < cnt ? c : 0) * a.mstride),
-          0, static_cast<uint32_t>(c) < cnt ? static_cast<int>(a.rows * 8) : 0, 0x00020000);
+  for (int k = 0; k < W; ++k)
+    src[k] = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint64_t*>(a.masks + static_cast<uint64_t>(static_cast<uint32_t>(k) < cnt ? k : 0) * a.mstride), 0,
+        static_cast<uint32_t>(k) < cnt ? static_cast<int>(a.rows * 8) : 0, 0x00020000);
+  auto load_row = [&](uint64_t r, uint64_t (&mk)[W]) {
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const uint32_t r = static_cast<uint32_t>(tile) + static_cast<uint32_t>(i) * kPlanThreads + t;
-        const v2u v = __builtin_bit_cast(v2u, __builtin_amdgcn_raw_buffer_load_b64(src, r * 8u, 0, 0));
-        mk[i][c] = static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32);
-      }
+    for (int k = 0; k < W; ++k) {
+      const v2u v = __builtin_bit_cast(v2u, __builtin_amdgcn_raw_buffer_load_b64(src[k], static_cast<uint32_t>(r) * 8u,
+                                                                                 0, 0));
+      mk[k] = static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32);
     }
-    uint32_t ex[R][NA];  // exclusive prefix inside the wave, per row and array
-    uint64_t ws[R], un[R];
+  };
+  auto write_set_of = [&](uint64_t r, const uint64_t (&mk)[W], uint64_t* u) {
+    uint64_t x = 0;
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const uint64_t r = tile + static_cast<uint64_t>(i) * kPlanThreads + t;
-      uint64_t u = 0;
+    for (int k = 0; k < W; ++k) x |= mk[k];
+    *u = x;
+    return (r < a.rows && r % a.rpp == 0) ? (x | all_lanes) : x;
+  };
+  // ---- 2. the chunk's totals (its rows kept in registers when it is one tile)
+  uint64_t mk[W], un = 0, wsr = 0;
+  uint32_t tot[NA];
 #pragma unroll
-      for (int c = 0; c < W; ++c) u |= mk[i][c];
-      un[i] = u;
-      ws[i] = (r < a.rows && r % a.rpp == 0) ? (u | all_lanes) : u;
+  for (uint32_t k = 0; k < NA; ++k) tot[k] = 0;
+  for (uint32_t i = 0; i < a.tiles; ++i) {
+    const uint64_t r = row0 + static_cast<uint64_t>(i) * kPlanThreads + t;
+    load_row(r, mk);
+    wsr = write_set_of(r, mk, &un);
 #pragma unroll
-      for (uint32_t k = 0; k < NA; ++k) {
-        const uint32_t v = static_cast<uint32_t>(__builtin_popcountll(k < W ? mk[i][k] : ws[i]));
-        const uint32_t inc = wave_incl_scan(v);
-        ex[i][k] = inc - v;
-        if (lane == 63) s_wtot[i * kPlanWaves + wave][k] = inc;
-      }
-    }
-    __syncthreads();
-    if (wave == 0) {  // every (row group, wave) total of the tile, in row order: lane e = i * 16 + w
-#pragma unroll
-      for (uint32_t k = 0; k < NA; ++k) {
-        const uint32_t v = lane < ENT ? s_wtot[lane][k] : 0u;
-        const uint32_t inc = wave_incl_scan(v);
-        const uint32_t base = __builtin_amdgcn_readlane(static_cast<int>(carry), static_cast<int>(k));
-        if (lane < ENT) s_base[lane][k] = base + inc - v;
-        const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
-        if (lane == k) carry += tot;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const uint64_t r = tile + static_cast<uint64_t>(i) * kPlanThreads + t;
-      if (r >= a.rows) continue;
-      a.write_set[r] = ws[i];
-      if (a.union_masks != nullptr) a.union_masks[r] = un[i];
-      if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
-      uint32_t bnd = kNone;  // the last shard bound equal to this row (empty shards repeat a bound)
-      for (uint32_t s = 0; s < a.nbounds; ++s)
-        if (s_bounds[s] == r) bnd = s;
-#pragma unroll
-      for (uint32_t k = 0; k < NA; ++k) {
-        if (k < W && k >= cnt) continue;
-        const uint32_t arr = k < W ? k : cnt;
-        const uint32_t pv = s_base[i * kPlanWaves + wave][k] + ex[i][k];
-        a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + r] = pv;
-        if (bnd != kNone)
-          for (uint32_t s = 0; s < a.nbounds; ++s)
-            if (s_bounds[s] == r)
-              __hip_atomic_store(&a.counts[arr * a.nbounds + s], pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-    __syncthreads();  // (s_wtot / s_base are refilled by the next tile)
+    for (uint32_t k = 0; k < NA; ++k)
+      tot[k] += static_cast<uint32_t>(__builtin_popcountll(k < static_cast<uint32_t>(W) ? mk[k] : wsr));
   }
-  // the totals: prefix[a][rows], and the counts of every bound at or past the end
-  if (wave == 0 && lane < NA && (lane == W || lane < cnt)) {
-    const uint32_t arr = lane < W ? lane : cnt;
-    a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + a.rows] = carry;
+#pragma unroll
+  for (uint32_t k = 0; k < NA; ++k) {
+    const uint32_t inc = wave_incl_scan(tot[k]);
+    if (lane == 63) s_wtot[wave][k] = inc;
+  }
+  __syncthreads();
+  // ---- 3. publish, then add the lower chunks' totals (tagged with seq: a stale word from an earlier launch is not it)
+  if (t < NA) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kPlanWaves; ++w) sum += s_wtot[w][t];
+    __hip_atomic_store(&a.ws[1 + static_cast<uint64_t>(c) * kPlanArrays + t], tag | sum, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (uint32_t j = t; j < c * NA; j += kPlanThreads) {
+    const uint32_t i = j / NA, k = j - i * NA;
+    uint64_t v;
+    while (((v = __hip_atomic_load(&a.ws[1 + static_cast<uint64_t>(i) * kPlanArrays + k], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT)) >> 32) != a.seq)
+      __builtin_amdgcn_s_sleep(1);
+    atomicAdd(&s_base[k], static_cast<uint32_t>(v));
+  }
+  if (c + 1 == a.nchunks && t == 0)  // every chunk has taken its ticket: re-arm the counter for the next launch
+    __hip_atomic_store(&a.ws[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  uint32_t carry[NA];  // the array's set bits before the tile
+#pragma unroll
+  for (uint32_t k = 0; k < NA; ++k) carry[k] = s_base[k];
+  // ---- 4. the rows' prefixes and stores, tile by tile
+  for (uint32_t i = 0; i < a.tiles; ++i) {
+    const uint64_t r = row0 + static_cast<uint64_t>(i) * kPlanThreads + t;
+    if (a.tiles > 1) {  // (a one-tile chunk still holds its rows from step 2)
+      load_row(r, mk);
+      wsr = write_set_of(r, mk, &un);
+    }
+    uint32_t ex[NA];
+    if (i > 0) __syncthreads();  // (s_wtot is refilled)
+#pragma unroll
+    for (uint32_t k = 0; k < NA; ++k) {
+      const uint32_t v = static_cast<uint32_t>(__builtin_popcountll(k < static_cast<uint32_t>(W) ? mk[k] : wsr));
+      const uint32_t inc = wave_incl_scan(v);
+      ex[k] = inc - v;
+      if (lane == 63) s_wtot[wave][k] = inc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < NA; ++k) {
+      uint32_t before = 0, all = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kPlanWaves; ++w) {
+        const uint32_t x = s_wtot[w][k];
+        before += w < wave ? x : 0u;
+        all += x;
+      }
+      ex[k] += carry[k] + before;
+      carry[k] += all;
+    }
+    if (r < a.rows) {
+      a.write_set[r] = wsr;
+      if (a.union_masks != nullptr) a.union_masks[r] = un;
+      if (a.zero_masks != nullptr) a.zero_masks[r] = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < NA; ++k) {
+        if (k < static_cast<uint32_t>(W) && k >= cnt) continue;
+        const uint32_t arr = k < static_cast<uint32_t>(W) ? k : cnt;
+        a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + r] = ex[k];
+      }
+      for (uint32_t s = 0; s < a.nbounds; ++s)  // (a row at a shard bound: its counts; empty shards repeat a bound)
+        if (s_bounds[s] == r)
+#pragma unroll
+          for (uint32_t k = 0; k < NA; ++k) {
+            if (k < static_cast<uint32_t>(W) && k >= cnt) continue;
+            const uint32_t arr = k < static_cast<uint32_t>(W) ? k : cnt;
+            __hip_atomic_store(&a.counts[arr * a.nbounds + s], tag | ex[k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+    }
+  }
+  // the totals: prefix[a][rows], and the counts of every bound at or past the end (the last chunk)
+  if (c + 1 == a.nchunks && t < NA && (t == static_cast<uint32_t>(W) || t < cnt)) {
+    uint32_t total = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NA; ++k) total = k == t ? carry[k] : total;
+    const uint32_t arr = t < static_cast<uint32_t>(W) ? t : cnt;
+    a.prefix[static_cast<uint64_t>(arr) * (a.rows + 1) + a.rows] = total;
     for (uint32_t s = 0; s < a.nbounds; ++s)
       if (s_bounds[s] >= a.rows)
-        __hip_atomic_store(&a.counts[arr * a.nbounds + s], carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.counts[arr * a.nbounds + s], tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if (a.done_flag == nullptr) return;
-  // completion notice for a host that polls instead of waiting on an event: the counts went out as system-scope
-  // (write-through) stores; once every thread has seen its own acknowledged and passed the barrier, one store posts the
-  // round's sequence number.  No L2 write-back: nothing the host reads sits in an L2.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) __hip_atomic_store(a.done_flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One launch: workgroup 0 the bookkeeping (plan_rows), then the aggregator chain (server.cc:86-96 min_next over the
-// union, one k_next segment each), then the shard sum's pair list (one unit per wave).  W >= count (2, 4, 8, 16), R rows
-// per thread and tile (W * R <= 32 masks in registers).
-template <int W, int R>
+// One launch: the chunks (plan_chunk), then the aggregator chain (server.cc:86-96 min_next over the union, one k_next
+// segment each), then the shard sum's pair list (one unit per wave).  W >= count (2, 4, 8, 16).
+template <int W>
 __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
-  if (blockIdx.x == 0) {
-    plan_rows<W, R>(a);
+  if (blockIdx.x < a.nchunks) {
+    plan_chunk<W>(a);
     return;
   }
-  if (blockIdx.x > a.chain_wgs) {  // the shard sum's pair list, one unit per wave
+  const uint32_t b = blockIdx.x - a.nchunks;
+  if (b >= a.chain_wgs) {  // the shard sum's pair list, one unit per wave
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    build_sum_list(a.list, static_cast<uint64_t>(blockIdx.x - 1 - a.chain_wgs) * kPlanWaves + w,
+    build_sum_list(a.list, static_cast<uint64_t>(b - a.chain_wgs) * kPlanWaves + w,
                    static_cast<uint64_t>(a.list_wgs) * kPlanWaves);
     return;
   }
   const uint64_t* m = a.masks;  // the aggregator chain over the union, one segment each
   const uint32_t cnt = a.count;
   const uint64_t ms = a.mstride;
-  next_segment<kPlanWaves>(a.chain, blockIdx.x - 1, [&](uint64_t r) {
+  next_segment<kPlanWaves>(a.chain, b, [&](uint64_t r) {
     uint64_t u = 0;
     for (uint32_t c = 0; c < cnt; ++c) u |= m[static_cast<uint64_t>(c) * ms + r];
     return u;
@@ -2556,41 +2605,24 @@ uint64_t omr_pack_send_offset(const uint64_t* shard_bounds, uint32_t num_shards,
   return r * row_floats;
 }
 
-int omr_round_plan_chain(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
-                         uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
-                         uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                         uint32_t* done_flag, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                         omr_stream_t stream) {
-  return omr_round_plan_ex(row_masks, count, rows, rows, rows_per_part, num_lanes, bounds, num_bounds, write_set,
-                           union_masks, prefix, counts, zero_masks, nullptr, 0, done_flag, seq, union_next, block_size,
-                           stream);
-}
-
-int omr_round_plan_ex(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
-                      uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
-                      uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                      uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* done_flag,
-                      uint32_t seq, uint32_t* union_next, uint32_t block_size, omr_stream_t stream) {
-  return omr_round_plan_list(row_masks, count, mask_stride, rows, rows_per_part, num_lanes, bounds, num_bounds,
-                             write_set, union_masks, prefix, counts, zero_masks, zero_counters, num_zero_counters,
-                             done_flag, seq, union_next, block_size, nullptr, stream);
-}
+uint64_t omr_round_plan_workspace_words(void) { return kPlanWorkspaceWords; }
 
 int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
                         uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
-                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint32_t* counts,
-                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters, uint32_t* done_flag,
-                        uint32_t seq, uint32_t* union_next, uint32_t block_size, const omr_sum_list* list,
-                        omr_stream_t stream) {
+                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint64_t* counts,
+                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters,
+                        uint64_t* workspace, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                        const omr_sum_list* list, omr_stream_t stream) {
   if (mask_stride < rows) return fail("round_plan: mask_stride %llu < rows", static_cast<unsigned long long>(mask_stride));
   if (num_zero_counters > kPlanThreads || (num_zero_counters > 0 && zero_counters == nullptr))
     return fail("round_plan: zero_counters");
   if (count == 0 || count > OMR_MAX_WORKERS) return fail("round_plan: count %u out of range", count);
   if (rows == 0 || rows_per_part == 0 || rows % rows_per_part != 0) return fail("round_plan: bad rows");
   if (num_lanes == 0 || num_lanes > 64) return fail("round_plan: num_lanes %u out of range", num_lanes);
-  if (row_masks == nullptr || write_set == nullptr || prefix == nullptr ||
+  if (row_masks == nullptr || write_set == nullptr || prefix == nullptr || workspace == nullptr ||
       (num_bounds > 0 && (bounds == nullptr || counts == nullptr)))
     return fail("round_plan: NULL pointer");
+  if (seq == 0) return fail("round_plan: seq 0 (a zero-filled workspace or counts word carries it)");
   if (rows > 0xFFFFFFFFull / 64) return fail("round_plan: too many rows");
   if (num_bounds > OMR_MAX_WORKERS + 2) return fail("round_plan: %u bounds > %d", num_bounds, OMR_MAX_WORKERS + 2);
   PlanArgs a;
@@ -2609,8 +2641,12 @@ int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask
   a.prefix = prefix;
   a.counts = counts;
   a.zero_masks = zero_masks;
-  a.done_flag = done_flag;
+  a.ws = workspace;
   a.seq = seq;
+  // Chunks: about one 256-row tile per workgroup while that keeps them <= 64 (config 4: 1024 rows, 4 chunks).
+  const uint64_t tiles_all = (rows + kPlanThreads - 1) / kPlanThreads;
+  a.tiles = static_cast<uint32_t>((tiles_all + kPlanChunksMax - 1) / kPlanChunksMax);
+  a.nchunks = static_cast<uint32_t>((tiles_all + a.tiles - 1) / a.tiles);
   memset(&a.chain, 0, sizeof(a.chain));
   uint32_t chain_wgs = 0;
   if (union_next != nullptr) {
@@ -2642,22 +2678,22 @@ int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask
     const uint64_t wgs = (units + kPlanWaves - 1) / kPlanWaves;
     a.list_wgs = static_cast<uint32_t>(wgs < 512 ? wgs : 512);
   }
-  const unsigned grid = 1 + chain_wgs + a.list_wgs;
+  const unsigned grid = a.nchunks + chain_wgs + a.list_wgs;
   hipStream_t st = S(stream);
-  // (the masks of W * R rows per thread and tile stay in registers: at most 16 of them)
-  if (count <= 2) k_round_plan<2, 4><<<grid, kPlanThreads, 0, st>>>(a);
-  else if (count <= 4) k_round_plan<4, 4><<<grid, kPlanThreads, 0, st>>>(a);
-  else if (count <= 8) k_round_plan<8, 2><<<grid, kPlanThreads, 0, st>>>(a);
-  else k_round_plan<OMR_MAX_WORKERS, 1><<<grid, kPlanThreads, 0, st>>>(a);
+  if (count <= 2) k_round_plan<2><<<grid, kPlanThreads, 0, st>>>(a);
+  else if (count <= 4) k_round_plan<4><<<grid, kPlanThreads, 0, st>>>(a);
+  else if (count <= 8) k_round_plan<8><<<grid, kPlanThreads, 0, st>>>(a);
+  else k_round_plan<OMR_MAX_WORKERS><<<grid, kPlanThreads, 0, st>>>(a);
   return launch_status("k_round_plan");
 }
 
 int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                    uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,
-                   uint64_t* union_masks, uint32_t* prefix, uint32_t* counts, uint64_t* zero_masks,
-                   uint32_t* done_flag, uint32_t seq, omr_stream_t stream) {
-  return omr_round_plan_chain(row_masks, count, rows, rows_per_part, num_lanes, bounds, num_bounds, write_set,
-                              union_masks, prefix, counts, zero_masks, done_flag, seq, nullptr, 0, stream);
+                   uint64_t* union_masks, uint32_t* prefix, uint64_t* counts, uint64_t* zero_masks,
+                   uint64_t* workspace, uint32_t seq, omr_stream_t stream) {
+  return omr_round_plan_list(row_masks, count, rows, rows, rows_per_part, num_lanes, bounds, num_bounds, write_set,
+                             union_masks, prefix, counts, zero_masks, nullptr, 0, workspace, seq, nullptr, 0, nullptr,
+                             stream);
 }
 
 int omr_move_blocks_f32(const float* src, float* dst, int dir, const uint64_t* row_masks, const uint32_t* prefix,

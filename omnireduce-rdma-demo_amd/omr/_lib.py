@@ -54,8 +54,7 @@ SIGNATURES = {
     "omr_worker_scan_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "omr_round_plan": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                c_u32, c_vp]),
-    "omr_round_plan_chain": (c_int, [c_vp, c_u32, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                     c_vp, c_u32, c_vp, c_u32, c_vp]),
+    "omr_round_plan_workspace_words": (c_u64, []),
     "omr_move_blocks_f32": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_u64, c_u32, c_u32, c_u64, c_u64, c_vp]),
     "omr_shard_sum_f32": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, c_vp, c_vp, c_u64, c_u64, c_u64, c_u32,
                                   c_u32, c_int, c_vp, c_vp]),
@@ -68,8 +67,6 @@ SIGNATURES = {
                                           c_vp, c_size, c_vp]),
     "omr_tally_publish": (c_int, [c_vp, c_u32, c_vp, c_u32, c_vp]),
     "omr_tally_slots": (c_u32, [c_u64, c_u32, c_u32, c_u32]),
-    "omr_round_plan_ex": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
-                                  c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_u32, c_vp]),
     "omr_round_plan_list": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
                                     c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_u32, c_vp, c_vp]),
     "omr_sum_list_geometry": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u64, c_u64, c_u32, c_vp, c_vp]),

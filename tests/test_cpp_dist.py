@@ -37,6 +37,8 @@ def dist_lib():
     L.omr_sparse_round_f32.argtypes = [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]
     L.omr_ar_plan_join.argtypes = [vp, vp]
     L.omr_ar_plan_exchange_time.argtypes = [vp, vp, vp, vp]
+    L.omr_ar_plan_device_bytes.restype = u64
+    L.omr_ar_plan_device_bytes.argtypes = [vp]
     L.omr_dist_last_error.restype = ctypes.c_char_p
     return L
 

@@ -2,7 +2,7 @@
 
 C4: 8 workers x 256 MiB fp32, -r 0.095 (seeds 1..8, the reference's 0.01f fill: client.cc:396-421):
   * the product's C++ multi-rank round (libomr_dist.so) with 8 loopback ranks sharing the GPU, reduce-scatter and
-    all-reduce modes, synchronous and pipelined;
+    all-reduce modes, synchronous and pipelined, and each rank's plan within 4x the tensor in device memory;
   * the m = 8 single-device sum k_scanm (omr_scan_sum_f32) over the same 8 tensors.
 C5: 4 GiB fp32, -r 0.49, pinned host memory, staged (H2D/scan/D2H) and zero-copy host plans.
 
@@ -70,7 +70,7 @@ def test_c4_cpp_round_loopback(gpu, c4, mode):
     board = D.omr_local_board_create(world)
     ka = ka_table(world)
     exp_blk = expected_blocks(counts, ka, gpu)
-    errs, res = [], [None] * world
+    errs, res, footprint = [], [None] * world, [0] * world
     rounds = 3
 
     def rank(r):
@@ -84,6 +84,7 @@ def test_c4_cpp_round_loopback(gpu, c4, mode):
             d, plan = ctypes.c_void_p(), ctypes.c_void_p()
             assert D.omr_dist_create_local(board, r, ctypes.byref(d)) == 0
             assert D.omr_ar_plan_create(d, L.n, 256, L.num_lanes, 8, ctypes.byref(plan)) == 0
+            footprint[r] = D.omr_ar_plan_device_bytes(plan)
             st = torch.cuda.Stream()
             for _ in range(rounds):  # x is never written; every round writes the same sums into out
                 rc = D.omr_sparse_round_f32(plan, x.data_ptr(), out.data_ptr(), flags.data_ptr(), nxt.data_ptr(),
@@ -104,6 +105,10 @@ def test_c4_cpp_round_loopback(gpu, c4, mode):
         t.join(timeout=300)
     D.omr_local_board_destroy(board)
     assert not errs, errs
+    # the plan's device memory for 256 MiB at world 8 (round sets, three send buffers of 7/8 of the tensor, one
+    # receive buffer): at most 4x the tensor (round 4 held about 9x)
+    for r in range(world):
+        assert 0 < footprint[r] <= 4 * L.nbytes, (r, footprint[r] / L.nbytes)
     bounds = [s * L.rows // world for s in range(world + 1)]
     rowsel = torch.arange(L.nb, device=gpu) // L.num_lanes
     for r in range(world):

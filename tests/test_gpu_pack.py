@@ -9,7 +9,7 @@ that overflow the waves' LDS slots (the re-read path), B = 512 / 1024 (two colum
 shards.
 
 omr_shard_sum_list_f32 (server.cc:83-99 over those streams): M workers' scans on one device, their streams
-concatenated as the transport would deliver them to an aggregator, the bookkeeping from omr_round_plan_ex over the
+concatenated as the transport would deliver them to an aggregator, the bookkeeping from omr_round_plan_list over the
 all-gathered masks + tables, the pair list built by the plan launch and by a launch of its own, then the shard sums —
 dense in place and packed in write-set order — bit-exact against the oracle's rank-order sum (0 ulp)."""
 import ctypes
@@ -185,9 +185,12 @@ def test_shard_sum_list(gpu, n, B, density, m, naggs, colocated, packed_out):
     umask = torch.zeros(rows, dtype=torch.int64, device=gpu)
     prefix = torch.zeros((m + 1) * (rows + 1), dtype=torch.int32, device=gpu)
     bdev = torch.from_numpy(bounds.astype(np.int64)).to(gpu)
-    counts = torch.zeros((m + 1) * (naggs + 1), dtype=torch.int32, device=gpu)
-    rc = lib.omr_round_plan_ex(P(masks_all), m, mstride, rows, L.rows_per_part, L.num_lanes, P(bdev), naggs + 1,
-                               P(wset), P(umask), P(prefix), P(counts), None, None, 0, None, 0, None, B, stream())
+    counts = torch.zeros((m + 1) * (naggs + 1), dtype=torch.int64, device=gpu)
+    ws = torch.zeros(int(lib.omr_round_plan_workspace_words()), dtype=torch.int64, device=gpu)
+    seq = 1
+    rc = lib.omr_round_plan_list(P(masks_all), m, mstride, rows, L.rows_per_part, L.num_lanes, P(bdev), naggs + 1,
+                                 P(wset), P(umask), P(prefix), P(counts), None, None, 0, P(ws), seq, None, B, None,
+                                 stream())
     assert rc == 0, lib.omr_last_error()
     torch.cuda.synchronize()
     ws_np = wset.cpu().numpy().view(np.uint64)
@@ -225,9 +228,10 @@ def test_shard_sum_list(gpu, n, B, density, m, naggs, colocated, packed_out):
             for w in range(m):
                 sl.recv_offsets[w] = int(offs[w])
             if how == "plan":
+                seq += 1
                 rc = lib.omr_round_plan_list(P(masks_all), m, mstride, rows, L.rows_per_part, L.num_lanes, P(bdev),
-                                             naggs + 1, P(wset), P(umask), P(prefix), P(counts), None, None, 0, None,
-                                             0, None, B, ctypes.byref(sl), stream())
+                                             naggs + 1, P(wset), P(umask), P(prefix), P(counts), None, None, 0, P(ws),
+                                             seq, None, B, ctypes.byref(sl), stream())
             else:
                 rc = lib.omr_sum_list_build(P(masks_all), m, mstride, L.n, B, L.num_lanes, L.num_threads,
                                             ctypes.byref(sl), stream())

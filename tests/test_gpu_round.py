@@ -1,5 +1,5 @@
 """GPU parity of the mask-addressed multi-rank round kernels, called through the C ABI (include/omr.h):
-omr_worker_scan_f32 (scan + row masks), omr_round_plan / omr_round_plan_chain (union / write set / prefixes / shard
+omr_worker_scan_f32 (scan + row masks), omr_round_plan / omr_round_plan_list (union / write set / prefixes / shard
 counts, the aggregator bookkeeping of server.cc:83-96, and the aggregator chain in the same launch), omr_move_blocks_f32 (pack common.cc:405-407 / unpack client.cc:89)
 and omr_shard_sum_f32 (server.cc:97-98 in rank order).  Checked against the oracle (flags, masks, next chains,
 block sums) and plain numpy restatements of the index arithmetic.  Bar: bit-exact (integer work and rank-order
@@ -78,19 +78,32 @@ def test_worker_scan_masks(gpu, n, B, density):
     assert torch.equal(xd, torch.from_numpy(x).to(gpu))  # out = NULL: the tensor is not written
 
 
+def plan_ws(lib, gpu):
+    """A zero-filled plan workspace (the kernel re-arms it after each launch)."""
+    return torch.zeros(int(lib.omr_round_plan_workspace_words()), dtype=torch.int64, device=gpu)
+
+
+def untag(counts, seq):
+    """The (seq << 32) | count words of omr_round_plan: every one carries `seq`; returns the counts."""
+    c = counts.cpu().numpy().view(np.uint64)
+    assert ((c >> np.uint64(32)) == np.uint64(seq)).all(), (c >> np.uint64(32))
+    return (c & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
 @pytest.mark.parametrize("count,rows,rpp,lanes,stride_pad", [
     (1, 64, 8, 64, 0), (3, 512, 64, 64, 5), (8, 4096, 512, 64, 1024), (5, 1280, 256, 16, 0), (16, 100, 25, 32, 3),
-    (2, 8192, 1024, 64, 0),                           # two 4096-row tiles
-    (7, 16384, 2048, 16, 0),                          # eight 2048-row tiles (W = 8, R = 2)
-    (3, 20480, 2560, 16, 0),                          # five tiles
+    (2, 8192, 1024, 64, 0),                           # 32 chunks of one 256-row tile
+    (7, 16384, 2048, 16, 0),                          # 64 chunks (the most)
+    (3, 20480, 2560, 16, 0),                          # 40 chunks of two tiles
     (8, 300, 30, 64, 7),                              # a partial tile
-    (16, 5000, 1000, 64, 0),                          # W = 16, R = 1: five 1024-row tiles, the last partial
+    (16, 5000, 1000, 64, 0),                          # W = 16: 20 chunks, the last partial
+    (4, 70000, 1000, 64, 0),                          # 55 chunks of five tiles, the last partial
 ])
 def test_round_plan(gpu, count, rows, rpp, lanes, stride_pad):
-    """omr_round_plan_list (round 5: ONE 1024-thread workgroup, every mask read once, row tiles of 1024 * R, DPP wave
-    scans) against numpy: union, write set, every array's prefix, the counts at the shard bounds, the zeroed own masks
-    and pack counters, the aggregator chain, and the completion notice three times in a row; worker arrays at a stride
-    whose tail (a position table) is not read as masks."""
+    """omr_round_plan_list (round 5: row chunks side by side, ticketed, handing each other their popcount totals through
+    the workspace; DPP wave scans) against numpy: union, write set, every array's prefix, the tagged counts at the shard
+    bounds, the zeroed own masks and pack counters, and the aggregator chain, three launches in a row on one workspace;
+    worker arrays at a stride whose tail (a position table) is not read as masks."""
     rng = np.random.default_rng(count * 31 + rows)
     stride = rows + stride_pad
     dens = rng.random(count) * 0.5
@@ -109,10 +122,10 @@ def test_round_plan(gpu, count, rows, rpp, lanes, stride_pad):
     wset = torch.zeros(rows, dtype=torch.int64, device=gpu)
     umask = torch.zeros(rows, dtype=torch.int64, device=gpu)
     prefix = torch.zeros((count + 1) * (rows + 1), dtype=torch.int32, device=gpu)
-    counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int32, device=gpu)
+    counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int64, device=gpu)
     zero = torch.full((rows,), -1, dtype=torch.int64, device=gpu)
     zc = torch.full((8,), -1, dtype=torch.int32, device=gpu)
-    done = torch.zeros(1, dtype=torch.int32, device=gpu)
+    ws = plan_ws(lib, gpu)
     B = 16384 // lanes
     unext = torch.full((rows * lanes,), -1, dtype=torch.int32, device=gpu)
     for seq in (7, 8, 9):
@@ -120,9 +133,10 @@ def test_round_plan(gpu, count, rows, rpp, lanes, stride_pad):
         umask.zero_()
         assert lib.omr_round_plan_list(P(md), count, stride, rows, rpp, lanes, P(bd), N + 1, P(wset),
                                        P(umask) if seq != 8 else None, P(prefix), P(counts), P(zero), P(zc), 8,
-                                       P(done), seq, P(unext), B, None, stream()) == 0, lib.omr_last_error()
+                                       P(ws), seq, P(unext), B, None, stream()) == 0, lib.omr_last_error()
         torch.cuda.synchronize()
-        assert int(done.item()) == seq
+        untag(counts, seq)
+        assert int(ws[0].item()) == 0  # the ticket counter re-armed
         if seq == 8:
             assert int(umask.count_nonzero()) == 0  # no union_masks asked for: not written
     mr = masks[:, :rows]
@@ -130,7 +144,7 @@ def test_round_plan(gpu, count, rows, rpp, lanes, stride_pad):
     assert (umask.cpu().numpy().view(np.uint64) == u).all()
     assert (wset.cpu().numpy().view(np.uint64) == w).all()
     pre = prefix.cpu().numpy().view(np.uint32).reshape(count + 1, rows + 1)
-    cn = counts.cpu().numpy().view(np.uint32).reshape(count + 1, N + 1)
+    cn = untag(counts, 9).reshape(count + 1, N + 1)
     for a in range(count + 1):
         exp = np_prefix(mr[a] if a < count else w)
         assert (pre[a] == exp).all(), a
@@ -142,7 +156,8 @@ def test_round_plan(gpu, count, rows, rpp, lanes, stride_pad):
 
 
 def test_round_plan_counts_past_the_end(gpu):
-    """Shard bounds that repeat (empty shards) and bounds at the end: every count = the prefix at its bound."""
+    """Shard bounds that repeat (empty shards) and bounds at the end: every count = the prefix at its bound; a
+    workspace reused across plans of different sizes (the chunk count changes) and a refused seq 0."""
     rows, lanes, rpp, count = 2048, 64, 256, 3
     rng = np.random.default_rng(5)
     masks = (rng.integers(0, 2 ** 63, size=(count, rows), dtype=np.int64)).view(np.uint64)
@@ -152,23 +167,31 @@ def test_round_plan_counts_past_the_end(gpu):
     bd = torch.from_numpy(bounds.view(np.int64)).to(gpu)
     wset = torch.zeros(rows, dtype=torch.int64, device=gpu)
     prefix = torch.zeros((count + 1) * (rows + 1), dtype=torch.int32, device=gpu)
-    counts = torch.full(((count + 1) * len(bounds),), -1, dtype=torch.int32, device=gpu)
-    assert lib.omr_round_plan_list(P(md), count, rows, rows, rpp, lanes, P(bd), len(bounds), P(wset), None, P(prefix),
-                                   P(counts), None, None, 0, None, 0, None, 64, None, stream()) == 0, lib.omr_last_error()
-    torch.cuda.synchronize()
+    counts = torch.full(((count + 1) * len(bounds),), -1, dtype=torch.int64, device=gpu)
+    ws = plan_ws(lib, gpu)
+    assert lib.omr_round_plan(P(md), count, rows, rpp, lanes, P(bd), len(bounds), P(wset), None, P(prefix),
+                              P(counts), None, P(ws), 0, stream()) != 0  # seq 0: refused
     _, w = np_write_set(masks, rpp, lanes)
-    cn = counts.cpu().numpy().view(np.uint32).reshape(count + 1, len(bounds))
-    for a in range(count + 1):
-        exp = np_prefix(masks[a] if a < count else w)
-        assert (cn[a] == exp[bounds.astype(np.int64)]).all(), a
+    for seq, r in ((1, rows), (2, 512), (3, rows)):  # 8 chunks, then 2 on the same workspace, then 8
+        b = np.minimum(bounds, r)
+        bd = torch.from_numpy(b.view(np.int64)).to(gpu)
+        assert lib.omr_round_plan_list(P(md), count, rows, r, rpp, lanes, P(bd), len(bounds), P(wset), None,
+                                       P(prefix), P(counts), None, None, 0, P(ws), seq, None, 64, None,
+                                       stream()) == 0, lib.omr_last_error()
+        torch.cuda.synchronize()
+        cn = untag(counts, seq).reshape(count + 1, len(bounds))
+        _, w = np_write_set(masks[:, :r], rpp, lanes)
+        for a in range(count + 1):
+            exp = np_prefix(masks[a, :r] if a < count else w)
+            assert (cn[a] == exp[b.astype(np.int64)]).all(), (seq, a)
 
 
 @pytest.mark.parametrize("count,rows,rpp,lanes", [(1, 64, 8, 64), (3, 512, 64, 64), (8, 4096, 512, 64),
                                                    (5, 1280, 256, 16), (16, 100, 25, 32), (3, 20480, 2560, 16)])
 def test_round_plan_chain(gpu, count, rows, rpp, lanes):
-    """omr_round_plan_chain: the plan's outputs exactly as omr_round_plan, plus the aggregator chain (server.cc:86-96,
-    min_next over the workers) computed by the same launch from the workers' masks = the oracle's next offsets over
-    the union of the workers' flags."""
+    """omr_round_plan_list with union_next: the plan's outputs exactly as without it, plus the aggregator chain
+    (server.cc:86-96, min_next over the workers) computed by the same launch from the workers' masks = the oracle's
+    next offsets over the union of the workers' flags."""
     rng = np.random.default_rng(count * 7 + rows)
     B = 16384 // lanes
     masks = np.zeros((count, rows), dtype=np.uint64)
@@ -180,18 +203,19 @@ def test_round_plan_chain(gpu, count, rows, rpp, lanes):
     lib = _lib.load()
     md = torch.from_numpy(masks.view(np.int64)).to(gpu)
     bd = torch.from_numpy(bounds.view(np.int64)).to(gpu)
+    ws = plan_ws(lib, gpu)
     outs = []
-    for chain in (False, True):
+    for seq, chain in ((1, False), (2, True)):
         wset = torch.zeros(rows, dtype=torch.int64, device=gpu)
         umask = torch.zeros(rows, dtype=torch.int64, device=gpu)
         prefix = torch.zeros((count + 1) * (rows + 1), dtype=torch.int32, device=gpu)
-        counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int32, device=gpu)
+        counts = torch.zeros((count + 1) * (N + 1), dtype=torch.int64, device=gpu)
         unext = torch.full((rows * lanes,), -1, dtype=torch.int32, device=gpu)
-        assert lib.omr_round_plan_chain(P(md), count, rows, rpp, lanes, P(bd), N + 1, P(wset), P(umask), P(prefix),
-                                        P(counts), None, None, 0, P(unext) if chain else None, B,
-                                        stream()) == 0, lib.omr_last_error()
+        assert lib.omr_round_plan_list(P(md), count, rows, rows, rpp, lanes, P(bd), N + 1, P(wset), P(umask),
+                                       P(prefix), P(counts), None, None, 0, P(ws), seq, P(unext) if chain else None,
+                                       B, None, stream()) == 0, lib.omr_last_error()
         torch.cuda.synchronize()
-        outs.append((wset.cpu(), umask.cpu(), prefix.cpu(), counts.cpu(), unext.cpu()))
+        outs.append((wset.cpu(), umask.cpu(), prefix.cpu(), torch.from_numpy(untag(counts, seq)), unext.cpu()))
     for a, b in zip(outs[0][:4], outs[1][:4]):
         assert torch.equal(a, b)
     assert (outs[0][4] == -1).all()  # no chain requested: union_next untouched

@@ -53,12 +53,13 @@ def setup(L, m, naggs, dev, stream):
     wset = torch.empty(L.rows, dtype=torch.int64, device=dev)
     umask = torch.empty(L.rows, dtype=torch.int64, device=dev)
     prefix = torch.empty((m + 1, L.rows + 1), dtype=torch.int32, device=dev)
-    counts = torch.empty((m + 1, naggs + 1), dtype=torch.int32, device=dev)
+    counts = torch.empty((m + 1, naggs + 1), dtype=torch.int64, device=dev)
+    pws = torch.zeros(int(lib.omr_round_plan_workspace_words()), dtype=torch.int64, device=dev)
     _lib.check(lib.omr_round_plan(masks.data_ptr(), m, L.rows, L.rows_per_part, L.num_lanes, bdev.data_ptr(),
                                   naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(), counts.data_ptr(),
-                                  None, None, 0, stream), "omr_round_plan")
+                                  None, pws.data_ptr(), 1, stream), "omr_round_plan")
     torch.cuda.synchronize()
-    cnt = counts.cpu().numpy().astype(np.int64)
+    cnt = counts.cpu().numpy() & 0xFFFFFFFF  # ((seq << 32) | count)
     r0, r1 = bounds[0], bounds[1]
     per = [int(cnt[c, 1] - cnt[c, 0]) for c in range(m)]
     recv_off = np.zeros(m, dtype=np.uint64)

@@ -81,11 +81,12 @@ def setup(a):
     wset = torch.empty(rows, dtype=torch.int64, device=dev)
     umask = torch.empty(rows, dtype=torch.int64, device=dev)
     prefix = torch.empty((m + 1) * (rows + 1), dtype=torch.int32, device=dev)
-    counts = torch.empty((m + 1) * (naggs + 1), dtype=torch.int32, device=dev)
+    counts = torch.empty((m + 1) * (naggs + 1), dtype=torch.int64, device=dev)
     bdev = torch.from_numpy(bounds.astype(np.int64)).to(dev)
-    _lib.check(lib.omr_round_plan_ex(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
-                                     naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
-                                     counts.data_ptr(), None, None, 0, None, 0, None, B, st), "plan")
+    pws5 = torch.zeros(int(lib.omr_round_plan_workspace_words()), dtype=torch.int64, device=dev)
+    _lib.check(lib.omr_round_plan_list(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                       naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                       counts.data_ptr(), None, None, 0, pws5.data_ptr(), 1, None, B, None, st), "plan")
     # the round-2 layout: masks [m][rows] contiguous, row-ordered streams packed by k_move
     masks = torch.stack([masks_all[w * mstride:w * mstride + rows] for w in range(m)]).contiguous()
     torch.cuda.synchronize()
@@ -108,7 +109,7 @@ def setup(a):
     return dict(L=L, m=m, naggs=naggs, rows=rows, B=B, NB=NB, ent=ent, mstride=mstride, bounds=bounds, bptr=bptr,
                 xs=xs, wsb=wsb, ws=ws, flags=flags, nxt=nxt, masks_all=masks_all, sends=sends, cnts=cnts, wset=wset,
                 umask=umask, prefix=prefix, counts=counts, bdev=bdev, masks=masks, r0=r0, r1=r1, pre=pre, roff=roff,
-                acc=acc, recv_c=recv_c, recv_r=recv_r, S=S_.value, gps=gps.value, dev=dev, st=st)
+                acc=acc, recv_c=recv_c, recv_r=recv_r, pws5=pws5, S=S_.value, gps=gps.value, dev=dev, st=st)
 
 
 TUNE_SRC = os.path.join(ROOT, "tools", "tune", "plan_r04.hip")
@@ -227,34 +228,39 @@ def main():
 
     unext = torch.empty(L.nb, dtype=torch.int32, device=dev)
 
-    # the round's own setting: counts into pinned host memory (system-scope stores), the completion notice posted, the
-    # own masks and pack counters cleared (scratch copies here), the pair list, no chain (bench asks for no union_next)
+    # the round's own setting: tagged counts into pinned host memory (system-scope stores), the own masks and pack
+    # counters cleared (scratch copies here), the pair list, no chain (bench asks for no union_next)
     pin = torch.zeros(4096, dtype=torch.int32).pin_memory()
     pin_d = ctypes.c_void_p()
     assert ctypes.CDLL("libamdhip64.so").hipHostGetDevicePointer(ctypes.byref(pin_d), ctypes.c_void_p(pin.data_ptr()),
                                                                  0) == 0
-    cnt_d, flag_d = pin_d.value, pin_d.value + 4 * 2048
+    cnt_d, flag_d = pin_d.value, pin_d.value + 4 * 2048  # (the notice: the round-3/4 form only)
     zmask = torch.empty(rows, dtype=torch.int64, device=dev)
     zcnt = torch.empty(naggs, dtype=torch.int32, device=dev)
     arrive = torch.zeros(1, dtype=torch.int32, device=dev)
-    seqs = [0]
+    seqs = [1]
+    pws5 = D["pws5"]
+
+    def nseq():  # every product plan launch shares pws5: a fresh sequence number each
+        seqs[0] += 1
+        return seqs[0]
 
     def plan():  # the round's bookkeeping launch: write set, union, prefixes, counts, aggregator chain
-        return lib.omr_round_plan_ex(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
-                                     naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
-                                     counts.data_ptr(), None, None, 0, None, 0, unext.data_ptr(), B, st)
+        return lib.omr_round_plan_list(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                       naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                       counts.data_ptr(), None, None, 0, pws5.data_ptr(), nseq(), unext.data_ptr(), B,
+                                       None, st)
 
     def plan_list():  # ... with shard 0's pair list built by the same launch (the round since round 3)
         return lib.omr_round_plan_list(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
                                        naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
-                                       counts.data_ptr(), None, None, 0, None, 0, unext.data_ptr(), B,
+                                       counts.data_ptr(), None, None, 0, pws5.data_ptr(), nseq(), unext.data_ptr(), B,
                                        ctypes.byref(sl), st)
 
-    def plan_round():  # exactly the round's call (round 5's single-workgroup plan)
-        seqs[0] += 1
+    def plan_round():  # exactly the round's call (round 5's row-chunk plan)
         return lib.omr_round_plan_list(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
                                        naggs + 1, wset.data_ptr(), None, prefix.data_ptr(), cnt_d, zmask.data_ptr(),
-                                       zcnt.data_ptr(), naggs, flag_d, seqs[0], None, B, ctypes.byref(sl), st)
+                                       zcnt.data_ptr(), naggs, pws5.data_ptr(), nseq(), None, B, ctypes.byref(sl), st)
 
     def plan_round_r04():  # the same call to the round-3/4 plan (one workgroup per mask array, arrival counter)
         seqs[0] += 1
@@ -272,9 +278,9 @@ def main():
                                          B, None, st)
 
     def plan_nochain():  # the plan without the aggregator chain
-        return lib.omr_round_plan_ex(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
-                                     naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
-                                     counts.data_ptr(), None, None, 0, None, 0, None, B, st)
+        return lib.omr_round_plan_list(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                       naggs + 1, wset.data_ptr(), umask.data_ptr(), prefix.data_ptr(),
+                                       counts.data_ptr(), None, None, 0, pws5.data_ptr(), nseq(), None, B, None, st)
 
     def plan_nochain_r04():  # the round-3/4 plan without the chain
         return t4.tune_round_plan_list_r04(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB,
@@ -298,7 +304,7 @@ def main():
                "round plan, no chain (round-3/4 k_round_plan_r04)": plan_nochain_r04,
                "round plan, no chain, row chunks (k_round_plan2)": plan_ws_nochain,
                "round plan + chain + pair list": plan_list,
-               "round plan as the round calls it (pair list, pinned counts, notice)": plan_round,
+               "round plan as the round calls it (pair list, pinned counts)": plan_round,
                "round plan as the round calls it, round-3/4 form": plan_round_r04,
                "pair list alone (k_sum_list)": list_only}
     cases = {**sums, **workers}
@@ -346,10 +352,10 @@ def main():
     wbytes["round plan, no chain, row chunks (k_round_plan2)"] = wbytes["round plan, no chain (k_round_plan)"]
     wbytes["round plan, no chain (round-3/4 k_round_plan_r04)"] = wbytes["round plan, no chain (k_round_plan)"]
     # the round's call: no union stored, no chain; its own masks cleared (rows words), the pair list
-    wbytes["round plan as the round calls it (pair list, pinned counts, notice)"] = (
+    wbytes["round plan as the round calls it (pair list, pinned counts)"] = (
         m * rows * 8 + rows * 8 + (m + 1) * (rows + 1) * 4 + rows * 8 + lbytes)
     wbytes["round plan as the round calls it, round-3/4 form"] = (
-        wbytes["round plan as the round calls it (pair list, pinned counts, notice)"] + rows * 8)  # (+ its union)
+        wbytes["round plan as the round calls it (pair list, pinned counts)"] + rows * 8)  # (+ its union)
     wbytes["pair list alone (k_sum_list)"] = lbytes
     report = {}
     print(f"## config 4 shapes, {m} workers, -r {a.density}: shard 0 write set {ub} blocks, received {nc}, own {own_blocks}: "
