@@ -19,9 +19,27 @@ def test_product_kernels_have_no_study_knobs():
     assert not os.path.isdir(os.path.join(ROOT, "omnireduce-rdma-demo_amd", "csrc", "tune"))
 
 
+def test_product_reads_only_documented_environment():
+    """the product libraries read the deadline, the host trace and the bucket write-back modes
+    from the environment, nothing else (no study knobs, no per-launch lookups)."""
+    import re
+    allowed = {"OMR_DIST_TIMEOUT_MS", "OMR_HOST_TRACE", "OMR_HOST_TRACE_FILE", "OMR_BUCKETS_STAGED_D2H",
+               "OMR_BUCKETS_SCAN_HOST", "OMR_HOST_STAGED_D2H"}
+    csrc = os.path.join(ROOT, "omnireduce-rdma-demo_amd", "csrc")
+    seen = set()
+    for f in sorted(os.listdir(csrc)):
+        src = open(os.path.join(csrc, f)).read()
+        for name in re.findall(r'getenv\("([A-Z0-9_]+)"\)', src):
+            assert name in allowed, (f, name)
+            seen.add(name)
+        assert src.count("getenv(") == len(re.findall(r'getenv\("[A-Z0-9_]+"\)', src)), f
+    assert "OMR_DIST_TIMEOUT_MS" in seen
+    assert "getenv" not in open(os.path.join(csrc, "omr_kernels.hip")).read()
+
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
 @pytest.mark.parametrize("name", ["fused_r02", "round_r02", "scanm_r02", "fused_variants", "plan_r04", "shard_r04",
-                                  "shard_r03"])
+                                  "shard_r03", "plan_v5_study"])
 def test_tune_harness_builds(tmp_path, name):
     out = str(tmp_path / f"{name}.o")
     p = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O1", "-std=c++17", "-fPIC", "-c",
