@@ -1097,6 +1097,16 @@ __device__ __forceinline__ uint64_t list_units(const ListArgs& a) {
 // group), as k_shard_sum's column-stream units.  Lane i holds row i of the group: ONE round trip fetches every worker's mask row
 // and position-table entry; ballots give each worker's column bits; a wave-wide exclusive scan places each lane's
 // pairs; records go straight to global memory.
+// Workgroup i of n consecutive ones (the first at grid position base) -> a logical index such that each XCD (the
+// hardware deals workgroups to the 8 XCDs round robin by grid position) takes one contiguous range of logical
+// indices.  The pair list's neighbouring units read the same mask rows and position-table entries (the 64 lanes of a
+// row group, 256 units), so with consecutive units on one XCD each XCD's L2 fetches a group once instead of every
+// XCD fetching every group.  n not a multiple of 8: identity.
+__device__ __forceinline__ uint32_t xcd_spread(uint32_t i, uint32_t base, uint32_t n) {
+  if (n % 8 != 0) return i;
+  return ((base + i) % 8) * (n / 8) + i / 8;
+}
+
 __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, uint64_t ustride) {
   const int lane = threadIdx.x & 63;
   const uint64_t units = list_units(a);
@@ -1393,8 +1403,8 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
   const uint32_t b = blockIdx.x - a.nchunks;
   if (b >= a.chain_wgs) {  // the shard sum's pair list, one unit per wave
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    build_sum_list(a.list, static_cast<uint64_t>(b - a.chain_wgs) * kPlanWaves + w,
-                   static_cast<uint64_t>(a.list_wgs) * kPlanWaves);
+    const uint32_t li = xcd_spread(b - a.chain_wgs, a.nchunks + a.chain_wgs, a.list_wgs);
+    build_sum_list(a.list, static_cast<uint64_t>(li) * kPlanWaves + w, static_cast<uint64_t>(a.list_wgs) * kPlanWaves);
     return;
   }
   const uint64_t* m = a.masks;  // the aggregator chain over the union, one segment each
@@ -2129,7 +2139,8 @@ __global__ __launch_bounds__(64) void k_publish_tally(const uint64_t* tally, uin
 uint64_t list_units_host(const ListArgs& a) { return ((a.r1 - a.r0) / a.S) * a.gps * kSumUnitsPerGroup * a.lanes; }
 
 __global__ __launch_bounds__(kWGThreads) void k_sum_list(ListArgs a) {
-  build_sum_list(a, static_cast<uint64_t>(blockIdx.x) * kWavesPerWG + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+  build_sum_list(a, static_cast<uint64_t>(xcd_spread(blockIdx.x, 0, gridDim.x)) * kWavesPerWG +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
                  static_cast<uint64_t>(gridDim.x) * kWavesPerWG);
 }
 }  // namespace
@@ -2676,7 +2687,8 @@ int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask
     if (int rc = make_list_args(L, row_masks, count, mask_stride, list, &a.list)) return rc;
     const uint64_t units = list_units_host(a.list);
     const uint64_t wgs = (units + kPlanWaves - 1) / kPlanWaves;
-    a.list_wgs = static_cast<uint32_t>(wgs < 512 ? wgs : 512);
+    // (a multiple of 8 from 8 up, so xcd_spread gives each XCD whole row groups; spare workgroups find no unit)
+    a.list_wgs = static_cast<uint32_t>(wgs < 512 ? (wgs >= 8 ? (wgs + 7) / 8 * 8 : wgs) : 512);
   }
   const unsigned grid = a.nchunks + chain_wgs + a.list_wgs;
   hipStream_t st = S(stream);

@@ -60,11 +60,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc_round.json"))
     ap.add_argument("--workdir", default=os.path.join(ROOT, "gpurun_out", "pmc_round"))
+    ap.add_argument("--only", default="", help="only the cases whose filter contains this")
     a = ap.parse_args()
     a.out, a.workdir = os.path.abspath(a.out), os.path.abspath(a.workdir)
     os.makedirs(a.workdir, exist_ok=True)
     res = {}
     for case, kernel in CASES:
+        if a.only and a.only not in case:
+            continue
         tag = case.split()[0] + "_" + str(abs(hash(case)) % 1000)
         alg = os.path.join(a.workdir, tag + "_alg.json")
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "tune_round_r03.py"), "--only", case, "--rounds",

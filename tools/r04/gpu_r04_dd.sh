@@ -1,8 +1,8 @@
 # Round 4: one side stream at world 1 by default: the whole -m gpu suite, config 5 at its shape and smoke
-# (tools/gpu_r04_final.sh), then the world-1 round (3 runs) and the in-process configurations.
+# (tools/r04/gpu_r04_final.sh), then the world-1 round (3 runs) and the in-process configurations.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-bash tools/gpu_r04_final.sh r04final5
+bash tools/r04/gpu_r04_final.sh r04final5
 O=gpurun_out/r4dd
 mkdir -p $O
 export MASTER_ADDR=127.0.0.1 RANK=0 LOCAL_RANK=0 WORLD_SIZE=1

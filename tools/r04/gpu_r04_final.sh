@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4 final check on one MI355X: the whole -m gpu suite, config 5 at its own shape, smoke (the bench lines and
-# profiles are tools/gpu_bench_r04.sh).  Each GPU step under its own limit; later steps run only if the suite ended
+# profiles are tools/r04/gpu_bench_r04.sh).  Each GPU step under its own limit; later steps run only if the suite ended
 # normally (passed, or tests failed: rc 0 / 1).
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
@@ -19,4 +19,4 @@ rc=$?
 echo "suite rc=$rc" >> $O/tests_c5.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
-# (the bench lines and profiles: tools/gpu_bench_r04.sh, a call of its own)
+# (the bench lines and profiles: tools/r04/gpu_bench_r04.sh, a call of its own)

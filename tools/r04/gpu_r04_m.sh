@@ -1,4 +1,4 @@
-# Round 4: the pair list on 16-row units, the round-gap study, then the final test check (tools/gpu_r04_final.sh).
+# Round 4: the pair list on 16-row units, the round-gap study, then the final test check (tools/r04/gpu_r04_final.sh).
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r4m
@@ -6,4 +6,4 @@ mkdir -p $O
 timeout -k 10 300 python3 -u tools/tune_round_r03.py > $O/tune_round.log 2>&1
 timeout -k 10 240 python3 -u tools/tune_shard_r04.py > $O/shard.log 2>&1
 timeout -k 10 240 python3 -u tools/round_gap_r04.py > $O/gap.log 2>&1
-bash tools/gpu_r04_final.sh r04final
+bash tools/r04/gpu_r04_final.sh r04final

@@ -9,4 +9,4 @@ timeout -k 10 200 python -u -m pytest -x -v -m gpu --timeout 120 --timeout-metho
 timeout -k 10 200 python3 -u tools/tune_round_r03.py > $O/tune_round.log 2>&1
 timeout -k 10 200 python3 -u tools/tune_shard_r04.py > $O/shard.log 2>&1
 timeout -k 10 200 python3 -u tools/round_gap_r04.py > $O/gap.log 2>&1
-bash tools/gpu_r04_final.sh r04final
+bash tools/r04/gpu_r04_final.sh r04final

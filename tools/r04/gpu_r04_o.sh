@@ -1,5 +1,5 @@
 # Round 4: the round-gap study with stream write/wait-value cases, then the round kernels' PMC traffic
-# (tools/gpu_r04_pmc_round.sh's second step).
+# (tools/r04/gpu_r04_pmc_round.sh's second step).
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r4o

@@ -9,7 +9,7 @@ twice:
                    the plan's side stream, RCCL calls): the N > 1 layout
   general / created
 Prints microseconds per round and the headline kernel's step for reference.
-usage: python tools/round_inproc_r05.py [--steps 200] [--torch-group]"""
+usage: python tools/round_inproc_r05.py [--steps 200] [--reps 2] [--torch-group]"""
 import argparse
 import json
 import os
@@ -42,6 +42,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--torch-group", action="store_true")
+    ap.add_argument("--reps", type=int, default=2, help="interleaved repetitions of the four layouts")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -60,7 +61,7 @@ def main():
     plan = ops.ScanSumPlan(L, 1, device=dev, fused=True)
     launches = [plan.bind(xs[0], out, null) for xs, out in sets]
     res = {}
-    for rep in range(2):
+    for rep in range(a.reps):
         for layout in ("solo", "general"):
             eng.test_world1_round(layout == "general")
             for sname, st in (("null", null), ("created", created)):
