@@ -3,6 +3,7 @@
 # (config 4's sum on one GPU), config 5 (host resident, N=1), the N>1 round at world 1 under torch.distributed.run;
 # rocprofv3 kernel stats of configs 2 and 3, and PMC HBM traffic of configs 2 and 3.  Chained with &&.
 set -e
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $GRAFT_REPO_ROOT/gpurun_out/smoke_r05.log 2>&1
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-bench_r05}
