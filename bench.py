@@ -187,6 +187,14 @@ def scan_only_bytes(L: Layout) -> int:
     return L.nbytes + L.nb * 8 + L.rows * 8
 
 
+def one_rank_round_bytes(L: Layout, bm) -> int:
+    """The one-rank round's single launch (omr_worker_scan_tally_f32): fused_bytes, plus one 8-byte tally slot per
+    workgroup written, and the previous round's slots read by workgroup 0 to publish its counts (no row masks)."""
+    from omr import _lib
+    slots = int(_lib.load().omr_tally_slots(L.n, L.block_size, L.num_lanes, L.num_threads))
+    return fused_bytes(L, bm) + 2 * slots * 8
+
+
 def scan_pack_bytes(L: Layout, bm: np.ndarray, rank: int, world: int) -> int:
     """The round's worker scan with the fused pack (omr_worker_scan_pack_f32): scan_only_bytes plus the rank's
     non-zero blocks of the other shards written to their send streams, and the position-table entries of the
@@ -332,7 +340,7 @@ def round_world1(args, L: Layout, sets, dev, stream, bm=None, torch_group=True):
     eng.close()
     scan_ms = stages["scan"]
     # a one-rank round's worker scan writes the shard sums itself (0.0f + x over the write set: omr_sparse_round_f32)
-    sb = (fused_bytes(L, bm) + L.rows * 8) if bm is not None else scan_only_bytes(L)
+    sb = one_rank_round_bytes(L, bm) if bm is not None else scan_only_bytes(L)
     return {"ms_per_round": round(dt * 1e3, 5), "value": round(L.nbytes / dt / 1e9, 2), "unit": "GB/s",
             "mode": "reduce-scatter (the N>1 bench default), deferred pipeline (OMR_ROUND_DEFER)",
             "transport": "RCCL, one-rank communicator made in this process, no torch group (no peers)",
@@ -581,15 +589,20 @@ def main():
     kev = [(timing.Event(), timing.Event()) for _ in range(args.steps)]
     every = max(1, args.event_every)
     one_kernel = (not dist_mode) and m == 1 and args.kernel == "fused"
+    # a one-rank round is ONE launch on the caller's stream (omr_worker_scan_tally_f32): timed as the headline is,
+    # events around all K rounds, instead of per-round stage events (a timing record between two rounds holds the next
+    # round's launch back 4.6-6 us, profiles/r05/final/w1_trace/; at one rank every other stage is empty)
+    one_launch = dist_mode and ranks == 1 and args.dist_mode != "dense"
     span = (timing.Event(), timing.Event())  # single-kernel step: the kernel's mean duration over the timed region
     if dist_mode:
         engine.host_stats(reset=True)
     t0 = time.perf_counter()
-    if one_kernel:
+    if one_kernel or one_launch:
         span[0].record(stream)
     for i in range(args.steps):
-        step(args.warmup + i, None if one_kernel else (kev[i] if i % every == 0 else None), timed_region=True)
-    if one_kernel:
+        step(args.warmup + i, None if (one_kernel or one_launch) else (kev[i] if i % every == 0 else None),
+             timed_region=True)
+    if one_kernel or one_launch:
         span[1].record(stream)
     host_wait_us = engine.host_stats(reset=True)[0] if dist_mode else 0.0  # (the timed calls' blocked time only)
     join()
@@ -611,7 +624,8 @@ def main():
     if dist_mode:
         kernel_name = ("k_scan1f (round worker scan: flags + next + row masks + the fused pack of the other shards' "
                        "blocks)" if engine_fused else
-                       "k_scan1f (one-rank round's worker scan: flags + next + row masks + the shard sums)"
+                       "k_scan1f (the one-rank round's single launch: flags + next + the shard sums + per-workgroup "
+                       "counts)"
                        if ranks == 1 and args.dist_mode != "dense" else
                        "k_scan1f (round worker scan: flags + next + row masks, no out)")
     scan_ms_dist = None
@@ -639,16 +653,20 @@ def main():
                     "host_issue_ms_per_call": round((host_s[0] * 1e6 - host_wait_us) / max(1, host_s[1]) * 1e-3, 5)}
     if not dist_mode:
         kev = kev[::every]
-    if one_kernel:  # every step is exactly one k_scan1f launch: events around all K steps, divided by K
+    if one_kernel or one_launch:  # every step is exactly one k_scan1f launch: events around all K steps, divided by K
         kms = span[0].elapsed_time(span[1]) / args.steps
     elif scan_ms_dist is not None:
         kms = scan_ms_dist
     else:
         kms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
+    if one_launch and exchange is not None:  # (no stage events in a one-rank run: its one stage is the launch)
+        exchange["stages_ms"]["scan"] = round(kms, 5)
+        exchange["timing"] = ("a one-rank round is one launch on the caller's stream: no per-round stage events; the "
+                              "scan stage is the roofline's kernel_ms (events around all K rounds)")
     if True:
         if dist_mode:
             if ranks == 1 and args.dist_mode != "dense":  # one rank: the scan writes the shard sums itself
-                kbytes = fused_bytes(L, bitmaps[0]) + L.rows * 8
+                kbytes = one_rank_round_bytes(L, bitmaps[0])
             else:
                 kbytes = (scan_pack_bytes(L, bitmaps[0], rank, ranks) if engine_fused else scan_only_bytes(L))
         elif m == 1 and args.kernel == "fused":
@@ -669,6 +687,8 @@ def main():
                                "the timed launches" + (" (all K, divided by K)" if one_kernel else
                                                        f" (every {every}th step)")
                                if scan_ms_dist is None else
+                               ("fence-free HIP events on the caller's stream around all K timed rounds, divided by K "
+                                "(a one-rank round is one launch)") if one_launch else
                                (f"HIP events on the round's stream around its worker scan, in every {every}th timed "
                                 f"round (inside the timed region, omr_ar_plan_timings)")),
                     "traffic_source": ("rocprofv3 PMC 2*FETCH_SIZE+WRITE_SIZE per launch, "

@@ -337,7 +337,7 @@ typedef struct omr_sum_list {
 } omr_sum_list;
 int omr_sum_list_geometry(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, uint64_t row_begin,
                           uint64_t row_end, uint32_t count, uint64_t* units, uint32_t* capacity);
-/* Build the list in a launch of its own (worker c's array at row_masks + c * mask_stride, as omr_round_plan_ex). */
+/* Build the list in a launch of its own (worker c's array at row_masks + c * mask_stride, as omr_round_plan_list). */
 int omr_sum_list_build(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t n,
                        uint32_t block_size, uint32_t num_lanes, uint32_t num_parts, const omr_sum_list* list,
                        omr_stream_t stream);

@@ -223,7 +223,7 @@ int omr_ar_plan_timings(omr_ar_plan* plan, float* scan_ms, float* exchange_ms, u
 int omr_ar_plan_stage_timings(omr_ar_plan* plan, float* stage_ms, uint64_t* bytes_out, uint64_t* bytes_in,
                               uint32_t* rounds);
 /* 1 if the plan's worker scan packs the blocks for the exchange itself (omr_worker_scan_pack_f32: every shard is
- * whole column segments of the scan, world > 1, OMR_PACK_MOVE unset), 0 if a separate pack pass does
+ * whole column segments of the scan, world > 1), 0 if a separate pack pass does
  * (omr_move_blocks_f32). */
 int omr_ar_plan_fused_pack(const omr_ar_plan* plan);
 /* Device memory the plan holds (bytes), through its transport: per round set the masks, write set, prefixes and pair

@@ -1537,9 +1537,12 @@ int timed_slot(omr_ar_plan* p, int* slot) {
   const int k = static_cast<int>(p->timed_next++ % omr_ar_plan::kTimed);
   if (p->timed_next - p->timed_first > omr_ar_plan::kTimed) p->timed_first = p->timed_next - omr_ar_plan::kTimed;
   omr_ar_plan::Timed& t = p->timed[k];
+  // timing-only events without the system-scope fence (as bench.py's own): a fenced record on the caller's stream
+  // held the world-1 round's next scan back 6 us (profiles/r05/final/w1_trace/), 1.2 us per round at one timed round
+  // in ten
   if (t.s0 == nullptr)
     for (hipEvent_t* e : {&t.s0, &t.s1, &t.x0, &t.x1, &t.q0, &t.q1, &t.a1})
-      TRY(hip_check(hipEventCreate(e), "hipEventCreate"));
+      TRY(hip_check(hipEventCreateWithFlags(e, hipEventDisableSystemFence), "hipEventCreate"));
   t.scan = t.xchg = t.prep = t.agg = false;
   t.open = true;
   *slot = k;

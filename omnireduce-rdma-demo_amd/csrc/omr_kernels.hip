@@ -296,8 +296,11 @@ constexpr uint32_t kPackGroupRows = 64;         // the position table's row gran
 
 constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
 
+// TALLY: at most 96 VGPRs (five waves per SIMD), as the headline form has (92): its tally registers had taken the
+// one-rank round's launch to 106, and 16-wave workgroups then could not overlap the next one on a CU by even one wave.
 template <int VEC, int WAVES, int LOADS = 16, int SKIP = 0, bool PACK = false, bool TALLY = false>
-__global__ __launch_bounds__(64 * WAVES) void k_scan1f(FusedArgs a) {
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(TALLY ? 5 : 1, 8))) void k_scan1f(
+    FusedArgs a) {
   constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
   static_assert(RB >= 1 && RB <= 32 && 32 % RB == 0, "a batch's bits lie inside one 32-bit word");
   [[maybe_unused]] constexpr uint32_t B4 = 64 * VEC;  // 16-byte vectors per block
