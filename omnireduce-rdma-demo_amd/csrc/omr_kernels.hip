@@ -296,8 +296,9 @@ constexpr uint32_t kPackGroupRows = 64;         // the position table's row gran
 
 constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor range: the store is discarded
 
-// TALLY: at most 96 VGPRs (five waves per SIMD), as the headline form has (92): its tally registers had taken the
-// one-rank round's launch to 106, and 16-wave workgroups then could not overlap the next one on a CU by even one wave.
+// TALLY: at most 96 VGPRs (five waves per SIMD), as the headline form has (92); its tally registers had taken the
+// one-rank round's launch to 106 (four waves per SIMD).  Capped: 48.03 / 49.80 us in / out of place against 48.65 /
+// 50.14, the headline 47.73 / 49.43 (profiles/r05/timing/vgpr96/tally.log, profiles/r05/plan_v5/tally.log).
 template <int VEC, int WAVES, int LOADS = 16, int SKIP = 0, bool PACK = false, bool TALLY = false>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(TALLY ? 5 : 1, 8))) void k_scan1f(
     FusedArgs a) {
