@@ -2041,6 +2041,25 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
     }
     return launch_status("k_scan1f (8 waves)");
   }
+  // Short segments (small tensors: config 1's 4 MiB has 8 rows per partition): one wave holds a whole segment, and
+  // 16-wave workgroups would leave 15 idle while taking a CU each (512 of them run in two turns on 256 CUs).
+  // Workgroups of one wave per 16-row batch instead.
+  const uint32_t rb = static_cast<uint32_t>(kFusedLoads) / L.vec;  // rows per batch
+  if (f.S <= 4 * rb) {
+    const int w = f.S <= rb ? 1 : (f.S <= 2 * rb ? 2 : 4);
+    switch (L.vec * 8 + w) {
+      case 9: k_scan1f<1, 1, kFusedLoads><<<grid, 64, 0, st>>>(a); break;
+      case 10: k_scan1f<1, 2, kFusedLoads><<<grid, 128, 0, st>>>(a); break;
+      case 12: k_scan1f<1, 4, kFusedLoads><<<grid, 256, 0, st>>>(a); break;
+      case 17: k_scan1f<2, 1, kFusedLoads><<<grid, 64, 0, st>>>(a); break;
+      case 18: k_scan1f<2, 2, kFusedLoads><<<grid, 128, 0, st>>>(a); break;
+      case 20: k_scan1f<2, 4, kFusedLoads><<<grid, 256, 0, st>>>(a); break;
+      case 33: k_scan1f<4, 1, kFusedLoads, 1><<<grid, 64, 0, st>>>(a); break;
+      case 34: k_scan1f<4, 2, kFusedLoads, 1><<<grid, 128, 0, st>>>(a); break;
+      default: k_scan1f<4, 4, kFusedLoads, 1><<<grid, 256, 0, st>>>(a); break;
+    }
+    return launch_status("k_scan1f (short segments)");
+  }
   switch (L.vec) {
     case 1: k_scan1f<1, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;
     case 2: k_scan1f<2, kFusedWaves, kFusedLoads><<<grid, T, 0, st>>>(a); break;

@@ -327,6 +327,11 @@ def assert_fused_parity(x, L, out_init=None, reps=2):
     (8 << 20, 512, 8, 0.49),       # B = 512
     (4 << 20, 256, 8, 0.0),        # all zero: every chain is the sentinel
     (4 << 20, 256, 8, 1.0),        # dense
+    # short segments (round 5): workgroups of 1, 2 or 4 waves, one per 16-row batch (k_scan1f's small-tensor shape)
+    (8 << 20, 256, 8, 0.2),        # S = 64: 4-wave workgroups
+    (1 << 20, 512, 8, 0.5),        # B = 512, S = 8: one wave
+    (2 << 20, 1024, 8, 0.3),       # B = 1024, S = 16: 4-wave workgroups of 4-row batches
+    (1 << 20, 256, 8, 1.0),        # config 1 itself, dense
 ])
 def test_fused_parity(gpu, n, B, parts, density):
     L = Layout(n=n, block_size=B, num_threads=parts)
