@@ -104,10 +104,11 @@ int omr_dist_poll(omr_dist* d);
  * half). */
 int omr_dist_inject_fault(omr_dist* d, int64_t after_pieces);
 int omr_dist_inject_allgather_fault(omr_dist* d);
-/* Test hook (on: 1): a one-rank group runs the multi-rank round's code path -- worker scan, mask all-gather, plan and
- * exchange on the side stream -- instead of the one-launch round, and an RCCL transport issues its all-gather, exchange
- * and reduce-scatter as RCCL calls instead of as copies.  So the fault tests reach RCCL's group and ncclCommAbort paths,
- * and the N > 1 round's stream layout can be timed, on a one-GPU box. */
+/* Test hook (on: 1): a one-rank group runs the multi-rank round's code path -- worker scan, mask all-gather and plan on
+ * the plan stream, exchange on the exchange stream -- instead of the one-launch round, and an RCCL transport issues its
+ * all-gather, exchange and reduce-scatter as RCCL calls instead of as copies.  Plans made after the call also take
+ * the N > 1 round's two side streams.  So the fault tests reach RCCL's group and ncclCommAbort paths, and the N > 1
+ * round's stream layout can be timed, on a one-GPU box. */
 int omr_dist_test_world1_round(omr_dist* d, int on);
 
 /* Workspaces for tensors of n floats on the layout (block_size, num_lanes, num_parts); allocated on the current

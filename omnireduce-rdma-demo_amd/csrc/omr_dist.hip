@@ -1017,11 +1017,11 @@ struct omr_ar_plan {
                                     // and shard sum run in order on the side stream
   int cur = 0;                      // the set the next round fills
   int last_async = -1;              // set of the last asynchronous round (for join)
-  // Asynchronous rounds run their steps after the worker scan on ONE side stream, in the order they are issued:
-  // round k-2's exchange and sums, then round k's all-gather and plan (round 5; two side streams before).  The caller's
-  // stream runs only the scans.
-  hipStream_t ps = nullptr;         // the side stream (cs == ps)
-  hipStream_t cs = nullptr;
+  // Asynchronous rounds run their steps after the worker scan on side streams: the plan stream (all-gather, plan) and,
+  // at N > 1, the exchange stream (exchange, shard sums [, return trip]); a deferred call issues round k-2's exchange
+  // before round k's plan.  At world 1 both are one stream (cs == ps).  The caller's stream runs only the scans.
+  hipStream_t ps = nullptr;         // the plan stream
+  hipStream_t cs = nullptr;         // the exchange stream (== ps at world 1)
   hipStream_t tail = nullptr;       // the stream of the last asynchronous round's last work (the bucket write-back)
   uint64_t* bounds_dev = nullptr;
   uint64_t* counts_host = nullptr;  // [kSets][M+1][A+1] per set: (seq << 32) | prefix[a][bounds[s]], pinned memory the
@@ -1343,7 +1343,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     bool idle = false;
     while (!idle) {
       idle = true;
-      for (hipStream_t s : {p->ps, p->s_in, p->s_out})
+      for (hipStream_t s : {p->ps, p->cs, p->s_in, p->s_out})
         if (s != nullptr && hipStreamQuery(s) == hipErrorNotReady) idle = false;
       if (idle || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(p->d->timeout_ms)) break;
       std::this_thread::sleep_for(std::chrono::microseconds(200));
@@ -1367,6 +1367,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     for (hipEvent_t e : {st.scanned, st.ready, st.done})
       if (e) (void)hipEventDestroy(e);
   }
+  if (p->cs && p->cs != p->ps) (void)hipStreamDestroy(p->cs);
   if (p->ps) (void)hipStreamDestroy(p->ps);
   for (int r = 0; r < omr_ar_plan::kStage; ++r) {
     p->d->release(p->stage[r]);
@@ -1465,13 +1466,17 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     for (hipEvent_t* e : {&st.scanned, &st.ready, &st.done})
       A(hip_check(hipEventCreateWithFlags(e, evflags), "hipEventCreate"));
   }
-  // The side stream: every asynchronous round's steps after its scan, in issue order (round 5).  Each stream the
-  // process makes takes one of its hardware queues (GPU_MAX_HW_QUEUES, 4 on the box) round robin, and streams that
-  // share a queue run one after the other: with two side streams the world-1 round ran 2x slower in the stream orders
-  // whose side stream shared the caller's queue (profiles/r04/inproc/).  One side stream halves that exposure, and the
-  // one-rank round (solo) uses none.
+  // The side streams.  Each stream the process makes takes one of its hardware queues (GPU_MAX_HW_QUEUES, 4 on the box)
+  // round robin, and streams that share a queue run one after the other: with two side streams the world-1 round ran
+  // 2x slower in the stream orders whose side stream shared the caller's queue (profiles/r04/inproc/).  World 1 has
+  // no exchange, so it keeps one side stream (and the one-rank round uses none); at N > 1 the exchange gets its own,
+  // so round k-2's exchange runs beside round k's all-gather and plan instead of before them: as 4 IPC ranks on one
+  // GPU one side stream took 2.18 ms per round (profiles/r05/ipc_cliff/ipc_w4.json) against 1.36-1.43 with two
+  // (round 4).  The multi-rank test hook at world 1 (omr_dist_test_world1_round) takes the N > 1 layout.
   A(hip_check(hipStreamCreateWithFlags(&p->ps, hipStreamNonBlocking), "hipStreamCreate"));
   p->cs = p->ps;
+  if (N > 1 || p->d->world1_general)
+    A(hip_check(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking), "hipStreamCreate"));
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, evflags), "hipEventCreate"));
   A(dev_alloc(p->d, &p->bounds_dev, NA + 1, DB));
   if (N > 1 && p->worker()) {
@@ -1665,6 +1670,9 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
   const uint32_t NS = static_cast<uint32_t>(NA + 1);  // count columns per array (shard bounds)
   const uint64_t* const tagged = p->counts_host + static_cast<size_t>(si) * (M + 1) * NS;
   uint32_t counts[(OMR_MAX_WORKERS + 1) * (OMR_MAX_WORKERS + 2)];
+  // at N > 1 the exchange stream waits for this round's plan on the plan stream (a deferred round's `ready` has
+  // normally fired long before: then no wait is queued)
+  if (async && p->cs != p->ps) TRY(wait_ev(p->cs, S.ready));
   const hipStream_t xs = async ? p->cs : st;
   ht_of(p).lap("2:cs wait ready");
   const omr_stream_t xstream = reinterpret_cast<omr_stream_t>(xs);
@@ -1859,7 +1867,8 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
   // a threaded round that is not deferred finishes the deferred ones first (rounds complete in call order)
   if (j.flush_first) TRY(flush_pending(p, j.st, nullptr, nullptr));
   // Deferred: the second half of the round kDeferDepth calls back goes first, on the side stream, so its exchange
-  // runs beside this round's scan instead of queueing behind this round's wait for it (round 5: one side stream).
+  // runs beside this round's scan (and, at N > 1, on the exchange stream beside this round's plan) instead of queueing
+  // behind this round's wait for it.
   // Its counts have long been in host memory, so the host does not wait either.
   if (j.defer && p->npend >= p->defer_depth) TRY(issue_oldest(p, sent_blocks, union_blocks));
   else if (j.defer) {

@@ -156,7 +156,8 @@ class CppSparseAllreduce:
 
     def test_world1_round(self, on: bool = True):
         """Test hook (omr_dist_test_world1_round): a one-rank group runs the multi-rank round's code path (all-gather,
-        plan, exchange on the side stream) and an RCCL transport issues its collectives as RCCL calls."""
+        plan, exchange) and an RCCL transport issues its collectives as RCCL calls.  Plans made after it also take the
+        N > 1 stream layout (a plan stream and an exchange stream; replan() to apply it to this engine's plan)."""
         _check(load().omr_dist_test_world1_round(self._d, int(on)), "omr_dist_test_world1_round")
 
     def replan(self, L: Optional[Layout] = None):

@@ -103,15 +103,19 @@ def _sleep_cycles_for(seconds):
     return int(per_s * seconds)
 
 
-def test_rccl_world1_calls_round(gpu):
+@pytest.mark.parametrize("layout", ["one side stream", "N>1 streams"])
+def test_rccl_world1_calls_round(gpu, layout):
     """With RCCL calls kept at world 1 (omr_dist_test_world1_round), the rounds that use the transport at world 1 -- the
     dense stand-in (ncclReduceScatter) and a bucket round (ncclAllGather of the masks, an empty grouped exchange) --
-    are bit-exact against the oracle."""
+    are bit-exact against the oracle; on the plan made before the hook (one side stream) and on one made after it (the
+    N > 1 layout: the exchange stream waits for the plan stream)."""
     B = 256
     L = Layout(n=1 << 20, block_size=B)
     eng = cdist.CppSparseAllreduce(L, gpu, transport="rccl1")
     try:
         eng.test_world1_round(True)
+        if layout == "N>1 streams":
+            eng.replan()
         x = oracle.fill(oracle.gen_bitmap(0, 0.3, L.nb), B, mode=1, seed=4)
         f = oracle.flags_from_data(x, B)
         exp = x.copy()

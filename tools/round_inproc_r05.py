@@ -5,8 +5,8 @@ communicator (optionally after a one-rank torch nccl group, as bench.py's N>1 pa
 twice:
   solo / null      the one-launch world-1 round (omr_worker_scan_tally_f32) on the caller's null stream
   solo / created   the same on a stream created after the plan
-  general / null   the multi-rank round's path at world 1 (omr_dist_test_world1_round: all-gather, plan, exchange on
-                   the plan's side stream, RCCL calls): the N > 1 layout
+  general / null   the multi-rank round's path at world 1 (omr_dist_test_world1_round: all-gather and plan on the plan
+                   stream, exchange on the exchange stream, RCCL calls): the N > 1 layout
   general / created
 Prints microseconds per round and the headline kernel's step for reference.
 usage: python tools/round_inproc_r05.py [--steps 200] [--reps 2] [--torch-group]"""
@@ -64,6 +64,8 @@ def main():
     for rep in range(a.reps):
         for layout in ("solo", "general"):
             eng.test_world1_round(layout == "general")
+            eng.replan()  # (the hook takes effect on plans made after it: general = the N>1 stream layout)
+            created = torch.cuda.Stream(dev)  # a stream created after the plan
             for sname, st in (("null", null), ("created", created)):
                 with torch.cuda.stream(st):
                     us = round_loop(eng, sets, st, a.steps)
