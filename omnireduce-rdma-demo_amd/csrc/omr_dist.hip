@@ -1916,6 +1916,20 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
     if (N > 1 && (mode & ~(kModeSolo | kModeTally)) != OMR_ROUND_DENSE_REDUCE_SCATTER && p->worker() &&
         !p->fused_pack) {
       const uint64_t r0 = p->colocated ? p->bounds[me] : 0, r1 = p->colocated ? p->bounds[me + 1] : 0;
+      // the send buffer is free once the round kPackBufs calls back is through with it (its exchange, and an
+      // all-reduce's return trip into it, on the exchange stream): this stream waits for that round's `done` unless
+      // the two are one stream (the fused-pack scan does the same wait itself)
+      if (qs != p->cs) {
+        bool w;
+        int ds;
+        {
+          std::lock_guard<std::mutex> g(p->mu);
+          w = p->pk[j.pki].scan_wait;
+          ds = p->pk[j.pki].done_set;
+          p->pk[j.pki].scan_wait = false;
+        }
+        if (w) TRY(wait_ev(qs, p->set[ds].done));
+      }
       TRY(omr_check(omr_move_blocks_f32(x, p->pk[j.pki].buf, 0, S.masks_all + static_cast<uint64_t>(me) * p->mstride,
                                         S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,
                                         r1, qstream), "omr_move_blocks_f32 pack"));
