@@ -87,6 +87,9 @@ def parse(argv=None):
                         "untimed probe rounds faster (max over ranks; a round whose host issue time reaches its GPU "
                         "time gains from the thread)")
     p.add_argument("--pipe-probe", type=int, default=12, help="--dist-pipe auto: untimed rounds per probe trial")
+    p.add_argument("--side-streams", choices=("1", "2", "auto"), default="auto",
+                   help="N>1: the round's side streams (omr_ar_plan_set_side_streams): one, two (plan + exchange), or "
+                        "auto = measured on the node by the probe, with the pipeline mode")
     p.add_argument("--dist-sync", action="store_true", help="same as --dist-pipe sync")
     p.add_argument("--dist-transport", choices=("rccl", "ipc"), default="rccl",
                    help="N>1 round transport: RCCL over xGMI, one process per GPU (the product path), or HIP IPC "
@@ -562,14 +565,26 @@ def main():
     torch.cuda.synchronize()
     if dist_mode and pipe == "auto" and args.pipe_probe < 1:
         pipe = "defer"
-    if dist_mode and pipe == "auto":
-        # untimed probe: the same rounds under defer and thread, alternated twice; every rank takes the candidate
-        # with the smaller max-over-ranks round time (so all ranks run one mode)
-        best = {"defer": float("inf"), "thread": float("inf")}
+    side = None  # the side streams the timed rounds ran on (N>1: measured on the node)
+    sides = ([2, 1] if args.side_streams == "auto" else [int(args.side_streams)]) if dist_mode and ranks > 1 else []
+    if len(sides) > 1 and args.pipe_probe < 1:  # (no probe rounds: the library's default layout)
+        sides = [2]
+    if dist_mode and ranks > 1 and pipe != "auto" and len(sides) == 1:
+        engine.set_side_streams(sides[0])
+        side = sides[0]
+    if dist_mode and (pipe == "auto" or len(sides) > 1):
+        # untimed probe: the same rounds under each candidate (pipeline mode defer / thread, and at N>1 one or two side
+        # streams), alternated twice; every rank takes the candidate with the smaller max-over-ranks round time (so
+        # all ranks run one mode)
+        pipes = ("defer", "thread") if pipe == "auto" else (pipe,)
+        cands = [(pp, sd) for sd in (sides or [None]) for pp in pipes]
+        best = {c: float("inf") for c in cands}
         k = args.warmup
         for _ in range(2):
-            for cand in ("defer", "thread"):
-                pipe = cand
+            for cand in cands:
+                pipe = cand[0]
+                if cand[1] is not None:
+                    engine.set_side_streams(cand[1])
                 torch.distributed.barrier()
                 t0 = time.perf_counter()
                 for _ in range(args.pipe_probe):
@@ -580,8 +595,11 @@ def main():
                 dt = torch.tensor([(time.perf_counter() - t0) / args.pipe_probe], dtype=torch.float64, device=tdev)
                 torch.distributed.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
                 best[cand] = min(best[cand], float(dt.item()))
-        pipe = min(best, key=best.get)
-        pipe_probe = {c: round(v * 1e3, 5) for c, v in best.items()}
+        pipe, side = min(best, key=best.get)
+        if side is not None:
+            engine.set_side_streams(side)
+        pipe_probe = {(c[0] if c[1] is None else f"{c[0]}, {c[1]} side stream{'s' if c[1] > 1 else ''}"):
+                      round(v * 1e3, 5) for c, v in best.items()}
         torch.distributed.barrier()
         torch.cuda.synchronize()
 
@@ -699,6 +717,7 @@ def main():
             roofline["step_frac"] = round(sbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
 
     if dist_mode:
+        engine_side_streams = engine.side_streams
         engine.close()  # every rank (the IPC transport's board is released when the last rank leaves)
     if rank != 0:
         if dist_mode:
@@ -750,6 +769,7 @@ def main():
     if exchange is not None:
         line["exchange"] = exchange
         line["exchange"]["pipe"] = pipe
+        line["exchange"]["side_streams"] = engine_side_streams
         if pipe_probe is not None:
             line["exchange"]["pipe_probe_ms_per_round"] = pipe_probe
     if not dist_mode and m == 1 and not args.no_round:

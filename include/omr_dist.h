@@ -235,6 +235,14 @@ int omr_ar_plan_fused_pack(const omr_ar_plan* plan);
 uint64_t omr_ar_plan_device_bytes(const omr_ar_plan* plan);
 /* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
 int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
+/* The asynchronous rounds' side streams: 2 (the default at world > 1) = a plan stream for the mask all-gather and the
+ * plan, an exchange stream for the exchange, the shard sums and the return trip, so round k-2's exchange runs beside
+ * round k's plan; 1 (the default at world 1) = everything after the scan on one stream, in issue order.  Which is
+ * faster depends on how the process's streams share its hardware queues: bench.py's N>1 lines measure
+ * both on the node.  Issues every queued round's remaining steps first; rounds after the call use the new layout.
+ * Returns OMR_EINVAL for n other than 1 or 2. */
+int omr_ar_plan_set_side_streams(omr_ar_plan* plan, int n);
+int omr_ar_plan_side_streams(const omr_ar_plan* plan);
 /* Join, then wait on the host until `stream` has run every round issued so far: the bounded counterpart of a stream
  * synchronise for a rank whose rounds wait on its peers.  Past the transport's deadline (or on a failure signal) the
  * transport is aborted and OMR_ETIMEDOUT / the error is returned, instead of blocking on a peer that is gone. */

@@ -1021,7 +1021,9 @@ struct omr_ar_plan {
   // at N > 1, the exchange stream (exchange, shard sums [, return trip]); a deferred call issues round k-2's exchange
   // before round k's plan.  At world 1 both are one stream (cs == ps).  The caller's stream runs only the scans.
   hipStream_t ps = nullptr;         // the plan stream
-  hipStream_t cs = nullptr;         // the exchange stream (== ps at world 1)
+  hipStream_t cs = nullptr;         // the exchange stream in use: xstream, or ps (world 1, omr_ar_plan_set_side_streams)
+  hipStream_t xstream = nullptr;    // the dedicated exchange stream (N > 1, or made by omr_ar_plan_set_side_streams)
+  hipEvent_t switch_ev = nullptr;   // orders the exchange stream's work across a switch of it
   hipStream_t tail = nullptr;       // the stream of the last asynchronous round's last work (the bucket write-back)
   uint64_t* bounds_dev = nullptr;
   uint64_t* counts_host = nullptr;  // [kSets][M+1][A+1] per set: (seq << 32) | prefix[a][bounds[s]], pinned memory the
@@ -1343,7 +1345,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     bool idle = false;
     while (!idle) {
       idle = true;
-      for (hipStream_t s : {p->ps, p->cs, p->s_in, p->s_out})
+      for (hipStream_t s : {p->ps, p->xstream, p->s_in, p->s_out})
         if (s != nullptr && hipStreamQuery(s) == hipErrorNotReady) idle = false;
       if (idle || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(p->d->timeout_ms)) break;
       std::this_thread::sleep_for(std::chrono::microseconds(200));
@@ -1367,7 +1369,8 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     for (hipEvent_t e : {st.scanned, st.ready, st.done})
       if (e) (void)hipEventDestroy(e);
   }
-  if (p->cs && p->cs != p->ps) (void)hipStreamDestroy(p->cs);
+  if (p->switch_ev) (void)hipEventDestroy(p->switch_ev);
+  if (p->xstream) (void)hipStreamDestroy(p->xstream);
   if (p->ps) (void)hipStreamDestroy(p->ps);
   for (int r = 0; r < omr_ar_plan::kStage; ++r) {
     p->d->release(p->stage[r]);
@@ -1475,8 +1478,10 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   // (round 4).  The multi-rank test hook at world 1 (omr_dist_test_world1_round) takes the N > 1 layout.
   A(hip_check(hipStreamCreateWithFlags(&p->ps, hipStreamNonBlocking), "hipStreamCreate"));
   p->cs = p->ps;
-  if (N > 1 || p->d->world1_general)
-    A(hip_check(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking), "hipStreamCreate"));
+  if (N > 1 || p->d->world1_general) {
+    A(hip_check(hipStreamCreateWithFlags(&p->xstream, hipStreamNonBlocking), "hipStreamCreate"));
+    if (rc == 0) p->cs = p->xstream;
+  }
   A(hip_check(hipEventCreateWithFlags(&p->st_ev, evflags), "hipEventCreate"));
   A(dev_alloc(p->d, &p->bounds_dev, NA + 1, DB));
   if (N > 1 && p->worker()) {
@@ -2440,6 +2445,32 @@ int omr_ar_plan_join(omr_ar_plan* p, omr_stream_t stream) {
                 "hipStreamWaitEvent"));
   return 0;
 }
+
+int omr_ar_plan_set_side_streams(omr_ar_plan* p, int n) {
+  if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_set_side_streams: NULL");
+  if (n != 1 && n != 2) return derr(OMR_EINVAL, "ar_plan_set_side_streams: %d side streams (1 or 2)", n);
+  TRY(plan_check(p, "ar_plan_set_side_streams"));
+  if (n == 2 && p->xstream == nullptr)
+    TRY(plan_fail(p, hip_check(hipStreamCreateWithFlags(&p->xstream, hipStreamNonBlocking), "hipStreamCreate")));
+  hipStream_t want = n == 1 ? p->ps : p->xstream;
+  if (want == p->cs) return 0;
+  // every queued round's steps are issued first, on the old layout; then the new exchange stream (and the plan stream)
+  // start after everything the old exchange stream holds: the set and send-buffer events it recorded are covered
+  TRY(plan_fail(p, thread_drain(p)));
+  TRY(plan_fail(p, flush_pending(p, p->ps, nullptr, nullptr)));
+  if (p->switch_ev == nullptr)
+    TRY(plan_fail(p, hip_check(hipEventCreateWithFlags(&p->switch_ev, hipEventDisableTiming |
+                                                                             hipEventDisableSystemFence),
+                               "hipEventCreate")));
+  TRY(plan_fail(p, hip_check(hipEventRecord(p->switch_ev, p->cs), "hipEventRecord")));
+  TRY(plan_fail(p, hip_check(hipStreamWaitEvent(want, p->switch_ev, 0), "hipStreamWaitEvent")));
+  if (want != p->ps) TRY(plan_fail(p, hip_check(hipStreamWaitEvent(p->ps, p->switch_ev, 0), "hipStreamWaitEvent")));
+  p->cs = want;
+  if (p->tail != nullptr) p->tail = want;
+  return 0;
+}
+
+int omr_ar_plan_side_streams(const omr_ar_plan* p) { return p == nullptr ? 0 : (p->cs != p->ps ? 2 : 1); }
 
 int omr_ar_plan_wait(omr_ar_plan* p, omr_stream_t stream) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_wait: NULL");

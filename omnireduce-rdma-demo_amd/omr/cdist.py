@@ -62,6 +62,8 @@ def load():
         "omr_sparse_allreduce_f32": (i, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "omr_sparse_round_f32": (i, [vp, vp, vp, vp, vp, vp, i, vp, vp, vp]),
         "omr_ar_plan_join": (i, [vp, vp]),
+        "omr_ar_plan_set_side_streams": (i, [vp, i]),
+        "omr_ar_plan_side_streams": (i, [vp]),
         "omr_ar_plan_fused_pack": (i, [vp]),
         "omr_ar_plan_device_bytes": (u64, [vp]),
         "omr_dist_test_world1_round": (i, [vp, i]),
@@ -159,6 +161,16 @@ class CppSparseAllreduce:
         plan, exchange) and an RCCL transport issues its collectives as RCCL calls.  Plans made after it also take the
         N > 1 stream layout (a plan stream and an exchange stream; replan() to apply it to this engine's plan)."""
         _check(load().omr_dist_test_world1_round(self._d, int(on)), "omr_dist_test_world1_round")
+
+    def set_side_streams(self, n: int):
+        """1 or 2 side streams for the asynchronous rounds (omr_ar_plan_set_side_streams); returns the previous count."""
+        old = int(load().omr_ar_plan_side_streams(self._p))
+        _check(load().omr_ar_plan_set_side_streams(self._p, int(n)), "omr_ar_plan_set_side_streams")
+        return old
+
+    @property
+    def side_streams(self) -> int:
+        return int(load().omr_ar_plan_side_streams(self._p))
 
     def replan(self, L: Optional[Layout] = None):
         """Destroy the plan and make a new one on the same transport, of the same shape or of layout L (collective: every

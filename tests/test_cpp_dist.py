@@ -39,6 +39,8 @@ def dist_lib():
     L.omr_ar_plan_exchange_time.argtypes = [vp, vp, vp, vp]
     L.omr_ar_plan_device_bytes.restype = u64
     L.omr_ar_plan_device_bytes.argtypes = [vp]
+    L.omr_ar_plan_set_side_streams.argtypes = [vp, i]
+    L.omr_ar_plan_side_streams.argtypes = [vp]
     L.omr_dist_last_error.restype = ctypes.c_char_p
     return L
 
@@ -97,6 +99,73 @@ def test_cpp_round_loopback(gpu, world, B, density):
         assert (fl == f).all()
         assert (nx == oracle.next_offsets(f, L.n, B, L.num_lanes, 8)).all()
         assert (unx == un).all()
+
+
+@pytest.mark.parametrize("world,mode", [(3, 0), (4, 1), (5, 0)])
+def test_cpp_round_side_streams_switch(gpu, world, mode):
+    """Pipelined rounds (async | defer) with the side streams switched between them (omr_ar_plan_set_side_streams:
+    2 -> 1 -> 2, and ragged shards at world 3 and 5, where a pack pass on the plan stream reuses send buffers the
+    exchange stream read): every round's output bit-exact against the oracle, inputs different per round."""
+    B = 256
+    L = Layout(n=1 << 20, block_size=B)
+    D = dist_lib()
+    K = 4  # rounds per layout phase, each on its own input
+    phases = [2, 1, 2]
+    nr = K * len(phases)
+    bufs = [[oracle.fill(oracle.gen_bitmap(w + 10 * k, 0.3, L.nb), B, mode=1, seed=w + 31 * k) for w in range(world)]
+            for k in range(nr)]
+    board = D.omr_local_board_create(world)
+    errs, outs = [], [None] * world
+
+    def rank(r):
+        try:
+            torch.cuda.set_device(0)
+            xs = [torch.from_numpy(bufs[k][r].copy()).cuda() for k in range(nr)]
+            os_ = [x.clone() for x in xs]
+            d, plan = ctypes.c_void_p(), ctypes.c_void_p()
+            assert D.omr_dist_create_local(board, r, ctypes.byref(d)) == 0
+            assert D.omr_ar_plan_create(d, L.n, B, L.num_lanes, 8, ctypes.byref(plan)) == 0
+            assert D.omr_ar_plan_side_streams(plan) == 2  # the default at world > 1
+            st = torch.cuda.Stream()
+            k = 0
+            for n in phases:
+                assert D.omr_ar_plan_set_side_streams(plan, n) == 0, D.omr_dist_last_error()
+                assert D.omr_ar_plan_side_streams(plan) == n
+                for _ in range(K):
+                    rc = D.omr_sparse_round_f32(plan, xs[k].data_ptr(), os_[k].data_ptr(), None, None, None,
+                                                mode | 0x100 | 0x400, None, None, st.cuda_stream)
+                    assert rc == 0, D.omr_dist_last_error()
+                    k += 1
+            assert D.omr_ar_plan_set_side_streams(plan, 3) != 0
+            assert D.omr_ar_plan_join(plan, st.cuda_stream) == 0
+            torch.cuda.synchronize()
+            outs[r] = [o.cpu().numpy() for o in os_]
+            D.omr_ar_plan_destroy(plan)
+            D.omr_dist_destroy(d)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    D.omr_local_board_destroy(board)
+    assert not errs, errs
+    bounds = [s * L.rows // world for s in range(world + 1)]
+    rowf = L.num_lanes * B
+    for k in range(nr):
+        uf = oracle.union_flags([oracle.flags_from_data(b, B) for b in bufs[k]])
+        for r in range(world):
+            full = bufs[k][r].copy()
+            oracle.block_sum(bufs[k], L.n, B, L.num_lanes, 8, uf, full)
+            if mode == 0:
+                exp = full
+            else:
+                exp = bufs[k][r].copy()
+                lo, hi = bounds[r] * rowf, bounds[r + 1] * rowf
+                exp[lo:hi] = full[lo:hi]
+            assert (outs[r][k].view(np.uint32) == exp.view(np.uint32)).all(), f"round {k} rank {r}"
 
 
 @pytest.mark.parametrize("world,rounds", [(3, 1), (8, 3)])

@@ -8,6 +8,7 @@ twice:
   general / null   the multi-rank round's path at world 1 (omr_dist_test_world1_round: all-gather and plan on the plan
                    stream, exchange on the exchange stream, RCCL calls): the N > 1 layout
   general / created
+  general1 / ...   the same on ONE side stream (omr_ar_plan_set_side_streams(1))
 Prints microseconds per round and the headline kernel's step for reference.
 usage: python tools/round_inproc_r05.py [--steps 200] [--reps 2] [--torch-group]"""
 import argparse
@@ -62,9 +63,11 @@ def main():
     launches = [plan.bind(xs[0], out, null) for xs, out in sets]
     res = {}
     for rep in range(a.reps):
-        for layout in ("solo", "general"):
-            eng.test_world1_round(layout == "general")
+        for layout in ("solo", "general", "general1"):
+            eng.test_world1_round(layout != "solo")
             eng.replan()  # (the hook takes effect on plans made after it: general = the N>1 stream layout)
+            if layout == "general1":
+                eng.set_side_streams(1)  # the N>1 round's path on one side stream
             created = torch.cuda.Stream(dev)  # a stream created after the plan
             for sname, st in (("null", null), ("created", created)):
                 with torch.cuda.stream(st):
