@@ -1594,6 +1594,7 @@ constexpr int kModeSolo = 0x10000;
 constexpr int kModeTally = 0x20000;
 
 int wait_ev(hipStream_t on, hipEvent_t ev);
+int order_after(omr_ar_plan* p, hipStream_t on, hipEvent_t ev, const char* what);
 
 // The one-rank round's counts: {seq, non-zero blocks, write-set blocks, seq} from omr_worker_scan_tally_f32's publishing
 // workgroup (or omr_tally_publish).  Bounded as wait_flag; `st` is the stream the publication went on.
@@ -1677,7 +1678,7 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
   uint32_t counts[(OMR_MAX_WORKERS + 1) * (OMR_MAX_WORKERS + 2)];
   // at N > 1 the exchange stream waits for this round's plan on the plan stream (a deferred round's `ready` has
   // normally fired long before: then no wait is queued)
-  if (async && p->cs != p->ps) TRY(wait_ev(p->cs, S.ready));
+  if (async && p->cs != p->ps) TRY(order_after(p, p->cs, S.ready, "round: its plan"));
   const hipStream_t xs = async ? p->cs : st;
   ht_of(p).lap("2:cs wait ready");
   const omr_stream_t xstream = reinterpret_cast<omr_stream_t>(xs);
@@ -1857,6 +1858,28 @@ int wait_ev(hipStream_t on, hipEvent_t ev) {
   return hip_check(q, "hipEventQuery");
 }
 
+// Order the work issued next on side stream `on` after `ev`.  On the progress thread (OMR_ROUND_THREAD) the thread
+// waits on the host until `ev` has completed and queues no wait packet: a side stream that shares a hardware queue
+// with the caller's stream then never holds the caller's later scans behind a wait (in FIFO order they were queued
+// before the step that waits), which is how a shared queue slows the round.  Elsewhere a device-side
+// wait, so the calling thread never blocks.  Bounded by the transport's deadline and failure signals.
+int order_after(omr_ar_plan* p, hipStream_t on, hipEvent_t ev, const char* what) {
+  if (!t_progress) return wait_ev(on, ev);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 1;; ++spin) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return p->d->contain(hip_check(q, what));
+    if ((spin & 1023) == 0) {
+      TRY(p->d->poll());
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(p->d->timeout_ms))
+        return p->d->contain(derr(OMR_ETIMEDOUT, "%s: rank %d waited %lld ms: a peer is stuck or gone", what,
+                                  p->d->rank, static_cast<long long>(p->d->timeout_ms)));
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 // Steps 2-7 of a round whose worker scan (and, when asynchronous, its `scanned` record) is queued: on the calling
 // thread, or on the progress thread (OMR_ROUND_THREAD) in call order.
 int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks, uint64_t* union_blocks) {
@@ -1889,11 +1912,11 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
     // the one-launch round: the scan tallied the bookkeeping (omr_worker_scan_tally_f32); nothing runs after it
     seq = j.seq;
   } else {
-    if (async) TRY(hip_check(hipStreamWaitEvent(qs, S.scanned, 0), "hipStreamWaitEvent"));
+    if (async) TRY(order_after(p, qs, S.scanned, "round: the worker scan"));
     // the rest of the set is refilled from here on: the round kSets calls back must be through with it (on the side
     // stream, in stream order already)
     if (S.pending) {
-      if (qs != p->cs) TRY(wait_ev(qs, S.done));
+      if (qs != p->cs) TRY(order_after(p, qs, S.done, "round: the set's last round"));
       S.pending = false;
     }
     // 2. every worker's row masks
@@ -1933,7 +1956,7 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
           ds = p->pk[j.pki].done_set;
           p->pk[j.pki].scan_wait = false;
         }
-        if (w) TRY(wait_ev(qs, p->set[ds].done));
+        if (w) TRY(order_after(p, qs, p->set[ds].done, "round: the send buffer's last round"));
       }
       TRY(omr_check(omr_move_blocks_f32(x, p->pk[j.pki].buf, 0, S.masks_all + static_cast<uint64_t>(me) * p->mstride,
                                         S.prefix + static_cast<uint64_t>(me) * (rows + 1), rows, p->lanes, p->B, r0,

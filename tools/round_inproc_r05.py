@@ -10,7 +10,7 @@ twice:
   general / created
   general1 / ...   the same on ONE side stream (omr_ar_plan_set_side_streams(1))
 Prints microseconds per round and the headline kernel's step for reference.
-usage: python tools/round_inproc_r05.py [--steps 200] [--reps 2] [--torch-group]"""
+usage: python tools/round_inproc_r05.py [--steps 200] [--reps 2] [--pipe defer|thread] [--torch-group]"""
 import argparse
 import json
 import os
@@ -25,15 +25,15 @@ import torch  # noqa: E402
 from omr import Layout, cdist, ops  # noqa: E402
 
 
-def round_loop(eng, sets, stream, steps):
+def round_loop(eng, sets, stream, steps, thread=False):
     outs = [out for _, out in sets]
     for i in range(20):
-        eng.run(sets[i % len(sets)][0][0], out=outs[i % len(sets)], mode=1, async_=True, defer=True)
+        eng.run(sets[i % len(sets)][0][0], out=outs[i % len(sets)], mode=1, async_=True, defer=True, thread=thread)
     eng.join(stream)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        eng.run(sets[i % len(sets)][0][0], out=outs[i % len(sets)], mode=1, async_=True, defer=True)
+        eng.run(sets[i % len(sets)][0][0], out=outs[i % len(sets)], mode=1, async_=True, defer=True, thread=thread)
     eng.join(stream)
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) / steps * 1e6
@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--torch-group", action="store_true")
     ap.add_argument("--reps", type=int, default=2, help="interleaved repetitions of the four layouts")
+    ap.add_argument("--pipe", choices=("defer", "thread"), default="defer",
+                    help="thread: the progress thread issues the steps after the scan (host-ordered side streams)")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -71,7 +73,7 @@ def main():
             created = torch.cuda.Stream(dev)  # a stream created after the plan
             for sname, st in (("null", null), ("created", created)):
                 with torch.cuda.stream(st):
-                    us = round_loop(eng, sets, st, a.steps)
+                    us = round_loop(eng, sets, st, a.steps, thread=a.pipe == "thread")
                 res.setdefault(f"{layout} / {sname}", []).append(round(us, 2))
                 print(f"rep {rep} {layout:8s} {sname:8s} {us:7.2f} us per round", flush=True)
         torch.cuda.synchronize()
@@ -86,7 +88,7 @@ def main():
     print(json.dumps(res))
     if a.json:
         with open(a.json, "w") as f:
-            json.dump({"torch_group": a.torch_group, "steps": a.steps, "us_per_round": res}, f, indent=1)
+            json.dump({"torch_group": a.torch_group, "pipe": a.pipe, "steps": a.steps, "us_per_round": res}, f, indent=1)
 
 
 if __name__ == "__main__":
