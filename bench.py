@@ -87,6 +87,8 @@ def parse(argv=None):
                         "untimed probe rounds faster (max over ranks; a round whose host issue time reaches its GPU "
                         "time gains from the thread)")
     p.add_argument("--pipe-probe", type=int, default=12, help="--dist-pipe auto: untimed rounds per probe trial")
+    p.add_argument("--probe-cands", default="",
+                   help="diagnostic: the probe's candidates in order, e.g. 'thread:1,defer:2' (pipeline:side streams)")
     p.add_argument("--side-streams", choices=("1", "2", "auto"), default="auto",
                    help="N>1: the round's side streams (omr_ar_plan_set_side_streams): one, two (plan + exchange), or "
                         "auto = measured on the node by the probe, with the pipeline mode")
@@ -578,6 +580,8 @@ def main():
         # all ranks run one mode)
         pipes = ("defer", "thread") if pipe == "auto" else (pipe,)
         cands = [(pp, sd) for sd in (sides or [None]) for pp in pipes]
+        if args.probe_cands:
+            cands = [(c.split(":")[0], int(c.split(":")[1]) if sides else None) for c in args.probe_cands.split(",")]
         best = {c: float("inf") for c in cands}
         k = args.warmup
         for _ in range(2):

@@ -465,6 +465,31 @@ struct IpcDist final : omr_dist {
   IpcEvents mine[kIpcChans][2];                          // this rank's events, generation g in [c][g % 2]
   std::vector<std::array<IpcEvents, kIpcChans * 2>> peer;  // peers' events, opened, [p][c * 2 + g % 2]
   std::vector<hipEvent_t> retired;                         // events of old generations, destroyed in batches
+  // A batch of retired events goes to a reaper thread, which destroys it behind a device sync of its own.  Round 4
+  // synchronised the device on the round's thread: with several ranks on one GPU that held every rank's host about
+  // 140 ms each 128 rounds (4 IPC ranks: 4.2-4.9 ms per round over 50 timed rounds that held one, 1.35-1.43 ms
+  // otherwise; profiles/r05/side_streams/).
+  std::thread reaper;
+  std::mutex rmu;
+  std::condition_variable rcv;
+  std::deque<std::vector<hipEvent_t>> rq;
+  bool rstop = false;
+  int rdev = 0;
+  void reap_main() {
+    (void)hipSetDevice(rdev);
+    std::unique_lock<std::mutex> lk(rmu);
+    for (;;) {
+      rcv.wait(lk, [&] { return rstop || !rq.empty(); });
+      if (rq.empty()) return;
+      std::vector<hipEvent_t> batch = std::move(rq.front());
+      rq.pop_front();
+      lk.unlock();
+      // every operation queued before this point (the batch's last records and waits among them) has completed
+      (void)hipDeviceSynchronize();
+      for (hipEvent_t e : batch) (void)hipEventDestroy(e);
+      lk.lock();
+    }
+  }
   uint64_t seq[kIpcChans] = {0, 0};
   // allocation (base, size) -> its handle and this rank's id for it.  The plans' exported allocations are never freed
   // while the transport lives (release() parks them), so an entry never outlives its allocation.  A
@@ -505,6 +530,14 @@ struct IpcDist final : omr_dist {
   }
 
   ~IpcDist() override {
+    if (reaper.joinable()) {
+      {
+        std::lock_guard<std::mutex> g(rmu);
+        rstop = true;
+      }
+      rcv.notify_all();
+      reaper.join();  // (it destroys what is queued first)
+    }
     if (b != nullptr) {
       // every rank's device work (copies out of its peers' buffers, waits on their events) ends before anyone
       // closes a mapping or an event
@@ -622,9 +655,16 @@ struct IpcDist final : omr_dist {
       }
     }
     if (retired.size() >= kIpcReap) {  // this rank's streams may still hold records of, or waits on, them
-      TRY(hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize"));
-      for (hipEvent_t e : retired) TRY(hip_check(hipEventDestroy(e), "hipEventDestroy"));
+      if (!reaper.joinable()) {
+        TRY(hip_check(hipGetDevice(&rdev), "hipGetDevice"));
+        reaper = std::thread(&IpcDist::reap_main, this);
+      }
+      {
+        std::lock_guard<std::mutex> g(rmu);
+        rq.push_back(std::move(retired));
+      }
       retired.clear();
+      rcv.notify_one();
     }
     return 0;
   }
