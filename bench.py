@@ -568,7 +568,10 @@ def main():
     if dist_mode and pipe == "auto" and args.pipe_probe < 1:
         pipe = "defer"
     side = None  # the side streams the timed rounds ran on (N>1: measured on the node)
-    sides = ([2, 1] if args.side_streams == "auto" else [int(args.side_streams)]) if dist_mode and ranks > 1 else []
+    # (auto: both, timed on the node; IPC ranks share GPUs, where a second side stream's hardware queue per rank adds
+    # up, so they keep the plan's default of one unless asked)
+    sides = (([2, 1] if not ipc else []) if args.side_streams == "auto" else [int(args.side_streams)]
+             ) if dist_mode and ranks > 1 else []
     if len(sides) > 1 and args.pipe_probe < 1:  # (no probe rounds: the library's default layout)
         sides = [2]
     if dist_mode and ranks > 1 and pipe != "auto" and len(sides) == 1:

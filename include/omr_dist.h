@@ -235,7 +235,8 @@ int omr_ar_plan_fused_pack(const omr_ar_plan* plan);
 uint64_t omr_ar_plan_device_bytes(const omr_ar_plan* plan);
 /* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
 int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
-/* The asynchronous rounds' side streams: 2 (the default at world > 1) = a plan stream for the mask all-gather and the
+/* The asynchronous rounds' side streams: 2 (the default at world > 1, except over IPC beyond 4 ranks, where ranks share
+ * GPUs and their hardware queues add up) = a plan stream for the mask all-gather and the
  * plan, an exchange stream for the exchange, the shard sums and the return trip, so round k-2's exchange runs beside
  * round k's plan; 1 (the default at world 1) = everything after the scan on one stream, in issue order.  Which is
  * faster depends on how the process's streams share its hardware queues: bench.py's N>1 lines measure

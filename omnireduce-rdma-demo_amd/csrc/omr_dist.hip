@@ -152,6 +152,8 @@ struct omr_dist {
   // other processes (HIP IPC) keeps every exported allocation alive until it is destroyed itself and hands it back
   // to the next alloc of the same size, so an address a peer has mapped is never freed and re-allocated under it.
   virtual int alloc(void** ptr, size_t bytes) { return hip_check(hipMalloc(ptr, bytes), "hipMalloc"); }
+  // a plan's default side streams at N > 1 (omr_ar_plan_set_side_streams): two, except where ranks share GPUs (IPC)
+  virtual int default_side_streams() const { return 2; }
   virtual void release(void* ptr) { (void)hipFree(ptr); }
 };
 
@@ -520,6 +522,12 @@ struct IpcDist final : omr_dist {
         return derr(OMR_EABORTED, "ipc transport: rank %d aborted the group", p);
     return 0;
   }
+  // Ranks that share a GPU add up their hardware queues, and HIP keeps a stream's queue for the process once made:
+  // as 8 ranks on one GPU the round took 11-13 ms on one side stream and 23-28 ms once each rank had an exchange
+  // stream too (bisected to that change; 45 ms on one side stream with the exchange stream's queue still held),
+  // while 4 ranks ran faster with two (1.43 against 2.47 ms).  So two up to 4 ranks, one beyond
+  // (omr_ar_plan_set_side_streams overrides it; profiles/r05/side_streams/).
+  int default_side_streams() const override { return world <= 4 ? 2 : 1; }
 
   static void release(IpcEvents& e, std::vector<hipEvent_t>& to) {
     for (int k = 0; k < kIpcRing; ++k) {
@@ -1518,7 +1526,7 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   // (round 4).  The multi-rank test hook at world 1 (omr_dist_test_world1_round) takes the N > 1 layout.
   A(hip_check(hipStreamCreateWithFlags(&p->ps, hipStreamNonBlocking), "hipStreamCreate"));
   p->cs = p->ps;
-  if (N > 1 || p->d->world1_general) {
+  if ((N > 1 && p->d->default_side_streams() == 2) || p->d->world1_general) {
     A(hip_check(hipStreamCreateWithFlags(&p->xstream, hipStreamNonBlocking), "hipStreamCreate"));
     if (rc == 0) p->cs = p->xstream;
   }
@@ -2528,8 +2536,17 @@ int omr_ar_plan_set_side_streams(omr_ar_plan* p, int n) {
   TRY(plan_fail(p, hip_check(hipEventRecord(p->switch_ev, p->cs), "hipEventRecord")));
   TRY(plan_fail(p, hip_check(hipStreamWaitEvent(want, p->switch_ev, 0), "hipStreamWaitEvent")));
   if (want != p->ps) TRY(plan_fail(p, hip_check(hipStreamWaitEvent(p->ps, p->switch_ev, 0), "hipStreamWaitEvent")));
+  const hipStream_t old = p->cs;
   p->cs = want;
   if (p->tail != nullptr) p->tail = want;
+  if (n == 1 && old == p->xstream) {
+    // the exchange stream goes once it is idle: a stream keeps its hardware queue mapped while it exists, and with
+    // several processes on one GPU the queues add up (8 IPC ranks: 45 ms per round on one side stream with the idle
+    // exchange stream alive, 13 ms without it; profiles/r05/side_streams/)
+    TRY(plan_fail(p, wait_event_bounded(p->d, p->switch_ev, "ar_plan_set_side_streams")));
+    TRY(plan_fail(p, hip_check(hipStreamDestroy(p->xstream), "hipStreamDestroy")));
+    p->xstream = nullptr;
+  }
   return 0;
 }
 
