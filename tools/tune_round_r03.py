@@ -10,7 +10,8 @@ Worker side, per launch (algorithmic bytes in brackets):
 Aggregator side, shard 0's sums from 8 contributions (own in place + 7 received streams) [received + own + write-set
 blocks, as tools/tune_round_r02.py counts them]:
   round-2 k_shard_sum (tools/tune/round_r02.hip), the product's k_shard_sum over row-ordered streams
-  (omr_shard_sum_f32) and over the fused pack's column-ordered streams (omr_shard_sum_cols_f32).
+  (omr_shard_sum_f32) and over the fused pack's column-ordered streams (round 3's omr_shard_sum_cols_f32, from
+  tools/tune/plan_r04.hip since round 5).
 Every variant's output is checked bit for bit against the others.  Batch-timed with events, interleaved.
 usage: python tools/tune_round_r03.py [--rounds 10] [--reps 20]"""
 import argparse

@@ -2,7 +2,7 @@
 """Where the round-3 shard sum's time goes, at config 4's 8-worker shard (tools/tune/shard_r03.hip, a stamped copy of
 the product kernel): batch-timed windows of 16 / 32 / 64 pair slots, grids, and a per-wave timeline of the phases
 (index data consumed, pair list written, first window summed, end with its stores acknowledged).  Outputs are
-checked bit for bit against the product (omr_shard_sum_cols_f32).
+checked bit for bit against the product (round 3's omr_shard_sum_cols_f32, now tools/tune/plan_r04.hip).
 usage: python tools/tune_shard_r03.py [--rounds 8] [--reps 20]"""
 import ctypes
 import os
@@ -41,6 +41,7 @@ def main():
     torch.cuda.init()
     tl = load()
     lib = _lib.load()
+    tcols = r03.load_r04()  # (round 3's column-stream sum left the product in round 5: tools/tune/plan_r04.hip)
     D = r03.setup(a)
     L, m, rows, B, NB = D["L"], D["m"], D["rows"], D["B"], D["NB"]
     st, dev = D["st"], D["dev"]
@@ -48,7 +49,7 @@ def main():
     roff = D["roff"].ctypes.data_as(ctypes.c_void_p)
     x0 = D["xs"][0]
     ref = x0.clone()
-    assert lib.omr_shard_sum_cols_f32(x0.data_ptr(), 0, D["recv_c"].data_ptr(), roff, D["masks_all"].data_ptr(), m,
+    assert tcols.tune_shard_sum_cols_r04(x0.data_ptr(), 0, D["recv_c"].data_ptr(), roff, D["masks_all"].data_ptr(), m,
                                       D["mstride"], 2 * rows, D["prefix"].data_ptr(), D["wset"].data_ptr(), L.n, B, NB,
                                       L.num_threads, r0, r1, 0, ref.data_ptr(), st) == 0
     units = tl.tune_shard_units(r0, r1, NB, D["S"], D["gps"], 1)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Round 4: the shard sum at config 4's 8-worker shard (tools/tune_round_r03.py's setup: 8 x 256 MiB, -r 0.095,
 shard 0 of 8, column-ordered streams from the fused pack), the round-3 kernel (tools/tune/shard_r03.hip's copy)
-against the product's (omr_shard_sum_cols_f32), batch-timed with events, interleaved, outputs checked bit for bit.
+against the product's (round 3's omr_shard_sum_cols_f32, now tools/tune/plan_r04.hip), batch-timed with events, interleaved, outputs checked bit for bit.
 Four rotating output buffers and --rotate input sets (separate worker tensors / receive streams), so a launch does not
 find the previous launch's data in the 256 MiB Infinity Cache.
 usage: python tools/tune_shard_r04.py [--rounds 8] [--reps 20]"""
@@ -70,6 +70,7 @@ def main():
     torch.cuda.init()
     tl = s03.load()
     lib = _lib.load()
+    tcols = r03.load_r04()  # (round 3's column-stream sum left the product in round 5: tools/tune/plan_r04.hip)
     D = r03.setup(a)
     L, m, rows, B, NB = D["L"], D["m"], D["rows"], D["B"], D["NB"]
     st = D["st"]
@@ -91,11 +92,11 @@ def main():
 
     def prod(k, out):
         x, rc = sets[k % len(sets)]
-        return lib.omr_shard_sum_cols_f32(x.data_ptr(), 0, rc.data_ptr(), roff, D["masks_all"].data_ptr(), m,
+        return tcols.tune_shard_sum_cols_r04(x.data_ptr(), 0, rc.data_ptr(), roff, D["masks_all"].data_ptr(), m,
                                           D["mstride"], 2 * rows, D["prefix"].data_ptr(), D["wset"].data_ptr(), L.n, B,
                                           NB, L.num_threads, r0, r1, 0, out.data_ptr(), st)
 
-    # the pair list of shard 0, built once (the round builds it in its plan launch: omr_round_plan_ws / _list)
+    # the pair list of shard 0, built once (the round builds it in its plan launch: omr_round_plan_list)
     units_l, cap = ctypes.c_uint64(), ctypes.c_uint32()
     _lib.check(lib.omr_sum_list_geometry(L.n, B, NB, L.num_threads, r0, r1, m, ctypes.byref(units_l),
                                          ctypes.byref(cap)), "geometry")
