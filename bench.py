@@ -87,6 +87,8 @@ def parse(argv=None):
                         "untimed probe rounds faster (max over ranks; a round whose host issue time reaches its GPU "
                         "time gains from the thread)")
     p.add_argument("--pipe-probe", type=int, default=12, help="--dist-pipe auto: untimed rounds per probe trial")
+    p.add_argument("--world1-general", action="store_true",
+                   help="diagnostic, one rank: time the multi-rank round's code path instead of the one-launch round")
     p.add_argument("--probe-cands", default="",
                    help="diagnostic: the probe's candidates in order, e.g. 'thread:1,defer:2' (pipeline:side streams)")
     p.add_argument("--side-streams", choices=("1", "2", "auto"), default="auto",
@@ -511,6 +513,11 @@ def main():
             engine = cdist.CppSparseAllreduce(L, dev, transport="ipc", uid=uid[0], rank=rank, world=ws)
         else:
             engine = cdist.CppSparseAllreduce(L, device=dev)
+        if args.world1_general and ws == 1:
+            # diagnostic: the multi-rank round's code path at world 1 (all-gather, plan, exchange as RCCL calls, on the
+            # N>1 side streams) instead of the one-launch round
+            engine.test_world1_round(True)
+            engine.replan()
         engine_fused = engine.fused_pack  # the worker scan packs the exchange's blocks itself
         for xs, out in sets:  # out-of-place result buffers keep every step's input pristine
             out.copy_(xs[0])
@@ -571,7 +578,7 @@ def main():
     # (auto: both, timed on the node; IPC ranks share GPUs, where a second side stream's hardware queue per rank adds
     # up, so they keep the plan's default of one unless asked)
     sides = (([2, 1] if not ipc else []) if args.side_streams == "auto" else [int(args.side_streams)]
-             ) if dist_mode and ranks > 1 else []
+             ) if dist_mode and (ranks > 1 or args.world1_general) else []
     if len(sides) > 1 and args.pipe_probe < 1:  # (no probe rounds: the library's default layout)
         sides = [2]
     if dist_mode and ranks > 1 and pipe != "auto" and len(sides) == 1:
@@ -625,7 +632,7 @@ def main():
     # a one-rank round is ONE launch on the caller's stream (omr_worker_scan_tally_f32): timed as the headline is,
     # events around all K rounds, instead of per-round stage events (a timing record between two rounds holds the next
     # round's launch back 4.6-6 us, profiles/r05/final/w1_trace/; at one rank every other stage is empty)
-    one_launch = dist_mode and ranks == 1 and args.dist_mode != "dense"
+    one_launch = dist_mode and ranks == 1 and args.dist_mode != "dense" and not args.world1_general
     span = (timing.Event(), timing.Event())  # single-kernel step: the kernel's mean duration over the timed region
     if dist_mode:
         engine.host_stats(reset=True)
@@ -698,7 +705,9 @@ def main():
                               "scan stage is the roofline's kernel_ms (events around all K rounds)")
     if True:
         if dist_mode:
-            if ranks == 1 and args.dist_mode != "dense":  # one rank: the scan writes the shard sums itself
+            if ranks == 1 and args.dist_mode != "dense" and args.world1_general:  # (the scan also writes masks)
+                kbytes = fused_bytes(L, bitmaps[0]) + L.rows * 8
+            elif ranks == 1 and args.dist_mode != "dense":  # one rank: the scan writes the shard sums itself
                 kbytes = one_rank_round_bytes(L, bitmaps[0])
             else:
                 kbytes = (scan_pack_bytes(L, bitmaps[0], rank, ranks) if engine_fused else scan_only_bytes(L))
