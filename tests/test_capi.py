@@ -129,3 +129,49 @@ def test_pack_supported_worlds(world):
     b = np.array([s * L.rows // world for s in range(world + 1)], dtype=np.uint64)
     rc = lib.omr_pack_supported(L.n, 256, L.num_lanes, L.num_threads, b.ctypes.data_as(ctypes.c_void_p), world)
     assert (rc == 0) == (world in (1, 2, 4, 8)), (world, rc)
+
+
+@pytest.mark.parametrize("world,own", [(8, 3), (4, 0), (2, 1), (8, -1), (3, 2)])
+def test_pack_send_offset(world, own):
+    """Round 5's compact send buffer (omr_pack_send_offset, host-only): the other shards' streams back to back in shard
+    order, the own shard left out; the buffer's size is the tensor less the own shard."""
+    lib = _lib.load()
+    L = Layout.from_bytes(256 << 20, 256)
+    b = np.array([s * L.rows // world for s in range(world + 1)], dtype=np.uint64)
+    rowf = L.num_lanes * 256
+    total = ctypes.c_uint64()
+    at = 0
+    for s in range(world):
+        off = lib.omr_pack_send_offset(b.ctypes.data_as(ctypes.c_void_p), world, own, s, L.num_lanes, 256,
+                                       ctypes.byref(total))
+        if s == own:
+            continue
+        assert off == at * rowf, (s, off, at)
+        at += int(b[s + 1] - b[s])
+    own_rows = int(b[own + 1] - b[own]) if own >= 0 else 0
+    assert total.value == (L.rows - own_rows) * rowf
+
+
+def test_round_plan_workspace_and_validation():
+    """The row-chunk plan's workspace size (one ticket word + 64 chunks x 17 tagged totals), and its argument checks,
+    which return before any launch: seq 0 (a zero-filled word carries it), count 0, a NULL workspace."""
+    lib = _lib.load()
+    assert lib.omr_round_plan_workspace_words() == 1 + 64 * 17
+    fake = ctypes.c_void_p(0x1000)  # (never dereferenced: the checks come first)
+    args = lambda count, ws, seq: (fake, count, 4096, 512, 64, fake, 9, fake, None, fake, fake, None, ws, seq, None)  # noqa: E731
+    assert lib.omr_round_plan(*args(8, fake, 0)) == _lib.OMR_EINVAL
+    assert b"seq 0" in lib.omr_last_error()
+    assert lib.omr_round_plan(*args(0, fake, 1)) == _lib.OMR_EINVAL
+    assert lib.omr_round_plan(*args(8, None, 1)) == _lib.OMR_EINVAL
+
+
+@pytest.mark.parametrize("mib,B", [(256, 256), (1024, 1024), (4, 256)])
+def test_tally_slots(mib, B):
+    """The one-rank round's tally: one slot per workgroup of its launch, (partition, lane) columns x segments."""
+    lib = _lib.load()
+    L = Layout.from_bytes(mib << 20, B)
+    s, g, e = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64()
+    assert lib.omr_pack_geometry(L.n, B, L.num_lanes, L.num_threads, ctypes.byref(s), ctypes.byref(g),
+                                 ctypes.byref(e)) == 0
+    segments = L.rows_per_part // s.value
+    assert lib.omr_tally_slots(L.n, B, L.num_lanes, L.num_threads) == L.num_threads * L.num_lanes * segments
