@@ -138,7 +138,8 @@ int omr_ar_plan_shard(omr_ar_plan* plan, int* shard, uint64_t* row_begin, uint64
  * *sent_blocks / *union_blocks (host, may be NULL) receive this rank's off-rank sent blocks and the write-set size.
  * Waits once mid-round for the block counts (the transport needs host-side sizes; the bookkeeping kernel stores
  * them straight into pinned host memory) and returns with the rest of the round enqueued on `stream`:
- * synchronise `stream` before reading out / flags / next_offsets / union_next. */
+ * synchronise `stream` before reading out / flags / next_offsets / union_next.  (A one-rank group's round is one
+ * launch; with both count pointers NULL it does not wait at all.) */
 int omr_sparse_allreduce_f32(omr_ar_plan* plan, const float* x, float* out, int32_t* flags,
                              uint32_t* next_offsets, uint32_t* union_next, uint64_t* sent_blocks,
                              uint64_t* union_blocks, omr_stream_t stream);

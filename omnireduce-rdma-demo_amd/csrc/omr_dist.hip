@@ -1709,7 +1709,9 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
   ht_of(p).start();
   if (tally) {
     // the one-launch round: its worker scan wrote the sums and tallied the counts; they reach the host through the next
-    // round's scan or, if none has been issued, a publication of their own
+    // round's scan or, if none has been issued, a publication of their own.  A caller that wants neither count waits
+    // for nothing: the launch is the whole round (its counts stay with the next scan, which publishes them anyway).
+    if (sent_blocks == nullptr && union_blocks == nullptr) return 0;
     if (p->pub_set == si && p->pub_seq == seq) TRY(publish_pending(p));
     uint32_t nz = 0, ws = 0;
     {

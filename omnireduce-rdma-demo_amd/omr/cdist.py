@@ -187,7 +187,7 @@ class CppSparseAllreduce:
 
     def run(self, x: Optional[torch.Tensor], out: Optional[torch.Tensor] = None, ev=None, flags=None, next_offsets=None,
             union_next=None, mode: int = 0, async_: bool = False, time_exchange: bool = False,
-            defer: bool = False, thread: bool = False):
+            defer: bool = False, thread: bool = False, counts: bool = True):
         """mode 0: all-reduce (every worker gets every shard's sums); 1: reduce-scatter (stop at the
         aggregators: `out` gets this rank's shard sums only); 2: the dense stand-in (the whole tensor reduce-scattered
         by RCCL, every block).  async_: only the worker scan runs on the caller's stream; the bookkeeping, the
@@ -197,7 +197,8 @@ class CppSparseAllreduce:
         aggregator exchange with timing events (read with timings() / exchange_time()).  defer: OMR_ROUND_DEFER,
         this round's exchange is issued two calls later (or by a call without the flag, or join()); the returned
         counts are those of the round whose exchange this call issued.  thread: OMR_ROUND_THREAD (implies async_),
-        the plan's progress thread issues everything after the worker scan; the returned counts are 0."""
+        the plan's progress thread issues everything after the worker scan; the returned counts are 0.
+        counts=False: ask for no counts (returns (None, None)); a one-rank round then does not wait at all."""
         if thread:
             mode |= self.THREAD
         if defer:
@@ -213,11 +214,12 @@ class CppSparseAllreduce:
             ev[0].record(st)
         ptr = (lambda t: t.data_ptr() if t is not None else None)
         _check(load().omr_sparse_round_f32(self._p, ptr(x), ptr(out), ptr(flags), ptr(next_offsets),
-                                           ptr(union_next), mode, ctypes.byref(sent), ctypes.byref(uni),
-                                           st.cuda_stream), "omr_sparse_round_f32")
+                                           ptr(union_next), mode, ctypes.byref(sent) if counts else None,
+                                           ctypes.byref(uni) if counts else None, st.cuda_stream),
+               "omr_sparse_round_f32")
         if ev is not None:
             ev[1].record(st)
-        return sent.value, uni.value
+        return (sent.value, uni.value) if counts else (None, None)
 
     def shard(self):
         """(shard, row_begin, row_end, sums, num_blocks) of this rank (omr_ar_plan_shard); `sums` is a device pointer

@@ -101,6 +101,49 @@ def test_cpp_round_loopback(gpu, world, B, density):
         assert (unx == un).all()
 
 
+@pytest.mark.parametrize("B,density", [(256, 0.095), (1024, 1.0)])
+def test_cpp_round_world1_counts_optional(gpu, B, density):
+    """A one-rank round asked for no counts does not wait for them (its one launch is the round): rounds with and
+    without count pointers interleaved on one plan, each bit-exact against the oracle, and every round that asks gets
+    the write-set size (the worker's non-zero blocks and every partition's lane heads) while the publications of the
+    rounds that did not ask are carried by the next scan."""
+    L = Layout(n=2 << 20, block_size=B)
+    D = dist_lib()
+    buf = oracle.fill(oracle.gen_bitmap(0, density, L.nb), B, mode=1, seed=3)
+    f = oracle.flags_from_data(buf, B)
+    exp = buf.copy()
+    oracle.block_sum([buf], L.n, B, L.num_lanes, 8, f, exp)
+    rows = L.nb // L.num_lanes
+    head = ((np.arange(L.nb) // L.num_lanes) % (rows // 8)) == 0
+    ws = int(np.count_nonzero((f != 0) | head))
+    board = D.omr_local_board_create(1)
+    d, plan = ctypes.c_void_p(), ctypes.c_void_p()
+    assert D.omr_dist_create_local(board, 0, ctypes.byref(d)) == 0
+    assert D.omr_ar_plan_create(d, L.n, B, L.num_lanes, 8, ctypes.byref(plan)) == 0
+    try:
+        x = torch.from_numpy(buf.copy()).cuda()
+        outs = [torch.full_like(x, float("nan")) for _ in range(3)]
+        st = torch.cuda.Stream()
+        sent, uni = ctypes.c_uint64(7), ctypes.c_uint64(7)
+        for k, want in enumerate([False, False, True, False, True, True, False]):
+            out = outs[k % 3]
+            out.copy_(x)
+            torch.cuda.synchronize()
+            uni.value = 7
+            rc = D.omr_sparse_allreduce_f32(plan, x.data_ptr(), out.data_ptr(), None, None, None,
+                                            ctypes.byref(sent) if want else None, ctypes.byref(uni) if want else None,
+                                            st.cuda_stream)
+            assert rc == 0, D.omr_dist_last_error()
+            st.synchronize()
+            assert (out.cpu().numpy().view(np.uint32) == exp.view(np.uint32)).all(), f"round {k}"
+            if want:
+                assert (sent.value, uni.value) == (0, ws), f"round {k}"
+    finally:
+        D.omr_ar_plan_destroy(plan)
+        D.omr_dist_destroy(d)
+        D.omr_local_board_destroy(board)
+
+
 @pytest.mark.parametrize("world,mode", [(3, 0), (4, 1), (5, 0)])
 def test_cpp_round_side_streams_switch(gpu, world, mode):
     """Pipelined rounds (async | defer) with the side streams switched between them (omr_ar_plan_set_side_streams:
