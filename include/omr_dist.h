@@ -65,6 +65,8 @@ int omr_dist_create_local(omr_local_board* board, int rank, omr_dist** out);
 
 int omr_dist_rank(const omr_dist* d);
 int omr_dist_world(const omr_dist* d);
+/* 0; OMR_ETIMEDOUT if, after an abort, the rank's streams were still busy (waiting on a gone peer) past the deadline:
+ * the transport's device-side state (mappings, events, exported allocations) is then left allocated */
 int omr_dist_destroy(omr_dist* d);
 
 /* The transport's two operations, as the round uses them (every rank of the group calls them in the same order).

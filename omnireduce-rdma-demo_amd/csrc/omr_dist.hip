@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <map>
 #include <mutex>
 #include <string>
@@ -35,6 +36,7 @@
 namespace {
 
 thread_local char g_derr[512];
+thread_local int g_destroy_rc = 0;  // a transport's teardown that left device-side state behind (omr_dist_destroy)
 
 int derr(int code, const char* fmt, ...) {
   va_list ap;
@@ -457,6 +459,33 @@ int ipc_spin(F ready, const char* what, int rank, int64_t timeout_ms, const IpcB
   }
 }
 
+// hipDeviceSynchronize within `ms` (run by a helper thread, left behind blocked if the device stays busy): after an
+// abort a stream may wait forever on a gone peer (an IPC event that is never recorded), and the teardown must not
+// (ADVICE r04).  true once the device is idle.
+bool device_sync_within(int64_t ms) {
+  struct Done {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+  };
+  auto d = std::make_shared<Done>();
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::thread t([d, dev] {
+    (void)hipSetDevice(dev);
+    (void)hipDeviceSynchronize();
+    std::lock_guard<std::mutex> g(d->mu);
+    d->done = true;
+    d->cv.notify_all();
+  });
+  std::unique_lock<std::mutex> lk(d->mu);
+  const bool ok = d->cv.wait_for(lk, std::chrono::milliseconds(ms), [&] { return d->done; });
+  lk.unlock();
+  if (ok) t.join();
+  else t.detach();
+  return ok;
+}
+
 struct IpcEvents {
   hipEvent_t ready[kIpcRing] = {}, rdone[kIpcRing] = {};
 };
@@ -471,26 +500,35 @@ struct IpcDist final : omr_dist {
   // synchronised the device on the round's thread: with several ranks on one GPU that held every rank's host about
   // 140 ms each 128 rounds (4 IPC ranks: 4.2-4.9 ms per round over 50 timed rounds that held one, 1.35-1.43 ms
   // otherwise; profiles/r05/side_streams/).
+  // The reaper's state is shared with it (not reached through `this`): after an abort its device sync may never return
+  // (a stream waiting on a gone peer's event), and the transport is then destroyed without it.
+  struct Reap {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::vector<hipEvent_t>> q;
+    bool stop = false, exited = false;
+    std::atomic<bool> leak{false};  // the group was aborted: drop batches instead of waiting for the device
+  };
+  std::shared_ptr<Reap> reap;
   std::thread reaper;
-  std::mutex rmu;
-  std::condition_variable rcv;
-  std::deque<std::vector<hipEvent_t>> rq;
-  bool rstop = false;
-  int rdev = 0;
-  void reap_main() {
-    (void)hipSetDevice(rdev);
-    std::unique_lock<std::mutex> lk(rmu);
+  static void reap_main(std::shared_ptr<Reap> r, int dev) {
+    (void)hipSetDevice(dev);
+    std::unique_lock<std::mutex> lk(r->mu);
     for (;;) {
-      rcv.wait(lk, [&] { return rstop || !rq.empty(); });
-      if (rq.empty()) return;
-      std::vector<hipEvent_t> batch = std::move(rq.front());
-      rq.pop_front();
+      r->cv.wait(lk, [&] { return r->stop || !r->q.empty(); });
+      if (r->q.empty()) break;
+      std::vector<hipEvent_t> batch = std::move(r->q.front());
+      r->q.pop_front();
       lk.unlock();
       // every operation queued before this point (the batch's last records and waits among them) has completed
-      (void)hipDeviceSynchronize();
-      for (hipEvent_t e : batch) (void)hipEventDestroy(e);
+      if (!r->leak.load(std::memory_order_acquire)) {
+        (void)hipDeviceSynchronize();
+        for (hipEvent_t e : batch) (void)hipEventDestroy(e);
+      }
       lk.lock();
     }
+    r->exited = true;
+    r->cv.notify_all();
   }
   uint64_t seq[kIpcChans] = {0, 0};
   // allocation (base, size) -> its handle and this rank's id for it.  The plans' exported allocations are never freed
@@ -538,18 +576,38 @@ struct IpcDist final : omr_dist {
   }
 
   ~IpcDist() override {
+    const bool dead = aborted.load(std::memory_order_acquire);
+    bool idle = true;  // the device is through with this transport's work
     if (reaper.joinable()) {
+      bool exited;
       {
-        std::lock_guard<std::mutex> g(rmu);
-        rstop = true;
+        std::unique_lock<std::mutex> lk(reap->mu);
+        reap->stop = true;
+        if (dead) reap->leak.store(true, std::memory_order_release);
+        reap->cv.notify_all();
+        // (it destroys what is queued first; after an abort it drops it, and is waited for within the deadline only)
+        exited = dead ? reap->cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return reap->exited; })
+                      : (reap->cv.wait(lk, [&] { return reap->exited; }), true);
       }
-      rcv.notify_all();
-      reaper.join();  // (it destroys what is queued first)
+      if (exited) reaper.join();
+      else reaper.detach();  // blocked in a device sync that waits on a gone peer: left behind with its shared state
+      idle = exited;
     }
     if (b != nullptr) {
       // every rank's device work (copies out of its peers' buffers, waits on their events) ends before anyone
-      // closes a mapping or an event
-      (void)hipDeviceSynchronize();
+      // closes a mapping or an event; after an abort within the deadline, or everything device-side is left as is
+      if (!dead) (void)hipDeviceSynchronize();
+      else if (idle) idle = device_sync_within(timeout_ms);
+      if (!idle) {
+        (void)derr(OMR_ETIMEDOUT, "ipc transport: rank %d's streams still busy %lld ms after the abort; its mappings, "
+                   "events and exported allocations are left as they are", rank, static_cast<long long>(timeout_ms));
+        g_destroy_rc = OMR_ETIMEDOUT;
+        b->rank[rank].left.store(1, std::memory_order_release);
+        const bool last = b->attached.fetch_sub(1) == 1;
+        munmap(b, sizeof(IpcBoard));
+        if (last) shm_unlink(name.c_str());
+        return;
+      }
       b->rank[rank].left.store(1, std::memory_order_release);
       // (an aborted group does not wait: a peer may never leave; the driver keeps an exported allocation's memory
       // alive while a peer still maps it)
@@ -664,15 +722,17 @@ struct IpcDist final : omr_dist {
     }
     if (retired.size() >= kIpcReap) {  // this rank's streams may still hold records of, or waits on, them
       if (!reaper.joinable()) {
-        TRY(hip_check(hipGetDevice(&rdev), "hipGetDevice"));
-        reaper = std::thread(&IpcDist::reap_main, this);
+        int dev = 0;
+        TRY(hip_check(hipGetDevice(&dev), "hipGetDevice"));
+        reap = std::make_shared<Reap>();
+        reaper = std::thread(&IpcDist::reap_main, reap, dev);
       }
       {
-        std::lock_guard<std::mutex> g(rmu);
-        rq.push_back(std::move(retired));
+        std::lock_guard<std::mutex> g(reap->mu);
+        reap->q.push_back(std::move(retired));
       }
       retired.clear();
-      rcv.notify_one();
+      reap->cv.notify_all();
     }
     return 0;
   }
@@ -1310,8 +1370,9 @@ int omr_dist_rank(const omr_dist* d) { return d ? d->rank : -1; }
 int omr_dist_world(const omr_dist* d) { return d ? d->world : -1; }
 
 int omr_dist_destroy(omr_dist* d) {
+  g_destroy_rc = 0;
   delete d;
-  return 0;
+  return g_destroy_rc;
 }
 
 int omr_dist_abort(omr_dist* d) {
@@ -1385,19 +1446,12 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p->failed == 0 && !p->d->aborted.load()) {
     (void)hipDeviceSynchronize();
   } else {
-    // After a failure the plan's streams may hold waits on a peer that will never come (an IPC peer's event; an aborted
-    // RCCL communicator has cancelled its queued operations, the IPC and loopback transports cannot): wait for them
-    // within the deadline only, and if they are still busy leave the plan's device memory allocated rather than free
-    // it under queued work (destroy must not block on a dead peer).
-    const auto t0 = std::chrono::steady_clock::now();
-    bool idle = false;
-    while (!idle) {
-      idle = true;
-      for (hipStream_t s : {p->ps, p->xstream, p->s_in, p->s_out})
-        if (s != nullptr && hipStreamQuery(s) == hipErrorNotReady) idle = false;
-      if (idle || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(p->d->timeout_ms)) break;
-      std::this_thread::sleep_for(std::chrono::microseconds(200));
-    }
+    // After a failure the device may hold waits on a peer that will never come (an IPC peer's event, on the plan's
+    // streams or the caller's; an aborted RCCL communicator has cancelled its queued operations, the IPC and loopback
+    // transports cannot): wait for the device within the deadline only, and if it is still busy leave the plan's
+    // device memory allocated rather than free it under queued work (hipFree would wait for the device itself;
+    // destroy must not block on a dead peer).
+    const bool idle = device_sync_within(p->d->timeout_ms);
     (void)hipGetLastError();
     if (!idle) {
       const int rc = derr(OMR_ETIMEDOUT, "ar_plan_destroy: the plan's streams were still busy %lld ms after its failure; "

@@ -338,13 +338,17 @@ class CppSparseAllreduce:
         return load().omr_dist_exchange(self._d, sp, sb, rp, rb, st.cuda_stream)
 
     def close(self):
+        """Destroy the plan and the transport; returns their codes (0, 0) when both released everything (after an
+        abort, OMR_ETIMEDOUT where the device was still busy past the deadline and device memory was left allocated)."""
         D = load()
+        rcs = [0, 0]
         if self._p:
-            D.omr_ar_plan_destroy(self._p)
+            rcs[0] = D.omr_ar_plan_destroy(self._p)
             self._p = ctypes.c_void_p()
         if self._d:
-            D.omr_dist_destroy(self._d)
+            rcs[1] = D.omr_dist_destroy(self._d)
             self._d = ctypes.c_void_p()
         if self._board:
             D.omr_local_board_destroy(self._board)
             self._board = None
+        return tuple(rcs)

@@ -46,8 +46,22 @@ def main():
     ap.add_argument("--fault-rank", type=int, default=-1, help="this rank's first exchange fails (omr_dist_inject_fault)")
     ap.add_argument("--fault-after", type=int, default=0)
     ap.add_argument("--status", default="", help="fault runs: write {error, seconds_to_error} here; exit 3 on an error")
+    ap.add_argument("--stall-ms", type=int, default=0,
+                    help="queue a busy kernel of about this long on the round's stream before the rounds (a peer that "
+                         "falls silent with its part of the exchange still queued)")
+    ap.add_argument("--drain", action="store_true", help="fault runs: synchronise the device before leaving")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
+    stall_per_ms = 0.0
+    if a.stall_ms:  # the busy kernel's clock, measured before the group meets (the rounds run under a short deadline)
+        torch.cuda.set_device(0)
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(10 ** 6)
+        s0.record()
+        torch.cuda._sleep(10 ** 7)
+        s1.record()
+        s1.synchronize()
+        stall_per_ms = 10 ** 7 / s0.elapsed_time(s1)
     L = Layout(n=a.n, block_size=a.block)
     L0 = Layout(n=a.replan_first_n, block_size=a.block) if a.replan and a.replan_first_n else L
     if a.transport == "rccl":
@@ -109,6 +123,8 @@ def main():
         flags.zero_()
         nxt.zero_()
         unx.zero_()
+    if a.stall_ms:
+        torch.cuda._sleep(int(stall_per_ms * a.stall_ms))
     t0 = time.monotonic()
     try:
         for r in range(a.rounds):
@@ -129,10 +145,14 @@ def main():
         # clean-up a dead group cannot do
         took = time.monotonic() - t0
         eng.abort()
+        c0 = time.monotonic()
+        rcs = eng.close()  # (bounded by the deadline even while the device still waits on a peer)
+        closed = time.monotonic() - c0
         with open(a.status, "w") as f:
-            json.dump({"error": str(e), "seconds_to_error": took}, f)
-        print(f"rank {a.rank} failed after {took:.2f} s: {e}", flush=True)
-        eng.close()
+            json.dump({"error": str(e), "seconds_to_error": took, "close_seconds": closed, "close_rcs": list(rcs)}, f)
+        print(f"rank {a.rank} failed after {took:.2f} s: {e}; closed in {closed:.2f} s {rcs}", flush=True)
+        if a.drain:
+            torch.cuda.synchronize()
         os._exit(3)
     torch.cuda.synchronize()
     if a.status:

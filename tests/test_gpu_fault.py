@@ -385,3 +385,35 @@ def test_ipc_one_sided_fault(gpu, tmp_path, after, pipe):
     assert st[0]["seconds_to_error"] < 20, st
     for r, p in enumerate(procs):
         assert p.returncode == 3, f"rank {r} exit {p.returncode}:\n{logs[r]}"
+
+
+def test_ipc_destroy_bounded_while_peer_silent(gpu, tmp_path):
+    """Two processes over HIP IPC; rank 1's stream is held by a 12 s kernel queued before its first round, so rank 0's
+    stream waits on the device for rank 1's part of the all-gather while both hosts run on.  With a 2 s deadline rank 0
+    fails (no counts), aborts, and closes: plan and transport teardown must end within their deadlines (reporting
+    OMR_ETIMEDOUT and leaving the device memory allocated) instead of waiting for the device.  Both ranks
+    then drain the device (the kernel ends and every wait resolves) before they leave."""
+    world, n = 2, 2 << 20
+    uid = cdist.ipc_unique_id().hex()
+    procs = []
+    for r in range(world):
+        cmd = [sys.executable, WORKER, "--rank", str(r), "--world", str(world), "--uid", uid, "--n", str(n),
+               "--density", "0.2", "--mode", "0", "--pipe", "sync", "--rounds", "2", "--timeout-ms", "2000",
+               "--stall-ms", "12000" if r == 1 else "0", "--drain", "--status", str(tmp_path / f"s{r}.json"),
+               "--out", str(tmp_path / f"r{r}.npz")]
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=200)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("an IPC rank hung")
+    st = [json.load(open(tmp_path / f"s{r}.json")) for r in range(world)]
+    for r, p in enumerate(procs):
+        assert p.returncode == 3, f"rank {r} exit {p.returncode}:\n{logs[r]}"
+    assert st[0]["error"] and st[0]["seconds_to_error"] < 6, (st, logs)
+    # two bounded waits of 2 s (plan, transport), well short of the 12 s the device stays busy
+    assert st[0]["close_seconds"] < 7, (st, logs)
+    assert st[0]["close_rcs"] == [ETIMEDOUT, ETIMEDOUT], (st, logs)
