@@ -86,6 +86,9 @@ def parse(argv=None):
                         "issued by the plan's progress thread; auto (default) = defer or thread, whichever ran the "
                         "untimed probe rounds faster (max over ranks; a round whose host issue time reaches its GPU "
                         "time gains from the thread)")
+    p.add_argument("--round-counts", action="store_true",
+                   help="N>1 path: ask every round for its block counts (the C API's optional outputs; the step "
+                        "reads none)")
     p.add_argument("--pipe-probe", type=int, default=12, help="--dist-pipe auto: untimed rounds per probe trial")
     p.add_argument("--world1-general", action="store_true",
                    help="diagnostic, one rank: time the multi-rank round's code path instead of the one-launch round")
@@ -533,9 +536,10 @@ def main():
             # aggregation) with HIP events on the streams they run on, inside the timed region
             # (omr_ar_plan_stage_timings)
             h0 = time.perf_counter()
+            # (the step reads no block counts: a one-rank round then never waits on the host for them)
             engine.run(xs[0], out=out, mode={"allreduce": 0, "reduce": 1, "dense": 2}[args.dist_mode],
                        async_=pipe != "sync", defer=pipe in ("defer", "thread"), thread=pipe == "thread",
-                       time_exchange=ev is not None)
+                       time_exchange=ev is not None, counts=args.round_counts)
             if timed_region:
                 host_s[0] += time.perf_counter() - h0
                 host_s[1] += 1
