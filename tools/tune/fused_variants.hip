@@ -362,6 +362,8 @@ const Variant kVariants[] = {
     {"w16 L16 st sc1", true, VA(16)},
     {"w16 L16 st nt", true, VA(2)},
     {"w16 L16 st sc0sc1nt", true, VA(19)},
+    {"w16 L16 st sc0sc1 (product)", true, VA(17)},
+    {"w16 L16 st sc1nt", true, VA(18)},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 }  // namespace

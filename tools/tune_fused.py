@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Time k_scan1f variants (waves per workgroup, loads in flight, XCD column mapping, segments per column K)
-side by side in one process, interleaved rounds, in place as the bench runs; every variant is checked against
+side by side in one process, interleaved rounds, in place as the bench runs (or --out-of-place); every variant is checked against
 the product kernel's flags and next offsets first.  usage: python tools/tune_fused.py [--rounds 12]"""
 import argparse
 import ctypes
@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--variants", default="", help="comma list of variant indices (default: all)")
     ap.add_argument("--ks", default="1,2,4")
     ap.add_argument("--block-size", type=int, default=256)
+    ap.add_argument("--out-of-place", action="store_true",
+                    help="write each input set's sums into an output of its own (as the world-1 round does)")
     a = ap.parse_args()
     torch.cuda.init()
     if not os.path.exists(LIB):
@@ -48,6 +50,7 @@ def main():
     L = Layout.from_bytes(a.size_mib << 20, a.block_size)
     bm = ops.gen_bitmap(0, a.density, L.nb)
     xs = [ops.fill_blocks(torch.from_numpy(bm).to(dev), L) for _ in range(4)]
+    outs = [x.clone() for x in xs] if a.out_of_place else xs
     flags = torch.zeros(L.nb, dtype=torch.int32, device=dev)
     nxt = torch.zeros(L.nb, dtype=torch.int32, device=dev)
     ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
@@ -61,7 +64,7 @@ def main():
     for v in vids:
         for K in [int(x) for x in a.ks.split(",")]:
             name = f"{lib.tune_fused_name(v).decode()} K{K}"
-            cases.append((name, lambda k, v=v, K=K: lib.tune_fused(v, xs[k].data_ptr(), xs[k].data_ptr(),
+            cases.append((name, lambda k, v=v, K=K: lib.tune_fused(v, xs[k].data_ptr(), outs[k].data_ptr(),
                                                                     flags.data_ptr(), nxt.data_ptr(), ws.data_ptr(),
                                                                     L.n, L.block_size, K, st)))
     for (name, fn), v in zip(cases, [v for v in vids for _ in a.ks.split(",")]):
