@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time k_scan1f variants (waves per workgroup, loads in flight, XCD column mapping, segments per column K)
-side by side in one process, interleaved rounds, in place as the bench runs (or --out-of-place); every variant is checked against
-the product kernel's flags and next offsets first.  usage: python tools/tune_fused.py [--rounds 12]"""
+side by side in one process, interleaved rounds, in place as the bench runs (or --out-of-place); every variant is
+checked against the product kernel's flags and next offsets first.  usage: python tools/tune_fused.py [--rounds 12]"""
 import argparse
 import ctypes
 import os
