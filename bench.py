@@ -302,6 +302,21 @@ def cpu_baseline(L: Layout, bm: np.ndarray, args):
     }
 
 
+def end_of_timed_region(device_barrier: bool, barrier: bool):
+    """The timed region's closing barrier and synchronize.  Over NCCL (RCCL) the barrier is queued behind every step
+    (its collective's stream waits for this rank's current stream, which the round's join() has made wait for the
+    side streams) and then waited for: 29 us on MI355X, against 70 us for a synchronize first (a host round trip more;
+    profiles/r05/timing/barrier/).  Over gloo (IPC ranks) the barrier is host-only, so the device is synchronised
+    first."""
+    if device_barrier:
+        torch.distributed.barrier()
+    else:
+        torch.cuda.synchronize()
+        if barrier:
+            torch.distributed.barrier()
+    torch.cuda.synchronize()
+
+
 def round_world1(args, L: Layout, sets, dev, stream, bm=None, torch_group=True):
     """The N>1 step's own code path at N=1, measured after the headline's timed region (which it does not touch): the
     C++ round (worker scan, mask all-gather, plan, exchange with no peers, the one-rank round's sums written by its
@@ -419,9 +434,7 @@ def host_resident(args, ws, rank, local):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
-    if dist_mode:
-        torch.distributed.barrier()
+    end_of_timed_region(dist_mode, dist_mode)
     elapsed = time.perf_counter() - t0
     if dist_mode:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -650,10 +663,7 @@ def main():
         span[1].record(stream)
     host_wait_us = engine.host_stats(reset=True)[0] if dist_mode else 0.0  # (the timed calls' blocked time only)
     join()
-    torch.cuda.synchronize()
-    if dist_mode:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
+    end_of_timed_region(dist_mode and not ipc, dist_mode)
     elapsed = time.perf_counter() - t0
     if dist_mode:
         t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
