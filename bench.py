@@ -254,7 +254,9 @@ def read_pmc_round(world: int, L: Layout):
     world-8 line over 256 MiB, B=256."""
     if world != 8 or L.nbytes != 256 << 20 or L.block_size != 256:
         return None, None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_round_r*.json")), reverse=True):  # newest round
+    paths = (glob.glob(os.path.join(ROOT, "profiles", "pmc_round_r*.json")) +
+             glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_round_r*.json")))
+    for path in sorted(paths, key=os.path.basename, reverse=True):  # newest round (profiles/rNN/ since round 5)
         try:
             with open(path) as f:
                 k = json.load(f)["kernels"]
