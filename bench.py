@@ -454,6 +454,9 @@ def host_resident(args, ws, rank, local):
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         n_gpus = max(ws, 1)  # RCCL: one rank per GPU (launch_plan)
+        # (omr_sparse_buckets_f32: a one-rank group reads its buckets straight from the mapped pinned buffer)
+        direct = not dist_mode and not any(os.environ.get(k)
+                                           for k in ("OMR_BUCKETS_STAGED_D2H", "OMR_BUCKETS_SCAN_HOST"))
         value = n_gpus * total.nbytes / (ms * 1e-3) / 1e9
         nz = float(bm.mean())
         print(json.dumps({
@@ -474,6 +477,9 @@ def host_resident(args, ws, rank, local):
                      "write_back": ("staged: the whole bucket copied back" if os.environ.get("OMR_BUCKETS_STAGED_D2H")
                                     else "zero-copy: the rounds store the write set (union + lane heads) into the "
                                          "pinned buffer"),
+                     "read_in": ("direct: one launch per bucket reads it from the pinned buffer (a one-rank group's "
+                                 "round, no staging copy)" if direct else
+                                 "staged: H2D copy of each bucket beside the previous bucket's round"),
                      "note": "per rank, over its own PCIe Gen5 x16 link: S in, the write set out"},
             "cpu_baseline": None}), flush=True)
     if dist_mode:

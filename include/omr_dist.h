@@ -206,9 +206,10 @@ int omr_ar_plan_exchange_time(omr_ar_plan* plan, float* ms, uint64_t* bytes_out,
  * four device buffers (H2D of bucket k+1 beside bucket k's scan and the earlier buckets' exchanges), each round
  * stores its write set (union + lane heads; the shard's, for reduce-scatter) straight into the pinned buffer
  * through its device mapping, and the call returns once the host buffer holds the result (a buffer without a
- * mapping, or OMR_BUCKETS_STAGED_D2H set: each bucket, or the rank's shard, is copied back whole instead).  Device
- * memory: returns with the work enqueued on `stream` (joined).  *sent_blocks / *union_blocks: sums over the
- * buckets. */
+ * mapping, or OMR_BUCKETS_STAGED_D2H set: each bucket, or the rank's shard, is copied back whole instead).  A
+ * one-rank group with a mapped buffer stages nothing: each bucket's round is one launch that reads the bucket from
+ * host memory and stores its write set back into it.  Device memory: returns with the work enqueued on `stream`
+ * (joined).  *sent_blocks / *union_blocks: sums over the buckets. */
 int omr_sparse_buckets_f32(omr_ar_plan* plan, float* buf, uint64_t total_n, int mode, uint64_t* sent_blocks,
                            uint64_t* union_blocks, omr_stream_t stream);
 /* Means over the OMR_ROUND_TIME_EXCHANGE rounds issued since the last call (at most the last 64): the worker scan

@@ -2184,9 +2184,10 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
   // single-GPU step): so the scan writes the sums (solo).  Its bookkeeping is two counts (the union is the worker's own
   // blocks, min_next its own chain), which the scan tallies too (tally): the round is ONE launch
   // (omr_worker_scan_tally_f32) on the caller's stream, no side stream, no event, and no progress thread (nothing to
-  // issue after the scan).  (Not in the bucket pipeline, whose `out` may be a pinned host buffer's mapping: there the
-  // write-back stays beside the next bucket's scan instead of inside it.  omr_dist_test_world1_round keeps the
-  // bookkeeping on the multi-rank round's path: all-gather and plan on the side stream.)
+  // issue after the scan).  (Not in the staged bucket pipeline, whose scan reads a staging buffer and whose write-back
+  // goes beside the next bucket's scan; a one-rank group's mapped buckets do run this way, reading and writing host
+  // memory in the one launch.  omr_dist_test_world1_round keeps the bookkeeping on the multi-rank round's path:
+  // all-gather and plan on the side stream.)
   const bool solo = p->N == 1 && p->worker() && p->colocated && p->scan_from == nullptr && !p->in_buckets &&
                     mode != OMR_ROUND_DENSE_REDUCE_SCATTER;
   const bool tally = solo && !p->d->world1_general;
@@ -2383,16 +2384,24 @@ int omr_sparse_round_f32(omr_ar_plan* p, const float* x, float* out, int32_t* fl
 
 namespace {
 
+// the device mapping of a pinned host buffer (NULL if it has none)
+float* host_mapping(float* buf, const hipPointerAttribute_t& attr) {
+  float* const hbuf = static_cast<float*>(attr.hostPointer ? attr.hostPointer : buf);
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, hbuf, 0) == hipSuccess && d != nullptr) return static_cast<float*>(d);
+  (void)hipGetLastError();
+  return nullptr;
+}
+
 // omr_sparse_buckets_f32; *started is set once the first round or copy has been issued (an error after that fails
 // the plan and aborts the transport)
 int sparse_buckets_issue(omr_ar_plan* p, float* buf, uint64_t total_n, int mode, uint64_t* sent_blocks,
                          uint64_t* union_blocks, omr_stream_t stream, bool* started) {
   TRY(thread_drain(p));
-  struct InBuckets {  // (the rounds of this call keep their shard sum off the scan: see omr_sparse_round_f32)
+  struct InBuckets {  // (staged rounds keep their shard sum off the scan: see omr_sparse_round_f32)
     omr_ar_plan* p;
     ~InBuckets() { p->in_buckets = false; }
   } in_buckets{p};
-  p->in_buckets = true;
   if (total_n == 0 || total_n % p->n != 0)
     return derr(OMR_EINVAL, "sparse_buckets: total_n %llu is not a multiple of the plan's bucket of %llu floats",
                 static_cast<unsigned long long>(total_n), static_cast<unsigned long long>(p->n));
@@ -2418,9 +2427,16 @@ int sparse_buckets_issue(omr_ar_plan* p, float* buf, uint64_t total_n, int mode,
     sent += s1;
     uni += u1;
   };
-  if (!host) {  // device-resident: one deferred round per bucket, in place
+  // A one-rank group over a pinned buffer with a device mapping needs no staging: its round is one launch (the worker
+  // scan writes the sums), which reads each bucket straight from host memory and stores the write set back into it,
+  // both directions of the link at once, as omr_host_scan_sum_zero_copy_f32 does.
+  float* const hmap = host ? host_mapping(buf, attr) : nullptr;
+  const bool direct = host && hmap != nullptr && p->N == 1 && p->worker() && p->colocated &&
+                      getenv("OMR_BUCKETS_STAGED_D2H") == nullptr && getenv("OMR_BUCKETS_SCAN_HOST") == nullptr;
+  if (!host || direct) {  // device-resident (or mapped, one rank): one deferred round per bucket, in place
+    float* const base = host ? hmap : buf;
     for (uint64_t k = 0; k < K; ++k) {
-      float* b = buf + k * p->n;
+      float* b = base + k * p->n;
       TRY(omr_sparse_round_f32(p, b, b, nullptr, nullptr, nullptr, rmode, &s1, &u1, stream));
       acc();
     }
@@ -2429,10 +2445,13 @@ int sparse_buckets_issue(omr_ar_plan* p, float* buf, uint64_t total_n, int mode,
       acc();
     }
     TRY(omr_ar_plan_join(p, stream));
+    // (host memory: the call returns once the buffer holds the result, as below)
+    if (host) TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
     if (sent_blocks) *sent_blocks = sent;
     if (union_blocks) *union_blocks = uni;
     return 0;
   }
+  p->in_buckets = true;
   // pinned host: H2D(k+1) on s_in || scan(k) on stream || exchange + sums(k-1) on the plan's stream || D2H(k-2)
   constexpr int R = omr_ar_plan::kStage;
   if (p->s_in == nullptr) {
@@ -2454,12 +2473,7 @@ int sparse_buckets_issue(omr_ar_plan* p, float* buf, uint64_t total_n, int mode,
   // reference's worker copies only the blocks it gets back (client.cc:89), and every other block already holds its
   // (all-zero) input.  Otherwise (or with OMR_BUCKETS_STAGED_D2H set) the bucket, or the rank's shard, is copied
   // back whole from its staging buffer.
-  float* hdev = nullptr;
-  {
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, hbuf, 0) == hipSuccess && d != nullptr) hdev = static_cast<float*>(d);
-    else (void)hipGetLastError();
-  }
+  float* const hdev = host_mapping(buf, attr);
   const bool zc = hdev != nullptr && getenv("OMR_BUCKETS_STAGED_D2H") == nullptr;
   // Read-in: each bucket is copied into a staging buffer (H2D on s_in).  With OMR_BUCKETS_SCAN_HOST=1 (and the
   // mapping) the worker scan instead reads the bucket straight from the pinned buffer and leaves its non-zero blocks
