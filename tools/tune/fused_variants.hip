@@ -332,6 +332,13 @@ void go_f(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
   k_scan1f_study<VEC, W, LOADS, ABL, MINW, SAUX><<<grid, 64 * W, 0, st>>>(a);
 }
 
+// the product's B = 1024 form (SKIP: a batch with no block to write skips its dropped stores)
+template <int VEC, int W, int LOADS>
+void go_fs(const Layout& L, const FusedShape& f, FusedArgs a, hipStream_t st) {
+  const unsigned grid = static_cast<unsigned>(static_cast<uint64_t>(L.parts) * L.lanes * f.K);
+  k_scan1f_study<VEC, W, LOADS, 0, 1, kStoreAux, 1><<<grid, 64 * W, 0, st>>>(a);
+}
+
 struct Variant {
   const char* name;
   bool checked;  // produces the full outputs (ablations do not)
@@ -364,6 +371,8 @@ const Variant kVariants[] = {
     {"w16 L16 st sc0sc1nt", true, VA(19)},
     {"w16 L16 st sc0sc1 (product)", true, VA(17)},
     {"w16 L16 st sc1nt", true, VA(18)},
+    {"w16 L16 skip (product at B=1024)", true, go_fs<1, 16, 16>, go_fs<4, 16, 16>},
+    {"w8 L16 skip", true, go_fs<1, 8, 16>, go_fs<4, 8, 16>},
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 }  // namespace

@@ -60,6 +60,10 @@ def main():
     heads = ((np.arange(L.nb) // L.num_lanes) % L.rows_per_part) == 0
     kbytes = L.nbytes + int(np.count_nonzero(bm.astype(bool) | heads)) * L.block_size * 4 + L.nb * 8
     cases = []
+    # the product launch itself (its own shape choice), for reference
+    pplan = ops.ScanSumPlan(L, 1, device=dev, fused=True)
+    plaunch = [pplan.bind(xs[k], outs[k], torch.cuda.current_stream()) for k in range(4)]
+    cases.append(("product", lambda k: plaunch[k]() or 0))
     vids = [int(x) for x in a.variants.split(",")] if a.variants else list(range(lib.tune_fused_count()))
     for v in vids:
         for K in [int(x) for x in a.ks.split(",")]:
@@ -67,7 +71,7 @@ def main():
             cases.append((name, lambda k, v=v, K=K: lib.tune_fused(v, xs[k].data_ptr(), outs[k].data_ptr(),
                                                                     flags.data_ptr(), nxt.data_ptr(), ws.data_ptr(),
                                                                     L.n, L.block_size, K, st)))
-    for (name, fn), v in zip(cases, [v for v in vids for _ in a.ks.split(",")]):
+    for (name, fn), v in zip(cases[1:], [v for v in vids for _ in a.ks.split(",")]):
         flags.zero_(); nxt.zero_()
         assert fn(0) == 0, name
         torch.cuda.synchronize()
