@@ -7,7 +7,9 @@
 //   -c  check the result against the rank-order sum of every worker's input (the working CHECK of
 //       client.cc:449-465)    -I  in place (the reference writes results into res->buf, so rounds after the first
 //       start from the previous round's output)    -L k  run k workers as threads of this process over the
-//       loopback transport (no server needed)
+//       loopback transport (no server needed)    -H  the tensor in pinned host memory, as the reference's registered
+//       res->buf: each round reads it and returns its results into it (omr_sparse_buckets_f32 with one bucket; a
+//       one-rank group reads and writes it in one launch, more ranks stage it through device buffers)
 //   -M  (with -L k) message mode: the k workers share one GPU and the round runs as the reference's messages
 //       (omr_msg_round_f32: every worker message and aggregator reply of the per-slot state machines, in the
 //       wire format of common.cc:399-443)    -T file  (with -M) write the last round's wire trace: per message
@@ -50,6 +52,7 @@ struct Opts {
   int warmups = 10, rounds = 101;  // client.cc:368-369
   int gpu = -1, local = 0;
   bool check = false, inplace = false, messages = false, colocated = false;
+  bool host = false;  // -H: the tensor in pinned host memory, as the reference's registered res->buf
   int transport = omrnet::kRccl, local_id = -1;
   const char* trace = nullptr;
 };
@@ -66,6 +69,8 @@ void usage(const char* argv0) {  // common.cc:1441-1457 (default port and -r tex
   fprintf(stdout, " -n <floats> -b <block size> -W <warm-ups> -R <rounds> -G <gpu> -c (check) -I (in place)\n");
   fprintf(stdout, " -L <k> run k workers in this process over the loopback transport\n");
   fprintf(stdout, " -M message mode: the round as the reference's wire messages; -T <file> trace them\n");
+  fprintf(stdout, " -H the tensor in pinned host memory (the reference's registered buffer): each round reads it and\n"
+                  "    returns its results into it (omr_sparse_buckets_f32, one bucket)\n");
   fprintf(stdout, " -X rccl|ipc transport to the servers (default rccl)  -C co-located aggregation  -l <k> local id\n");
   fprintf(stdout, " -h, --help show this help message\n");
 }
@@ -114,7 +119,7 @@ int host_check(const Opts& o, int workers, const float* d_result) {
     ka[k] = acc;
   }
   std::vector<float> got(o.n);
-  if (hipMemcpy(got.data(), d_result, o.n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpy(got.data(), d_result, o.n * sizeof(float), hipMemcpyDefault) != hipSuccess) return -1;
   for (uint64_t b = 0; b < nb; ++b) {
     const float e = ka[cnt[b]];
     for (uint64_t i = b * o.block; i < (b + 1) * o.block; ++i)
@@ -152,12 +157,19 @@ int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer, int num_worker
   HIPOK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   // -c with -I: every round starts from the generator's input, as the reference's CHECK restores res.buf = input
   // after each checked round (client.cc:463-464); without it the in-place rounds would compound
-  const bool restore = o.check && o.inplace;
+  const bool restore = o.check && (o.inplace || o.host);
   float* d_in = nullptr;
   if (restore) {
     HIPOK(hipMalloc(&d_in, o.n * sizeof(float)));
     HIPOK(hipMemcpyAsync(d_in, d_x, o.n * sizeof(float), hipMemcpyDeviceToDevice, st));
     HIPOK(hipStreamSynchronize(st));
+  }
+  // -H: the round's tensor lives in pinned host memory with a device mapping (the reference's res->buf, registered
+  // for RDMA: common.cc:873-914); each round reads it and stores its results back into it (client.cc:89)
+  float* h_x = nullptr;
+  if (o.host) {
+    HIPOK(hipHostMalloc(reinterpret_cast<void**>(&h_x), o.n * sizeof(float), hipHostMallocMapped));
+    HIPOK(hipMemcpy(h_x, d_x, o.n * sizeof(float), hipMemcpyDeviceToHost));
   }
   if (printer) std::cout << "density: " << o.density << std::endl;  // client.cc:405
   const double gib = o.n * sizeof(float) / (1024.0 * 1024.0 * 1024.0);
@@ -167,8 +179,10 @@ int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer, int num_worker
   auto start = std::chrono::steady_clock::now();
   for (int round = 0; round < o.warmups + o.rounds; ++round) {
     float* out = o.inplace ? d_x : d_out;
-    // (no counts asked for: the reference's round reports none, and a one-rank round then never waits mid-round)
-    if (omr_sparse_allreduce_f32(plan, d_x, out, nullptr, nullptr, nullptr, nullptr, nullptr, st)) {
+    // (no counts asked for: the reference's round reports none, and a one-rank round then never waits mid-round;
+    // -H: the call returns once the host buffer holds the results)
+    if (o.host ? omr_sparse_buckets_f32(plan, h_x, o.n, OMR_ROUND_ALLREDUCE, nullptr, nullptr, st)
+               : omr_sparse_allreduce_f32(plan, d_x, out, nullptr, nullptr, nullptr, nullptr, nullptr, st)) {
       fprintf(stderr, "failed to run the round: %s\n", omr_dist_last_error());  // client.cc:131-135
       return 1;
     }
@@ -189,16 +203,20 @@ int run_worker(omr_dist* d, const Opts& o, int gpu, bool printer, int num_worker
       start = std::chrono::steady_clock::now();
     }
     if (restore && round + 1 < o.warmups + o.rounds) {  // res.buf = input (client.cc:463-464), outside the timing
-      HIPOK(hipMemcpyAsync(d_x, d_in, o.n * sizeof(float), hipMemcpyDeviceToDevice, st));
+      HIPOK(hipMemcpyAsync(o.host ? h_x : d_x, d_in, o.n * sizeof(float), hipMemcpyDefault, st));
       HIPOK(hipStreamSynchronize(st));
       start = std::chrono::steady_clock::now();
     }
   }
   (void)hipFree(d_in);
   int rc = 0;
+  struct FreeHost {  // (after the check, which reads it)
+    float* h;
+    ~FreeHost() { (void)hipHostFree(h); }
+  } free_host{h_x};
   if (o.check) {  // the CHECK of client.cc:449-465, done right: expected = rank-order sum of every input
     HIPOK(hipDeviceSynchronize());
-    const int c = host_check(o, world, o.inplace ? d_x : d_out);
+    const int c = host_check(o, world, o.host ? h_x : (o.inplace ? d_x : d_out));
     if (c == 0) std::cout << "check OK" << std::endl;  // every worker reports its own check (client.cc:460)
     if (c < 0) fprintf(stderr, "check skipped: %s\n", omr_last_error());
     if (c == 1) rc = 1;
@@ -484,7 +502,7 @@ int main(int argc, char* argv[]) {
                               {"service-level", 1, nullptr, 's'}, {"density-ratio", 1, nullptr, 'r'},
                               {"help", 0, nullptr, 'h'},          {nullptr, 0, nullptr, 0}};
   while (true) {
-    int c = getopt_long(argc, argv, "p:d:i:g:s:r:n:b:W:R:G:L:T:X:l:cIMCh", longopts, nullptr);
+    int c = getopt_long(argc, argv, "p:d:i:g:s:r:n:b:W:R:G:L:T:X:l:cIMCHh", longopts, nullptr);
     if (c == -1) break;
     switch (c) {
       case 'p': o.port = static_cast<int>(strtoul(optarg, nullptr, 0)); break;
@@ -516,8 +534,14 @@ int main(int argc, char* argv[]) {
         break;
       case 'l': o.local_id = atoi(optarg); break;
       case 'C': o.colocated = true; break;
+      case 'H': o.host = true; break;
       default: usage(argv[0]); return 1;
     }
+  }
+  if (o.host && o.messages) {  // (the message round runs on device tensors only)
+    fprintf(stderr, "-H and -M cannot be combined\n");
+    usage(argv[0]);
+    return 1;
   }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {

@@ -420,6 +420,22 @@ def test_client_loopback_check_in_place(gpu, mode):
     assert "check OK" in out and "test result is 0" in out
 
 
+@pytest.mark.parametrize("workers,r", [(1, "0.095"), (1, "1.0"), (3, "0.3")])
+def test_client_loopback_host_resident(gpu, workers, r):
+    """-H: each worker's tensor lives in pinned host memory, as the reference's registered res->buf, and every round
+    reads it and returns its results into it (one worker: one launch per round on the mapped buffer; three: staged
+    through device buffers); the CHECK restores the input before each round and checks the last one."""
+    rc, out = _run([os.path.join(BIN, "omr_client"), "-L", str(workers), "-H", "-n", str(1 << 20), "-r", r, "-W", "2",
+                    "-R", "3", "-c"])
+    assert rc == 0, out
+    assert "check OK" in out and "average alg bw" in out and "test result is 0" in out
+
+
+def test_client_host_with_messages_refused(gpu):
+    rc, out = _run([os.path.join(BIN, "omr_client"), "-L", "2", "-H", "-M", "-n", str(1 << 20)])
+    assert rc != 0 and "cannot be combined" in out, out
+
+
 def test_server_client_rccl_one_worker(gpu):
     port = "19877"
     srv = subprocess.Popen([os.path.join(BIN, "omr_server"), "-p", port, "127.0.0.1"], stdout=subprocess.PIPE,
