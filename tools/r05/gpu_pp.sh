@@ -13,6 +13,5 @@ flow() {  # $1 port, $2 tag, $3 server binary, $4 client binary, rest: client ar
   return 0
 }
 rm -f $O/summary.txt
-flow 19901 plain_onecore "taskset -c 3 $B/omr_server" "taskset -c 3 $B/omr_client" -n 4194304
-flow 19902 plain_slowcli $B/omr_server "taskset -c 5 nice -n 19 $B/omr_client" -n 4194304
-flow 19903 plain_onecore_big "taskset -c 3 $B/omr_server" "taskset -c 3 $B/omr_client" -n 16777216
+flow 19904 plainsrv_asanexe_plainlib $B/omr_server build/asan_exe/omr_client -n 4194304
+flow 19905 mixed_again $B/omr_server $A/omr_client -n 4194304
