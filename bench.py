@@ -94,6 +94,9 @@ def parse(argv=None):
                    help="diagnostic, one rank: time the multi-rank round's code path instead of the one-launch round")
     p.add_argument("--probe-cands", default="",
                    help="diagnostic: the probe's candidates in order, e.g. 'thread:1,defer:2' (pipeline:side streams)")
+    p.add_argument("--queue-check", choices=("on", "off"), default="on",
+                   help="N>1: check the side streams' hardware queues against the caller's stream (omr_ar_plan_"
+                        "set_queue_check; on: the library's default)")
     p.add_argument("--side-streams", choices=("1", "2", "auto"), default="auto",
                    help="N>1: the round's side streams (omr_ar_plan_set_side_streams): one, two (plan + exchange), or "
                         "auto = measured on the node by the probe, with the pipeline mode")
@@ -542,6 +545,8 @@ def main():
             # N>1 side streams) instead of the one-launch round
             engine.test_world1_round(True)
             engine.replan()
+        if args.queue_check == "off":
+            engine.set_queue_check(False)
         engine_fused = engine.fused_pack  # the worker scan packs the exchange's blocks itself
         for xs, out in sets:  # out-of-place result buffers keep every step's input pristine
             out.copy_(xs[0])
@@ -725,45 +730,45 @@ def main():
         exchange["stages_ms"]["scan"] = round(kms, 5)
         exchange["timing"] = ("a one-rank round is one launch on the caller's stream: no per-round stage events; the "
                               "scan stage is the roofline's kernel_ms (events around all K rounds)")
-    if True:
-        if dist_mode:
-            if ranks == 1 and args.dist_mode != "dense" and args.world1_general:  # (the scan also writes masks)
-                kbytes = fused_bytes(L, bitmaps[0]) + L.rows * 8
-            elif ranks == 1 and args.dist_mode != "dense":  # one rank: the scan writes the shard sums itself
-                kbytes = one_rank_round_bytes(L, bitmaps[0])
-            else:
-                kbytes = (scan_pack_bytes(L, bitmaps[0], rank, ranks) if engine_fused else scan_only_bytes(L))
-        elif m == 1 and args.kernel == "fused":
-            kbytes = fused_bytes(L, bitmaps[0])
+    if dist_mode:
+        if ranks == 1 and args.dist_mode != "dense" and args.world1_general:  # (the scan also writes masks)
+            kbytes = fused_bytes(L, bitmaps[0]) + L.rows * 8
+        elif ranks == 1 and args.dist_mode != "dense":  # one rank: the scan writes the shard sums itself
+            kbytes = one_rank_round_bytes(L, bitmaps[0])
         else:
-            kbytes = algorithmic_scan_bytes(L, bitmaps, m)
-        achieved = kbytes / (kms * 1e-3) / 1e9
-        if dist_mode and ranks > 1 and engine_fused and args.dist_mode != "dense":
-            traffic, pmc_src = read_pmc_round(ranks, L)
-        else:
-            traffic, pmc_src = read_pmc(args.pmc, workload, dist_mode)
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "kernel": kernel_name,
-                    "kernel_ms": round(kms, 5),
-                    "algorithmic_bytes_per_launch": kbytes,
-                    "timing": ("fence-free HIP events (hipEventDisableSystemFence) on the kernel's stream around "
-                               "the timed launches" + (" (all K, divided by K)" if one_kernel else
-                                                       f" (every {every}th step)")
-                               if scan_ms_dist is None else
-                               ("fence-free HIP events on the caller's stream around all K timed rounds, divided by K "
-                                "(a one-rank round is one launch)") if one_launch else
-                               (f"HIP events on the round's stream around its worker scan, in every {every}th timed "
-                                f"round (inside the timed region, omr_ar_plan_timings)")),
-                    "traffic_source": ("rocprofv3 PMC 2*FETCH_SIZE+WRITE_SIZE per launch, "
-                                       + os.path.relpath(pmc_src, ROOT)) if traffic else None}
-        if not dist_mode:
-            sbytes = step_algorithmic_bytes(L, bitmaps, m)
-            roofline["step_algorithmic_bytes"] = sbytes
-            roofline["step_frac"] = round(sbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+            kbytes = (scan_pack_bytes(L, bitmaps[0], rank, ranks) if engine_fused else scan_only_bytes(L))
+    elif m == 1 and args.kernel == "fused":
+        kbytes = fused_bytes(L, bitmaps[0])
+    else:
+        kbytes = algorithmic_scan_bytes(L, bitmaps, m)
+    achieved = kbytes / (kms * 1e-3) / 1e9
+    if dist_mode and ranks > 1 and engine_fused and args.dist_mode != "dense":
+        traffic, pmc_src = read_pmc_round(ranks, L)
+    else:
+        traffic, pmc_src = read_pmc(args.pmc, workload, dist_mode)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "kernel": kernel_name,
+                "kernel_ms": round(kms, 5),
+                "algorithmic_bytes_per_launch": kbytes,
+                "timing": ("fence-free HIP events (hipEventDisableSystemFence) on the kernel's stream around "
+                           "the timed launches" + (" (all K, divided by K)" if one_kernel else
+                                                   f" (every {every}th step)")
+                           if scan_ms_dist is None else
+                           ("fence-free HIP events on the caller's stream around all K timed rounds, divided by K "
+                            "(a one-rank round is one launch)") if one_launch else
+                           (f"HIP events on the round's stream around its worker scan, in every {every}th timed "
+                            f"round (inside the timed region, omr_ar_plan_timings)")),
+                "traffic_source": ("rocprofv3 PMC 2*FETCH_SIZE+WRITE_SIZE per launch, "
+                                   + os.path.relpath(pmc_src, ROOT)) if traffic else None}
+    if not dist_mode:
+        sbytes = step_algorithmic_bytes(L, bitmaps, m)
+        roofline["step_algorithmic_bytes"] = sbytes
+        roofline["step_frac"] = round(sbytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
 
     if dist_mode:
         engine_side_streams = engine.side_streams
+        engine_queues = engine.queue_report()
         engine.close()  # every rank (the IPC transport's board is released when the last rank leaves)
     if rank != 0:
         if dist_mode:
@@ -816,6 +821,8 @@ def main():
         line["exchange"] = exchange
         line["exchange"]["pipe"] = pipe
         line["exchange"]["side_streams"] = engine_side_streams
+        # the side streams' hardware-queue check against the caller's stream (omr_ar_plan_queue_report)
+        line["exchange"]["side_stream_queues"] = engine_queues
         if pipe_probe is not None:
             line["exchange"]["pipe_probe_ms_per_round"] = pipe_probe
     if not dist_mode and m == 1 and not args.no_round:

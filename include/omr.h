@@ -273,9 +273,12 @@ uint64_t omr_pack_send_offset(const uint64_t* shard_bounds, uint32_t num_shards,
  *   zero_masks (device uint64[rows] or NULL) is cleared (the next round's omr_worker_scan_f32 target);
  *   union_masks may be NULL (not stored).
  * workspace: device uint64[omr_round_plan_workspace_words()], zero-filled before its first launch and left to the
- * plan between launches (the kernel re-arms it); launches sharing a workspace run in stream order.  seq != 0 and
- * differs from the previous launch's on the same workspace and counts.  Row chunks of the launch run side by side
- * and hand each other their popcount totals through the workspace (ABI 2; ABI 1 took an arrival counter). */
+ * plan between launches (the kernel re-arms it); launches sharing a workspace run in stream order.  seq != 0 and must
+ * not repeat the seq of ANY earlier launch on the same workspace and counts (a strictly increasing counter, as the
+ * multi-rank round's, skipping 0 when it wraps): chunk totals are tagged, never cleared, so a launch with an earlier
+ * launch's seq could take that launch's stale totals for chunks it has more of.  Row chunks of the launch
+ * run side by side and hand each other their popcount totals through the workspace (ABI 2; ABI 1 took an arrival
+ * counter). */
 uint64_t omr_round_plan_workspace_words(void);
 int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                    uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,

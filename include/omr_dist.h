@@ -239,8 +239,8 @@ int omr_ar_plan_fused_pack(const omr_ar_plan* plan);
 uint64_t omr_ar_plan_device_bytes(const omr_ar_plan* plan);
 /* Make `stream` wait for every OMR_ROUND_ASYNC round issued so far on this plan (no-op if none). */
 int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
-/* The asynchronous rounds' side streams: 2 (the default at world > 1, except over IPC beyond 4 ranks, where ranks share
- * GPUs and their hardware queues add up) = a plan stream for the mask all-gather and the
+/* The asynchronous rounds' side streams: 2 (the default at world > 1, except over IPC where more than 4 ranks share this
+ * rank's GPU and their hardware queues add up) = a plan stream for the mask all-gather and the
  * plan, an exchange stream for the exchange, the shard sums and the return trip, so round k-2's exchange runs beside
  * round k's plan; 1 (the default at world 1) = everything after the scan on one stream, in issue order.  Which is
  * faster depends on how the process's streams share its hardware queues: bench.py's N>1 lines measure
@@ -248,6 +248,19 @@ int omr_ar_plan_join(omr_ar_plan* plan, omr_stream_t stream);
  * Returns OMR_EINVAL for n other than 1 or 2. */
 int omr_ar_plan_set_side_streams(omr_ar_plan* plan, int n);
 int omr_ar_plan_side_streams(const omr_ar_plan* plan);
+/* Side streams on hardware queues of their own (round 6).  HIP maps each stream onto one of the process's hardware
+ * queues when it is made, and streams that share one run as one FIFO: a side-stream step queued between two worker
+ * scans then holds the next scan.  So before the first asynchronous round on a caller's stream (again
+ * whenever the caller's stream changes, or after omr_ar_plan_set_side_streams) the plan drains its side streams and
+ * probes them: a one-wave kernel holds one stream's queue while a mark is queued on the other; a side stream whose mark
+ * cannot run while the caller's queue (or the other side stream's) is held is replaced by a fresh stream that passes
+ * (up to six tried).  About a millisecond once per caller stream.  On by default, except for the loopback transport
+ * (threads sharing one process's queues); omr_ar_plan_set_queue_check(plan, 0) turns it off.
+ * omr_ar_plan_queue_report: *disjoint = 1 when the last check left every side stream on a queue of its own, 0 when
+ * some stream still shares one, -1 before any check; *probes / *replaced count the probes run and the side streams
+ * replaced so far (any pointer may be NULL). */
+int omr_ar_plan_set_queue_check(omr_ar_plan* plan, int on);
+int omr_ar_plan_queue_report(const omr_ar_plan* plan, int* disjoint, int* probes, int* replaced);
 /* Join, then wait on the host until `stream` has run every round issued so far: the bounded counterpart of a stream
  * synchronise for a rank whose rounds wait on its peers.  Past the transport's deadline (or on a failure signal) the
  * transport is aborted and OMR_ETIMEDOUT / the error is returned, instead of blocking on a peer that is gone. */

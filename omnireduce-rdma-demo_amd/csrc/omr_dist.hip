@@ -156,6 +156,9 @@ struct omr_dist {
   virtual int alloc(void** ptr, size_t bytes) { return hip_check(hipMalloc(ptr, bytes), "hipMalloc"); }
   // a plan's default side streams at N > 1 (omr_ar_plan_set_side_streams): two, except where ranks share GPUs (IPC)
   virtual int default_side_streams() const { return 2; }
+  // whether a plan checks its side streams' hardware queues against the caller's stream (seat_side_streams): not for
+  // the loopback transport, whose ranks are threads sharing one process's queues
+  virtual bool queue_check_default() const { return true; }
   virtual void release(void* ptr) { (void)hipFree(ptr); }
 };
 
@@ -166,32 +169,36 @@ namespace {
 // (on the caller's stream) — RCCL forbids concurrent use of ONE communicator from two streams.  Each is used in
 // the same order on every rank.
 struct RcclDist final : omr_dist {
-  ncclComm_t comm = nullptr, xcomm = nullptr;
   // Cross-thread abort (omr_dist_abort may run on another thread while this rank waits): ncclCommAbort
-  // frees a communicator, so every use of comm / xcomm holds `cm`, and the aborting thread takes it before aborting.
-  // The owner's calls that can block inside RCCL (a group end waiting on a peer) are not held back by it: the aborter
-  // waits for them at most the deadline, then aborts anyway (which is what ends such a wait).
+  // frees a communicator, so the handles are atomics that every owner-thread call reads ONCE (live() hands out the
+  // snapshot) and the aborting thread clears before aborting, under `cm` (which do_poll holds too).  The
+  // owner's calls that can block inside RCCL (a group end waiting on a peer) are not held back by it: the aborter
+  // waits for them a short grace (kAbortGraceMs, or the deadline if shorter), then aborts anyway, which is what ends
+  // such a wait.
+  static constexpr int64_t kAbortGraceMs = 500;
+  std::atomic<ncclComm_t> comm{nullptr}, xcomm{nullptr};
   std::mutex cm;
   std::atomic<int> in_rccl{0};  // owner-thread RCCL calls in progress (outside `cm`)
   ~RcclDist() override {
-    if (xcomm) (void)ncclCommDestroy(xcomm);
-    if (comm) (void)ncclCommDestroy(comm);
+    if (ncclComm_t c = xcomm.load()) (void)ncclCommDestroy(c);
+    if (ncclComm_t c = comm.load()) (void)ncclCommDestroy(c);
   }
   // ncclCommAbort on both communicators (the split one first): the operations queued on them are cancelled on the
   // device, so this rank's streams drain; the peers' matching operations are left to their own deadlines
   void abort_group() override {
     const auto t0 = std::chrono::steady_clock::now();
+    const int64_t grace = std::min<int64_t>(timeout_ms, kAbortGraceMs);
     while (in_rccl.load(std::memory_order_acquire) != 0 &&
-           std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(timeout_ms))
+           std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(grace))
       std::this_thread::sleep_for(std::chrono::microseconds(50));
     std::lock_guard<std::mutex> g(cm);
-    if (xcomm) (void)ncclCommAbort(xcomm);
-    if (comm) (void)ncclCommAbort(comm);
-    xcomm = comm = nullptr;
+    const ncclComm_t x = xcomm.exchange(nullptr), c = comm.exchange(nullptr);
+    if (x) (void)ncclCommAbort(x);
+    if (c) (void)ncclCommAbort(c);
   }
   int do_poll() override {
     std::lock_guard<std::mutex> g(cm);
-    for (ncclComm_t c : {comm, xcomm}) {
+    for (ncclComm_t c : {comm.load(), xcomm.load()}) {
       if (c == nullptr) continue;
       ncclResult_t a = ncclSuccess;
       TRY(nccl_check(ncclCommGetAsyncError(c, &a), "ncclCommGetAsyncError"));
@@ -199,14 +206,16 @@ struct RcclDist final : omr_dist {
     }
     return 0;
   }
-  // an owner-thread RCCL call: counted (an aborter waits for it up to the deadline), and refused once aborted
+  // an owner-thread RCCL call: counted (an aborter waits for it up to the grace), and refused once aborted
   struct InRccl {
     RcclDist* d;
     explicit InRccl(RcclDist* dd) : d(dd) { d->in_rccl.fetch_add(1, std::memory_order_acq_rel); }
     ~InRccl() { d->in_rccl.fetch_sub(1, std::memory_order_acq_rel); }
   };
-  int live(const char* what) {
-    if (comm == nullptr || xcomm == nullptr || aborted.load(std::memory_order_acquire))
+  // the communicator for this call (`x`: the exchange's), read once
+  int live(const char* what, bool x, ncclComm_t* out) {
+    *out = (x ? xcomm : comm).load(std::memory_order_acquire);
+    if (*out == nullptr || aborted.load(std::memory_order_acquire))
       return derr(OMR_EABORTED, "%s: rank %d's communicators were aborted", what, rank);
     return 0;
   }
@@ -217,13 +226,15 @@ struct RcclDist final : omr_dist {
     if (world == 1 && !world1_general)
       return in == out ? 0 : hip_check(hipMemcpyAsync(out, in, bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
     InRccl g(this);
-    TRY(live("allgather"));
-    return nccl_check(ncclAllGather(in, out, bytes, ncclUint8, comm, st), "ncclAllGather");
+    ncclComm_t c = nullptr;
+    TRY(live("allgather", false, &c));
+    return nccl_check(ncclAllGather(in, out, bytes, ncclUint8, c, st), "ncclAllGather");
   }
   int do_exchange(const std::vector<Slices>& sends, const std::vector<Slices>& recvs, hipStream_t st) override {
     if (world == 1 && !world1_general) return fault(0);  // no peers: nothing to send or receive
     InRccl g(this);
-    TRY(live("exchange"));
+    ncclComm_t xc = nullptr;
+    TRY(live("exchange", true, &xc));
     TRY(nccl_check(ncclGroupStart(), "ncclGroupStart"));
     // The group is closed on every path: a group left open would capture every later RCCL call of this thread (the
     // next round's all-gather and exchange would be queued into it and never launched).  After a failed piece the
@@ -235,10 +246,10 @@ struct RcclDist final : omr_dist {
       if (p == rank) continue;
       for (const Slice& r : recvs[p])
         if (r.bytes && rc == 0 && (rc = fault(k++)) == 0)
-          rc = nccl_check(ncclRecv(r.ptr, r.bytes, ncclUint8, p, xcomm, st), "ncclRecv");
+          rc = nccl_check(ncclRecv(r.ptr, r.bytes, ncclUint8, p, xc, st), "ncclRecv");
       for (const Slice& t : sends[p])
         if (t.bytes && rc == 0 && (rc = fault(k++)) == 0)
-          rc = nccl_check(ncclSend(t.ptr, t.bytes, ncclUint8, p, xcomm, st), "ncclSend");
+          rc = nccl_check(ncclSend(t.ptr, t.bytes, ncclUint8, p, xc, st), "ncclSend");
     }
     if (rc == 0) rc = fault(k);
     const int rc_end = nccl_check(ncclGroupEnd(), "ncclGroupEnd");
@@ -250,8 +261,9 @@ struct RcclDist final : omr_dist {
                        : hip_check(hipMemcpyAsync(out, in, count * sizeof(float), hipMemcpyDeviceToDevice, st),
                                    "hipMemcpyAsync");
     InRccl g(this);
-    TRY(live("reduce_scatter"));
-    return nccl_check(ncclReduceScatter(in, out, count, ncclFloat32, ncclSum, xcomm, st), "ncclReduceScatter");
+    ncclComm_t xc = nullptr;
+    TRY(live("reduce_scatter", true, &xc));
+    return nccl_check(ncclReduceScatter(in, out, count, ncclFloat32, ncclSum, xc, st), "ncclReduceScatter");
   }
 };
 
@@ -313,6 +325,7 @@ namespace {
 // and a peer must not touch its buffers again until every reader is through.
 struct LocalDist final : omr_dist {
   omr_local_board* b = nullptr;
+  bool queue_check_default() const override { return false; }
   // (an error return makes omr_dist abort the group: the peers' barriers then end at once, with an error)
   void abort_group() override { b->abort(rank); }
   int do_poll() override {
@@ -423,6 +436,7 @@ struct IpcRank {
   std::atomic<uint32_t> joined, left;
   std::atomic<uint32_t> aborted;  // this rank aborted its transport (its peers' waits end with an error)
   std::atomic<uint64_t> evgen[kIpcChans][2];  // 1 + the generation whose handles slot [c][g % 2] holds (0: none)
+  std::atomic<uint64_t> gpu;                  // 1 + the rank's GPU (PCI domain, bus, device), set before `joined`
   hipIpcEventHandle_t ready[kIpcChans][2][kIpcRing], rdone[kIpcChans][2][kIpcRing];
 };
 struct IpcBoard {
@@ -490,6 +504,63 @@ struct IpcEvents {
   hipEvent_t ready[kIpcRing] = {}, rdone[kIpcRing] = {};
 };
 
+// OMR_IPC_TRACE=<path prefix> (diagnostic, round 6): stamps of the transport's ordering, written to <prefix>.<rank>.txt
+// when the transport is destroyed.  Per operation (channel, sequence number): the sender's device clock just before its
+// "ready" record (a one-wave kernel on the stream, queued behind the producing work) and the receiver's just after its
+// wait on that event (queued before the copy), with the host-side hipEventQuery of the peer's event at the wait.  A
+// receiver stamp earlier than its sender's means the device-side wait did not hold.  wall_clock64 is the GPU's
+// constant 100 MHz clock, one per device, so stamps of processes on one GPU compare directly.
+__global__ void k_ipc_stamp(uint64_t* dst) {
+  if (threadIdx.x == 0) __hip_atomic_store(dst, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+struct IpcTrace {
+  struct Rec {
+    uint32_t chan;
+    uint64_t seq;
+    int32_t peer;   // -1: this rank's own ready record; else the peer whose ready this rank waited for
+    int32_t query;  // hipEventQuery of the peer's event right before the wait (hipSuccess 0, hipErrorNotReady 600)
+    int64_t host_ns;
+    uint32_t slot;  // its device stamp
+  };
+  std::string path;
+  uint64_t* host = nullptr;
+  uint64_t* dev = nullptr;
+  uint32_t cap = 0, used = 0;
+  std::vector<Rec> recs;
+  bool on() const { return host != nullptr; }
+  int open(const char* prefix, int rank) {
+    path = std::string(prefix) + "." + std::to_string(rank) + ".txt";
+    cap = 1u << 16;
+    TRY(hip_check(hipHostMalloc(reinterpret_cast<void**>(&host), cap * sizeof(uint64_t),
+                                hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
+    memset(host, 0, cap * sizeof(uint64_t));
+    return hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), host, 0), "hipHostGetDevicePointer");
+  }
+  void stamp(hipStream_t st, uint32_t chan, uint64_t seq, int peer, int query) {
+    if (used == cap) return;
+    const uint32_t slot = used++;
+    k_ipc_stamp<<<1, 64, 0, st>>>(dev + slot);
+    recs.push_back(Rec{chan, seq, peer, query,
+                       std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           std::chrono::steady_clock::now().time_since_epoch()).count(), slot});
+  }
+  // (after an abort the device is not waited for: stamps still pending read 0)
+  void close(bool dead) {
+    if (!on()) return;
+    if (!dead) (void)hipDeviceSynchronize();
+    if (FILE* f = fopen(path.c_str(), "w")) {
+      fprintf(f, "# chan seq peer query host_ns device_clock\n");
+      for (const Rec& r : recs)
+        fprintf(f, "%u %llu %d %d %lld %llu\n", r.chan, static_cast<unsigned long long>(r.seq), r.peer, r.query,
+                static_cast<long long>(r.host_ns), static_cast<unsigned long long>(host[r.slot]));
+      fclose(f);
+    }
+    (void)hipHostFree(host);
+    host = dev = nullptr;
+  }
+};
+
 struct IpcDist final : omr_dist {
   IpcBoard* b = nullptr;
   std::string name;
@@ -531,6 +602,7 @@ struct IpcDist final : omr_dist {
     r->cv.notify_all();
   }
   uint64_t seq[kIpcChans] = {0, 0};
+  IpcTrace trace;  // OMR_IPC_TRACE (diagnostic)
   // allocation (base, size) -> its handle and this rank's id for it.  The plans' exported allocations are never freed
   // while the transport lives (release() parks them), so an entry never outlives its allocation.  A
   // caller's buffer (an input or output tensor) must stay allocated while the transport lives, as omr_dist.h says.
@@ -565,7 +637,10 @@ struct IpcDist final : omr_dist {
   // stream too (bisected to that change; 45 ms on one side stream with the exchange stream's queue still held),
   // while 4 ranks ran faster with two (1.43 against 2.47 ms).  So two up to 4 ranks, one beyond
   // (omr_ar_plan_set_side_streams overrides it; profiles/r05/side_streams/).
-  int default_side_streams() const override { return world <= 4 ? 2 : 1; }
+  // Counted per GPU: the ranks that share THIS rank's GPU (the board has every rank's PCI address), so IPC
+  // ranks spread over separate GPUs keep the exchange stream.
+  int share_gpu = 1;
+  int default_side_streams() const override { return share_gpu <= 4 ? 2 : 1; }
 
   static void release(IpcEvents& e, std::vector<hipEvent_t>& to) {
     for (int k = 0; k < kIpcRing; ++k) {
@@ -577,6 +652,7 @@ struct IpcDist final : omr_dist {
 
   ~IpcDist() override {
     const bool dead = aborted.load(std::memory_order_acquire);
+    trace.close(dead);
     bool idle = true;  // the device is through with this transport's work
     if (reaper.joinable()) {
       bool exited;
@@ -641,6 +717,7 @@ struct IpcDist final : omr_dist {
     } rendezvous{timeout_ms, timeout_ms};
     timeout_ms = std::max<int64_t>(timeout_ms, 120000);
     name = ipc_board_name(id);
+    if (const char* t = getenv("OMR_IPC_TRACE")) TRY(trace.open(t, rank));
     const size_t bytes = sizeof(IpcBoard);
     int fd = -1;
     if (rank == 0) {
@@ -671,6 +748,16 @@ struct IpcDist final : omr_dist {
       return derr(OMR_EINVAL, "ipc transport: board world %u, this rank says %d", b->world, world);
     b->attached.fetch_add(1);
     IpcRank& me = b->rank[rank];
+    {
+      int dev = 0, dom = 0, bus = 0, slot = 0;
+      TRY(hip_check(hipGetDevice(&dev), "hipGetDevice"));
+      TRY(hip_check(hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, dev), "hipDeviceGetAttribute"));
+      TRY(hip_check(hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dev), "hipDeviceGetAttribute"));
+      TRY(hip_check(hipDeviceGetAttribute(&slot, hipDeviceAttributePciDeviceId, dev), "hipDeviceGetAttribute"));
+      me.gpu.store(1 + ((static_cast<uint64_t>(static_cast<uint32_t>(dom)) << 32) |
+                        (static_cast<uint64_t>(static_cast<uint32_t>(bus)) << 8) | static_cast<uint32_t>(slot)),
+                   std::memory_order_relaxed);
+    }
     for (int c = 0; c < kIpcChans; ++c) {
       TRY(publish(c, 0));
       TRY(publish(c, 1));
@@ -684,6 +771,9 @@ struct IpcDist final : omr_dist {
     peer.assign(world, {});
     for (int p = 0; p < world; ++p)
       TRY(spin([&] { return b->rank[p].joined.load(std::memory_order_acquire) != 0; }, "peers to join"));
+    share_gpu = 0;
+    for (int p = 0; p < world; ++p)
+      share_gpu += b->rank[p].gpu.load(std::memory_order_relaxed) == me.gpu.load(std::memory_order_relaxed) ? 1 : 0;
     for (int c = 0; c < kIpcChans; ++c) TRY(open_gen(c, 0));
     return 0;
   }
@@ -846,6 +936,7 @@ struct IpcDist final : omr_dist {
       }
       P.e[P.nent++] = IpcEntry{it.first, hi, off, it.second.bytes};
     }
+    if (trace.on()) trace.stamp(st, static_cast<uint32_t>(c), s, -1, 0);
     TRY(hip_check(hipEventRecord(mine_of(c, s).ready[k], st), "hipEventRecord"));
     b->rank[rank].posted[c].store(s, std::memory_order_release);
     for (int p = 0; p < world; ++p)
@@ -855,7 +946,11 @@ struct IpcDist final : omr_dist {
   }
   // st waits until peer p's offered pieces are ready on the device
   int wait_ready(int c, uint64_t s, int p, hipStream_t st) {
-    return hip_check(hipStreamWaitEvent(st, peer_of(c, s, p).ready[s % kIpcRing], 0), "hipStreamWaitEvent");
+    const hipEvent_t ev = peer_of(c, s, p).ready[s % kIpcRing];
+    const int q = trace.on() ? static_cast<int>(hipEventQuery(ev)) : 0;
+    TRY(hip_check(hipStreamWaitEvent(st, ev, 0), "hipStreamWaitEvent"));
+    if (trace.on()) trace.stamp(st, static_cast<uint32_t>(c), s, p, q);
+    return 0;
   }
   // this rank is through reading its peers; st then waits until every peer is through reading this rank
   int end(int c, uint64_t s, hipStream_t st) {
@@ -1240,6 +1335,14 @@ struct omr_ar_plan {
   // count wait, the set-reuse waits, the drain), so a caller can tell issue time from waiting
   std::atomic<uint64_t> host_wait_ns{0};
   std::atomic<uint64_t> host_waits{0};
+  // Side streams on hardware queues of their own (round 6, seat_side_streams): the caller's stream they were last
+  // checked against, and the outcome (omr_ar_plan_queue_report)
+  bool queue_check = true;
+  hipStream_t seated_st = nullptr;
+  bool seated = false;
+  int q_disjoint = -1, q_probes = 0, q_replaced = 0;
+  uint32_t* qflags_host = nullptr;  // pinned: {hold running, release, mark}
+  uint32_t* qflags_dev = nullptr;
 };
 
 namespace {
@@ -1291,6 +1394,148 @@ int plan_check(omr_ar_plan* p, const char* what) {
   if (p->failed == 0) return 0;
   return derr(OMR_EABORTED, "%s: the plan failed in an earlier round (%s)", what, p->failed_why.c_str());
 }
+
+// ---------------------------------------------------------------- side streams on hardware queues of their own
+//
+// HIP maps each stream of a process onto one of the process's hardware queues (GPU_MAX_HW_QUEUES, 4 on the box) when
+// the stream is made, and the streams that share a queue run as ONE FIFO: a side-stream step queued between two worker
+// scans then holds the next scan until it has run.  Round 5 measured the N > 1 layout at 69.5-75.6 us per round on a
+// stream created after the plan against 53.5-54.1 on the null stream, for the same code.  Which streams
+// share a queue depends on the order the process made them (tools/queue_probe.hip on the box: the null stream shared
+// with the second stream made, the third with the sixth, the fourth with the fifth; profiles/r06/queues/), so the plan
+// checks instead of guessing.  A probe: stream a holds its queue with a one-wave kernel that spins on a host-mapped
+// flag, stream b stores a mark; if the mark lands while a holds, a and b are on different queues.  The hold ends on its
+// own after kHoldTicks (and at the release the host stores once the mark has landed or kMarkWindow has passed).
+constexpr uint64_t kHoldTicks = 100ull * 1000 * 100;  // wall clock at 100 MHz: 100 ms at most
+constexpr auto kMarkWindow = std::chrono::milliseconds(5);
+constexpr int kSeatTries = 6;  // fresh streams tried per side stream before keeping the shared one
+
+__global__ void k_queue_hold(uint32_t* flags, uint64_t max_ticks) {
+  if (threadIdx.x != 0) return;
+  __hip_atomic_store(&flags[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(&flags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u && wall_clock64() - t0 < max_ticks)
+    __builtin_amdgcn_s_sleep(8);
+}
+
+__global__ void k_queue_mark(uint32_t* flags) {
+  if (threadIdx.x == 0) __hip_atomic_store(&flags[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// *disjoint = work queued on b runs while a's hardware queue is held (so a and b are on different queues).  Work
+// queued on a before the probe finishes first (bounded by the transport's deadline); b should be idle.
+int queue_probe(omr_ar_plan* p, hipStream_t a, hipStream_t b, bool* disjoint) {
+  uint32_t* const h = p->qflags_host;
+  __atomic_store_n(&h[0], 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(&h[1], 0u, __ATOMIC_RELAXED);
+  __atomic_store_n(&h[2], 0u, __ATOMIC_RELAXED);
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  k_queue_hold<<<1, 64, 0, a>>>(p->qflags_dev, kHoldTicks);
+  TRY(hip_check(hipGetLastError(), "k_queue_hold"));
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = 0;
+  while (__atomic_load_n(&h[0], __ATOMIC_ACQUIRE) == 0) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(p->d->timeout_ms)) {
+      rc = derr(OMR_ETIMEDOUT, "queue probe: the caller's stream did not reach the probe within %lld ms",
+                static_cast<long long>(p->d->timeout_ms));
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  bool got = false;
+  if (rc == 0) {
+    k_queue_mark<<<1, 64, 0, b>>>(p->qflags_dev);
+    rc = hip_check(hipGetLastError(), "k_queue_mark");
+    const auto t1 = std::chrono::steady_clock::now();
+    while (rc == 0 && std::chrono::steady_clock::now() - t1 < kMarkWindow)
+      if (__atomic_load_n(&h[2], __ATOMIC_ACQUIRE) != 0) {
+        got = true;
+        break;
+      }
+  }
+  __atomic_store_n(&h[1], 1u, __ATOMIC_RELEASE);  // the hold ends (it would by itself after kHoldTicks)
+  TRY(rc);
+  TRY(hip_check(hipStreamSynchronize(b), "hipStreamSynchronize"));
+  TRY(hip_check(hipStreamSynchronize(a), "hipStreamSynchronize"));
+  ++p->q_probes;
+  *disjoint = got;
+  return 0;
+}
+
+// A fresh stream whose queue differs from avoid1's (and avoid2's, if given), or nullptr when kSeatTries fresh streams all
+// shared one (the streams tried are kept until the end, so each one made takes another queue, then destroyed).
+int fresh_stream(omr_ar_plan* p, hipStream_t avoid1, hipStream_t avoid2, bool check2, hipStream_t* out) {
+  *out = nullptr;
+  std::vector<hipStream_t> tried;
+  int rc = 0;
+  for (int i = 0; i < kSeatTries && rc == 0 && *out == nullptr; ++i) {
+    hipStream_t c = nullptr;
+    if ((rc = hip_check(hipStreamCreateWithFlags(&c, hipStreamNonBlocking), "hipStreamCreate")) != 0) break;
+    bool d1 = false, d2 = true;
+    rc = queue_probe(p, avoid1, c, &d1);
+    if (rc == 0 && d1 && check2) rc = queue_probe(p, avoid2, c, &d2);
+    if (rc == 0 && d1 && d2) *out = c;
+    else tried.push_back(c);
+  }
+  for (hipStream_t s : tried) (void)hipStreamDestroy(s);
+  return rc;
+}
+
+// Make the plan's side streams run on hardware queues apart from the caller's stream `st` and from each other, before the
+// first asynchronous round on `st`: the side streams are drained (every step already issued on them has run; a deferred
+// round's second half not issued yet goes on the seated streams later), probed, and each one that shares a queue is
+// replaced by a fresh stream that does not (the old one is idle, so nothing needs ordering across the switch).  When no
+// fresh stream helps (fewer hardware queues than streams) the shared stream is kept and the report says so.
+int seat_side_streams(omr_ar_plan* p, hipStream_t st) {
+  p->seated_st = st;
+  p->seated = true;
+  if (p->switch_ev == nullptr)
+    TRY(hip_check(hipEventCreateWithFlags(&p->switch_ev, hipEventDisableTiming | hipEventDisableSystemFence),
+                  "hipEventCreate"));
+  for (hipStream_t s : {p->ps, p->xstream}) {
+    if (s == nullptr) continue;
+    TRY(hip_check(hipEventRecord(p->switch_ev, s), "hipEventRecord"));
+    TRY(wait_event_bounded(p->d, p->switch_ev, "seat side streams"));
+  }
+  const bool two = p->cs != p->ps;
+  bool ok = true;
+  bool d = false;
+  TRY(queue_probe(p, st, p->ps, &d));
+  if (!d) {
+    hipStream_t c = nullptr;
+    TRY(fresh_stream(p, st, p->cs, two, &c));
+    if (c != nullptr) {
+      const hipStream_t old = p->ps;
+      p->ps = c;
+      if (!two) p->cs = c;
+      if (p->tail == old) p->tail = c;
+      (void)hipStreamDestroy(old);
+      ++p->q_replaced;
+    } else {
+      ok = false;
+    }
+  }
+  if (two) {
+    bool d1 = false, d2 = false;
+    TRY(queue_probe(p, st, p->cs, &d1));
+    if (d1) TRY(queue_probe(p, p->ps, p->cs, &d2));
+    if (!(d1 && d2)) {
+      hipStream_t c = nullptr;
+      TRY(fresh_stream(p, st, p->ps, true, &c));
+      if (c != nullptr) {
+        const hipStream_t old = p->xstream;
+        p->xstream = p->cs = c;
+        if (p->tail == old) p->tail = c;
+        (void)hipStreamDestroy(old);
+        ++p->q_replaced;
+      } else {
+        ok = false;
+      }
+    }
+  }
+  p->q_disjoint = ok ? 1 : 0;
+  return 0;
+}
 }  // namespace
 
 extern "C" {
@@ -1311,8 +1556,11 @@ int omr_dist_create_rccl(const void* id, int rank, int world, omr_dist** out) {
   d->world = world;
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof(uid));
-  int rc = nccl_check(ncclCommInitRank(&d->comm, world, uid, rank), "ncclCommInitRank");
-  if (rc == 0) rc = nccl_check(ncclCommSplit(d->comm, 0, rank, &d->xcomm, nullptr), "ncclCommSplit");
+  ncclComm_t c = nullptr, x = nullptr;
+  int rc = nccl_check(ncclCommInitRank(&c, world, uid, rank), "ncclCommInitRank");
+  d->comm.store(c);
+  if (rc == 0) rc = nccl_check(ncclCommSplit(c, 0, rank, &x, nullptr), "ncclCommSplit");
+  d->xcomm.store(x);
   if (rc != 0) {
     delete d;
     return rc;
@@ -1488,6 +1736,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
       if (e) (void)hipEventDestroy(e);
   (void)hipHostFree(p->counts_host);
   (void)hipHostFree(p->pub_host);
+  (void)hipHostFree(p->qflags_host);
   delete p;
   return 0;
 }
@@ -1617,6 +1866,20 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->pub_map), p->pub_host, 0),
                 "hipHostGetDevicePointer"));
   }
+  p->queue_check = p->d->queue_check_default();
+  A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->qflags_host), 64, hipHostMallocMapped | hipHostMallocCoherent),
+              "hipHostMalloc"));
+  if (rc == 0) {
+    memset(p->qflags_host, 0, 64);
+    A(hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->qflags_dev), p->qflags_host, 0),
+                "hipHostGetDevicePointer"));
+  }
+  if (rc == 0) {  // the probe's kernels loaded before any probe times them (a first launch loads the code object)
+    p->qflags_host[1] = 1;
+    k_queue_hold<<<1, 64, 0, p->ps>>>(p->qflags_dev, 0);
+    k_queue_mark<<<1, 64, 0, p->ps>>>(p->qflags_dev);
+    A(hip_check(hipGetLastError(), "queue probe warm-up"));
+  }
   for (int i = 0; i < p->nsets && rc == 0; ++i) {
     omr_ar_plan::Set& st = p->set[i];
     A(hip_check(hipMemset(st.own, 0, p->mstride * sizeof(uint64_t)), "hipMemset own masks"));
@@ -1669,6 +1932,13 @@ int timed_exchange(omr_ar_plan* p, int slot) {
   p->xt0 = t.x0;  // the last timed exchange (omr_ar_plan_exchange_time)
   p->xt1 = t.x1;
   return 0;
+}
+
+// The next round's sequence number: never 0 (the tag of no round: the plan launch refuses it), so a plan that runs
+// past 2^32 rounds wraps to 1.  Every rank of a group issues the same rounds, so their numbers agree.
+uint32_t next_seq(omr_ar_plan* p) {
+  if (++p->seq == 0) ++p->seq;
+  return p->seq;
 }
 
 // Worker w's stream of this rank's shard lands at a fixed region of `recv`, so the shard sum's pairs can be addressed
@@ -1965,10 +2235,12 @@ int wait_ev(hipStream_t on, hipEvent_t ev) {
 // Order the work issued next on side stream `on` after `ev`.  On the progress thread (OMR_ROUND_THREAD) the thread
 // waits on the host until `ev` has completed and queues no wait packet: a side stream that shares a hardware queue
 // with the caller's stream then never holds the caller's later scans behind a wait (in FIFO order they were queued
-// before the step that waits), which is how a shared queue slows the round.  Elsewhere a device-side
-// wait, so the calling thread never blocks.  Bounded by the transport's deadline and failure signals.
+// before the step that waits), which is how a shared queue slows the round.  Elsewhere, and on the
+// thread too once the side streams are checked to be on queues apart from the caller's (seat_side_streams: a wait
+// packet there holds nothing of the caller's), a device-side wait, so no thread blocks.  Bounded by the transport's
+// deadline and failure signals.
 int order_after(omr_ar_plan* p, hipStream_t on, hipEvent_t ev, const char* what) {
-  if (!t_progress) return wait_ev(on, ev);
+  if (!t_progress || (p->seated && p->q_disjoint == 1)) return wait_ev(on, ev);
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t spin = 1;; ++spin) {
     const hipError_t q = hipEventQuery(ev);
@@ -2032,7 +2304,7 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
     //    straight into pinned host memory: no copy-engine hop before the host sees them)
     //    ... and, by extra workgroups of the same launch, the aggregator chain (server.cc:86-96 min_next) over the
     //    union, when asked for, and the shard sum's pair list (sum_list)
-    seq = ++p->seq;
+    seq = next_seq(p);
     const omr_sum_list sl = p->sum_list ? list_desc(p, S) : omr_sum_list{};
     TRY(omr_check(omr_round_plan_list(S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes,
                                       p->bounds_dev, NS, S.wset, nullptr, S.prefix,
@@ -2192,6 +2464,12 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
                     mode != OMR_ROUND_DENSE_REDUCE_SCATTER;
   const bool tally = solo && !p->d->world1_general;
   if (tally) threaded = false;
+  // before the first asynchronous round on a caller's stream: the side streams on hardware queues apart from its queue
+  // (seat_side_streams; a one-launch round uses none)
+  if (async && !tally && p->queue_check && (!p->seated || p->seated_st != st)) {
+    TRY(thread_drain(p));
+    TRY(seat_side_streams(p, st));
+  }
   // a threaded round hands its steps after the scan to the progress thread; any other call first lets the thread
   // issue everything queued (the plan's state is then this thread's alone)
   TRY(threaded ? thread_start(p) : thread_drain(p));
@@ -2233,7 +2511,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
     if (p->pub_set >= 0 && p->pub_st != st) TRY(publish_pending(p));
     const int ps_i = p->pub_set;
     p->pub_set = -1;
-    solo_seq = ++p->seq;
+    solo_seq = next_seq(p);
     const size_t TS = p->tally_slots;
     TRY(omr_check(omr_worker_scan_tally_f32(x, p->n, p->B, p->lanes, p->parts, fl, nx, out, p->tally + TS * si,
                                             ps_i >= 0 ? p->tally + TS * ps_i : nullptr,
@@ -2608,6 +2886,7 @@ int omr_ar_plan_set_side_streams(omr_ar_plan* p, int n) {
   if (want != p->ps) TRY(plan_fail(p, hip_check(hipStreamWaitEvent(p->ps, p->switch_ev, 0), "hipStreamWaitEvent")));
   const hipStream_t old = p->cs;
   p->cs = want;
+  p->seated = false;  // (the next asynchronous round checks the new layout's queues)
   if (p->tail != nullptr) p->tail = want;
   if (n == 1 && old == p->xstream) {
     // the exchange stream goes once it is idle: a stream keeps its hardware queue mapped while it exists, and with
@@ -2621,6 +2900,21 @@ int omr_ar_plan_set_side_streams(omr_ar_plan* p, int n) {
 }
 
 int omr_ar_plan_side_streams(const omr_ar_plan* p) { return p == nullptr ? 0 : (p->cs != p->ps ? 2 : 1); }
+
+int omr_ar_plan_set_queue_check(omr_ar_plan* p, int on) {
+  if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_set_queue_check: NULL");
+  p->queue_check = on != 0;
+  p->seated = false;
+  return 0;
+}
+
+int omr_ar_plan_queue_report(const omr_ar_plan* p, int* disjoint, int* probes, int* replaced) {
+  if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_queue_report: NULL");
+  if (disjoint) *disjoint = p->q_disjoint;
+  if (probes) *probes = p->q_probes;
+  if (replaced) *replaced = p->q_replaced;
+  return 0;
+}
 
 int omr_ar_plan_wait(omr_ar_plan* p, omr_stream_t stream) {
   if (p == nullptr) return derr(OMR_EINVAL, "ar_plan_wait: NULL");

@@ -64,6 +64,8 @@ def load():
         "omr_ar_plan_join": (i, [vp, vp]),
         "omr_ar_plan_set_side_streams": (i, [vp, i]),
         "omr_ar_plan_side_streams": (i, [vp]),
+        "omr_ar_plan_set_queue_check": (i, [vp, i]),
+        "omr_ar_plan_queue_report": (i, [vp, vp, vp, vp]),
         "omr_ar_plan_fused_pack": (i, [vp]),
         "omr_ar_plan_device_bytes": (u64, [vp]),
         "omr_dist_test_world1_round": (i, [vp, i]),
@@ -171,6 +173,18 @@ class CppSparseAllreduce:
     @property
     def side_streams(self) -> int:
         return int(load().omr_ar_plan_side_streams(self._p))
+
+    def set_queue_check(self, on: bool = True):
+        """Check (default) or not the side streams' hardware queues against the caller's stream before its first
+        asynchronous round (omr_ar_plan_set_queue_check)."""
+        _check(load().omr_ar_plan_set_queue_check(self._p, int(on)), "omr_ar_plan_set_queue_check")
+
+    def queue_report(self) -> dict:
+        """{"disjoint": 1 / 0 / -1 (not checked yet), "probes": n, "replaced": n} (omr_ar_plan_queue_report)."""
+        d, pr, rp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(load().omr_ar_plan_queue_report(self._p, ctypes.byref(d), ctypes.byref(pr), ctypes.byref(rp)),
+               "omr_ar_plan_queue_report")
+        return {"disjoint": d.value, "probes": pr.value, "replaced": rp.value}
 
     def replan(self, L: Optional[Layout] = None):
         """Destroy the plan and make a new one on the same transport, of the same shape or of layout L (collective: every

@@ -10,7 +10,9 @@ twice:
   general / created
   general1 / ...   the same on ONE side stream (omr_ar_plan_set_side_streams(1))
 Prints microseconds per round and the headline kernel's step for reference.
-usage: python tools/round_inproc_r05.py [--steps 200] [--reps 2] [--pipe defer|thread] [--torch-group]"""
+Round 6: the side streams are checked against the caller's stream's hardware queue before its first asynchronous round
+(omr_ar_plan_queue_report is printed per cell); --no-queue-check turns the check off (round 5's behaviour).
+usage: python tools/round_inproc_r05.py [--steps 200] [--reps 2] [--pipe defer|thread] [--torch-group] [--no-queue-check]"""
 import argparse
 import json
 import os
@@ -46,6 +48,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2, help="interleaved repetitions of the four layouts")
     ap.add_argument("--pipe", choices=("defer", "thread"), default="defer",
                     help="thread: the progress thread issues the steps after the scan (host-ordered side streams)")
+    ap.add_argument("--no-queue-check", action="store_true", help="side streams as made (round 5)")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -70,12 +73,15 @@ def main():
             eng.replan()  # (the hook takes effect on plans made after it: general = the N>1 stream layout)
             if layout == "general1":
                 eng.set_side_streams(1)  # the N>1 round's path on one side stream
+            if a.no_queue_check:
+                eng.set_queue_check(False)
             created = torch.cuda.Stream(dev)  # a stream created after the plan
             for sname, st in (("null", null), ("created", created)):
                 with torch.cuda.stream(st):
                     us = round_loop(eng, sets, st, a.steps, thread=a.pipe == "thread")
                 res.setdefault(f"{layout} / {sname}", []).append(round(us, 2))
-                print(f"rep {rep} {layout:8s} {sname:8s} {us:7.2f} us per round", flush=True)
+                print(f"rep {rep} {layout:8s} {sname:8s} {us:7.2f} us per round  queues {eng.queue_report()}",
+                      flush=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(a.steps):
@@ -88,7 +94,7 @@ def main():
     print(json.dumps(res))
     if a.json:
         with open(a.json, "w") as f:
-            json.dump({"torch_group": a.torch_group, "pipe": a.pipe, "steps": a.steps, "us_per_round": res}, f, indent=1)
+            json.dump({"torch_group": a.torch_group, "pipe": a.pipe, "queue_check": not a.no_queue_check, "steps": a.steps, "us_per_round": res}, f, indent=1)
 
 
 if __name__ == "__main__":
