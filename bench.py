@@ -421,15 +421,25 @@ def host_resident(args, ws, rank, local):
     included).  N=1: a one-rank group (no peers); N>1: RCCL over xGMI between the ranks' staged buckets."""
     from omr import cdist
     dist_mode = ws > 1
+    ipc = dist_mode and args.dist_transport == "ipc"  # a rehearsal: ranks share the box's GPUs over HIP IPC
     if dist_mode:
+        local = local % max(1, torch.cuda.device_count()) if ipc else local
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if ipc:
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local if dist_mode else 0)
     Lb = Layout.from_bytes(args.bucket_mib << 20, args.block_size)
     total = Layout.from_bytes(args.size_mib << 20, args.block_size)
     bm = ops.gen_bitmap(rank, args.density, total.nb)
     host = ops.fill_blocks(torch.from_numpy(bm).to(dev), total).cpu().pin_memory()
-    eng = cdist.CppSparseAllreduce(Lb, dev, transport="rccl" if dist_mode else "local1")
+    if ipc:
+        uid = [cdist.ipc_unique_id() if rank == 0 else None]
+        torch.distributed.broadcast_object_list(uid, src=0)
+        eng = cdist.CppSparseAllreduce(Lb, dev, transport="ipc", uid=uid[0], rank=rank, world=ws)
+    else:
+        eng = cdist.CppSparseAllreduce(Lb, dev, transport="rccl" if dist_mode else "local1")
     step = lambda: eng.run_buckets(host, mode=cdist.CppSparseAllreduce.ALLREDUCE)  # noqa: E731
     for _ in range(args.warmup):
         step()
@@ -439,10 +449,10 @@ def host_resident(args, ws, rank, local):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    end_of_timed_region(dist_mode, dist_mode)
+    end_of_timed_region(dist_mode and not ipc, dist_mode)
     elapsed = time.perf_counter() - t0
     if dist_mode:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if ipc else dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     # the link's own ceiling on this box: one plain pinned H2D and one D2H of a bucket
@@ -456,11 +466,13 @@ def host_resident(args, ws, rank, local):
     eng.close()
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        n_gpus = max(ws, 1)  # RCCL: one rank per GPU (launch_plan)
-        # (omr_sparse_buckets_f32: a one-rank group reads its buckets straight from the mapped pinned buffer)
-        direct = not dist_mode and not any(os.environ.get(k)
-                                           for k in ("OMR_BUCKETS_STAGED_D2H", "OMR_BUCKETS_SCAN_HOST"))
-        value = n_gpus * total.nbytes / (ms * 1e-3) / 1e9
+        # RCCL: one rank per GPU (launch_plan); IPC: the ranks share the box's GPUs
+        n_gpus = max(1, min(ws, torch.cuda.device_count())) if ipc else max(ws, 1)
+        # (omr_sparse_buckets_f32 reads and writes the mapped pinned buckets in place unless a staging mode is set)
+        direct = (not dist_mode and not os.environ.get("OMR_BUCKETS_STAGED")
+                  or dist_mode and bool(os.environ.get("OMR_BUCKETS_DIRECT"))) and not any(
+            os.environ.get(k) for k in ("OMR_BUCKETS_STAGED_D2H", "OMR_BUCKETS_SCAN_HOST"))
+        value = max(ws, 1) * total.nbytes / (ms * 1e-3) / 1e9
         nz = float(bm.mean())
         print(json.dumps({
             "metric": (f"GB/s end-to-end sparse all-reduce from pinned host memory, {args.size_mib} MiB fp32 @ "
@@ -472,7 +484,9 @@ def host_resident(args, ws, rank, local):
             "config": {"workload": (f"{args.size_mib} MiB fp32 per rank in pinned host memory, block_size="
                                     f"{args.block_size}, -r {args.density}, buckets of {args.bucket_mib} MiB, "
                                     f"all-reduce in place (BASELINE config 5)"),
-                       "parallelism": f"dp{n_gpus}", "nonzero_fraction": round(nz, 5)},
+                       "parallelism": (f"dp{ws} over HIP IPC, {ws} ranks on {n_gpus} GPU(s): a rehearsal, not a "
+                                       f"scaling figure" if ipc else f"dp{n_gpus}"),
+                       "ranks": max(ws, 1), "nonzero_fraction": round(nz, 5)},
             "roofline": None,
             "pcie": {"per_rank_GBps": round(total.nbytes / (ms * 1e-3) / 1e9, 2),
                      "plain_h2d_GBps": round(h2d, 2), "plain_d2h_GBps": round(d2h, 2),
@@ -480,8 +494,9 @@ def host_resident(args, ws, rank, local):
                      "write_back": ("staged: the whole bucket copied back" if os.environ.get("OMR_BUCKETS_STAGED_D2H")
                                     else "zero-copy: the rounds store the write set (union + lane heads) into the "
                                          "pinned buffer"),
-                     "read_in": ("direct: one launch per bucket reads it from the pinned buffer (a one-rank group's "
-                                 "round, no staging copy)" if direct else
+                     "read_in": ("direct: each bucket's round reads it from the mapped pinned buffer (the worker "
+                                 "scan over PCIe; N > 1: its pack writes the other shards' blocks to device send "
+                                 "buffers), no staging copy" if direct else
                                  "staged: H2D copy of each bucket beside the previous bucket's round"),
                      "note": "per rank, over its own PCIe Gen5 x16 link: S in, the write set out"},
             "cpu_baseline": None}), flush=True)

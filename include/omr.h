@@ -230,6 +230,21 @@ int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, 
                              const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard, float* send,
                              uint32_t* shard_counters, uint32_t* pos_table, void* workspace, size_t workspace_bytes,
                              omr_stream_t stream);
+/* The round check (round 6).  The two worker scans above with check_slots (device
+ * uint64[omr_round_check_slots()], or NULL: none): workgroup b also stores check_slots[b] = (check_seq << 32) | the
+ * non-zero blocks it found, i.e. the number of row-mask bits it set.  Put in the array the round all-gathers (after
+ * the masks and position table), they let the plan launch check on the device that each worker's gathered array is
+ * the one its scan of THIS round wrote (omr_round_plan_check). */
+uint32_t omr_round_check_slots(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts);
+int omr_worker_scan_check_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                              int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out, void* workspace,
+                              size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq, omr_stream_t stream);
+int omr_worker_scan_pack_check_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes,
+                                   uint32_t num_parts, int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks,
+                                   float* out, const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard,
+                                   float* send, uint32_t* shard_counters, uint32_t* pos_table, void* workspace,
+                                   size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq,
+                                   omr_stream_t stream);
 /* The one-rank round's worker scan (a world-1 group: one worker, one aggregator; server.cc:83-96 with one worker:
  * the union is the worker's own blocks and min_next its own chain, so the aggregator's bookkeeping is two counts).
  * As omr_scan_sum_fused_f32 (flags, next offsets, out = 0.0f + x over the write set if non-NULL), plus
@@ -299,6 +314,20 @@ int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask
                         uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters,
                         uint64_t* workspace, uint32_t seq, uint32_t* union_next, uint32_t block_size,
                         const struct omr_sum_list* list, omr_stream_t stream);
+/* omr_round_plan_list plus the round check, by one more workgroup of the launch (check_status NULL: none): worker c's
+ * check slots are words [check_offset, check_offset + check_slots) of its array (row_masks + c * mask_stride); the
+ * check stores *check_status = (seq << 32) | code at system scope (it may be pinned host memory, polled as the
+ * counts): 0 when every slot carries `seq` and each worker's slots add up to its masks' popcount; 0x100 + c when a
+ * slot of worker c carries another round's seq (its array was read before its scan wrote it, or another buffer was
+ * read); 0x200 + c when worker c's masks hold fewer (or other) bits than its scan counted (the array was read before
+ * the scan finished: an array only gains bits between the plan that clears it and the scan that refills it). */
+int omr_round_plan_check(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                         uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                         uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint64_t* counts,
+                         uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters,
+                         uint64_t* workspace, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                         const struct omr_sum_list* list, uint64_t check_offset, uint32_t check_slots,
+                         uint64_t* check_status, omr_stream_t stream);
 
 /* Block movement addressed by a row mask and its prefix (no block list): the k-th set bit of `row_masks` over
  * rows [0, rows) minus [skip_begin, skip_end) is block k of the packed stream.
@@ -318,6 +347,12 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
                       const uint64_t* row_masks, uint32_t count, const uint32_t* prefix, const uint64_t* write_set,
                       uint64_t rows, uint64_t row_begin, uint64_t row_end, uint32_t num_lanes, uint32_t block_size,
                       int packed_out, float* out, omr_stream_t stream);
+/* The same with worker c's masks at row_masks + c * mask_stride (mask_stride >= rows: the round's all-gathered arrays,
+ * which carry the round check's slots after the masks). */
+int omr_shard_sum_stride_f32(const float* own, uint32_t me, const float* recv, const uint64_t* recv_offsets,
+                             const uint64_t* row_masks, uint64_t mask_stride, uint32_t count, const uint32_t* prefix,
+                             const uint64_t* write_set, uint64_t rows, uint64_t row_begin, uint64_t row_end,
+                             uint32_t num_lanes, uint32_t block_size, int packed_out, float* out, omr_stream_t stream);
 
 /* The shard sum over the fused pack's column-ordered streams (omr_worker_scan_pack_f32; the multi-rank round's form),
  * in two steps: its (block, contributor) pair list, which depends only on the all-gathered masks and position tables

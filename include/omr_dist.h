@@ -35,6 +35,10 @@ extern "C" {
 #define OMR_EABORTED (-2)
 /* A host-side wait of the transport or of a round passed the transport's deadline (omr_dist_set_timeout). */
 #define OMR_ETIMEDOUT (-3)
+/* The round check failed (round 6): a worker's all-gathered row masks were not the ones its scan of that round wrote
+ * (read before the scan wrote or finished them, or from another buffer); the round is failed and the transport aborted
+ * before any exchange is sized from them (omr_round_plan_check in omr.h). */
+#define OMR_ESTALE (-4)
 
 typedef struct omr_dist omr_dist;               /* a transport endpoint (one rank) */
 typedef struct omr_local_board omr_local_board; /* shared state of an in-process group */

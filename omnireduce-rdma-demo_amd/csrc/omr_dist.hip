@@ -437,6 +437,7 @@ struct IpcRank {
   std::atomic<uint32_t> aborted;  // this rank aborted its transport (its peers' waits end with an error)
   std::atomic<uint64_t> evgen[kIpcChans][2];  // 1 + the generation whose handles slot [c][g % 2] holds (0: none)
   std::atomic<uint64_t> gpu;                  // 1 + the rank's GPU (PCI domain, bus, device), set before `joined`
+  hipIpcMemHandle_t canary;                   // the rank's canary allocation (IpcDist::check_canaries), before `joined`
   hipIpcEventHandle_t ready[kIpcChans][2][kIpcRing], rdone[kIpcChans][2][kIpcRing];
 };
 struct IpcBoard {
@@ -514,11 +515,38 @@ __global__ void k_ipc_stamp(uint64_t* dst) {
   if (threadIdx.x == 0) __hip_atomic_store(dst, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// (OMR_IPC_TRACE) popcount of `words` 64-bit words: the all-gather's checksum, by its sender before its ready record
+// and by each receiver after its copy
+__global__ void k_ipc_popcount(const uint64_t* p, uint64_t words, uint64_t* dst) {
+  __shared__ uint64_t part[256];
+  uint64_t c = 0;
+  for (uint64_t i = threadIdx.x; i < words; i += blockDim.x) c += static_cast<uint64_t>(__popcll(p[i]));
+  part[threadIdx.x] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int i = 0; i < 256; ++i) t += part[i];
+    __hip_atomic_store(dst, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+std::string hex64(const uint64_t* w) {  // an IPC handle's 64 bytes
+  std::string o;
+  char b[20];
+  for (int i = 0; i < 8; ++i) {
+    snprintf(b, sizeof(b), "%016llx", static_cast<unsigned long long>(w[i]));
+    o += b;
+  }
+  return o;
+}
+
 struct IpcTrace {
   struct Rec {
     uint32_t chan;
     uint64_t seq;
-    int32_t peer;   // -1: this rank's own ready record; else the peer whose ready this rank waited for
+    int32_t peer;   // -1 / -2: this rank's own ready / done record; p: after its wait for peer p's ready, 100 + p: for
+                    // peer p's done; -3 / 200 + p: all-gather checksums (popcounts), of what this rank offers / of
+                    // what it copied from peer p
     int32_t query;  // hipEventQuery of the peer's event right before the wait (hipSuccess 0, hipErrorNotReady 600)
     int64_t host_ns;
     uint32_t slot;  // its device stamp
@@ -528,7 +556,16 @@ struct IpcTrace {
   uint64_t* dev = nullptr;
   uint32_t cap = 0, used = 0;
   std::vector<Rec> recs;
+  std::vector<std::string> notes;  // exported / mapped allocations
   bool on() const { return host != nullptr; }
+  void note(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    notes.emplace_back(buf);
+  }
   int open(const char* prefix, int rank) {
     path = std::string(prefix) + "." + std::to_string(rank) + ".txt";
     cap = 1u << 16;
@@ -537,10 +574,13 @@ struct IpcTrace {
     memset(host, 0, cap * sizeof(uint64_t));
     return hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), host, 0), "hipHostGetDevicePointer");
   }
-  void stamp(hipStream_t st, uint32_t chan, uint64_t seq, int peer, int query) {
+  // words != 0: the record's value is the popcount of `words` words at `data` instead of a clock
+  void stamp(hipStream_t st, uint32_t chan, uint64_t seq, int peer, int query, const void* data = nullptr,
+             uint64_t words = 0) {
     if (used == cap) return;
     const uint32_t slot = used++;
-    k_ipc_stamp<<<1, 64, 0, st>>>(dev + slot);
+    if (words) k_ipc_popcount<<<1, 256, 0, st>>>(static_cast<const uint64_t*>(data), words, dev + slot);
+    else k_ipc_stamp<<<1, 64, 0, st>>>(dev + slot);
     recs.push_back(Rec{chan, seq, peer, query,
                        std::chrono::duration_cast<std::chrono::nanoseconds>(
                            std::chrono::steady_clock::now().time_since_epoch()).count(), slot});
@@ -550,6 +590,7 @@ struct IpcTrace {
     if (!on()) return;
     if (!dead) (void)hipDeviceSynchronize();
     if (FILE* f = fopen(path.c_str(), "w")) {
+      for (const std::string& n : notes) fprintf(f, "# %s\n", n.c_str());
       fprintf(f, "# chan seq peer query host_ns device_clock\n");
       for (const Rec& r : recs)
         fprintf(f, "%u %llu %d %d %lld %llu\n", r.chan, static_cast<unsigned long long>(r.seq), r.peer, r.query,
@@ -603,6 +644,7 @@ struct IpcDist final : omr_dist {
   }
   uint64_t seq[kIpcChans] = {0, 0};
   IpcTrace trace;  // OMR_IPC_TRACE (diagnostic)
+  void* canary = nullptr;  // exported at attach, freed once every peer has left
   // allocation (base, size) -> its handle and this rank's id for it.  The plans' exported allocations are never freed
   // while the transport lives (release() parks them), so an entry never outlives its allocation.  A
   // caller's buffer (an input or output tensor) must stay allocated while the transport lives, as omr_dist.h says.
@@ -695,6 +737,7 @@ struct IpcDist final : omr_dist {
     }
     // every peer has left (closed its mappings of them): the parked allocations can go now
     for (auto& kv : parked) (void)hipFree(kv.second);
+    if (canary) (void)hipFree(canary);
     for (auto& v : peer)
       for (IpcEvents& e : v) release(e, retired);
     for (auto& row : mine)
@@ -748,6 +791,7 @@ struct IpcDist final : omr_dist {
       return derr(OMR_EINVAL, "ipc transport: board world %u, this rank says %d", b->world, world);
     b->attached.fetch_add(1);
     IpcRank& me = b->rank[rank];
+    TRY(make_canary(me));
     {
       int dev = 0, dom = 0, bus = 0, slot = 0;
       TRY(hip_check(hipGetDevice(&dev), "hipGetDevice"));
@@ -774,7 +818,65 @@ struct IpcDist final : omr_dist {
     share_gpu = 0;
     for (int p = 0; p < world; ++p)
       share_gpu += b->rank[p].gpu.load(std::memory_order_relaxed) == me.gpu.load(std::memory_order_relaxed) ? 1 : 0;
+    if (int rc = check_canaries()) {  // (the peers' checks fail too: none waits on this rank)
+      abort_group();
+      return rc;
+    }
     for (int c = 0; c < kIpcChans; ++c) TRY(open_gen(c, 0));
+    return 0;
+  }
+
+  // The IPC memory handles must open at the exporter's address in every process.  They do not between a process that
+  // loads the AddressSanitizer runtime and one that does not (round 6): ROCm's runtime then gives
+  // every device allocation a 4 KiB leading redzone, and each process opens a handle with ITS OWN convention, so a
+  // plain importer of a sanitized exporter's buffer lands 4 KiB before the data and a sanitized importer of a plain
+  // one 4 KiB after it (OMR_IPC_TRACE: the exporter's handle names its allocation 0x1000 below the pointer; the
+  // importers' pointers differ by 0x1000; profiles/r06/ipc_mix/).  The all-gather then copied the wrong 8 KiB and
+  // the ranks' block counts disagreed.  So at attach each rank exports a canary (word i = rank << 32 | i) and opens
+  // every peer's: a peer whose canary does not read back from offset 0 fails the group at creation, with the offset.
+  // Only the canary's first kCanaryRead bytes are read back, so a handle that opens up to 48 KiB off either way still
+  // reads inside the 64 KiB allocation (a device read outside a mapping faults the GPU).
+  static constexpr size_t kCanaryWords = 8192;  // 64 KiB
+  static constexpr size_t kCanaryRead = 2048;   // words read back: 16 KiB
+  int make_canary(IpcRank& me) {
+    TRY(hip_check(hipMalloc(&canary, kCanaryWords * 8), "hipMalloc canary"));
+    std::vector<uint64_t> h(kCanaryWords);
+    for (size_t i = 0; i < kCanaryWords; ++i) h[i] = (static_cast<uint64_t>(rank) << 32) | i;
+    TRY(hip_check(hipMemcpy(canary, h.data(), kCanaryWords * 8, hipMemcpyHostToDevice), "hipMemcpy canary"));
+    return hip_check(hipIpcGetMemHandle(&me.canary, canary), "hipIpcGetMemHandle canary");
+  }
+  int check_canaries() {
+    std::vector<uint64_t> h(kCanaryRead);
+    for (int p = 0; p < world; ++p) {
+      if (p == rank) continue;
+      void* mp = nullptr;
+      TRY(hip_check(hipIpcOpenMemHandle(&mp, b->rank[p].canary, hipIpcMemLazyEnablePeerAccess),
+                    "hipIpcOpenMemHandle canary"));
+      const hipError_t e = hipMemcpy(h.data(), mp, kCanaryRead * 8, hipMemcpyDeviceToHost);
+      (void)hipIpcCloseMemHandle(mp);
+      TRY(hip_check(e, "hipMemcpy canary"));
+      const uint64_t tag = static_cast<uint64_t>(p) << 32;
+      if (h[0] == tag) continue;  // word 0 at offset 0: the handle opens at the exporter's address
+      long long off = 0;
+      bool found = false;
+      if ((h[0] >> 32) == static_cast<uint64_t>(p) && (h[0] & 0xFFFFFFFFu) < kCanaryWords) {
+        off = static_cast<long long>(h[0] & 0xFFFFFFFFu) * 8;  // opened past the start: this much after it
+        found = true;
+      } else {
+        for (size_t i = 1; i < kCanaryRead && !found; ++i)
+          if (h[i] == tag) {
+            off = -static_cast<long long>(i * 8);  // opened before the start
+            found = true;
+          }
+      }
+      if (found)
+        return derr(OMR_EINVAL, "ipc transport: rank %d's IPC memory handles open %+lld bytes off its buffers in rank "
+                    "%d: the two processes' HIP runtimes lay out device allocations differently (a process that loads "
+                    "the AddressSanitizer runtime gets a 4 KiB leading redzone per allocation); they cannot share device "
+                    "buffers", p, off, rank);
+      return derr(OMR_EINVAL, "ipc transport: rank %d's canary buffer reads back wrong in rank %d (word 0 = %016llx)", p,
+                  rank, static_cast<unsigned long long>(h[0]));
+    }
     return 0;
   }
 
@@ -845,6 +947,11 @@ struct IpcDist final : omr_dist {
                     hipGetErrorString(e), ptr, reinterpret_cast<void*>(base), size);
       oh.id = next_id++;
       it = own.emplace(key, oh).first;
+      if (trace.on()) {
+        const uint64_t* hw = reinterpret_cast<const uint64_t*>(&oh.h);
+        trace.note("export id %llu: ptr %p base %p size %zu handle %s",
+                   static_cast<unsigned long long>(oh.id), ptr, reinterpret_cast<void*>(base), size, hex64(hw).c_str());
+      }
     }
     *h = it->second.h;
     *id = it->second.id;
@@ -905,6 +1012,15 @@ struct IpcDist final : omr_dist {
       void* mp = nullptr;
       TRY(hip_check(hipIpcOpenMemHandle(&mp, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle"));
       it = opened.emplace(key, Mapping{id, static_cast<char*>(mp)}).first;
+      if (trace.on()) {
+        hipDeviceptr_t mb = nullptr;
+        size_t ms = 0;
+        const hipError_t e = hipMemGetAddressRange(&mb, &ms, mp);
+        const uint64_t* hw = reinterpret_cast<const uint64_t*>(&h);
+        trace.note("map peer %d id %llu: at %p (range %p size %zu, %s) handle %s", p,
+                   static_cast<unsigned long long>(id), mp, reinterpret_cast<void*>(mb), ms, hipGetErrorString(e),
+                   hex64(hw).c_str());
+      }
     }
     *out = it->second.base + e.off;
     return 0;
@@ -955,12 +1071,16 @@ struct IpcDist final : omr_dist {
   // this rank is through reading its peers; st then waits until every peer is through reading this rank
   int end(int c, uint64_t s, hipStream_t st) {
     const int k = static_cast<int>(s % kIpcRing);
+    if (trace.on()) trace.stamp(st, static_cast<uint32_t>(c), s, -2, 0);
     TRY(hip_check(hipEventRecord(mine_of(c, s).rdone[k], st), "hipEventRecord"));
     b->rank[rank].done[c].store(s, std::memory_order_release);
     for (int p = 0; p < world; ++p) {
       if (p == rank) continue;
       TRY(spin([&] { return b->rank[p].done[c].load(std::memory_order_acquire) >= s; }, "a peer's copies"));
-      TRY(hip_check(hipStreamWaitEvent(st, peer_of(c, s, p).rdone[k], 0), "hipStreamWaitEvent"));
+      const hipEvent_t ev = peer_of(c, s, p).rdone[k];
+      const int q = trace.on() ? static_cast<int>(hipEventQuery(ev)) : 0;
+      TRY(hip_check(hipStreamWaitEvent(st, ev, 0), "hipStreamWaitEvent"));
+      if (trace.on()) trace.stamp(st, static_cast<uint32_t>(c), s, 100 + p, q);
     }
     return 0;
   }
@@ -968,6 +1088,8 @@ struct IpcDist final : omr_dist {
 
   int do_allgather(const void* in, void* out, size_t bytes, hipStream_t st) override {
     uint64_t s = 0;
+    // (trace: the sender's checksum of what it offers, peer -3, before its ready record)
+    if (trace.on()) trace.stamp(st, 0, seq[0] + 1, -3, 0, in, bytes / 8);
     TRY(begin(0, st, {{kIpcAll, Slice{const_cast<void*>(in), bytes}}}, &s));
     int rc = 0;
     for (int p = 0; p < world && rc == 0; ++p) {
@@ -986,6 +1108,7 @@ struct IpcDist final : omr_dist {
       rc = map(p, P, P.e[0], &src);
       if (rc == 0) rc = wait_ready(0, s, p, st);
       if (rc == 0) rc = hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+      if (rc == 0 && trace.on()) trace.stamp(st, 0, s, 200 + p, 0, dst, bytes / 8);  // checksum of the copy
     }
     // (on an error this rank aborts instead of ending the operation: the peers' waits for it end at once)
     TRY(rc);
@@ -1181,7 +1304,12 @@ struct omr_ar_plan {
                                     // the default since round 4)
   uint64_t list_units = 0;
   uint32_t list_cap = 0;
-  uint64_t mstride = 0;           // uint64 words per rank in masks_all (rows without the fused pack)
+  uint64_t mstride = 0;           // uint64 words per rank in masks_all: masks [, position table], check slots
+  // The round check (round 6): each worker's scan leaves one slot per workgroup, (seq << 32) | its non-zero blocks, after
+  // its masks (and position table) in the array the round all-gathers; the plan launch checks every worker's
+  // (omr_round_plan_check) and stores a status word after the counts, which the host reads with them.
+  uint64_t chk_off = 0;           // the slots' word offset in a rank's array
+  uint32_t chk_slots = 0;
   // per-round state, kSets sets used in turn: an asynchronous round's bookkeeping and exchange still read their
   // set while the next rounds' scans fill the others.  Four: one more round between a set's plan and the scan that
   // refills it (with three the world-1 round took 58.1-64.1 us, with four 56.9-57.3; profiles/r04/round_sets/).
@@ -1331,6 +1459,7 @@ struct omr_ar_plan {
   int failed = 0;
   std::string failed_why;
   hipEvent_t wait_done = nullptr;  // omr_ar_plan_wait's event
+  hipEvent_t host_done = nullptr;  // omr_sparse_buckets_f32 on a mapped host buffer: its results stored (system scope)
   // omr_ar_plan_host_stats: the calling thread's time blocked on the GPU or on the progress thread inside rounds (the
   // count wait, the set-reuse waits, the drain), so a caller can tell issue time from waiting
   std::atomic<uint64_t> host_wait_ns{0};
@@ -1393,6 +1522,28 @@ int plan_check(omr_ar_plan* p, const char* what) {
   std::lock_guard<std::mutex> g(p->mu);
   if (p->failed == 0) return 0;
   return derr(OMR_EABORTED, "%s: the plan failed in an earlier round (%s)", what, p->failed_why.c_str());
+}
+
+// Words of one set's counts in pinned memory: (seq << 32) | count per (array, shard bound), then the round check's status.
+size_t count_words(const omr_ar_plan* p) { return static_cast<size_t>(p->M + 1) * (p->A + 1) + 1; }
+
+// The round's block counts (wait_counts) and its round check's status (omr_round_plan_check): a failed check fails the
+// round with OMR_ESTALE, naming the worker, before any exchange is sized from the counts.
+int wait_round_counts(omr_ar_plan* p, const uint64_t* tagged, uint32_t seq, hipStream_t st, uint32_t* counts) {
+  const uint32_t n = static_cast<uint32_t>(count_words(p));
+  uint32_t all[(OMR_MAX_WORKERS + 1) * (OMR_MAX_WORKERS + 2) + 1];
+  TRY(wait_counts(p->d, tagged, n, seq, st, all));
+  memcpy(counts, all, (n - 1) * sizeof(uint32_t));
+  const uint32_t status = all[n - 1];
+  if (status == 0) return 0;
+  const unsigned w = status & 0xFFu;
+  if (status & 0x100u)
+    return p->d->contain(derr(OMR_ESTALE, "round check (seq %u): worker %u's all-gathered masks carry another round's "
+                                          "scan slot: the all-gather read its array before its scan of this round "
+                                          "wrote it, or read another buffer (DESIGN.md §5)", seq, w));
+  return p->d->contain(derr(OMR_ESTALE, "round check (seq %u): worker %u's all-gathered masks do not hold the blocks its "
+                                        "scan of this round counted: the all-gather read them before the scan finished "
+                                        "(DESIGN.md §5)", seq, w));
 }
 
 // ---------------------------------------------------------------- side streams on hardware queues of their own
@@ -1593,7 +1744,9 @@ int omr_dist_create_ipc(const void* id, int rank, int world, omr_dist** out) {
   d->rank = rank;
   d->world = world;
   if (int rc = d->attach(id)) {
+    const std::string why = g_derr;  // (the teardown's own waits may overwrite the message)
     delete d;
+    snprintf(g_derr, sizeof(g_derr), "%s", why.c_str());
     return rc;
   }
   *out = d;
@@ -1731,6 +1884,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
   if (p->s_out) (void)hipStreamDestroy(p->s_out);
   if (p->st_ev) (void)hipEventDestroy(p->st_ev);
   if (p->wait_done) (void)hipEventDestroy(p->wait_done);
+  if (p->host_done) (void)hipEventDestroy(p->host_done);
   for (auto& t : p->timed)
     for (hipEvent_t e : {t.s0, t.s1, t.x0, t.x1, t.q0, t.q1, t.a1})
       if (e) (void)hipEventDestroy(e);
@@ -1797,6 +1951,9 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
       p->sum_list = p->list_units > 0;
     }
   }
+  p->chk_off = p->mstride;
+  p->chk_slots = omr_round_check_slots(n, block_size, num_lanes, num_parts);
+  p->mstride += p->chk_slots;
   int rc = 0;
   auto A = [&](int r) {
     if (rc == 0) rc = r;
@@ -1851,7 +2008,7 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   p->tally_slots = omr_tally_slots(n, block_size, num_lanes, num_parts);
   A(dev_alloc(p->d, &p->tally, static_cast<size_t>(p->tally_slots) * omr_ar_plan::kSets, DB));
   constexpr int NSETS = omr_ar_plan::kSets;
-  const size_t ncounts = static_cast<size_t>(NSETS) * (M + 1) * (NA + 1);
+  const size_t ncounts = static_cast<size_t>(NSETS) * count_words(p);
   A(hip_check(hipHostMalloc(reinterpret_cast<void**>(&p->counts_host), ncounts * sizeof(uint64_t),
                             hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   if (rc == 0) {
@@ -2048,7 +2205,7 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
     return 0;
   }
   const uint32_t NS = static_cast<uint32_t>(NA + 1);  // count columns per array (shard bounds)
-  const uint64_t* const tagged = p->counts_host + static_cast<size_t>(si) * (M + 1) * NS;
+  const uint64_t* const tagged = p->counts_host + static_cast<size_t>(si) * count_words(p);
   uint32_t counts[(OMR_MAX_WORKERS + 1) * (OMR_MAX_WORKERS + 2)];
   // at N > 1 the exchange stream waits for this round's plan on the plan stream (a deferred round's `ready` has
   // normally fired long before: then no wait is queued)
@@ -2086,7 +2243,7 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
     if (async) TRY(finish_async(false));
     if (sent_blocks != nullptr || union_blocks != nullptr) {
       HostWait hw(p);
-      TRY(wait_counts(p->d, tagged, (M + 1) * NS, seq, st, counts));
+      TRY(wait_round_counts(p, tagged, seq, st, counts));
     }
     if (sent_blocks) *sent_blocks = (r1 - r0) * p->lanes * static_cast<uint64_t>(N - 1);
     if (union_blocks) *union_blocks = per(M, me);
@@ -2094,7 +2251,7 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
   }
   {
     HostWait hw(p);
-    TRY(wait_counts(p->d, tagged, (M + 1) * NS, seq, st, counts));
+    TRY(wait_round_counts(p, tagged, seq, st, counts));
   }
   ht_of(p).lap("2:wait counts");
   const bool wk = p->worker();
@@ -2157,9 +2314,10 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
                                            S.wset, wprefix, dense_out ? 0 : 1, sums, xstream),
                     "omr_shard_sum_list_f32"));
     } else {  // row-ordered streams (the pack pass of ragged shards)
-      TRY(omr_check(omr_shard_sum_f32(own, own_idx, p->recv, roff.data(), S.masks_all, static_cast<uint32_t>(M),
-                                      S.prefix, S.wset, rows, r0, r1, p->lanes, p->B, dense_out ? 0 : 1, sums, xstream),
-                    "omr_shard_sum_f32"));
+      TRY(omr_check(omr_shard_sum_stride_f32(own, own_idx, p->recv, roff.data(), S.masks_all, p->mstride,
+                                             static_cast<uint32_t>(M), S.prefix, S.wset, rows, r0, r1, p->lanes, p->B,
+                                             dense_out ? 0 : 1, sums, xstream),
+                    "omr_shard_sum_stride_f32"));
     }
     if (!p->colocated) p->last_sums_blocks = per(M, sh);
   }
@@ -2304,14 +2462,15 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
     //    straight into pinned host memory: no copy-engine hop before the host sees them)
     //    ... and, by extra workgroups of the same launch, the aggregator chain (server.cc:86-96 min_next) over the
     //    union, when asked for, and the shard sum's pair list (sum_list)
-    seq = next_seq(p);
+    seq = j.seq;  // (taken when its scan was issued: the scan's check slots carry it)
     const omr_sum_list sl = p->sum_list ? list_desc(p, S) : omr_sum_list{};
-    TRY(omr_check(omr_round_plan_list(S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes,
-                                      p->bounds_dev, NS, S.wset, nullptr, S.prefix,
-                                      p->counts_map + static_cast<size_t>(si) * (M + 1) * NS, S.own, S.pack_cnt,
-                                      S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, S.plan_ws, seq, j.un, p->B,
-                                      p->sum_list ? &sl : nullptr, qstream),
-                  "omr_round_plan_list"));
+    uint64_t* const cw = p->counts_map + static_cast<size_t>(si) * count_words(p);
+    TRY(omr_check(omr_round_plan_check(S.masks_all, static_cast<uint32_t>(M), p->mstride, rows, p->rpp, p->lanes,
+                                       p->bounds_dev, NS, S.wset, nullptr, S.prefix, cw, S.own, S.pack_cnt,
+                                       S.pack_cnt ? static_cast<uint32_t>(p->A) : 0u, S.plan_ws, seq, j.un, p->B,
+                                       p->sum_list ? &sl : nullptr, p->chk_off, p->chk_slots,
+                                       cw + static_cast<size_t>(M + 1) * NS, qstream),
+                  "omr_round_plan_check"));
     ht.lap("1:plan");
     // 4a. pack own non-zero blocks of the other shards (block order == shard order, common.cc:405-407) where the scan
     //     could not (ragged shards): addressed by device-side data only, so it is queued before the host learns the
@@ -2530,6 +2689,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
     }
     p->ht.lap("1:scan");
   } else {
+    solo_seq = next_seq(p);  // (the round's number, carried by its scan's check slots)
     if (threaded) {  // that plan has been issued (and this set's `scanned` waited for) by the progress thread
       HostWait hw(p);
       std::unique_lock<std::mutex> lk(p->mu);
@@ -2566,16 +2726,18 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
       // (a one-rank round's scan writes the sums; a bucket's writes the staging buffer's blocks when it reads the
       // pinned host buffer, and the sums come from the round's own shard sum)
       float* sout = p->scan_from ? const_cast<float*>(x) : (solo ? out : nullptr);
+      uint64_t* const chk = S.own + p->chk_off;  // (the round check's slots, after the masks [and position table])
       if (pack_scan)  // the scan also writes this worker's blocks of the other shards into their send streams
-        TRY(omr_check(omr_worker_scan_pack_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout,
-                                               p->bounds.data(), static_cast<uint32_t>(p->A),
-                                               p->colocated ? me_shard(p) : -1, p->pk[pki].buf, S.pack_cnt,
-                                               reinterpret_cast<uint32_t*>(S.own + p->rows), p->scan_ws,
-                                               p->scan_ws_bytes, stream),
-                      "omr_worker_scan_pack_f32"));
+        TRY(omr_check(omr_worker_scan_pack_check_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout,
+                                                     p->bounds.data(), static_cast<uint32_t>(p->A),
+                                                     p->colocated ? me_shard(p) : -1, p->pk[pki].buf, S.pack_cnt,
+                                                     reinterpret_cast<uint32_t*>(S.own + p->rows), p->scan_ws,
+                                                     p->scan_ws_bytes, chk, solo_seq, stream),
+                      "omr_worker_scan_pack_check_f32"));
       else
-        TRY(omr_check(omr_worker_scan_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout, p->scan_ws,
-                                          p->scan_ws_bytes, stream), "omr_worker_scan_f32"));
+        TRY(omr_check(omr_worker_scan_check_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout, p->scan_ws,
+                                                p->scan_ws_bytes, chk, solo_seq, stream),
+                      "omr_worker_scan_check_f32"));
       if (timed) {
         TRY(hip_check(hipEventRecord(p->timed[tslot].s1, st), "hipEventRecord"));
         p->timed[tslot].scan = true;
@@ -2705,13 +2867,22 @@ int sparse_buckets_issue(omr_ar_plan* p, float* buf, uint64_t total_n, int mode,
     sent += s1;
     uni += u1;
   };
-  // A one-rank group over a pinned buffer with a device mapping needs no staging: its round is one launch (the worker
-  // scan writes the sums), which reads each bucket straight from host memory and stores the write set back into it,
-  // both directions of the link at once, as omr_host_scan_sum_zero_copy_f32 does.
+  // A pinned buffer with a device mapping needs no staging (the reference's registered res->buf is read and written in
+  // place too: common.cc:873-914, client.cc:89).  Each bucket's round runs on the mapped bucket itself: the worker scan
+  // reads it over PCIe and (N > 1) packs the other shards' non-zero blocks into the device send buffers, the shard sum
+  // reads this rank's own blocks in place and stores the shard's write set back into it, and an all-reduce's returned
+  // sums are scattered straight into it -- both link directions at once, as omr_host_scan_sum_zero_copy_f32 does.  A
+  // one-rank group's round is one launch that does all of it: at N = 1 this is the default (config 5's shape: 52.5 GB/s
+  // against 46.7 staged, round 5).  At N > 1 the rounds' PCIe traffic is split over kernels on two streams (the scan's
+  // reads, the shard sum's reads of the rank's own blocks, the unpack's write-back), and as 2 IPC ranks on one GPU it
+  // ran at half the staged rate (21.6 against 45.0 GB/s; profiles/r06/c5_ipc/), so there it is
+  // opt-in (OMR_BUCKETS_DIRECT=1) and the staging ring stays the default.  OMR_BUCKETS_STAGED=1 (or either staging
+  // mode below) stages a one-rank group too.
   float* const hmap = host ? host_mapping(buf, attr) : nullptr;
-  const bool direct = host && hmap != nullptr && p->N == 1 && p->worker() && p->colocated &&
+  const bool direct = host && hmap != nullptr && p->worker() &&
+                      (p->N == 1 ? getenv("OMR_BUCKETS_STAGED") == nullptr : getenv("OMR_BUCKETS_DIRECT") != nullptr) &&
                       getenv("OMR_BUCKETS_STAGED_D2H") == nullptr && getenv("OMR_BUCKETS_SCAN_HOST") == nullptr;
-  if (!host || direct) {  // device-resident (or mapped, one rank): one deferred round per bucket, in place
+  if (!host || direct) {  // device-resident (or mapped): one deferred round per bucket, in place
     float* const base = host ? hmap : buf;
     for (uint64_t k = 0; k < K; ++k) {
       float* b = base + k * p->n;
@@ -2723,8 +2894,15 @@ int sparse_buckets_issue(omr_ar_plan* p, float* buf, uint64_t total_n, int mode,
       acc();
     }
     TRY(omr_ar_plan_join(p, stream));
-    // (host memory: the call returns once the buffer holds the result, as below)
-    if (host) TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
+    // (host memory: the call returns once the buffer holds the result, as below: an event with the system-scope release
+    // after the last round's last work, whichever stream it is on, then the caller's stream)
+    if (host) {
+      if (p->host_done == nullptr)
+        TRY(hip_check(hipEventCreateWithFlags(&p->host_done, hipEventDisableTiming), "hipEventCreate"));
+      TRY(hip_check(hipEventRecord(p->host_done, p->tail != nullptr ? p->tail : st), "hipEventRecord"));
+      TRY(hip_check(hipEventSynchronize(p->host_done), "hipEventSynchronize"));
+      TRY(hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"));
+    }
     if (sent_blocks) *sent_blocks = sent;
     if (union_blocks) *union_blocks = uni;
     return 0;

@@ -261,6 +261,10 @@ struct FusedArgs {
   const uint64_t* pub_src;
   uint32_t* pub_dst;
   uint32_t pub_seq, pub_slots;
+  // CHK (the multi-rank round's worker scan, round 6): workgroup b stores chk[b] = (chk_seq << 32) | its non-zero
+  // blocks, the count its row-mask bits must add up to; the plan launch checks every worker's (omr_round_plan_check)
+  uint64_t* chk;
+  uint32_t chk_seq;
 };
 
 // The one-rank round's counts, from an earlier launch's slots, one wave: lane i sums slots i, i + 64, ... (loaded by
@@ -299,7 +303,7 @@ constexpr uint32_t kDropStore = 0x40000000u;  // voffset past every descriptor r
 // TALLY: at most 96 VGPRs (five waves per SIMD), as the headline form has (92); its tally registers had taken the
 // one-rank round's launch to 106 (four waves per SIMD).  Capped: 48.03 / 49.80 us in / out of place against 48.65 /
 // 50.14, the headline 47.73 / 49.43 (profiles/r05/timing/vgpr96/tally.log, profiles/r05/plan_v5/tally.log).
-template <int VEC, int WAVES, int LOADS = 16, int SKIP = 0, bool PACK = false, bool TALLY = false>
+template <int VEC, int WAVES, int LOADS = 16, int SKIP = 0, bool PACK = false, bool TALLY = false, bool CHK = false>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(TALLY ? 5 : 1, 8))) void k_scan1f(
     FusedArgs a) {
   constexpr int RB = LOADS / VEC;  // rows per batch (<= 32)
@@ -313,6 +317,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(TALL
   extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
   __shared__ uint32_t s_wcnt[(PACK || TALLY) ? WAVES : 1], s_wpre[PACK ? WAVES : 1];
   __shared__ uint32_t s_base, s_total;
+  __shared__ uint32_t s_wnz[CHK ? WAVES : 1];
+  [[maybe_unused]] uint32_t nzc = 0;  // CHK: the wave's non-zero blocks (wave-uniform)
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t T = gridDim.x, bid = blockIdx.x;
@@ -431,6 +437,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(TALL
       cnt_w += static_cast<uint32_t>(__builtin_popcount(bits));
       if (r0 + rr == 0 && !(bits & 1u)) head0 = 1;
     }
+    if constexpr (CHK) nzc += static_cast<uint32_t>(__builtin_popcount(bits));
     if (bits != 0) {
       if (wlast == kNone) wlast = rr + 31 - static_cast<uint32_t>(__builtin_clz(bits));
       carry = rr + static_cast<uint32_t>(__builtin_ctz(bits));
@@ -440,8 +447,17 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(TALL
     s_wfirst[wave] = carry;  // first non-zero row of the wave's range (kNone: all zero)
     s_wlast[wave] = wlast;   // last one
     if constexpr (TALLY) s_wcnt[wave] = cnt_w | (head0 << 31);
+    if constexpr (CHK) s_wnz[wave] = nzc;
   }
   __syncthreads();
+  if constexpr (CHK) {  // the round check's slot: one plain store per workgroup (its order against the mask atomics does
+                        // not matter: a reader that sees this slot before some of the bits sees too few bits)
+    if (threadIdx.x == 0 && a.chk != nullptr) {
+      uint32_t t = 0;
+      for (uint32_t w2 = 0; w2 < WAVES; ++w2) t += s_wnz[w2];
+      a.chk[bid] = (static_cast<uint64_t>(a.chk_seq) << 32) | t;
+    }
+  }
   if constexpr (TALLY) {  // the one-rank round's bookkeeping: one slot store per workgroup, no atomic
     if (threadIdx.x == 0) {
       uint32_t nz = 0, heads = 0;
@@ -1216,6 +1232,11 @@ struct PlanArgs {
   uint32_t chain_wgs;   //   null: none)
   uint32_t list_wgs;    // the shard sum's pair list, by the workgroups after the chain's (0: none)
   ListArgs list;
+  // the round check (omr_round_plan_check), by one workgroup after the list's: worker c's scan slots (k_scan1f CHK) at
+  // masks + c * mstride + chk_off; chk_status null: no check
+  uint64_t chk_off;
+  uint32_t chk_slots;
+  uint64_t* chk_status;
 };
 
 // Inclusive prefix sum over the 64 lanes of a wave in six DPP steps (no LDS): row_shr 1, 2, 4, 8 inside each 16-lane
@@ -1396,8 +1417,67 @@ __device__ __forceinline__ void plan_chunk(const PlanArgs& a) {
   }
 }
 
+// The round check (round 6): is every worker's all-gathered mask array the one its scan of THIS round
+// wrote?  Each of the worker's scan workgroups left a slot (seq << 32) | its non-zero blocks in the array; the check
+// reads them all and the chunks' popcount totals of the worker's masks (plan_chunk step 3, tagged with seq).  A slot of
+// another round means the copy read the worker's buffer before its scan wrote the slot (or read another buffer); a
+// count sum above the masks' popcount means the copy read masks its scan had not finished (a mask array only gains
+// bits between the plan that zeroes it and the scan that refills it, so a copy that overtakes its producer always
+// reads too few).  Status (one system-scope store beside the counts): (seq << 32) | 0, or | 0x100 + worker for a
+// stale slot, | 0x200 + worker for a count mismatch.  The round's host fails the round on it, by name, instead of
+// relying on the exchange's size check.
+constexpr uint32_t kCheckStale = 0x100u, kCheckCount = 0x200u;
+
+template <int W>
+__device__ __forceinline__ void plan_check(const PlanArgs& a) {
+  __shared__ uint32_t s_sum[OMR_MAX_WORKERS];
+  __shared__ uint32_t s_stale, s_bad;  // 1 + a worker (0: none)
+  const uint32_t t = threadIdx.x;
+  if (t < OMR_MAX_WORKERS) s_sum[t] = 0;
+  if (t == 0) s_stale = s_bad = 0;
+  __syncthreads();
+  const uint32_t ns = a.chk_slots, words = a.count * ns;
+  constexpr uint32_t U = 8;  // loads in flight per thread
+  for (uint32_t base = 0; base < words; base += kPlanThreads * U) {
+    uint64_t v[U];
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) {
+      const uint32_t idx = base + i * kPlanThreads + t;
+      const uint32_t c = idx / ns;
+      v[i] = idx < words ? a.masks[static_cast<uint64_t>(c) * a.mstride + a.chk_off + (idx - c * ns)] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < U; ++i) {
+      const uint32_t idx = base + i * kPlanThreads + t;
+      if (idx >= words) continue;
+      const uint32_t c = idx / ns;
+      if (static_cast<uint32_t>(v[i] >> 32) != a.seq) (void)atomicCAS(&s_stale, 0u, c + 1);
+      (void)atomicAdd(&s_sum[c], static_cast<uint32_t>(v[i]));
+    }
+  }
+  __syncthreads();
+  if (t < a.count) {  // the worker's mask total: the chunks' tagged totals of its array
+    uint32_t tot = 0;
+    for (uint32_t i = 0; i < a.nchunks; ++i) {
+      uint64_t v;
+      while (((v = __hip_atomic_load(&a.ws[1 + static_cast<uint64_t>(i) * kPlanArrays + t], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT)) >> 32) != a.seq)
+        __builtin_amdgcn_s_sleep(1);
+      tot += static_cast<uint32_t>(v);
+    }
+    if (tot != s_sum[t]) (void)atomicCAS(&s_bad, 0u, t + 1);
+  }
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t code = s_stale ? (kCheckStale | (s_stale - 1)) : (s_bad ? (kCheckCount | (s_bad - 1)) : 0u);
+    __hip_atomic_store(a.chk_status, (static_cast<uint64_t>(a.seq) << 32) | code, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // One launch: the chunks (plan_chunk), then the aggregator chain (server.cc:86-96 min_next over the union, one k_next
-// segment each), then the shard sum's pair list (one unit per wave).  W >= count (2, 4, 8, 16).
+// segment each), then the shard sum's pair list (one unit per wave), then the round check (one workgroup, if asked).
+// W >= count (2, 4, 8, 16).
 template <int W>
 __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
   if (blockIdx.x < a.nchunks) {
@@ -1405,6 +1485,10 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
     return;
   }
   const uint32_t b = blockIdx.x - a.nchunks;
+  if (a.chk_status != nullptr && b == a.chain_wgs + a.list_wgs) {
+    plan_check<W>(a);
+    return;
+  }
   if (b >= a.chain_wgs) {  // the shard sum's pair list, one unit per wave
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t li = xcd_spread(b - a.chain_wgs, a.nchunks + a.chain_wgs, a.list_wgs);
@@ -1944,7 +2028,7 @@ template <int VEC, int SKIP, int WAVES = kPackWaves>
 int launch_fused_pack(const FusedArgs& a, const Layout& L, const FusedShape& f, unsigned grid, hipStream_t st) {
   const uint32_t bits_words = ((f.S + 31) / 32 + 3) & ~3u;
   const size_t lds = bits_words * sizeof(uint32_t) + static_cast<size_t>(WAVES) * a.wcap * L.block * 4;
-  auto* fn = &k_scan1f<VEC, WAVES, kFusedLoads, SKIP, true>;
+  auto* fn = &k_scan1f<VEC, WAVES, kFusedLoads, SKIP, true, false, true>;
   // dynamic LDS beyond 64 KiB is opted into per instantiation, raised when a layout needs more (S sizes the bits)
   static std::atomic<size_t> attr{0};
   if (lds > attr.load()) {
@@ -1972,9 +2056,12 @@ struct TallySpec {
 
 int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* out, int32_t* flags, uint32_t* next,
                  void* ws, hipStream_t st, uint64_t* masks = nullptr, uint32_t part_begin = 0,
-                 uint32_t part_count = 0, const PackSpec* pk = nullptr, const TallySpec* tl = nullptr) {
+                 uint32_t part_count = 0, const PackSpec* pk = nullptr, const TallySpec* tl = nullptr,
+                 uint64_t* chk = nullptr, uint32_t chk_seq = 0) {
   if (part_count == 0) part_count = L.parts - part_begin;
   FusedArgs a{};
+  a.chk = chk;
+  a.chk_seq = chk_seq;
   a.part0 = part_begin;
   a.x = x;
   a.out = out;
@@ -2035,9 +2122,9 @@ int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* ou
   // waves (47.8 against 49.6 us alone; profiles/r04/scan_waves/).
   if (masks != nullptr) {
     switch (L.vec) {
-      case 1: k_scan1f<1, 8, kFusedLoads><<<grid, 512, 0, st>>>(a); break;
-      case 2: k_scan1f<2, 8, kFusedLoads><<<grid, 512, 0, st>>>(a); break;
-      default: k_scan1f<4, 8, kFusedLoads, 1><<<grid, 512, 0, st>>>(a); break;
+      case 1: k_scan1f<1, 8, kFusedLoads, 0, false, false, true><<<grid, 512, 0, st>>>(a); break;
+      case 2: k_scan1f<2, 8, kFusedLoads, 0, false, false, true><<<grid, 512, 0, st>>>(a); break;
+      default: k_scan1f<4, 8, kFusedLoads, 1, false, false, true><<<grid, 512, 0, st>>>(a); break;
     }
     return launch_status("k_scan1f (8 waves)");
   }
@@ -2541,6 +2628,19 @@ int omr_scatter_blocks_f32(const float* packed, const uint32_t* block_list, uint
 int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
                         int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out, void* workspace,
                         size_t workspace_bytes, omr_stream_t stream) {
+  return omr_worker_scan_check_f32(buf, n, block_size, num_lanes, num_parts, flags, next_offsets, row_masks, out,
+                                   workspace, workspace_bytes, nullptr, 0, stream);
+}
+
+uint32_t omr_round_check_slots(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts) {
+  Layout L;
+  if (make_layout(n, block_size, num_lanes, num_parts, &L)) return 0;
+  return static_cast<uint32_t>(static_cast<uint64_t>(L.parts) * L.lanes * fused_shape(L).K);
+}
+
+int omr_worker_scan_check_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
+                              int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out, void* workspace,
+                              size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq, omr_stream_t stream) {
   Layout L;
   if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
   if (buf == nullptr || next_offsets == nullptr || row_masks == nullptr)
@@ -2551,7 +2651,8 @@ int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint3
   const size_t need = fused_workspace_bytes(L, f);
   if (need > 0 && (workspace == nullptr || workspace_bytes < need))
     return fail("worker_scan: needs a zero-initialised workspace of %zu bytes", need);
-  return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks);
+  return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks, 0, 0,
+                      nullptr, nullptr, check_slots, check_seq);
 }
 
 int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
@@ -2559,6 +2660,17 @@ int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, 
                              const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard, float* send,
                              uint32_t* shard_counters, uint32_t* pos_table, void* workspace, size_t workspace_bytes,
                              omr_stream_t stream) {
+  return omr_worker_scan_pack_check_f32(buf, n, block_size, num_lanes, num_parts, flags, next_offsets, row_masks, out,
+                                        shard_bounds, num_shards, own_shard, send, shard_counters, pos_table, workspace,
+                                        workspace_bytes, nullptr, 0, stream);
+}
+
+int omr_worker_scan_pack_check_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes,
+                                   uint32_t num_parts, int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks,
+                                   float* out, const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard,
+                                   float* send, uint32_t* shard_counters, uint32_t* pos_table, void* workspace,
+                                   size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq,
+                                   omr_stream_t stream) {
   Layout L;
   if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
   if (buf == nullptr || next_offsets == nullptr || row_masks == nullptr || send == nullptr ||
@@ -2575,7 +2687,8 @@ int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, 
   if (need > 0 && (workspace == nullptr || workspace_bytes < need))
     return fail("worker_scan_pack: needs a zero-initialised workspace of %zu bytes", need);
   const PackSpec pk{send, shard_counters, pos_table, shard_bounds, num_shards, own_shard};
-  return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks, 0, 0, &pk);
+  return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks, 0, 0, &pk,
+                      nullptr, check_slots, check_seq);
 }
 
 uint32_t omr_tally_slots(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts) {
@@ -2641,13 +2754,18 @@ uint64_t omr_pack_send_offset(const uint64_t* shard_bounds, uint32_t num_shards,
 
 uint64_t omr_round_plan_workspace_words(void) { return kPlanWorkspaceWords; }
 
-int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
-                        uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
-                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint64_t* counts,
-                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters,
-                        uint64_t* workspace, uint32_t seq, uint32_t* union_next, uint32_t block_size,
-                        const omr_sum_list* list, omr_stream_t stream) {
+int omr_round_plan_check(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                         uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                         uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint64_t* counts,
+                         uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters,
+                         uint64_t* workspace, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                         const omr_sum_list* list, uint64_t check_offset, uint32_t check_slots,
+                         uint64_t* check_status, omr_stream_t stream) {
   if (mask_stride < rows) return fail("round_plan: mask_stride %llu < rows", static_cast<unsigned long long>(mask_stride));
+  if (check_status != nullptr && (check_slots == 0 || check_offset < rows || check_offset + check_slots > mask_stride))
+    return fail("round_plan: check slots [%llu, +%u) outside the mask arrays (rows %llu, stride %llu)",
+                static_cast<unsigned long long>(check_offset), check_slots, static_cast<unsigned long long>(rows),
+                static_cast<unsigned long long>(mask_stride));
   if (num_zero_counters > kPlanThreads || (num_zero_counters > 0 && zero_counters == nullptr))
     return fail("round_plan: zero_counters");
   if (count == 0 || count > OMR_MAX_WORKERS) return fail("round_plan: count %u out of range", count);
@@ -2713,13 +2831,27 @@ int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask
     // (a multiple of 8 from 8 up, so xcd_spread gives each XCD whole row groups; spare workgroups find no unit)
     a.list_wgs = static_cast<uint32_t>(wgs < 512 ? (wgs >= 8 ? (wgs + 7) / 8 * 8 : wgs) : 512);
   }
-  const unsigned grid = a.nchunks + chain_wgs + a.list_wgs;
+  a.chk_off = check_offset;
+  a.chk_slots = check_slots;
+  a.chk_status = check_status;
+  const unsigned grid = a.nchunks + chain_wgs + a.list_wgs + (check_status != nullptr ? 1u : 0u);
   hipStream_t st = S(stream);
   if (count <= 2) k_round_plan<2><<<grid, kPlanThreads, 0, st>>>(a);
   else if (count <= 4) k_round_plan<4><<<grid, kPlanThreads, 0, st>>>(a);
   else if (count <= 8) k_round_plan<8><<<grid, kPlanThreads, 0, st>>>(a);
   else k_round_plan<OMR_MAX_WORKERS><<<grid, kPlanThreads, 0, st>>>(a);
   return launch_status("k_round_plan");
+}
+
+int omr_round_plan_list(const uint64_t* row_masks, uint32_t count, uint64_t mask_stride, uint64_t rows,
+                        uint32_t rows_per_part, uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds,
+                        uint64_t* write_set, uint64_t* union_masks, uint32_t* prefix, uint64_t* counts,
+                        uint64_t* zero_masks, uint32_t* zero_counters, uint32_t num_zero_counters,
+                        uint64_t* workspace, uint32_t seq, uint32_t* union_next, uint32_t block_size,
+                        const omr_sum_list* list, omr_stream_t stream) {
+  return omr_round_plan_check(row_masks, count, mask_stride, rows, rows_per_part, num_lanes, bounds, num_bounds,
+                              write_set, union_masks, prefix, counts, zero_masks, zero_counters, num_zero_counters,
+                              workspace, seq, union_next, block_size, list, 0, 0, nullptr, stream);
 }
 
 int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
@@ -2817,11 +2949,20 @@ int omr_shard_sum_f32(const float* own, uint32_t me, const float* recv, const ui
                       const uint64_t* row_masks, uint32_t count, const uint32_t* prefix, const uint64_t* write_set,
                       uint64_t rows, uint64_t row_begin, uint64_t row_end, uint32_t num_lanes, uint32_t block_size,
                       int packed_out, float* out, omr_stream_t stream) {
+  return omr_shard_sum_stride_f32(own, me, recv, recv_offsets, row_masks, rows, count, prefix, write_set, rows,
+                                  row_begin, row_end, num_lanes, block_size, packed_out, out, stream);
+}
+
+int omr_shard_sum_stride_f32(const float* own, uint32_t me, const float* recv, const uint64_t* recv_offsets,
+                             const uint64_t* row_masks, uint64_t mask_stride, uint32_t count, const uint32_t* prefix,
+                             const uint64_t* write_set, uint64_t rows, uint64_t row_begin, uint64_t row_end,
+                             uint32_t num_lanes, uint32_t block_size, int packed_out, float* out, omr_stream_t stream) {
+  if (mask_stride < rows) return fail("shard_sum: mask_stride %llu < rows", static_cast<unsigned long long>(mask_stride));
   SumArgs a{};
   a.own = own;
   a.recv = recv;
   a.masks = row_masks;
-  a.mstride = rows;
+  a.mstride = mask_stride;
   a.prefix = prefix;
   a.write_set = write_set;
   a.out = out;

@@ -69,6 +69,15 @@ SIGNATURES = {
     "omr_tally_slots": (c_u32, [c_u64, c_u32, c_u32, c_u32]),
     "omr_round_plan_list": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
                                     c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_u32, c_vp, c_vp]),
+    "omr_round_check_slots": (c_u32, [c_u64, c_u32, c_u32, c_u32]),
+    "omr_shard_sum_stride_f32": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u64, c_u32, c_vp, c_vp, c_u64, c_u64, c_u64,
+                                         c_u32, c_u32, c_int, c_vp, c_vp]),
+    "omr_worker_scan_check_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_size,
+                                          c_vp, c_u32, c_vp]),
+    "omr_worker_scan_pack_check_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32,
+                                               ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp, c_u32, c_vp]),
+    "omr_round_plan_check": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_u32, c_vp, c_u64, c_u32, c_vp, c_vp]),
     "omr_sum_list_geometry": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u64, c_u64, c_u32, c_vp, c_vp]),
     "omr_sum_list_build": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp]),
     "omr_shard_sum_list_f32": (c_int, [c_vp, c_vp, c_vp, c_u32, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_int, c_vp,

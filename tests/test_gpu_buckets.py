@@ -127,6 +127,31 @@ def test_buckets_config5_full_shape(gpu, mode):
           f"(inputs, 16 buckets x 8 ranks, check)", flush=True)
 
 
+@pytest.mark.parametrize("world,mode", [(1, AR), (2, AR), (4, RS), (8, AR)])
+def test_buckets_loopback_direct(gpu, world, mode, monkeypatch):
+    """OMR_BUCKETS_DIRECT=1 (round 6): at N > 1 too, each bucket's round reads and writes the
+    mapped pinned bucket in place (the worker scan over PCIe, its pack into device send buffers, the shard sum and the
+    unpack storing straight into host memory) instead of the staging ring; N = 1 does so by default."""
+    monkeypatch.setenv("OMR_BUCKETS_DIRECT", "1")
+    test_buckets_loopback(gpu, world, mode, True, 16, 64)
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("mode", [AR, RS])
+def test_buckets_config5_full_shape_direct(gpu, mode, monkeypatch):
+    """Config 5 at its own shape (8 loopback ranks, 4 GiB pinned per rank, 256 MiB buckets, -r 0.49) on the direct
+    path: no staging buffer, every rank checked against ka[count]."""
+    monkeypatch.setenv("OMR_BUCKETS_DIRECT", "1")
+    test_buckets_loopback(gpu, 8, mode, True, 256, 4096)
+
+
+def test_buckets_one_rank_staging_ring(gpu, monkeypatch):
+    """OMR_BUCKETS_STAGED=1: a one-rank group through the four-buffer staging ring instead of its direct launches."""
+    monkeypatch.setenv("OMR_BUCKETS_STAGED", "1")
+    test_buckets_loopback(gpu, 1, AR, True, 16, 64)
+
+
 @pytest.mark.parametrize("world,mode", [(2, AR), (4, RS)])
 def test_buckets_loopback_staged_writeback(gpu, world, mode, monkeypatch):
     """The previous write-back (each bucket, or the rank's shard, copied back whole from its staging buffer), kept

@@ -312,3 +312,105 @@ def test_shard_sum(gpu, count, me, B, packed_out, span):
         want = (xs[me].copy() if me < count else np.zeros(L.n, np.float32)).reshape(-1, B)
         want[wblocks] = exp_blocks
         assert (got.view(np.uint32) == want.ravel().view(np.uint32)).all()
+
+
+# ---------------------------------------------------------------- the round check (round 6)
+
+@pytest.mark.parametrize("n,B,density,pack", [(4 << 20, 256, 0.095, False), (16 << 20, 1024, 0.0099, False),
+                                              (8 << 20, 256, 0.3, True), (64 << 20, 256, 0.095, True)])
+def test_round_check_slots(gpu, n, B, density, pack):
+    """omr_worker_scan_check_f32 / omr_worker_scan_pack_check_f32: one slot per scan workgroup, (seq << 32) | its
+    non-zero blocks; the slots add up to the masks' popcount, the oracle's non-zero block count."""
+    L = Layout(n=n, block_size=B)
+    x = oracle.fill(oracle.gen_bitmap(4, density, L.nb), B, mode=1, seed=9)
+    f = oracle.flags_from_data(x, B)
+    lib = _lib.load()
+    ns = int(lib.omr_round_check_slots(L.n, B, L.num_lanes, L.num_threads))
+    assert ns == int(lib.omr_tally_slots(L.n, B, L.num_lanes, L.num_threads)) > 0
+    xd = torch.from_numpy(x).to(gpu)
+    flags = torch.zeros(L.nb, dtype=torch.int32, device=gpu)
+    nxt = torch.zeros(L.nb, dtype=torch.int32, device=gpu)
+    masks = torch.zeros(L.rows, dtype=torch.int64, device=gpu)
+    slots = torch.zeros(ns, dtype=torch.int64, device=gpu)
+    wsb = lib.omr_scan_workspace_bytes(L.n, B, L.num_lanes, L.num_threads)
+    ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=gpu)
+    for seq in (7, 8):
+        masks.zero_()
+        if pack:
+            bounds = np.array([0, L.rows // 2, L.rows], dtype=np.uint64)
+            ent = ctypes.c_uint64()
+            assert lib.omr_pack_geometry(L.n, B, L.num_lanes, L.num_threads, None, None, ctypes.byref(ent)) == 0
+            send = torch.zeros(L.n, dtype=torch.float32, device=gpu)
+            cnt = torch.zeros(2, dtype=torch.int32, device=gpu)
+            pos = torch.zeros(int(ent.value), dtype=torch.int32, device=gpu)
+            rc = lib.omr_worker_scan_pack_check_f32(P(xd), L.n, B, L.num_lanes, L.num_threads, P(flags), P(nxt),
+                                                    P(masks), None, bounds.ctypes.data, 2, 0, P(send), P(cnt), P(pos),
+                                                    P(ws), wsb, P(slots), seq, stream())
+        else:
+            rc = lib.omr_worker_scan_check_f32(P(xd), L.n, B, L.num_lanes, L.num_threads, P(flags), P(nxt), P(masks),
+                                               None, P(ws), wsb, P(slots), seq, stream())
+        assert rc == 0, lib.omr_last_error()
+        torch.cuda.synchronize()
+        s = slots.cpu().numpy().view(np.uint64)
+        assert ((s >> np.uint64(32)) == np.uint64(seq)).all()
+        assert int((s & np.uint64(0xFFFFFFFF)).sum()) == int(f.sum()) == int(popc(masks.cpu().numpy()).sum())
+        assert (masks.cpu().numpy().view(np.uint64) == oracle.row_masks(f, L.num_lanes)).all()
+
+
+def test_round_plan_check(gpu):
+    """omr_round_plan_check: status (seq << 32) | 0 on the workers' own arrays; | 0x100 + c when a slot of worker c
+    carries another round's number (its array read before its scan wrote it); | 0x200 + c when worker c's masks hold
+    fewer bits than its slots count (read before its scan finished).  The plan's other outputs are unchanged."""
+    B, m = 256, 3
+    L = Layout(n=4 << 20, block_size=B)
+    lib = _lib.load()
+    ns = int(lib.omr_round_check_slots(L.n, B, L.num_lanes, L.num_threads))
+    stride = L.rows + ns + 3
+    arrays = torch.zeros(m, stride, dtype=torch.int64, device=gpu)
+    wsb = lib.omr_scan_workspace_bytes(L.n, B, L.num_lanes, L.num_threads)
+    ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=gpu)
+    flags = torch.zeros(L.nb, dtype=torch.int32, device=gpu)
+    nxt = torch.zeros(L.nb, dtype=torch.int32, device=gpu)
+    seq = 41
+    fl = []
+    for c in range(m):
+        x = oracle.fill(oracle.gen_bitmap(c, 0.2, L.nb), B, mode=1, seed=c)
+        fl.append(oracle.flags_from_data(x, B))
+        xd = torch.from_numpy(x).to(gpu)
+        row = arrays[c]
+        assert lib.omr_worker_scan_check_f32(P(xd), L.n, B, L.num_lanes, L.num_threads, P(flags), P(nxt),
+                                             ctypes.c_void_p(row.data_ptr()), None, P(ws), wsb,
+                                             ctypes.c_void_p(row.data_ptr() + 8 * (L.rows + 3)), seq, stream()) == 0
+    torch.cuda.synchronize()
+    pws = plan_ws(lib, gpu)
+    bounds = torch.tensor([0, L.rows // 2, L.rows], dtype=torch.int64, device=gpu)
+    wset = torch.zeros(L.rows, dtype=torch.int64, device=gpu)
+    prefix = torch.zeros((m + 1) * (L.rows + 1), dtype=torch.int32, device=gpu)
+    counts = torch.zeros((m + 1) * 3, dtype=torch.int64, device=gpu)
+    status = torch.zeros(1, dtype=torch.int64, device=gpu)
+
+    def plan(s):
+        assert lib.omr_round_plan_check(P(arrays), m, stride, L.rows, L.rows_per_part, L.num_lanes, P(bounds), 3,
+                                        P(wset), None, P(prefix), P(counts), None, None, 0, P(pws), s, None, B, None,
+                                        L.rows + 3, ns, P(status), stream()) == 0, lib.omr_last_error()
+        torch.cuda.synchronize()
+        v = int(status.cpu().numpy().view(np.uint64)[0])
+        assert v >> 32 == s
+        return v & 0xFFFFFFFF
+
+    assert plan(seq) == 0
+    masks = arrays[:, :L.rows].cpu().numpy().view(np.uint64)
+    exp_c = np.array([[np_prefix(masks[a])[b] for b in (0, L.rows // 2, L.rows)] for a in range(m)])
+    assert (untag(counts, seq).reshape(m + 1, 3)[:m] == exp_c).all()
+    # the same arrays checked as another round's: every slot is stale (the first worker found is reported)
+    assert plan(seq + 1) & 0xF00 == 0x100
+    # worker 2's last slot from an earlier round
+    sl = arrays[2, L.rows + 3 + ns - 1].item()
+    arrays[2, L.rows + 3 + ns - 1] = ((seq - 4) << 32) | (sl & 0xFFFFFFFF)
+    assert plan(seq) == 0x100 | 2
+    arrays[2, L.rows + 3 + ns - 1] = sl
+    assert plan(seq) == 0
+    # worker 1's masks missing a row's bits (a copy that overtook its scan)
+    r = int(np.nonzero(masks[1])[0][5])
+    arrays[1, r] = 0
+    assert plan(seq) == 0x200 | 1
