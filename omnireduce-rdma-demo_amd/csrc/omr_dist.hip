@@ -832,16 +832,18 @@ struct IpcDist final : omr_dist {
   // plain importer of a sanitized exporter's buffer lands 4 KiB before the data and a sanitized importer of a plain
   // one 4 KiB after it (OMR_IPC_TRACE: the exporter's handle names its allocation 0x1000 below the pointer; the
   // importers' pointers differ by 0x1000; profiles/r06/ipc_mix/).  The all-gather then copied the wrong 8 KiB and
-  // the ranks' block counts disagreed.  So at attach each rank exports a canary (word i = rank << 32 | i) and opens
+  // the ranks' block counts disagreed.  So at attach each rank exports a canary (word i = (0xC0DE0000 | rank) << 32 | i:
+  // no word is zero, so a zero-filled redzone never passes for one) and opens
   // every peer's: a peer whose canary does not read back from offset 0 fails the group at creation, with the offset.
   // Only the canary's first kCanaryRead bytes are read back, so a handle that opens up to 48 KiB off either way still
   // reads inside the 64 KiB allocation (a device read outside a mapping faults the GPU).
   static constexpr size_t kCanaryWords = 8192;  // 64 KiB
   static constexpr size_t kCanaryRead = 2048;   // words read back: 16 KiB
+  static uint64_t canary_word(int r, size_t i) { return ((0xC0DE0000ull | static_cast<uint64_t>(r)) << 32) | i; }
   int make_canary(IpcRank& me) {
     TRY(hip_check(hipMalloc(&canary, kCanaryWords * 8), "hipMalloc canary"));
     std::vector<uint64_t> h(kCanaryWords);
-    for (size_t i = 0; i < kCanaryWords; ++i) h[i] = (static_cast<uint64_t>(rank) << 32) | i;
+    for (size_t i = 0; i < kCanaryWords; ++i) h[i] = canary_word(rank, i);
     TRY(hip_check(hipMemcpy(canary, h.data(), kCanaryWords * 8, hipMemcpyHostToDevice), "hipMemcpy canary"));
     return hip_check(hipIpcGetMemHandle(&me.canary, canary), "hipIpcGetMemHandle canary");
   }
@@ -855,16 +857,18 @@ struct IpcDist final : omr_dist {
       const hipError_t e = hipMemcpy(h.data(), mp, kCanaryRead * 8, hipMemcpyDeviceToHost);
       (void)hipIpcCloseMemHandle(mp);
       TRY(hip_check(e, "hipMemcpy canary"));
-      const uint64_t tag = static_cast<uint64_t>(p) << 32;
-      if (h[0] == tag) continue;  // word 0 at offset 0: the handle opens at the exporter's address
+      bool whole = true;  // every word read back where it was written: the handle opens at the exporter's address
+      for (size_t i = 0; i < kCanaryRead && whole; ++i) whole = h[i] == canary_word(p, i);
+      if (whole) continue;
       long long off = 0;
       bool found = false;
-      if ((h[0] >> 32) == static_cast<uint64_t>(p) && (h[0] & 0xFFFFFFFFu) < kCanaryWords) {
-        off = static_cast<long long>(h[0] & 0xFFFFFFFFu) * 8;  // opened past the start: this much after it
+      const uint64_t j = h[0] & 0xFFFFFFFFu;
+      if ((h[0] >> 32) == (canary_word(p, 0) >> 32) && j < kCanaryWords && h[1] == canary_word(p, j + 1)) {
+        off = static_cast<long long>(j) * 8;  // opened past the start: this much after it
         found = true;
       } else {
-        for (size_t i = 1; i < kCanaryRead && !found; ++i)
-          if (h[i] == tag) {
+        for (size_t i = 1; i + 1 < kCanaryRead && !found; ++i)
+          if (h[i] == canary_word(p, 0) && h[i + 1] == canary_word(p, 1)) {
             off = -static_cast<long long>(i * 8);  // opened before the start
             found = true;
           }

@@ -1225,7 +1225,8 @@ struct PlanArgs {
   uint32_t* prefix;
   uint64_t* counts;       // (seq << 32) | prefix at a bound; device or host-mapped memory (stored at system scope)
   uint64_t* zero_masks;   // or null
-  uint64_t* ws;           // [0] ticket counter (zero between launches), [1 + chunk * kPlanArrays + a] chunk totals
+  uint64_t* ws;           // [0] ticket counter (zero between launches), [1 + chunk * (W + 1) + a] chunk totals
+                          //   (packed at the launch's W: a chunk's lower chunks' totals are consecutive words)
   uint32_t seq;           // this launch's tag (differs from the previous launch's on the workspace)
   uint32_t nchunks, tiles;  // chunks of tiles * 256 rows
   NextArgs chain;       // union_next: the aggregator chain over the union, by workgroups after the chunks' (chain.next
@@ -1337,13 +1338,13 @@ __device__ __forceinline__ void plan_chunk(const PlanArgs& a) {
     uint32_t sum = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kPlanWaves; ++w) sum += s_wtot[w][t];
-    __hip_atomic_store(&a.ws[1 + static_cast<uint64_t>(c) * kPlanArrays + t], tag | sum, __ATOMIC_RELAXED,
+    __hip_atomic_store(&a.ws[1 + static_cast<uint64_t>(c) * NA + t], tag | sum, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
   for (uint32_t j = t; j < c * NA; j += kPlanThreads) {
     const uint32_t i = j / NA, k = j - i * NA;
     uint64_t v;
-    while (((v = __hip_atomic_load(&a.ws[1 + static_cast<uint64_t>(i) * kPlanArrays + k], __ATOMIC_RELAXED,
+    while (((v = __hip_atomic_load(&a.ws[1 + static_cast<uint64_t>(i) * NA + k], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT)) >> 32) != a.seq)
       __builtin_amdgcn_s_sleep(1);
     atomicAdd(&s_base[k], static_cast<uint32_t>(v));
@@ -1430,14 +1431,18 @@ constexpr uint32_t kCheckStale = 0x100u, kCheckCount = 0x200u;
 
 template <int W>
 __device__ __forceinline__ void plan_check(const PlanArgs& a) {
-  __shared__ uint32_t s_sum[OMR_MAX_WORKERS];
-  __shared__ uint32_t s_stale, s_bad;  // 1 + a worker (0: none)
-  const uint32_t t = threadIdx.x;
-  if (t < OMR_MAX_WORKERS) s_sum[t] = 0;
-  if (t == 0) s_stale = s_bad = 0;
-  __syncthreads();
+  // every slot is loaded in one or two batches of U per thread; each thread keeps its own per-worker sums and its
+  // lowest stale worker in registers and the waves reduce them once (a shared-memory atomic per slot, all lanes of a
+  // wave on one worker's address, serialised 64 ways: 7 us at config 4's 4096 slots, profiles/r06/INDEX.md)
+  __shared__ uint32_t s_sum[kPlanWaves][W];
+  __shared__ uint32_t s_stale, s_bad;  // the lowest worker found (OMR_MAX_WORKERS: none)
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t == 0) s_stale = s_bad = OMR_MAX_WORKERS;
   const uint32_t ns = a.chk_slots, words = a.count * ns;
-  constexpr uint32_t U = 8;  // loads in flight per thread
+  constexpr uint32_t U = 16;  // loads in flight per thread
+  uint32_t sum[W], stale = OMR_MAX_WORKERS;
+#pragma unroll
+  for (int k = 0; k < W; ++k) sum[k] = 0;
   for (uint32_t base = 0; base < words; base += kPlanThreads * U) {
     uint64_t v[U];
 #pragma unroll
@@ -1451,25 +1456,37 @@ __device__ __forceinline__ void plan_check(const PlanArgs& a) {
       const uint32_t idx = base + i * kPlanThreads + t;
       if (idx >= words) continue;
       const uint32_t c = idx / ns;
-      if (static_cast<uint32_t>(v[i] >> 32) != a.seq) (void)atomicCAS(&s_stale, 0u, c + 1);
-      (void)atomicAdd(&s_sum[c], static_cast<uint32_t>(v[i]));
+      if (static_cast<uint32_t>(v[i] >> 32) != a.seq) stale = min(stale, c);
+#pragma unroll
+      for (int k = 0; k < W; ++k) sum[k] += c == static_cast<uint32_t>(k) ? static_cast<uint32_t>(v[i]) : 0u;
     }
   }
-  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    const uint32_t inc = wave_incl_scan(sum[k]);
+    if (lane == 63) s_sum[wave][k] = inc;
+  }
+  __syncthreads();  // (s_stale initialised, s_sum filled)
+  if (stale < OMR_MAX_WORKERS) (void)atomicMin(&s_stale, stale);
   if (t < a.count) {  // the worker's mask total: the chunks' tagged totals of its array
-    uint32_t tot = 0;
+    uint32_t tot = 0, got = 0;
     for (uint32_t i = 0; i < a.nchunks; ++i) {
       uint64_t v;
-      while (((v = __hip_atomic_load(&a.ws[1 + static_cast<uint64_t>(i) * kPlanArrays + t], __ATOMIC_RELAXED,
+      while (((v = __hip_atomic_load(&a.ws[1 + static_cast<uint64_t>(i) * (W + 1) + t], __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT)) >> 32) != a.seq)
         __builtin_amdgcn_s_sleep(1);
       tot += static_cast<uint32_t>(v);
     }
-    if (tot != s_sum[t]) (void)atomicCAS(&s_bad, 0u, t + 1);
+#pragma unroll
+    for (uint32_t w = 0; w < kPlanWaves; ++w)
+#pragma unroll
+      for (int k = 0; k < W; ++k) got += t == static_cast<uint32_t>(k) ? s_sum[w][k] : 0u;
+    if (tot != got) (void)atomicMin(&s_bad, t);
   }
   __syncthreads();
   if (t == 0) {
-    const uint32_t code = s_stale ? (kCheckStale | (s_stale - 1)) : (s_bad ? (kCheckCount | (s_bad - 1)) : 0u);
+    const uint32_t code = s_stale < OMR_MAX_WORKERS ? (kCheckStale | s_stale)
+                                                    : (s_bad < OMR_MAX_WORKERS ? (kCheckCount | s_bad) : 0u);
     __hip_atomic_store(a.chk_status, (static_cast<uint64_t>(a.seq) << 32) | code, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }

@@ -20,11 +20,12 @@ def test_product_kernels_have_no_study_knobs():
 
 
 def test_product_reads_only_documented_environment():
-    """the product libraries read the deadline, the host trace and the bucket write-back modes
-    from the environment, nothing else (no study knobs, no per-launch lookups)."""
+    """the product libraries read the deadline, the host and IPC traces and the bucket modes from
+    the environment, nothing else (no study knobs, no per-launch lookups); DESIGN.md §7 lists every one."""
     import re
     allowed = {"OMR_DIST_TIMEOUT_MS", "OMR_HOST_TRACE", "OMR_HOST_TRACE_FILE", "OMR_BUCKETS_STAGED_D2H",
-               "OMR_BUCKETS_SCAN_HOST", "OMR_HOST_STAGED_D2H"}
+               "OMR_BUCKETS_SCAN_HOST", "OMR_HOST_STAGED_D2H", "OMR_IPC_TRACE", "OMR_BUCKETS_DIRECT",
+               "OMR_BUCKETS_STAGED"}
     csrc = os.path.join(ROOT, "omnireduce-rdma-demo_amd", "csrc")
     seen = set()
     for f in sorted(os.listdir(csrc)):
@@ -35,6 +36,9 @@ def test_product_reads_only_documented_environment():
         assert src.count("getenv(") == len(re.findall(r'getenv\("[A-Z0-9_]+"\)', src)), f
     assert "OMR_DIST_TIMEOUT_MS" in seen
     assert "getenv" not in open(os.path.join(csrc, "omr_kernels.hip")).read()
+    design = open(os.path.join(ROOT, "DESIGN.md")).read()
+    for name in seen:
+        assert name in design, name
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")

@@ -14,8 +14,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = [  # (tune_round_r03 case filter, kernel name in the trace)
     ("product k_shard_sum_list", "::k_shard_sum_list<"),
-    ("scan + fused pack", "::k_scan1f<"),
+    ("scan + fused pack (product)", "::k_scan1f<"),
+    ("scan + fused pack + round-check", "::k_scan1f<"),
     ("round plan as the round calls it (pair", "::k_round_plan<"),
+    ("round plan as the round calls it + round check", "::k_round_plan<"),
     ("round plan as the round calls it, round-3/4", "::k_round_plan_r04("),
     ("round plan, no chain (k_round_plan)", "::k_round_plan<"),
     ("round plan, no chain (round-3/4", "::k_round_plan_r04("),

@@ -223,6 +223,16 @@ def main():
                                             send0.data_ptr(), cntbig[i * naggs:].data_ptr(),
                                             own_masks[rows:].data_ptr(), ws.data_ptr(), wsb, st)
 
+    ns = int(lib.omr_round_check_slots(L.n, B, NB, L.num_threads))
+    chk_slots = torch.zeros(ns, dtype=torch.int64, device=dev)
+
+    def scan_pack_chk(i=0):  # the round's worker scan since round 6: + its round-check slots
+        return lib.omr_worker_scan_pack_check_f32(xs[0].data_ptr(), L.n, B, NB, L.num_threads, flags.data_ptr(),
+                                                  nxt.data_ptr(), own_masks.data_ptr(), None, bptr, naggs, 0,
+                                                  send0.data_ptr(), cntbig[i * naggs:].data_ptr(),
+                                                  own_masks[rows:].data_ptr(), ws.data_ptr(), wsb,
+                                                  chk_slots.data_ptr(), 1, st)
+
     def pack():
         return lib.omr_move_blocks_f32(xs[0].data_ptr(), packed.data_ptr(), 0, masks[0].data_ptr(), pre[0].data_ptr(),
                                        rows, NB, B, r0, r1, st)
@@ -263,6 +273,15 @@ def main():
                                        naggs + 1, wset.data_ptr(), None, prefix.data_ptr(), cnt_d, zmask.data_ptr(),
                                        zcnt.data_ptr(), naggs, pws5.data_ptr(), nseq(), None, B, ctypes.byref(sl), st)
 
+    chk_status = cnt_d + 12 * 1024  # (pinned, beside the counts and the round-3/4 notice)
+
+    def plan_round_chk():  # the round's call since round 6: + the round check's workgroup (timing only: the words it
+        # checks here are position-table entries, so its status reports a mismatch)
+        return lib.omr_round_plan_check(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
+                                        naggs + 1, wset.data_ptr(), None, prefix.data_ptr(), cnt_d, zmask.data_ptr(),
+                                        zcnt.data_ptr(), naggs, pws5.data_ptr(), nseq(), None, B, ctypes.byref(sl),
+                                        rows, min(ns, mstride - rows), chk_status, st)
+
     def plan_round_r04():  # the same call to the round-3/4 plan (one workgroup per mask array, arrival counter)
         seqs[0] += 1
         return t4.tune_round_plan_list_r04(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB,
@@ -299,6 +318,8 @@ def main():
                                       st)
 
     workers = {"scan (omr_worker_scan_f32)": scan, "scan + fused pack (product)": scan_pack,
+               "scan + fused pack + round-check slots (the round's, round 6)": scan_pack_chk,
+               "round plan as the round calls it + round check (round 6)": plan_round_chk,
                "pack pass (k_move, round 2)": pack, "round plan + chain (k_round_plan)": plan,
                "round plan + chain, row chunks (k_round_plan2)": plan_ws,
                "round plan, no chain (k_round_plan)": plan_nochain,
@@ -323,7 +344,7 @@ def main():
             for i in range(a.reps):
                 if name in sums:
                     fn(outs[i % 2])
-                elif fn is scan_pack:
+                elif fn is scan_pack or fn is scan_pack_chk:
                     fn(i)
                 else:
                     fn()
@@ -358,6 +379,11 @@ def main():
     wbytes["round plan as the round calls it, round-3/4 form"] = (
         wbytes["round plan as the round calls it (pair list, pinned counts)"] + rows * 8)  # (+ its union)
     wbytes["pair list alone (k_sum_list)"] = lbytes
+    # round 6: the scan's slots (8 B per workgroup) and the check's reads of every worker's slots
+    wbytes["scan + fused pack + round-check slots (the round's, round 6)"] = (
+        wbytes["scan + fused pack (product)"] + ns * 8)
+    wbytes["round plan as the round calls it + round check (round 6)"] = (
+        wbytes["round plan as the round calls it (pair list, pinned counts)"] + m * min(ns, mstride - rows) * 8)
     report = {}
     print(f"## config 4 shapes, {m} workers, -r {a.density}: shard 0 write set {ub} blocks, received {nc}, own {own_blocks}: "
           f"{sbytes} B per shard sum; worker 0 packs {other} blocks", flush=True)
