@@ -259,7 +259,9 @@ int omr_ar_plan_side_streams(const omr_ar_plan* plan);
  * probes them: a one-wave kernel holds one stream's queue while a mark is queued on the other; a side stream whose mark
  * cannot run while the caller's queue (or the other side stream's) is held is replaced by a fresh stream that passes
  * (up to six tried).  About a millisecond once per caller stream.  On by default, except for the loopback transport
- * (threads sharing one process's queues); omr_ar_plan_set_queue_check(plan, 0) turns it off.
+ * (threads sharing one process's queues) and IPC ranks that share their GPU with other ranks (their processes' queues
+ * oversubscribe the hardware's, so a probe would time the other ranks' load); omr_ar_plan_set_queue_check(plan, 0|1)
+ * overrides it.
  * omr_ar_plan_queue_report: *disjoint = 1 when the last check left every side stream on a queue of its own, 0 when
  * some stream still shares one, -1 before any check; *probes / *replaced count the probes run and the side streams
  * replaced so far (any pointer may be NULL). */

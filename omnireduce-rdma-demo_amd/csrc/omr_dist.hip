@@ -683,6 +683,11 @@ struct IpcDist final : omr_dist {
   // ranks spread over separate GPUs keep the exchange stream.
   int share_gpu = 1;
   int default_side_streams() const override { return share_gpu <= 4 ? 2 : 1; }
+  // No queue check where ranks share this rank's GPU: the processes' queues together oversubscribe the hardware queue
+  // slots, which the scheduler then time-slices, and the other ranks' kernels run in between, so whether the probe's
+  // mark lands inside its window says more about the other ranks' load than about this process's queue mapping (and
+  // every failed probe costs the window).  One rank per GPU checks, as over RCCL.
+  bool queue_check_default() const override { return share_gpu <= 1; }
 
   static void release(IpcEvents& e, std::vector<hipEvent_t>& to) {
     for (int k = 0; k < kIpcRing; ++k) {

@@ -37,8 +37,8 @@ def run_ranks(tmp_path, world, n, B, density, mode, pipe, rounds=3, workers=0, c
             for q in procs:
                 q.kill()
             pytest.fail("an IPC rank hung:\n" + "\n".join(q.communicate()[0] or "" for q in procs))
-    for r, p in enumerate(procs):
-        assert p.returncode == 0, f"rank {r} failed:\n{logs[r]}"
+    bad = [r for r, p in enumerate(procs) if p.returncode != 0]
+    assert not bad, "\n".join(f"rank {r} failed (rc {procs[r].returncode}):\n{logs[r][-2000:]}" for r in bad)
     return [np.load(o) for o in outs]
 
 

@@ -390,6 +390,9 @@ def test_round_plan_check(gpu):
     status = torch.zeros(1, dtype=torch.int64, device=gpu)
 
     def plan(s):
+        # (a fresh workspace per launch: the arrays' slots carry `seq`, so the launches here repeat it, which the plan's
+        # contract forbids on one workspace -- its chunks' tagged totals of the previous launch would pass as this one's)
+        pws = plan_ws(lib, gpu)
         assert lib.omr_round_plan_check(P(arrays), m, stride, L.rows, L.rows_per_part, L.num_lanes, P(bounds), 3,
                                         P(wset), None, P(prefix), P(counts), None, None, 0, P(pws), s, None, B, None,
                                         L.rows + 3, ns, P(status), stream()) == 0, lib.omr_last_error()

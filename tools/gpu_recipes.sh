@@ -10,10 +10,13 @@
 #                             rocprofv3 --kernel-trace --stats of the default line, PMC HBM traffic of config 2
 #   bench TAG                 the other bench lines: config 3, m = 8, config 5 (N = 1), the N > 1 path at world 1
 #                             (one-launch and general layouts), config 1; rocprofv3 stats of config 3; PMC of config 3
-#   round TAG                 the round's kernels at config 4's shapes: timings (tools/tune_round_r03.py), then their
-#                             PMC HBM traffic (tools/pmc_round.py -> pmc_round_<TAG>.json)
+#   round TAG [filter]        the round's kernels at config 4's shapes: the launch floor (tools/tune/launch_floor.hip,
+#                             built into tools/bin/ on the CPU side), timings (tools/tune_round_r03.py), then their PMC
+#                             HBM traffic (tools/pmc_round.py -> pmc_round_<TAG>.json; filter: only matching cases)
 #   layouts TAG               the world-1 round in its stream layouts (tools/round_inproc_r05.py: deferred, thread,
 #                             after a torch group, without the queue check) and bench --world1-general with a host trace
+#   w1g_trace TAG             bench --world1-general (the N > 1 path at world 1) under rocprofv3's kernel trace, deferred
+#                             and with the progress thread, and its HBM bytes per round by kernel (PMC)
 #   ipc_mix TAG               one ./omr_server + two ./omr_client over HIP IPC with CHECK on and OMR_IPC_TRACE: all
 #                             plain, then host-AddressSanitizer clients (build/asan, tools/r05/asan_build.sh, built on
 #                             the CPU side first); expected: plain passes, the mix is refused at creation
@@ -74,6 +77,7 @@ bench)
     --block-size 1024 --density 0.0099 --steps 20 --warmup 5 --no-cpu --no-round
   ;;
 round)
+  [ -x tools/bin/launch_floor ] && step 60 launch_floor.log tools/bin/launch_floor
   step 600 tune_round.log python3 -u tools/tune_round_r03.py --rounds 6 --reps 20 --json "$O/tune_round.json"
   step 900 pmc_round.log python3 -u tools/pmc_round.py --out "$O/pmc_round_$tag.json" --workdir "$O/pmc_work" --only "${1:-}"
   grep -v '^#' "$O/tune_round.log" | tail -25
@@ -90,6 +94,17 @@ layouts)
   jstep 200 w1g_thread env OMR_HOST_TRACE=1 "${DIST1[@]}" --master-port $((PORT++)) bench.py --force-dist --world1-general --no-cpu --dist-pipe thread \
     --side-streams 2 --steps 100 --warmup 10
   grep -h "us per round" "$O"/inproc*.log
+  ;;
+w1g_trace)
+  for pipe in defer thread; do
+    ( cd /tmp && RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=$((PORT++)) timeout -k 10 240 \
+        rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_$pipe" -o w1g -- python3 "$R/bench.py" \
+        --force-dist --world1-general --no-cpu --dist-pipe $pipe --side-streams 2 --steps 100 --warmup 10 \
+        > "$O/trace_$pipe.json" 2> "$O/trace_$pipe.err" ) || { echo "trace $pipe failed"; tail -20 "$O/trace_$pipe.err"; exit 1; }
+  done
+  step 300 pmc_w1g.log env RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=$((PORT++)) \
+    python3 tools/pmc_traffic.py --kernel k_scan1f --also k_round_plan,k_shard_sum_list --out "$O/pmc_w1g.json" \
+    --workdir "$O/pmc_w1g" -- --force-dist --world1-general --no-cpu --steps 20 --warmup 5
   ;;
 ipc_mix)
   B=omnireduce-rdma-demo_amd/bin; A=build/asan

@@ -8,7 +8,9 @@ of a wide (16 B/lane) coalesced streaming read, so hbm_read = 2 * FETCH_SIZE * 1
 16 B/lane streaming stores.  Each pass runs `python bench.py` under rocprofv3 with the counters only
 (no --sys-trace / --runtime-trace), from /tmp as the guide asks.
 
-usage: python tools/pmc_traffic.py [--kernel k_scan1] [--out profiles/pmc_r01.json] [-- bench args]
+usage: python tools/pmc_traffic.py [--kernel k_scan1] [--also k_round_plan,k_shard_sum_list] [--out ...] [-- bench args]
+--also: further kernels of the same run, each reported per launch under "also" (round 6: every kernel of the N>1
+path's round at world 1, so the round's HBM bytes can be added up).
 """
 import argparse
 import csv
@@ -53,6 +55,7 @@ def main():
     ap.add_argument("--kernel", default="k_scan1f")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc_r01.json"))
     ap.add_argument("--workdir", default=os.path.join(ROOT, "gpurun_out", "pmc"))
+    ap.add_argument("--also", default="", help="comma-separated further kernel names, reported per launch")
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     a.out, a.workdir = os.path.abspath(a.out), os.path.abspath(a.workdir)  # the passes run from /tmp
@@ -77,6 +80,14 @@ def main():
         "correction": "read = 2 x FETCH_SIZE (gfx950 16 B/lane streaming reads), write = WRITE_SIZE, KiB",
         "bench_args": bench_args,
     }
+    also = {}
+    for k in [x for x in a.also.split(",") if x]:
+        fk, nfk = per_launch(fetch_csv, k, "FETCH_SIZE")
+        wk, nwk = per_launch(write_csv, k, "WRITE_SIZE")
+        also[k] = {"launches": {"fetch_pass": nfk, "write_pass": nwk}, "hbm_read_bytes_per_launch": 2 * fk * 1024,
+                   "hbm_write_bytes_per_launch": wk * 1024, "hbm_bytes_per_launch": int(2 * fk * 1024 + wk * 1024)}
+    if also:
+        res["also"] = also
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
