@@ -1441,7 +1441,6 @@ struct omr_ar_plan {
   std::thread progress;
   std::mutex mu;
   std::condition_variable cv_job, cv_done;
-  std::atomic<uint64_t> epoch{0};  // advanced at every notify of cv_job / cv_done (handoff_wait spins on it)
   std::deque<Job> jobs;
   uint64_t rounds_begun = 0, first_halves = 0;  // rounds whose scan is queued / whose bookkeeping is issued
   uint64_t second_halves = 0;  // rounds whose exchange and aggregation are issued (or abandoned on an error)
@@ -1500,34 +1499,6 @@ struct HostWait {
   explicit HostWait(omr_ar_plan* pp);
   ~HostWait();
 };
-
-// The caller and the progress thread (OMR_ROUND_THREAD) hand each other work twice per round: a job, then its first
-// half issued.  Waking a thread that sleeps on a condition variable takes microseconds to tens of microseconds on a busy
-// host, so each side first spins, without the lock, on the plan's `epoch` (advanced by every notify) for up to
-// kHandoffSpin, as the reference's threads poll their completion queues, and sleeps only after that.
-constexpr auto kHandoffSpin = std::chrono::microseconds(200);
-void notify_job(omr_ar_plan* p) {
-  p->epoch.fetch_add(1, std::memory_order_release);
-  p->cv_job.notify_one();
-}
-void notify_done(omr_ar_plan* p) {
-  p->epoch.fetch_add(1, std::memory_order_release);
-  p->cv_done.notify_all();
-}
-template <typename Pred>
-void handoff_wait(omr_ar_plan* p, std::unique_lock<std::mutex>& lk, std::condition_variable& cv, Pred pred) {
-  const auto t0 = std::chrono::steady_clock::now();
-  while (!pred()) {
-    if (std::chrono::steady_clock::now() - t0 > kHandoffSpin) {
-      cv.wait(lk, pred);
-      return;
-    }
-    const uint64_t e = p->epoch.load(std::memory_order_acquire);
-    lk.unlock();
-    for (int i = 0; i < 1024 && p->epoch.load(std::memory_order_acquire) == e; ++i) __builtin_ia32_pause();
-    lk.lock();
-  }
-}
 
 // A round that had started failed: record it (first error wins) and abort the transport, so that no peer waits for
 // this rank's part of the round (the reference exits on a failed post, common.cc:450-451).  Returns rc.
@@ -2219,7 +2190,7 @@ int round_finish(omr_ar_plan* p, int si, int pki, const float* x, float* out, in
         std::lock_guard<std::mutex> g(p->mu);
         ++p->second_halves;
       }
-      notify_done(p);
+      p->cv_done.notify_all();
     }
   } count_half{p};
   omr_ar_plan::Set& S = p->set[si];
@@ -2550,7 +2521,7 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
     std::lock_guard<std::mutex> g(p->mu);
     ++p->first_halves;
   }
-  notify_done(p);
+  p->cv_done.notify_all();
   ht.lap("1:next+ready");
   (void)NS;
   // (a one-rank round's counts come on the caller's stream: the wait for them watches that stream)
@@ -2579,7 +2550,7 @@ void progress_main(omr_ar_plan* p) {
   (void)hipSetDevice(p->device);
   std::unique_lock<std::mutex> lk(p->mu);
   for (;;) {
-    handoff_wait(p, lk, p->cv_job, [&] { return p->stop || !p->jobs.empty(); });
+    p->cv_job.wait(lk, [&] { return p->stop || !p->jobs.empty(); });
     if (p->jobs.empty()) return;  // stop requested, nothing left
     const omr_ar_plan::Job j = p->jobs.front();
     p->jobs.pop_front();
@@ -2596,7 +2567,7 @@ void progress_main(omr_ar_plan* p) {
     }
     if (p->thread_rc != 0) p->first_halves = p->second_halves = p->rounds_begun;
     p->busy = false;
-    notify_done(p);
+    p->cv_done.notify_all();
   }
 }
 
@@ -2617,7 +2588,7 @@ int thread_drain(omr_ar_plan* p) {
   if (!p->progress.joinable()) return 0;
   HostWait hw(p);
   std::unique_lock<std::mutex> lk(p->mu);
-  handoff_wait(p, lk, p->cv_done, [&] { return p->jobs.empty() && !p->busy; });
+  p->cv_done.wait(lk, [&] { return p->jobs.empty() && !p->busy; });
   if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
   return 0;
 }
@@ -2628,7 +2599,7 @@ void thread_stop(omr_ar_plan* p) {
     std::lock_guard<std::mutex> g(p->mu);
     p->stop = true;
   }
-  notify_job(p);
+  p->cv_job.notify_one();
   p->progress.join();
 }
 
@@ -2732,7 +2703,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
       HostWait hw(p);
       std::unique_lock<std::mutex> lk(p->mu);
       const uint64_t need = p->rounds_begun >= static_cast<uint64_t>(p->nsets - 1) ? p->rounds_begun - (p->nsets - 1) : 0;
-      handoff_wait(p, lk, p->cv_done, [&] { return p->first_halves >= need || p->thread_rc != 0; });
+      p->cv_done.wait(lk, [&] { return p->first_halves >= need || p->thread_rc != 0; });
       if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
     }
     if (S.plan_pending) {
@@ -2749,7 +2720,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
       const uint64_t need = p->rounds_begun >= KP ? p->rounds_begun - (KP - 1) : 0;
       if (threaded) {
         HostWait hw(p);
-        handoff_wait(p, lk, p->cv_done, [&] { return p->second_halves >= need || p->thread_rc != 0; });
+        p->cv_done.wait(lk, [&] { return p->second_halves >= need || p->thread_rc != 0; });
       }
       if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
       const bool w = p->pk[pki].scan_wait;
@@ -2815,7 +2786,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
         p->second_halves = std::max(p->second_halves, p->rounds_begun);
       }
       if (tslot >= 0) p->timed[tslot].open = false;
-      notify_done(p);
+      p->cv_done.notify_all();
     }
     return rc;
   }
@@ -2826,7 +2797,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
     ++p->rounds_begun;
     p->jobs.push_back(j);
   }
-  notify_job(p);
+  p->cv_job.notify_one();
   return 0;
 }
 
