@@ -645,6 +645,10 @@ struct IpcDist final : omr_dist {
   uint64_t seq[kIpcChans] = {0, 0};
   IpcTrace trace;  // OMR_IPC_TRACE (diagnostic)
   void* canary = nullptr;  // exported at attach, freed once every peer has left
+  // the peers' canaries as mapped here, kept open (like every other mapping) until the transport goes: an imported
+  // range closed during the group's life comes back from a later hipMalloc, and ROCm then refuses to export that
+  // allocation (hipIpcGetMemHandle: invalid argument; 8 IPC ranks, profiles/r06/tests/)
+  std::vector<void*> canary_maps;
   // allocation (base, size) -> its handle and this rank's id for it.  The plans' exported allocations are never freed
   // while the transport lives (release() parks them), so an entry never outlives its allocation.  A
   // caller's buffer (an input or output tensor) must stay allocated while the transport lives, as omr_dist.h says.
@@ -739,6 +743,7 @@ struct IpcDist final : omr_dist {
                      timeout_ms, b, world) != 0)
           break;
       for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second.base);
+      for (void* m : canary_maps) (void)hipIpcCloseMemHandle(m);
     }
     // every peer has left (closed its mappings of them): the parked allocations can go now
     for (auto& kv : parked) (void)hipFree(kv.second);
@@ -859,8 +864,8 @@ struct IpcDist final : omr_dist {
       void* mp = nullptr;
       TRY(hip_check(hipIpcOpenMemHandle(&mp, b->rank[p].canary, hipIpcMemLazyEnablePeerAccess),
                     "hipIpcOpenMemHandle canary"));
+      canary_maps.push_back(mp);
       const hipError_t e = hipMemcpy(h.data(), mp, kCanaryRead * 8, hipMemcpyDeviceToHost);
-      (void)hipIpcCloseMemHandle(mp);
       TRY(hip_check(e, "hipMemcpy canary"));
       bool whole = true;  // every word read back where it was written: the handle opens at the exporter's address
       for (size_t i = 0; i < kCanaryRead && whole; ++i) whole = h[i] == canary_word(p, i);
@@ -2713,12 +2718,17 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
     // A fused-pack scan refills the round's send buffer: the round kPackBufs calls back, which read it (its exchange
     // issued up to kDeferDepth calls later, on the side stream), must be through first.  The progress thread may not
     // have issued it yet: wait until it has (at most one call behind then), then for it on the device.
+    // A one-rank group's send buffer is empty (no other shard: the scan packs nothing), so its scan waits for nothing:
+    // that wait put the tail of the exchange three rounds back (at world 1 over RCCL, its group's small kernels, run
+    // only once the previous scan's workgroups drain) between two scans, 8-10 us per round (profiles/r06/world1_general/
+    // trace/), and on the host for the progress thread.
     const bool pack_scan = p->fused_pack && p->worker() && mode != OMR_ROUND_DENSE_REDUCE_SCATTER;
+    const bool pack_wait = pack_scan && p->pack_floats > 0;
     if (pack_scan) {
       std::unique_lock<std::mutex> lk(p->mu);
       constexpr uint64_t KP = omr_ar_plan::kPackBufs;
       const uint64_t need = p->rounds_begun >= KP ? p->rounds_begun - (KP - 1) : 0;
-      if (threaded) {
+      if (threaded && pack_wait) {
         HostWait hw(p);
         p->cv_done.wait(lk, [&] { return p->second_halves >= need || p->thread_rc != 0; });
       }
@@ -2727,7 +2737,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
       const int ds = p->pk[pki].done_set;
       p->pk[pki].scan_wait = false;
       lk.unlock();
-      if (w) TRY(wait_ev(st, p->set[ds].done));
+      if (w && pack_wait) TRY(wait_ev(st, p->set[ds].done));
     }
     if (p->worker()) {
       if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));

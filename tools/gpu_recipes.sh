@@ -103,7 +103,7 @@ w1g_trace)
         > "$O/trace_$pipe.json" 2> "$O/trace_$pipe.err" ) || { echo "trace $pipe failed"; tail -20 "$O/trace_$pipe.err"; exit 1; }
   done
   step 300 pmc_w1g.log env RANK=0 LOCAL_RANK=0 WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=$((PORT++)) \
-    python3 tools/pmc_traffic.py --kernel k_scan1f --also k_round_plan,k_shard_sum_list --out "$O/pmc_w1g.json" \
+    python3 tools/pmc_traffic.py --kernel k_scan1f --also k_round_plan,k_shard_sum_list,__amd_rocclr_copyBuffer --out "$O/pmc_w1g.json" \
     --workdir "$O/pmc_w1g" -- --force-dist --world1-general --no-cpu --steps 20 --warmup 5
   ;;
 ipc_mix)

@@ -82,8 +82,12 @@ def main():
     }
     also = {}
     for k in [x for x in a.also.split(",") if x]:
-        fk, nfk = per_launch(fetch_csv, k, "FETCH_SIZE")
-        wk, nwk = per_launch(write_csv, k, "WRITE_SIZE")
+        try:
+            fk, nfk = per_launch(fetch_csv, k, "FETCH_SIZE")
+            wk, nwk = per_launch(write_csv, k, "WRITE_SIZE")
+        except SystemExit:  # (not launched in this run)
+            also[k] = None
+            continue
         also[k] = {"launches": {"fetch_pass": nfk, "write_pass": nwk}, "hbm_read_bytes_per_launch": 2 * fk * 1024,
                    "hbm_write_bytes_per_launch": wk * 1024, "hbm_bytes_per_launch": int(2 * fk * 1024 + wk * 1024)}
     if also:

@@ -8,6 +8,11 @@
 //   pinned1     1 workgroup, one system-scope 8-byte store into pinned host memory (the plan's counts)
 //   chain64     64 workgroups: a ticket atomic, one load, one agent-scope publish, a wait for the previous ticket's
 //               publish (the plan chunks' look-back, one link), one store
+//   spin           1024 x 256 workgroups that each spin 20 us on the wall clock (a stand-in for the worker scan: a full
+//                  chip for a fixed time), back to back
+//   spin+rec       the same with an event recorded after each launch (the round's `scanned` record, which the side
+//                  stream waits on: DisableTiming | DisableSystemFence)
+//   spin+rec+wait  and a second stream waiting on each record and running a one-wave kernel (the all-gather's start)
 // Every case: 200 launches back to back on one stream, timed with events (mean per launch), three interleaved passes;
 // run under `rocprofv3 --kernel-trace --stats` for the kernels' own durations.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/bin/launch_floor tools/tune/launch_floor.hip && tools/bin/launch_floor
@@ -28,6 +33,11 @@
 
 __global__ __launch_bounds__(256) void k_empty(uint64_t* sink) {
   if (sink != nullptr && threadIdx.x == 0 && blockIdx.x == 0xFFFFFFFFu) sink[0] = 1;  // never taken
+}
+
+__global__ __launch_bounds__(256) void k_spin(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
 }
 
 __global__ __launch_bounds__(256) void k_touch(const uint64_t* src, uint64_t* dst) {
@@ -79,17 +89,31 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   uint32_t seq = 0;
-  const char* names[] = {"empty1", "empty577", "touch577", "pinned1", "chain64"};
-  double sum[5] = {0, 0, 0, 0, 0};
+  const char* names[] = {"empty1", "empty577", "touch577", "pinned1", "chain64", "spin", "spin+rec", "spin+rec+wait"};
+  constexpr int kCases = 8;
+  double sum[kCases] = {};
+  hipStream_t side;
+  CK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+  hipEvent_t rec;
+  CK(hipEventCreateWithFlags(&rec, hipEventDisableTiming | hipEventDisableSystemFence));
+  const uint64_t spin_ticks = 2000;  // 20 us at the wall clock's 100 MHz
   for (int pass = 0; pass < 3; ++pass) {
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < kCases; ++k) {
       auto launch = [&]() {
         switch (k) {
           case 0: k_empty<<<1, 64, 0, st>>>(nullptr); break;
           case 1: k_empty<<<577, 256, 0, st>>>(nullptr); break;
           case 2: k_touch<<<577, 256, 0, st>>>(src, dst); break;
           case 3: k_pinned<<<1, 64, 0, st>>>(host_d, ++seq); break;
-          default: k_chain<<<64, 256, 0, st>>>(ws, src, dst, ++seq == 0 ? ++seq : seq); break;
+          case 4: k_chain<<<64, 256, 0, st>>>(ws, src, dst, ++seq == 0 ? ++seq : seq); break;
+          default:
+            k_spin<<<1024, 256, 0, st>>>(spin_ticks);
+            if (k >= 6) CK(hipEventRecord(rec, st));
+            if (k == 7) {
+              CK(hipStreamWaitEvent(side, rec, 0));
+              k_empty<<<1, 64, 0, side>>>(nullptr);
+            }
+            break;
         }
       };
       for (int i = 0; i < 10; ++i) launch();
@@ -103,10 +127,11 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       const double us = 1000.0 * ms / reps;
       sum[k] += us;
-      printf("pass %d %-9s %7.2f us per launch (events over %d back to back)\n", pass, names[k], us, reps);
+      printf("pass %d %-13s %7.2f us per launch (events over %d back to back)\n", pass, names[k], us, reps);
     }
   }
-  for (int k = 0; k < 5; ++k) printf("mean %-9s %7.2f us\n", names[k], sum[k] / 3);
+  for (int k = 0; k < kCases; ++k) printf("mean %-13s %7.2f us\n", names[k], sum[k] / 3);
+  CK(hipStreamSynchronize(side));
   CK(hipStreamSynchronize(st));
   return 0;
 }
