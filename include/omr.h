@@ -234,16 +234,21 @@ int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, 
  * uint64[omr_round_check_slots()], or NULL: none): workgroup b also stores check_slots[b] = (check_seq << 32) | the
  * non-zero blocks it found, i.e. the number of row-mask bits it set.  Put in the array the round all-gathers (after
  * the masks and position table), they let the plan launch check on the device that each worker's gathered array is
- * the one its scan of THIS round wrote (omr_round_plan_check). */
+ * the one its scan of THIS round wrote (omr_round_plan_check).
+ * done (device uint32[2], or NULL): the launch's completion, signalled on the device.  done[0] must be zero before the
+ * first launch (each launch leaves it zero); the launch's last workgroup to finish stores check_seq (nonzero) into
+ * done[1] after every workgroup's stores are visible at device scope, so work on another stream may wait for the word
+ * (e.g. a kernel polling done[1] - seq >= 0 as int32) instead of for an event recorded behind the scan. */
 uint32_t omr_round_check_slots(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts);
 int omr_worker_scan_check_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
                               int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out, void* workspace,
-                              size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq, omr_stream_t stream);
+                              size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq, uint32_t* done,
+                              omr_stream_t stream);
 int omr_worker_scan_pack_check_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes,
                                    uint32_t num_parts, int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks,
                                    float* out, const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard,
                                    float* send, uint32_t* shard_counters, uint32_t* pos_table, void* workspace,
-                                   size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq,
+                                   size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq, uint32_t* done,
                                    omr_stream_t stream);
 /* The one-rank round's worker scan (a world-1 group: one worker, one aggregator; server.cc:83-96 with one worker:
  * the union is the worker's own blocks and min_next its own chain, so the aggregator's bookkeeping is two counts).
@@ -293,7 +298,8 @@ uint64_t omr_pack_send_offset(const uint64_t* shard_bounds, uint32_t num_shards,
  * multi-rank round's, skipping 0 when it wraps): chunk totals are tagged, never cleared, so a launch with an earlier
  * launch's seq could take that launch's stale totals for chunks it has more of.  Row chunks of the launch
  * run side by side and hand each other their popcount totals through the workspace (ABI 2; ABI 1 took an arrival
- * counter). */
+ * counter); the round check (omr_round_plan_check) hands the last chunk its findings there too (1106 words since
+ * round 6). */
 uint64_t omr_round_plan_workspace_words(void);
 int omr_round_plan(const uint64_t* row_masks, uint32_t count, uint64_t rows, uint32_t rows_per_part,
                    uint32_t num_lanes, const uint64_t* bounds, uint32_t num_bounds, uint64_t* write_set,

@@ -1437,6 +1437,7 @@ struct omr_ar_plan {
     int si = 0, mode = 0, tslot = -1, pki = 0;
     uint32_t seq = 0;  // a one-rank round's sequence number (taken when its scan was issued)
     bool async = false, defer = false, timed = false, flush_first = false;
+    bool signal = false;  // the scan signals its completion in scan_done (no `scanned` record)
     const float* x = nullptr;
     float* out = nullptr;
     uint32_t* un = nullptr;
@@ -1484,6 +1485,9 @@ struct omr_ar_plan {
   hipStream_t seated_st = nullptr;
   bool seated = false;
   int q_disjoint = -1, q_probes = 0, q_replaced = 0;
+  // the worker scan's completion word (omr_worker_scan_check_f32's `done`): {workgroups out, seq of the last scan
+  // that finished}; the side stream waits on it with k_wait_seq where the side streams are checked apart (scan_signal)
+  uint32_t* scan_done = nullptr;
   uint32_t* qflags_host = nullptr;  // pinned: {hold running, release, mark}
   uint32_t* qflags_dev = nullptr;
 };
@@ -1585,6 +1589,19 @@ __global__ void k_queue_hold(uint32_t* flags, uint64_t max_ticks) {
 
 __global__ void k_queue_mark(uint32_t* flags) {
   if (threadIdx.x == 0) __hip_atomic_store(&flags[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The side stream's wait for a worker scan that signals its completion (omr_worker_scan_check_f32's `done`): one wave
+// polls done[1] until it has reached `seq` (as int32: the word only moves forward, and a later scan may already have
+// moved it on).  Bounded: after max_ticks of the wall clock it ends anyway and the round goes on, and the round check
+// then fails the round on the stale masks (OMR_ESTALE) instead of the GPU hanging on a scan that never runs.
+constexpr uint64_t kScanWaitTicks = 2ull * 1000 * 1000 * 100;  // 2 s at 100 MHz
+__global__ void k_wait_seq(const uint32_t* done, uint32_t seq, uint64_t max_ticks) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = wall_clock64();
+  while (static_cast<int32_t>(__hip_atomic_load(&done[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0 &&
+         wall_clock64() - t0 < max_ticks)
+    __builtin_amdgcn_s_sleep(2);
 }
 
 // *disjoint = work queued on b runs while a's hardware queue is held (so a and b are on different queues).  Work
@@ -1877,7 +1894,7 @@ int omr_ar_plan_destroy(omr_ar_plan* p) {
     }
   }
   // back to the transport, which keeps the exported ones alive for the next plan (omr_dist::alloc)
-  void* devs[] = {p->bounds_dev, p->results, p->flags_ws, p->next_ws, p->scan_ws, p->recv, p->tally};
+  void* devs[] = {p->bounds_dev, p->results, p->flags_ws, p->next_ws, p->scan_ws, p->recv, p->tally, p->scan_done};
   for (void* v : devs) p->d->release(v);
   for (auto& b : p->pk) p->d->release(b.buf);
   for (auto& st : p->set) {
@@ -2017,6 +2034,7 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
   if (p->shard >= 0) A(dev_alloc(p->d, &p->results, p->shard_nb * block_size, DB));
   A(dev_alloc(p->d, &p->flags_ws, p->nb, DB));
   A(dev_alloc(p->d, &p->next_ws, p->nb, DB));
+  A(dev_alloc(p->d, &p->scan_done, 2, DB));
   p->scan_ws_bytes = omr_scan_workspace_bytes(n, block_size, num_lanes, num_parts);
   A(dev_alloc(p->d, reinterpret_cast<char**>(&p->scan_ws), p->scan_ws_bytes, DB));
   p->tally_slots = omr_tally_slots(n, block_size, num_lanes, num_parts);
@@ -2059,6 +2077,7 @@ int omr_ar_plan_create_roles(omr_dist* d, uint32_t num_workers, uint64_t n, uint
     if (rc == 0 && st.pack_cnt) A(hip_check(hipMemset(st.pack_cnt, 0, NA * sizeof(uint32_t)), "hipMemset pack counters"));
   }
   if (rc == 0 && p->scan_ws_bytes) A(hip_check(hipMemset(p->scan_ws, 0, p->scan_ws_bytes), "hipMemset scan ws"));
+  if (rc == 0) A(hip_check(hipMemset(p->scan_done, 0, 2 * sizeof(uint32_t)), "hipMemset scan done"));
   if (rc == 0)
     A(hip_check(hipMemcpy(p->bounds_dev, p->bounds.data(), (NA + 1) * sizeof(uint64_t), hipMemcpyHostToDevice),
                 "hipMemcpy bounds"));
@@ -2460,7 +2479,12 @@ int round_rest(omr_ar_plan* p, const omr_ar_plan::Job& j, uint64_t* sent_blocks,
     // the one-launch round: the scan tallied the bookkeeping (omr_worker_scan_tally_f32); nothing runs after it
     seq = j.seq;
   } else {
-    if (async) TRY(order_after(p, qs, S.scanned, "round: the worker scan"));
+    if (async && j.signal) {
+      k_wait_seq<<<1, 64, 0, qs>>>(p->scan_done, j.seq, kScanWaitTicks);
+      TRY(hip_check(hipGetLastError(), "k_wait_seq"));
+    } else if (async) {
+      TRY(order_after(p, qs, S.scanned, "round: the worker scan"));
+    }
     // the rest of the set is refilled from here on: the round kSets calls back must be through with it (on the side
     // stream, in stream order already)
     if (S.pending) {
@@ -2677,6 +2701,7 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
   int tslot = -1;
   if (timed) TRY(timed_slot(p, &tslot));
   uint32_t solo_seq = 0;
+  bool signal = false;  // (below: the scan signals its completion on the device)
   if (tally) {
     if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
     // the previous one-rank round's counts go out with this scan's extra workgroup (on its own stream if it was
@@ -2739,6 +2764,12 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
       lk.unlock();
       if (w && pack_wait) TRY(wait_ev(st, p->set[ds].done));
     }
+    // An asynchronous round's side stream starts behind the scan.  Where the side streams are checked to run on queues
+    // apart from the caller's, the scan signals its own completion on the device (scan_done) and the side stream
+    // waits for that with a one-wave kernel, so nothing is queued on the caller's stream between two scans; elsewhere
+    // (and for a bucket's scan, or a rank with nothing to scan) an event recorded behind the scan.
+    signal = async && p->worker() && p->seated && p->seated_st == st && p->q_disjoint == 1 && !p->in_buckets &&
+             p->scan_from == nullptr;
     if (p->worker()) {
       if (timed) TRY(hip_check(hipEventRecord(p->timed[tslot].s0, st), "hipEventRecord"));
       const float* src = p->scan_from ? p->scan_from : x;
@@ -2751,11 +2782,13 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
                                                      p->bounds.data(), static_cast<uint32_t>(p->A),
                                                      p->colocated ? me_shard(p) : -1, p->pk[pki].buf, S.pack_cnt,
                                                      reinterpret_cast<uint32_t*>(S.own + p->rows), p->scan_ws,
-                                                     p->scan_ws_bytes, chk, solo_seq, stream),
+                                                     p->scan_ws_bytes, chk, solo_seq,
+                                                     signal ? p->scan_done : nullptr, stream),
                       "omr_worker_scan_pack_check_f32"));
       else
         TRY(omr_check(omr_worker_scan_check_f32(src, p->n, p->B, p->lanes, p->parts, fl, nx, S.own, sout, p->scan_ws,
-                                                p->scan_ws_bytes, chk, solo_seq, stream),
+                                                p->scan_ws_bytes, chk, solo_seq, signal ? p->scan_done : nullptr,
+                                                stream),
                       "omr_worker_scan_check_f32"));
       if (timed) {
         TRY(hip_check(hipEventRecord(p->timed[tslot].s1, st), "hipEventRecord"));
@@ -2764,13 +2797,14 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
       p->ht.lap("1:scan");
     }
     // (a dedicated aggregator has nothing to scan: the side stream starts behind whatever the caller queued)
-    if (async) TRY(hip_check(hipEventRecord(S.scanned, st), "hipEventRecord"));
+    if (async && !signal) TRY(hip_check(hipEventRecord(S.scanned, st), "hipEventRecord"));
   }
   p->ht.lap("1:scan events");
   omr_ar_plan::Job j;
   j.si = si;
   j.pki = pki;
   j.seq = solo_seq;
+  j.signal = signal;
   j.mode = mode | (solo ? kModeSolo : 0) | (tally ? kModeTally : 0);
   j.tslot = tslot;
   j.async = async;

@@ -265,6 +265,37 @@ struct FusedArgs {
   // blocks, the count its row-mask bits must add up to; the plan launch checks every worker's (omr_round_plan_check)
   uint64_t* chk;
   uint32_t chk_seq;
+  // ... and the launch's completion (round 6): done[0] counts workgroups out (zero between launches), the last one
+  // stores chk_seq into done[1]; null: no signal
+  uint32_t* done;
+};
+
+// CHK: the launch's completion signalled on the device.  Every workgroup counts itself out at its end and the last one
+// stores the launch's seq into done[1] (and re-arms the counter).  The multi-rank round's side stream waits for that
+// word with a one-wave kernel (omr_dist.hip k_wait_seq) instead of for an event recorded on the caller's stream after
+// the scan: such a record sits between two scans, and a record with a waiter on another queue costs the next kernel
+// about 2.7 us (tools/tune/launch_floor.hip, profiles/r06/round_kernels/launch_floor.log).  What the side stream reads
+// before the launch ends -- the row masks (device-scope atomics), the position table and the check slots (stored
+// through to memory, sc1), the packed blocks (write-through) -- is at the coherence point once the workgroup's stores
+// are acknowledged (s_waitcnt vmcnt(0)), so no workgroup writes its L2 back: an agent-scope release fence per
+// workgroup (buffer_wbl2) took the scan from 50 to 99 us per round.
+template <bool ON>
+struct ScanDone {
+  const FusedArgs& a;
+  __device__ ~ScanDone() {
+    if constexpr (ON) {
+      if (a.done == nullptr) return;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores and atomics acknowledged
+      __syncthreads();                                   // (every exit of k_scan1f is workgroup-uniform)
+      if (threadIdx.x == 0) {
+        const uint32_t n = __hip_atomic_fetch_add(&a.done[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n + 1 == gridDim.x) {
+          __hip_atomic_store(&a.done[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&a.done[1], a.chk_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
 };
 
 // The one-rank round's counts, from an earlier launch's slots, one wave: lane i sums slots i, i + 64, ... (loaded by
@@ -319,6 +350,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(TALL
   __shared__ uint32_t s_base, s_total;
   __shared__ uint32_t s_wnz[CHK ? WAVES : 1];
   [[maybe_unused]] uint32_t nzc = 0;  // CHK: the wave's non-zero blocks (wave-uniform)
+  const ScanDone<CHK> scan_done{a};   // (signals at whichever exit the workgroup takes)
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t T = gridDim.x, bid = blockIdx.x;
@@ -455,7 +487,9 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(TALL
     if (threadIdx.x == 0 && a.chk != nullptr) {
       uint32_t t = 0;
       for (uint32_t w2 = 0; w2 < WAVES; ++w2) t += s_wnz[w2];
-      a.chk[bid] = (static_cast<uint64_t>(a.chk_seq) << 32) | t;
+      // (stored through to memory, sc1: with a completion word the side stream reads it before this launch ends)
+      __hip_atomic_store(&a.chk[bid], (static_cast<uint64_t>(a.chk_seq) << 32) | t, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if constexpr (TALLY) {  // the one-rank round's bookkeeping: one slot store per workgroup, no atomic
@@ -501,7 +535,8 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(TALL
         for (uint32_t j = threadIdx.x; j < a.gps; j += 64 * WAVES) {
           uint32_t c = 0;
           for (uint32_t wd = 0; wd < j * (kPackGroupRows / 32); ++wd) c += static_cast<uint32_t>(__builtin_popcount(s_bits[wd]));
-          a.pos[(seg * a.gps + j) * a.lanes + l] = base + c;
+          __hip_atomic_store(&a.pos[(seg * a.gps + j) * a.lanes + l], base + c, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);  // (through to memory: read before the launch ends, as chk)
         }
         // the wave's blocks: its range's non-zero rows take stream places base + s_wpre[wave] + (rank among them)
         float* const sbase = a.send + static_cast<uint64_t>(a.send_row[shard]) * row_stride;
@@ -1272,7 +1307,11 @@ constexpr uint32_t kPlanThreads = 256;
 constexpr uint32_t kPlanWaves = kPlanThreads / 64;
 constexpr uint32_t kPlanChunksMax = 64;
 constexpr uint32_t kPlanArrays = OMR_MAX_WORKERS + 1;
-constexpr uint64_t kPlanWorkspaceWords = 1 + static_cast<uint64_t>(kPlanChunksMax) * kPlanArrays;
+// ... then the round check's findings (plan_check): per worker the sum of its scan's slots, and the lowest stale worker,
+// tagged with seq, which the last chunk compares with its totals
+constexpr uint64_t kPlanCheckWords = 1 + static_cast<uint64_t>(kPlanChunksMax) * kPlanArrays;
+constexpr uint64_t kPlanWorkspaceWords = kPlanCheckWords + OMR_MAX_WORKERS + 1;
+constexpr uint32_t kCheckStale = 0x100u, kCheckCount = 0x200u;
 
 template <int W>
 __device__ __forceinline__ void plan_chunk(const PlanArgs& a) {
@@ -1416,49 +1455,73 @@ __device__ __forceinline__ void plan_chunk(const PlanArgs& a) {
       if (s_bounds[s] >= a.rows)
         __hip_atomic_store(&a.counts[arr * a.nbounds + s], tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  // the round check's verdict (the last chunk: it holds every worker's mask total), from the check workgroup's findings
+  if (c + 1 == a.nchunks && a.chk_status != nullptr) {
+    __shared__ uint32_t s_bad, s_stale;
+    if (t == 0) s_bad = OMR_MAX_WORKERS;
+    __syncthreads();
+    if (t <= cnt) {  // threads < cnt: worker t's slot sum; thread cnt: the lowest stale worker
+      uint64_t v;
+      while (((v = __hip_atomic_load(&a.ws[kPlanCheckWords + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) !=
+             a.seq)
+        __builtin_amdgcn_s_sleep(2);
+      uint32_t total = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < static_cast<uint32_t>(W); ++k) total = k == t ? carry[k] : total;
+      if (t == cnt) s_stale = static_cast<uint32_t>(v);
+      else if (static_cast<uint32_t>(v) != total) (void)atomicMin(&s_bad, t);
+    }
+    __syncthreads();
+    if (t == 0) {
+      const uint32_t code = s_stale < OMR_MAX_WORKERS ? (kCheckStale | s_stale)
+                                                      : (s_bad < OMR_MAX_WORKERS ? (kCheckCount | s_bad) : 0u);
+      __hip_atomic_store(a.chk_status, tag | code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // The round check (round 6): is every worker's all-gathered mask array the one its scan of THIS round
-// wrote?  Each of the worker's scan workgroups left a slot (seq << 32) | its non-zero blocks in the array; the check
-// reads them all and the chunks' popcount totals of the worker's masks (plan_chunk step 3, tagged with seq).  A slot of
-// another round means the copy read the worker's buffer before its scan wrote the slot (or read another buffer); a
-// count sum above the masks' popcount means the copy read masks its scan had not finished (a mask array only gains
-// bits between the plan that zeroes it and the scan that refills it, so a copy that overtakes its producer always
-// reads too few).  Status (one system-scope store beside the counts): (seq << 32) | 0, or | 0x100 + worker for a
-// stale slot, | 0x200 + worker for a count mismatch.  The round's host fails the round on it, by name, instead of
-// relying on the exchange's size check.
-constexpr uint32_t kCheckStale = 0x100u, kCheckCount = 0x200u;
-
+// wrote?  Each of the worker's scan workgroups left a slot (seq << 32) | its non-zero blocks in the array.  One more
+// workgroup of the plan launch (plan_check) reads them all and publishes, tagged with seq, each worker's slot sum and the
+// lowest worker with a slot of another round; the last chunk, which holds every worker's mask popcount total, compares
+// them (plan_chunk's end) and stores the status beside the counts: (seq << 32) | 0, | 0x100 + worker for a stale slot
+// (the copy read the worker's buffer before its scan wrote the slot, or another buffer), | 0x200 + worker when the slot
+// sum differs from the masks' popcount (a copy that overtook its producer: a mask array only gains bits between the plan
+// that zeroes it and the scan that refills it, so it reads too few).  The round's host fails the round on it, by name,
+// instead of relying on the exchange's size check.  (The first form had the check workgroup wait for the chunks' totals
+// and add its slots with a shared-memory atomic each: 6 us more than the plan; profiles/r06/INDEX.md.)
 template <int W>
 __device__ __forceinline__ void plan_check(const PlanArgs& a) {
-  // every slot is loaded in one or two batches of U per thread; each thread keeps its own per-worker sums and its
-  // lowest stale worker in registers and the waves reduce them once (a shared-memory atomic per slot, all lanes of a
-  // wave on one worker's address, serialised 64 ways: 7 us at config 4's 4096 slots, profiles/r06/INDEX.md)
   __shared__ uint32_t s_sum[kPlanWaves][W];
-  __shared__ uint32_t s_stale, s_bad;  // the lowest worker found (OMR_MAX_WORKERS: none)
+  __shared__ uint32_t s_stale;  // the lowest stale worker (OMR_MAX_WORKERS: none)
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  if (t == 0) s_stale = s_bad = OMR_MAX_WORKERS;
+  if (t == 0) s_stale = OMR_MAX_WORKERS;
   const uint32_t ns = a.chk_slots, words = a.count * ns;
+  const float inv_ns = 1.0f / static_cast<float>(ns);
+  auto worker_of = [&](uint32_t idx) {  // idx / ns without an integer division (the quotient is < 17: exact after a fix)
+    uint32_t c = static_cast<uint32_t>(static_cast<float>(idx) * inv_ns);
+    c = c * ns > idx ? c - 1 : c;
+    return (c + 1) * ns <= idx ? c + 1 : c;
+  };
   constexpr uint32_t U = 16;  // loads in flight per thread
   uint32_t sum[W], stale = OMR_MAX_WORKERS;
 #pragma unroll
   for (int k = 0; k < W; ++k) sum[k] = 0;
   for (uint32_t base = 0; base < words; base += kPlanThreads * U) {
     uint64_t v[U];
+    uint32_t cw[U];
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) {
       const uint32_t idx = base + i * kPlanThreads + t;
-      const uint32_t c = idx / ns;
-      v[i] = idx < words ? a.masks[static_cast<uint64_t>(c) * a.mstride + a.chk_off + (idx - c * ns)] : 0ull;
+      cw[i] = idx < words ? worker_of(idx) : OMR_MAX_WORKERS;
+      v[i] = idx < words ? a.masks[static_cast<uint64_t>(cw[i]) * a.mstride + a.chk_off + (idx - cw[i] * ns)] : 0ull;
     }
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) {
-      const uint32_t idx = base + i * kPlanThreads + t;
-      if (idx >= words) continue;
-      const uint32_t c = idx / ns;
-      if (static_cast<uint32_t>(v[i] >> 32) != a.seq) stale = min(stale, c);
+      if (cw[i] == OMR_MAX_WORKERS) continue;
+      if (static_cast<uint32_t>(v[i] >> 32) != a.seq) stale = min(stale, cw[i]);
 #pragma unroll
-      for (int k = 0; k < W; ++k) sum[k] += c == static_cast<uint32_t>(k) ? static_cast<uint32_t>(v[i]) : 0u;
+      for (int k = 0; k < W; ++k) sum[k] += cw[i] == static_cast<uint32_t>(k) ? static_cast<uint32_t>(v[i]) : 0u;
     }
   }
 #pragma unroll
@@ -1468,27 +1531,17 @@ __device__ __forceinline__ void plan_check(const PlanArgs& a) {
   }
   __syncthreads();  // (s_stale initialised, s_sum filled)
   if (stale < OMR_MAX_WORKERS) (void)atomicMin(&s_stale, stale);
-  if (t < a.count) {  // the worker's mask total: the chunks' tagged totals of its array
-    uint32_t tot = 0, got = 0;
-    for (uint32_t i = 0; i < a.nchunks; ++i) {
-      uint64_t v;
-      while (((v = __hip_atomic_load(&a.ws[1 + static_cast<uint64_t>(i) * (W + 1) + t], __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT)) >> 32) != a.seq)
-        __builtin_amdgcn_s_sleep(1);
-      tot += static_cast<uint32_t>(v);
-    }
+  __syncthreads();
+  const uint64_t tag = static_cast<uint64_t>(a.seq) << 32;
+  if (t < a.count) {
+    uint32_t got = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kPlanWaves; ++w)
 #pragma unroll
       for (int k = 0; k < W; ++k) got += t == static_cast<uint32_t>(k) ? s_sum[w][k] : 0u;
-    if (tot != got) (void)atomicMin(&s_bad, t);
-  }
-  __syncthreads();
-  if (t == 0) {
-    const uint32_t code = s_stale < OMR_MAX_WORKERS ? (kCheckStale | s_stale)
-                                                    : (s_bad < OMR_MAX_WORKERS ? (kCheckCount | s_bad) : 0u);
-    __hip_atomic_store(a.chk_status, (static_cast<uint64_t>(a.seq) << 32) | code, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&a.ws[kPlanCheckWords + t], tag | got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (t == a.count) {
+    __hip_atomic_store(&a.ws[kPlanCheckWords + t], tag | s_stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2074,11 +2127,12 @@ struct TallySpec {
 int launch_fused(const Layout& L, const FusedShape& f, const float* x, float* out, int32_t* flags, uint32_t* next,
                  void* ws, hipStream_t st, uint64_t* masks = nullptr, uint32_t part_begin = 0,
                  uint32_t part_count = 0, const PackSpec* pk = nullptr, const TallySpec* tl = nullptr,
-                 uint64_t* chk = nullptr, uint32_t chk_seq = 0) {
+                 uint64_t* chk = nullptr, uint32_t chk_seq = 0, uint32_t* done = nullptr) {
   if (part_count == 0) part_count = L.parts - part_begin;
   FusedArgs a{};
   a.chk = chk;
   a.chk_seq = chk_seq;
+  a.done = done;
   a.part0 = part_begin;
   a.x = x;
   a.out = out;
@@ -2646,7 +2700,7 @@ int omr_worker_scan_f32(const float* buf, uint64_t n, uint32_t block_size, uint3
                         int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out, void* workspace,
                         size_t workspace_bytes, omr_stream_t stream) {
   return omr_worker_scan_check_f32(buf, n, block_size, num_lanes, num_parts, flags, next_offsets, row_masks, out,
-                                   workspace, workspace_bytes, nullptr, 0, stream);
+                                   workspace, workspace_bytes, nullptr, 0, nullptr, stream);
 }
 
 uint32_t omr_round_check_slots(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts) {
@@ -2657,7 +2711,8 @@ uint32_t omr_round_check_slots(uint64_t n, uint32_t block_size, uint32_t num_lan
 
 int omr_worker_scan_check_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
                               int32_t* flags, uint32_t* next_offsets, uint64_t* row_masks, float* out, void* workspace,
-                              size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq, omr_stream_t stream) {
+                              size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq, uint32_t* done,
+                              omr_stream_t stream) {
   Layout L;
   if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
   if (buf == nullptr || next_offsets == nullptr || row_masks == nullptr)
@@ -2668,8 +2723,9 @@ int omr_worker_scan_check_f32(const float* buf, uint64_t n, uint32_t block_size,
   const size_t need = fused_workspace_bytes(L, f);
   if (need > 0 && (workspace == nullptr || workspace_bytes < need))
     return fail("worker_scan: needs a zero-initialised workspace of %zu bytes", need);
+  if (done != nullptr && check_seq == 0) return fail("worker_scan: a completion word needs a nonzero seq");
   return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks, 0, 0,
-                      nullptr, nullptr, check_slots, check_seq);
+                      nullptr, nullptr, check_slots, check_seq, done);
 }
 
 int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts,
@@ -2679,7 +2735,7 @@ int omr_worker_scan_pack_f32(const float* buf, uint64_t n, uint32_t block_size, 
                              omr_stream_t stream) {
   return omr_worker_scan_pack_check_f32(buf, n, block_size, num_lanes, num_parts, flags, next_offsets, row_masks, out,
                                         shard_bounds, num_shards, own_shard, send, shard_counters, pos_table, workspace,
-                                        workspace_bytes, nullptr, 0, stream);
+                                        workspace_bytes, nullptr, 0, nullptr, stream);
 }
 
 int omr_worker_scan_pack_check_f32(const float* buf, uint64_t n, uint32_t block_size, uint32_t num_lanes,
@@ -2687,7 +2743,7 @@ int omr_worker_scan_pack_check_f32(const float* buf, uint64_t n, uint32_t block_
                                    float* out, const uint64_t* shard_bounds, uint32_t num_shards, int32_t own_shard,
                                    float* send, uint32_t* shard_counters, uint32_t* pos_table, void* workspace,
                                    size_t workspace_bytes, uint64_t* check_slots, uint32_t check_seq,
-                                   omr_stream_t stream) {
+                                   uint32_t* done, omr_stream_t stream) {
   Layout L;
   if (int rc = make_layout(n, block_size, num_lanes, num_parts, &L)) return rc;
   if (buf == nullptr || next_offsets == nullptr || row_masks == nullptr || send == nullptr ||
@@ -2704,8 +2760,9 @@ int omr_worker_scan_pack_check_f32(const float* buf, uint64_t n, uint32_t block_
   if (need > 0 && (workspace == nullptr || workspace_bytes < need))
     return fail("worker_scan_pack: needs a zero-initialised workspace of %zu bytes", need);
   const PackSpec pk{send, shard_counters, pos_table, shard_bounds, num_shards, own_shard};
+  if (done != nullptr && check_seq == 0) return fail("worker_scan_pack: a completion word needs a nonzero seq");
   return launch_fused(L, f, buf, out, flags, next_offsets, need ? workspace : nullptr, S(stream), row_masks, 0, 0, &pk,
-                      nullptr, check_slots, check_seq);
+                      nullptr, check_slots, check_seq, done);
 }
 
 uint32_t omr_tally_slots(uint64_t n, uint32_t block_size, uint32_t num_lanes, uint32_t num_parts) {

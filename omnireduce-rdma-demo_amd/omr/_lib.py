@@ -73,9 +73,10 @@ SIGNATURES = {
     "omr_shard_sum_stride_f32": (c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u64, c_u32, c_vp, c_vp, c_u64, c_u64, c_u64,
                                          c_u32, c_u32, c_int, c_vp, c_vp]),
     "omr_worker_scan_check_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_size,
-                                          c_vp, c_u32, c_vp]),
+                                          c_vp, c_u32, c_vp, c_vp]),
     "omr_worker_scan_pack_check_f32": (c_int, [c_vp, c_u64, c_u32, c_u32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_u32,
-                                               ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp, c_u32, c_vp]),
+                                               ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_size, c_vp, c_u32, c_vp,
+                                               c_vp]),
     "omr_round_plan_check": (c_int, [c_vp, c_u32, c_u64, c_u64, c_u32, c_u32, c_vp, c_u32, c_vp, c_vp, c_vp, c_vp,
                                      c_vp, c_vp, c_u32, c_vp, c_u32, c_vp, c_u32, c_vp, c_u64, c_u32, c_vp, c_vp]),
     "omr_sum_list_geometry": (c_int, [c_u64, c_u32, c_u32, c_u32, c_u64, c_u64, c_u32, c_vp, c_vp]),

@@ -153,10 +153,11 @@ def test_pack_send_offset(world, own):
 
 
 def test_round_plan_workspace_and_validation():
-    """The row-chunk plan's workspace size (one ticket word + 64 chunks x 17 tagged totals), and its argument checks,
+    """The row-chunk plan's workspace size (one ticket word + 64 chunks x 17 tagged totals + the round check's 17
+    tagged findings), and its argument checks,
     which return before any launch: seq 0 (a zero-filled word carries it), count 0, a NULL workspace."""
     lib = _lib.load()
-    assert lib.omr_round_plan_workspace_words() == 1 + 64 * 17
+    assert lib.omr_round_plan_workspace_words() == 1 + 64 * 17 + 17
     fake = ctypes.c_void_p(0x1000)  # (never dereferenced: the checks come first)
     args = lambda count, ws, seq: (fake, count, 4096, 512, 64, fake, 9, fake, None, fake, fake, None, ws, seq, None)  # noqa: E731
     assert lib.omr_round_plan(*args(8, fake, 0)) == _lib.OMR_EINVAL

@@ -320,7 +320,8 @@ def test_shard_sum(gpu, count, me, B, packed_out, span):
                                               (8 << 20, 256, 0.3, True), (64 << 20, 256, 0.095, True)])
 def test_round_check_slots(gpu, n, B, density, pack):
     """omr_worker_scan_check_f32 / omr_worker_scan_pack_check_f32: one slot per scan workgroup, (seq << 32) | its
-    non-zero blocks; the slots add up to the masks' popcount, the oracle's non-zero block count."""
+    non-zero blocks; the slots add up to the masks' popcount, the oracle's non-zero block count.  The completion word:
+    done[1] = seq after each launch, done[0] back at zero."""
     L = Layout(n=n, block_size=B)
     x = oracle.fill(oracle.gen_bitmap(4, density, L.nb), B, mode=1, seed=9)
     f = oracle.flags_from_data(x, B)
@@ -334,6 +335,7 @@ def test_round_check_slots(gpu, n, B, density, pack):
     slots = torch.zeros(ns, dtype=torch.int64, device=gpu)
     wsb = lib.omr_scan_workspace_bytes(L.n, B, L.num_lanes, L.num_threads)
     ws = torch.zeros(max(wsb, 16), dtype=torch.uint8, device=gpu)
+    done = torch.zeros(2, dtype=torch.int32, device=gpu)
     for seq in (7, 8):
         masks.zero_()
         if pack:
@@ -345,12 +347,13 @@ def test_round_check_slots(gpu, n, B, density, pack):
             pos = torch.zeros(int(ent.value), dtype=torch.int32, device=gpu)
             rc = lib.omr_worker_scan_pack_check_f32(P(xd), L.n, B, L.num_lanes, L.num_threads, P(flags), P(nxt),
                                                     P(masks), None, bounds.ctypes.data, 2, 0, P(send), P(cnt), P(pos),
-                                                    P(ws), wsb, P(slots), seq, stream())
+                                                    P(ws), wsb, P(slots), seq, P(done), stream())
         else:
             rc = lib.omr_worker_scan_check_f32(P(xd), L.n, B, L.num_lanes, L.num_threads, P(flags), P(nxt), P(masks),
-                                               None, P(ws), wsb, P(slots), seq, stream())
+                                               None, P(ws), wsb, P(slots), seq, P(done), stream())
         assert rc == 0, lib.omr_last_error()
         torch.cuda.synchronize()
+        assert done.cpu().tolist() == [0, seq]
         s = slots.cpu().numpy().view(np.uint64)
         assert ((s >> np.uint64(32)) == np.uint64(seq)).all()
         assert int((s & np.uint64(0xFFFFFFFF)).sum()) == int(f.sum()) == int(popc(masks.cpu().numpy()).sum())
@@ -380,7 +383,8 @@ def test_round_plan_check(gpu):
         row = arrays[c]
         assert lib.omr_worker_scan_check_f32(P(xd), L.n, B, L.num_lanes, L.num_threads, P(flags), P(nxt),
                                              ctypes.c_void_p(row.data_ptr()), None, P(ws), wsb,
-                                             ctypes.c_void_p(row.data_ptr() + 8 * (L.rows + 3)), seq, stream()) == 0
+                                             ctypes.c_void_p(row.data_ptr() + 8 * (L.rows + 3)), seq, None,
+                                             stream()) == 0
     torch.cuda.synchronize()
     pws = plan_ws(lib, gpu)
     bounds = torch.tensor([0, L.rows // 2, L.rows], dtype=torch.int64, device=gpu)

@@ -5,7 +5,7 @@
 # Results go to gpurun_out/<tag>/.  Every GPU step runs under its own time limit and the steps are chained: the first
 # failure ends the recipe (no retries).
 #   list                      this list
-#   tests TAG [pytest args]   the -m gpu suite (add -m "gpu and not slow" or test files to narrow it)
+#   tests TAG [files / ids]   the -m gpu suite, or only the test files / node ids given
 #   final TAG                 -m gpu (slow included), smoke, bench with the driver's arguments and with its defaults,
 #                             rocprofv3 --kernel-trace --stats of the default line, PMC HBM traffic of config 2
 #   bench TAG                 the other bench lines: config 3, m = 8, config 5 (N = 1), the N > 1 path at world 1
@@ -49,7 +49,8 @@ list)
   sed -n '2,/^set -o pipefail/p' "$0" | sed '$d' | sed 's/^# \{0,1\}//'
   ;;
 tests)
-  step 1100 tests.log python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider "$@"
+  [ $# -gt 0 ] || set -- tests  # (test files or node ids given: only those)
+  step 1100 tests.log python3 -u -m pytest -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider "$@"
   tail -2 "$O/tests.log"
   ;;
 final)

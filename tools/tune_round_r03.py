@@ -225,13 +225,14 @@ def main():
 
     ns = int(lib.omr_round_check_slots(L.n, B, NB, L.num_threads))
     chk_slots = torch.zeros(ns, dtype=torch.int64, device=dev)
+    done = torch.zeros(2, dtype=torch.int32, device=dev)  # (the scan's completion word, as the round passes it)
 
     def scan_pack_chk(i=0):  # the round's worker scan since round 6: + its round-check slots
         return lib.omr_worker_scan_pack_check_f32(xs[0].data_ptr(), L.n, B, NB, L.num_threads, flags.data_ptr(),
                                                   nxt.data_ptr(), own_masks.data_ptr(), None, bptr, naggs, 0,
                                                   send0.data_ptr(), cntbig[i * naggs:].data_ptr(),
                                                   own_masks[rows:].data_ptr(), ws.data_ptr(), wsb,
-                                                  chk_slots.data_ptr(), 1, st)
+                                                  chk_slots.data_ptr(), 1, done.data_ptr(), st)
 
     def pack():
         return lib.omr_move_blocks_f32(xs[0].data_ptr(), packed.data_ptr(), 0, masks[0].data_ptr(), pre[0].data_ptr(),
