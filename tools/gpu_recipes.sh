@@ -8,6 +8,7 @@
 #   tests TAG [files / ids]   the -m gpu suite, or only the test files / node ids given
 #   final TAG                 -m gpu (slow included), smoke, bench with the driver's arguments and with its defaults,
 #                             rocprofv3 --kernel-trace --stats of the default line, PMC HBM traffic of config 2
+#   finalb TAG                the same without the test suite
 #   bench TAG                 the other bench lines: config 3, m = 8, config 5 (N = 1), the N > 1 path at world 1
 #                             (one-launch and general layouts), config 1; rocprofv3 stats of config 3; PMC of config 3
 #   round TAG [filter]        the round's kernels at config 4's shapes: the launch floor (tools/tune/launch_floor.hip,
@@ -53,9 +54,11 @@ tests)
   step 1100 tests.log python3 -u -m pytest -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider "$@"
   tail -2 "$O/tests.log"
   ;;
-final)
-  step 1000 gpu_tests.log python3 -u -m pytest tests -m gpu -v --timeout 900 --timeout-method thread -p no:cacheprovider
-  tail -2 "$O/gpu_tests.log"
+final|finalb)
+  if [ "$recipe" = final ]; then
+    step 1000 gpu_tests.log python3 -u -m pytest tests -m gpu -v --timeout 900 --timeout-method thread -p no:cacheprovider
+    tail -2 "$O/gpu_tests.log"
+  fi
   step 300 smoke.log python3 -c "import __graft_entry__ as g; g.smoke()"
   jstep 240 c2_driver_args python3 bench.py --gpus 1 --steps 20 --warmup 5
   jstep 300 c2 python3 bench.py
