@@ -41,6 +41,8 @@ def parser():
     ap.add_argument("--density", type=float, default=0.095)
     ap.add_argument("--only", default="", help="time only the cases whose name contains this (PMC passes)")
     ap.add_argument("--json", default="", help="also write {case: {us, bytes}} here")
+    ap.add_argument("--check-slots", type=int, default=-1,
+                    help="the round check case reads this many slots per worker (default: the round's count)")
     return ap
 
 
@@ -275,13 +277,14 @@ def main():
                                        zcnt.data_ptr(), naggs, pws5.data_ptr(), nseq(), None, B, ctypes.byref(sl), st)
 
     chk_status = cnt_d + 12 * 1024  # (pinned, beside the counts and the round-3/4 notice)
+    nchk = min(ns, mstride - rows) if a.check_slots < 0 else min(a.check_slots, mstride - rows)
 
     def plan_round_chk():  # the round's call since round 6: + the round check's workgroup (timing only: the words it
         # checks here are position-table entries, so its status reports a mismatch)
         return lib.omr_round_plan_check(masks_all.data_ptr(), m, mstride, rows, L.rows_per_part, NB, bdev.data_ptr(),
                                         naggs + 1, wset.data_ptr(), None, prefix.data_ptr(), cnt_d, zmask.data_ptr(),
                                         zcnt.data_ptr(), naggs, pws5.data_ptr(), nseq(), None, B, ctypes.byref(sl),
-                                        rows, min(ns, mstride - rows), chk_status, st)
+                                        rows, nchk, chk_status, st)
 
     def plan_round_r04():  # the same call to the round-3/4 plan (one workgroup per mask array, arrival counter)
         seqs[0] += 1
@@ -384,7 +387,7 @@ def main():
     wbytes["scan + fused pack + round-check slots (the round's, round 6)"] = (
         wbytes["scan + fused pack (product)"] + ns * 8)
     wbytes["round plan as the round calls it + round check (round 6)"] = (
-        wbytes["round plan as the round calls it (pair list, pinned counts)"] + m * min(ns, mstride - rows) * 8)
+        wbytes["round plan as the round calls it (pair list, pinned counts)"] + m * nchk * 8)
     report = {}
     print(f"## config 4 shapes, {m} workers, -r {a.density}: shard 0 write set {ub} blocks, received {nc}, own {own_blocks}: "
           f"{sbytes} B per shard sum; worker 0 packs {other} blocks", flush=True)
