@@ -263,7 +263,9 @@ def read_pmc_round(world: int, L: Layout):
         try:
             with open(path) as f:
                 k = json.load(f)["kernels"]
-            return k["scan + fused pack (product)"]["hbm_bytes_per_launch"], path
+            kk = next((n for n in ("scan + fused pack + round-check slots (the round's, round 6)",
+                                   "scan + fused pack (product)") if n in k), None)  # (the round's own form first)
+            return k[kk]["hbm_bytes_per_launch"], path
         except (OSError, ValueError, KeyError):
             continue
     return None, None

@@ -1307,8 +1307,8 @@ constexpr uint32_t kPlanThreads = 256;
 constexpr uint32_t kPlanWaves = kPlanThreads / 64;
 constexpr uint32_t kPlanChunksMax = 64;
 constexpr uint32_t kPlanArrays = OMR_MAX_WORKERS + 1;
-// ... then the round check's findings (plan_check): per worker the sum of its scan's slots, and the lowest stale worker,
-// tagged with seq, which the last chunk compares with its totals
+// ... then the round check's findings (plan_check): per worker the sum of its scan's slots or a stale flag, tagged with
+// seq, which the last chunk compares with its totals
 constexpr uint64_t kPlanCheckWords = 1 + static_cast<uint64_t>(kPlanChunksMax) * kPlanArrays;
 constexpr uint64_t kPlanWorkspaceWords = kPlanCheckWords + OMR_MAX_WORKERS + 1;
 constexpr uint32_t kCheckStale = 0x100u, kCheckCount = 0x200u;
@@ -1460,7 +1460,9 @@ __device__ __forceinline__ void plan_chunk(const PlanArgs& a) {
     __shared__ uint32_t s_bad, s_stale;
     if (t == 0) s_bad = OMR_MAX_WORKERS;
     __syncthreads();
-    if (t <= cnt) {  // threads < cnt: worker t's slot sum; thread cnt: the lowest stale worker
+    if (t == 0) s_stale = OMR_MAX_WORKERS;
+    __syncthreads();
+    if (t < cnt) {  // worker t's check word: its slots' sum, or the top bit for a slot of another round
       uint64_t v;
       while (((v = __hip_atomic_load(&a.ws[kPlanCheckWords + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) !=
              a.seq)
@@ -1468,7 +1470,7 @@ __device__ __forceinline__ void plan_chunk(const PlanArgs& a) {
       uint32_t total = 0;
 #pragma unroll
       for (uint32_t k = 0; k < static_cast<uint32_t>(W); ++k) total = k == t ? carry[k] : total;
-      if (t == cnt) s_stale = static_cast<uint32_t>(v);
+      if (static_cast<uint32_t>(v) & 0x80000000u) (void)atomicMin(&s_stale, t);
       else if (static_cast<uint32_t>(v) != total) (void)atomicMin(&s_bad, t);
     }
     __syncthreads();
@@ -1482,66 +1484,51 @@ __device__ __forceinline__ void plan_chunk(const PlanArgs& a) {
 
 // The round check (round 6): is every worker's all-gathered mask array the one its scan of THIS round
 // wrote?  Each of the worker's scan workgroups left a slot (seq << 32) | its non-zero blocks in the array.  One more
-// workgroup of the plan launch (plan_check) reads them all and publishes, tagged with seq, each worker's slot sum and the
-// lowest worker with a slot of another round; the last chunk, which holds every worker's mask popcount total, compares
-// them (plan_chunk's end) and stores the status beside the counts: (seq << 32) | 0, | 0x100 + worker for a stale slot
+// workgroup per worker in the plan launch (plan_check) reads that worker's slots and publishes, tagged with seq, their
+// sum, or a flag when one carries another round's number; the last chunk, which holds every worker's mask popcount
+// total, compares them (plan_chunk's end) and stores the status beside the counts: (seq << 32) | 0, | 0x100 + worker for a stale slot
 // (the copy read the worker's buffer before its scan wrote the slot, or another buffer), | 0x200 + worker when the slot
 // sum differs from the masks' popcount (a copy that overtook its producer: a mask array only gains bits between the plan
 // that zeroes it and the scan that refills it, so it reads too few).  The round's host fails the round on it, by name,
-// instead of relying on the exchange's size check.  (The first form had the check workgroup wait for the chunks' totals
-// and add its slots with a shared-memory atomic each: 6 us more than the plan; profiles/r06/INDEX.md.)
+// instead of relying on the exchange's size check.  (The first form had one check workgroup wait for the chunks' totals
+// and add the slots with a shared-memory atomic each: 6 us more than the plan; one workgroup reading every worker's
+// slots, 3 us more; profiles/r06/INDEX.md.)
 template <int W>
-__device__ __forceinline__ void plan_check(const PlanArgs& a) {
-  __shared__ uint32_t s_sum[kPlanWaves][W];
-  __shared__ uint32_t s_stale;  // the lowest stale worker (OMR_MAX_WORKERS: none)
+__device__ __forceinline__ void plan_check(const PlanArgs& a, uint32_t c) {
+  // worker c's slots, a few per thread, all in flight at once (512 at config 4: two per thread); a slot of another
+  // round sets the published word's top bit, else it carries the slots' sum (< 2^28 blocks)
+  __shared__ uint32_t s_sum[kPlanWaves], s_stale;
   const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  if (t == 0) s_stale = OMR_MAX_WORKERS;
-  const uint32_t ns = a.chk_slots, words = a.count * ns;
-  const float inv_ns = 1.0f / static_cast<float>(ns);
-  auto worker_of = [&](uint32_t idx) {  // idx / ns without an integer division (the quotient is < 17: exact after a fix)
-    uint32_t c = static_cast<uint32_t>(static_cast<float>(idx) * inv_ns);
-    c = c * ns > idx ? c - 1 : c;
-    return (c + 1) * ns <= idx ? c + 1 : c;
-  };
-  constexpr uint32_t U = 16;  // loads in flight per thread
-  uint32_t sum[W], stale = OMR_MAX_WORKERS;
-#pragma unroll
-  for (int k = 0; k < W; ++k) sum[k] = 0;
-  for (uint32_t base = 0; base < words; base += kPlanThreads * U) {
+  if (t == 0) s_stale = 0;
+  const uint32_t ns = a.chk_slots;
+  const uint64_t* const slots = a.masks + static_cast<uint64_t>(c) * a.mstride + a.chk_off;
+  constexpr uint32_t U = 8;  // loads in flight per thread
+  uint32_t sum = 0, stale = 0;
+  for (uint32_t base = 0; base < ns; base += kPlanThreads * U) {
     uint64_t v[U];
-    uint32_t cw[U];
 #pragma unroll
-    for (uint32_t i = 0; i < U; ++i) {
+    for (uint32_t i = 0; i < U; ++i) {  // (unconditional loads from clamped indices)
       const uint32_t idx = base + i * kPlanThreads + t;
-      cw[i] = idx < words ? worker_of(idx) : OMR_MAX_WORKERS;
-      v[i] = idx < words ? a.masks[static_cast<uint64_t>(cw[i]) * a.mstride + a.chk_off + (idx - cw[i] * ns)] : 0ull;
+      v[i] = slots[idx < ns ? idx : 0u];
     }
 #pragma unroll
     for (uint32_t i = 0; i < U; ++i) {
-      if (cw[i] == OMR_MAX_WORKERS) continue;
-      if (static_cast<uint32_t>(v[i] >> 32) != a.seq) stale = min(stale, cw[i]);
-#pragma unroll
-      for (int k = 0; k < W; ++k) sum[k] += cw[i] == static_cast<uint32_t>(k) ? static_cast<uint32_t>(v[i]) : 0u;
+      if (base + i * kPlanThreads + t >= ns) continue;
+      stale |= static_cast<uint32_t>(v[i] >> 32) != a.seq ? 1u : 0u;
+      sum += static_cast<uint32_t>(v[i]);
     }
   }
-#pragma unroll
-  for (int k = 0; k < W; ++k) {
-    const uint32_t inc = wave_incl_scan(sum[k]);
-    if (lane == 63) s_sum[wave][k] = inc;
-  }
+  const uint32_t inc = wave_incl_scan(sum);
+  if (lane == 63) s_sum[wave] = inc;
   __syncthreads();  // (s_stale initialised, s_sum filled)
-  if (stale < OMR_MAX_WORKERS) (void)atomicMin(&s_stale, stale);
+  if (stale) s_stale = 1;
   __syncthreads();
-  const uint64_t tag = static_cast<uint64_t>(a.seq) << 32;
-  if (t < a.count) {
-    uint32_t got = 0;
+  if (t == 0) {
+    uint32_t total = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < kPlanWaves; ++w)
-#pragma unroll
-      for (int k = 0; k < W; ++k) got += t == static_cast<uint32_t>(k) ? s_sum[w][k] : 0u;
-    __hip_atomic_store(&a.ws[kPlanCheckWords + t], tag | got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (t == a.count) {
-    __hip_atomic_store(&a.ws[kPlanCheckWords + t], tag | s_stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t w = 0; w < kPlanWaves; ++w) total += s_sum[w];
+    const uint64_t word = (static_cast<uint64_t>(a.seq) << 32) | (s_stale ? 0x80000000u : (total & 0x7FFFFFFFu));
+    __hip_atomic_store(&a.ws[kPlanCheckWords + c], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1555,8 +1542,8 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
     return;
   }
   const uint32_t b = blockIdx.x - a.nchunks;
-  if (a.chk_status != nullptr && b == a.chain_wgs + a.list_wgs) {
-    plan_check<W>(a);
+  if (a.chk_status != nullptr && b >= a.chain_wgs + a.list_wgs) {  // the round check, one workgroup per worker
+    plan_check<W>(a, b - a.chain_wgs - a.list_wgs);
     return;
   }
   if (b >= a.chain_wgs) {  // the shard sum's pair list, one unit per wave
@@ -2908,7 +2895,7 @@ int omr_round_plan_check(const uint64_t* row_masks, uint32_t count, uint64_t mas
   a.chk_off = check_offset;
   a.chk_slots = check_slots;
   a.chk_status = check_status;
-  const unsigned grid = a.nchunks + chain_wgs + a.list_wgs + (check_status != nullptr ? 1u : 0u);
+  const unsigned grid = a.nchunks + chain_wgs + a.list_wgs + (check_status != nullptr ? count : 0u);
   hipStream_t st = S(stream);
   if (count <= 2) k_round_plan<2><<<grid, kPlanThreads, 0, st>>>(a);
   else if (count <= 4) k_round_plan<4><<<grid, kPlanThreads, 0, st>>>(a);
