@@ -2737,7 +2737,12 @@ int sparse_round_issue(omr_ar_plan* p, const float* x, float* out, int32_t* flag
       if (p->thread_rc != 0) return derr(p->thread_rc, "%s", p->thread_err.c_str());
     }
     if (S.plan_pending) {
-      TRY(wait_ev(st, S.ready));
+      // (threaded, the caller runs up to kSets rounds ahead of the GPU, so that plan has usually not run yet when this
+      // scan is issued: a device-side wait would sit between two scans on the caller's stream and hold the next one
+      // 3-7 us (profiles/r06/world1_general/trace_signalled/).  The caller waits for it on the host instead, which
+      // keeps it two to three rounds ahead, as the deferred caller is.)
+      if (threaded) TRY(wait_event_bounded(p->d, S.ready, "round: the set's last plan"));
+      else TRY(wait_ev(st, S.ready));
       S.plan_pending = false;
     }
     // A fused-pack scan refills the round's send buffer: the round kPackBufs calls back, which read it (its exchange

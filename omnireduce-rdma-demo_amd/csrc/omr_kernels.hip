@@ -1162,6 +1162,9 @@ __device__ __forceinline__ uint32_t xcd_spread(uint32_t i, uint32_t base, uint32
   return ((base + i) % 8) * (n / 8) + i / 8;
 }
 
+// W >= count: the workers' mask rows a unit loads (the plan launch's width: at 8 workers half the loads, registers and
+// L2 requests of the 16-wide form, whose 2 048 units each fetched every group's rows for 16 workers)
+template <int W = OMR_MAX_WORKERS>
 __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, uint64_t ustride) {
   const int lane = threadIdx.x & 63;
   const uint64_t units = list_units(a);
@@ -1186,9 +1189,9 @@ __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, u
     }
     const bool rl = static_cast<uint32_t>(lane) < nload;
     const uint64_t r = g0 + (rl ? static_cast<uint32_t>(lane) : 0u);
-    uint64_t mk[OMR_MAX_WORKERS];  // (unconditional loads from clamped addresses: one round trip, see plan_rows)
+    uint64_t mk[W];  // (unconditional loads from clamped addresses: one round trip, see plan_rows)
 #pragma unroll
-    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) {
+    for (uint32_t c = 0; c < W; ++c) {
       const uint64_t v = a.masks[(c < a.count ? c : 0u) * a.mstride + r];
       mk[c] = (c < a.count && rl) ? v : 0ull;
     }
@@ -1197,13 +1200,13 @@ __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, u
         cl ? reinterpret_cast<const uint32_t*>(a.masks + lane * a.mstride)[a.pos_off + gidx * a.lanes + l] : 0u;
     uint64_t un = 0;
 #pragma unroll
-    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) un |= mk[c];
+    for (uint32_t c = 0; c < W; ++c) un |= mk[c];
     const uint64_t w = (rl && r % a.rpp == 0) ? (un | a.all_lanes) : un;  // write set: union + lane heads
     const bool mine = static_cast<uint32_t>(lane) >= h0 && static_cast<uint32_t>(lane) < h1;
     const bool wb = mine && ((w >> l) & 1ull);
     uint32_t cb = 0;
 #pragma unroll
-    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) cb |= static_cast<uint32_t>((mk[c] >> l) & 1ull) << c;
+    for (uint32_t c = 0; c < W; ++c) cb |= static_cast<uint32_t>((mk[c] >> l) & 1ull) << c;
     const uint32_t np = wb ? (cb ? static_cast<uint32_t>(__builtin_popcount(cb)) : 1u) : 0u;
     uint32_t inc = np;
 #pragma unroll
@@ -1217,9 +1220,9 @@ __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, u
       a.records[u * a.cap + total] = kRecEnd;
     }
     if (total == 0) continue;
-    uint64_t ccol[OMR_MAX_WORKERS];  // worker c's bits of column l over the group's rows
+    uint64_t ccol[W];  // worker c's bits of column l over the group's rows
 #pragma unroll
-    for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) ccol[c] = c < a.count ? __ballot((mk[c] >> l) & 1ull) : 0ull;
+    for (uint32_t c = 0; c < W; ++c) ccol[c] = c < a.count ? __ballot((mk[c] >> l) & 1ull) : 0ull;
     if (np != 0) {
       uint64_t* const rec = a.records + u * a.cap;
       uint32_t k = inc - np;
@@ -1229,7 +1232,7 @@ __device__ __forceinline__ void build_sum_list(const ListArgs& a, uint64_t u0, u
         rec[k] = hdr | kRecZero | kRecFirst | kRecLast;
       } else {
 #pragma unroll
-        for (uint32_t c = 0; c < OMR_MAX_WORKERS; ++c) {
+        for (uint32_t c = 0; c < W; ++c) {
           if (!((cb >> c) & 1u)) continue;
           uint64_t v;
           if (c == a.me) {
@@ -1549,7 +1552,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(PlanArgs a) {
   if (b >= a.chain_wgs) {  // the shard sum's pair list, one unit per wave
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t li = xcd_spread(b - a.chain_wgs, a.nchunks + a.chain_wgs, a.list_wgs);
-    build_sum_list(a.list, static_cast<uint64_t>(li) * kPlanWaves + w, static_cast<uint64_t>(a.list_wgs) * kPlanWaves);
+    build_sum_list<W>(a.list, static_cast<uint64_t>(li) * kPlanWaves + w, static_cast<uint64_t>(a.list_wgs) * kPlanWaves);
     return;
   }
   const uint64_t* m = a.masks;  // the aggregator chain over the union, one segment each
