@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Round 5: summarise the kernel trace of bench.py's N>1 path rehearsed as 8 IPC ranks on one GPU
-(tools/r05/gpu_h.sh: one rocprofv3 --kernel-trace file per rank): per rank, the GPU time by kernel kind (the round's
+(tools/gpu_recipes.sh ipc_ranks TAG 8 trace: one rocprofv3 --kernel-trace file per rank): per rank, the GPU time by kernel kind (the round's
 kernels, ROCclr's device-side waits for IPC events `__amd_rocclr_streamOpsWait`, its event writes, copies), the hardware
 queues each rank used, the fraction of the span its queues and the whole GPU had a kernel running, and rank 0's
 per-round intervals (scan to scan).
